@@ -1,0 +1,408 @@
+"""CPU oracle for the MRA-GAN CycleGAN hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker for the HIP engine in ``mra-gan_amd/``.  It is a
+functional restatement, in PyTorch-CPU (fp32 or fp64), of the reference's
+``CycleGANModel.optimize_parameters()`` step and everything under it:
+
+* ResnetGenerator / ResnetBlock      (reference models/networks3D.py:173-263)
+* NLayerDiscriminator                (reference models/networks3D.py:381-425)
+* InstanceNorm3d(affine=False, track_running_stats=True) in train mode
+                                     (reference models/networks3D.py:15-24)
+* GANLoss (BCE or LSGAN), L1 losses  (reference models/networks3D.py:130-150,
+                                      models/cycle_gan_model.py:103-105)
+* ImagePool                          (reference models/cycle_gan_model.py:8-35)
+* torch.optim.Adam                   (reference models/cycle_gan_model.py:107-110)
+* the step orchestration             (reference models/cycle_gan_model.py:121-240)
+* deterministic init (same RNG consumption as the reference's constructors +
+  init_weights, so a given torch seed yields bit-identical initial weights)
+                                     (reference models/networks3D.py:44-81)
+
+Pinning: the oracle is checked against golden fixtures produced by running the
+reference itself in the build container (``tools/gen_fixtures.py`` →
+``tests/golden/``; test ``tests/test_oracle_golden.py``).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this module.  The product path never does.
+"""
+from __future__ import annotations
+
+import math
+import random
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch.nn import init
+
+IN_EPS = 1e-5          # nn.InstanceNorm3d default eps
+IN_MOMENTUM = 0.1      # nn.InstanceNorm3d default momentum
+LRELU_SLOPE = 0.2      # networks3D.py:393
+
+
+# --------------------------------------------------------------------------------------
+# Architecture specs (state_dict indices identical to the reference's nn.Sequential)
+# --------------------------------------------------------------------------------------
+
+def resnet_generator_layers(input_nc: int, output_nc: int, ngf: int, n_blocks: int) -> List[dict]:
+    """Layer list of ResnetGenerator (networks3D.py:173-220) with the reference's
+    Sequential indices as state_dict prefixes.  Each entry is one conv (+ its norm/act)."""
+    layers = []
+    idx = 0
+    # RPad3 (idx 0) → Conv k7 (1) → IN (2) → ReLU (3)   networks3D.py:185-189
+    layers.append(dict(kind="conv", name=f"model.{idx+1}", cin=input_nc, cout=ngf, k=7, s=1, p=0,
+                       prepad=3, bias=True, norm=f"model.{idx+2}", act="relu"))
+    idx += 4
+    # 2 × [Conv k3 s2 p1 → IN → ReLU]                      networks3D.py:191-197
+    for i in range(2):
+        mult = 2 ** i
+        layers.append(dict(kind="conv", name=f"model.{idx}", cin=ngf * mult, cout=ngf * mult * 2, k=3, s=2,
+                           p=1, prepad=0, bias=True, norm=f"model.{idx+1}", act="relu"))
+        idx += 3
+    # ResnetBlocks                                       networks3D.py:199-201, 224-263
+    dim = ngf * 4
+    for b in range(n_blocks):
+        pre = f"model.{idx}.conv_block"
+        layers.append(dict(kind="resblock", name=f"model.{idx}", dim=dim,
+                           conv1=f"{pre}.1", norm1=f"{pre}.2", conv2=f"{pre}.5", norm2=f"{pre}.6"))
+        idx += 1
+    # 2 × [ConvT k3 s2 p1 op1 → IN → ReLU]                 networks3D.py:203-210
+    for i in range(2):
+        mult = 2 ** (2 - i)
+        layers.append(dict(kind="convT", name=f"model.{idx}", cin=ngf * mult, cout=ngf * mult // 2, k=3,
+                           s=2, p=1, op=1, bias=True, norm=f"model.{idx+1}", act="relu"))
+        idx += 3
+    # RPad3 → Conv k7 (ngf → output_nc) → Tanh             networks3D.py:211-213
+    layers.append(dict(kind="conv", name=f"model.{idx+1}", cin=ngf, cout=output_nc, k=7, s=1, p=0,
+                       prepad=3, bias=True, norm=None, act="tanh"))
+    return layers
+
+
+def nlayer_discriminator_layers(input_nc: int, ndf: int, n_layers: int, use_sigmoid: bool) -> List[dict]:
+    """Layer list of NLayerDiscriminator (networks3D.py:381-425)."""
+    layers = [dict(kind="conv", name="model.0", cin=input_nc, cout=ndf, k=4, s=2, p=1, prepad=0,
+                   bias=True, norm=None, act="lrelu")]
+    idx = 2
+    nf_mult = 1
+    for n in range(1, n_layers):
+        nf_prev, nf_mult = nf_mult, min(2 ** n, 8)
+        layers.append(dict(kind="conv", name=f"model.{idx}", cin=ndf * nf_prev, cout=ndf * nf_mult, k=4, s=2,
+                           p=1, prepad=0, bias=True, norm=f"model.{idx+1}", act="lrelu"))
+        idx += 3
+    nf_prev, nf_mult = nf_mult, min(2 ** n_layers, 8)
+    layers.append(dict(kind="conv", name=f"model.{idx}", cin=ndf * nf_prev, cout=ndf * nf_mult, k=4, s=1, p=1,
+                       prepad=0, bias=True, norm=f"model.{idx+1}", act="lrelu"))
+    idx += 3
+    layers.append(dict(kind="conv", name=f"model.{idx}", cin=ndf * nf_mult, cout=1, k=4, s=1, p=1, prepad=0,
+                       bias=True, norm=None, act="sigmoid" if use_sigmoid else None))
+    return layers
+
+
+# --------------------------------------------------------------------------------------
+# Deterministic init — consumes the global torch RNG exactly like the reference
+# --------------------------------------------------------------------------------------
+
+def _conv_param_shapes(layer: dict) -> List[Tuple[str, tuple, int]]:
+    """(prefix, weight shape, fan_in for bias bound) for each conv of a layer entry."""
+    if layer["kind"] == "resblock":
+        d = layer["dim"]
+        w = (d, d, 3, 3, 3)
+        return [(layer["conv1"], w), (layer["conv2"], w)]
+    k = layer["k"]
+    if layer["kind"] == "convT":     # ConvTranspose3d weight is [Cin, Cout, k, k, k]
+        return [(layer["name"], (layer["cin"], layer["cout"], k, k, k))]
+    return [(layer["name"], (layer["cout"], layer["cin"], k, k, k))]
+
+
+def _norm_entries(layer: dict) -> List[Tuple[str, int]]:
+    if layer["kind"] == "resblock":
+        return [(layer["norm1"], layer["dim"]), (layer["norm2"], layer["dim"])]
+    if layer.get("norm"):
+        return [(layer["norm"], layer["cout"])]
+    return []
+
+
+def init_net_state(layers: List[dict], init_gain: float = 0.02, dtype=torch.float32) -> "OrderedDict[str, torch.Tensor]":
+    """Build the state_dict of a net.  RNG consumption mirrors:
+    (1) nn.Conv3d / nn.ConvTranspose3d constructors (kaiming_uniform_(a=√5) on the weight,
+        uniform_ on the bias) in module-construction order, then
+    (2) init_weights (networks3D.py:44-65): normal_(0, gain) on every conv weight, bias = 0,
+        in net.apply order (= module order for these nets)."""
+    state: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    convs = []
+    for layer in layers:
+        for prefix, wshape in _conv_param_shapes(layer):
+            w = torch.empty(wshape, dtype=torch.float32)
+            init.kaiming_uniform_(w, a=math.sqrt(5))
+            b = torch.empty(wshape[0] if layer["kind"] != "convT" else wshape[1], dtype=torch.float32)
+            fan_in, _ = init._calculate_fan_in_and_fan_out(w)
+            bound = 1.0 / math.sqrt(fan_in)
+            init.uniform_(b, -bound, bound)
+            convs.append((prefix, w, b))
+    for prefix, w, b in convs:
+        init.normal_(w, 0.0, init_gain)
+        b.zero_()
+    # assemble in state_dict order (module order; norms interleaved after their conv)
+    conv_map = {p: (w, b) for p, w, b in convs}
+    for layer in layers:
+        if layer["kind"] == "resblock":
+            order = [("conv", layer["conv1"]), ("norm", layer["norm1"]), ("conv", layer["conv2"]), ("norm", layer["norm2"])]
+            dims = {layer["norm1"]: layer["dim"], layer["norm2"]: layer["dim"]}
+        else:
+            order = [("conv", layer["name"])]
+            if layer.get("norm"):
+                order.append(("norm", layer["norm"]))
+            dims = {layer.get("norm"): layer["cout"]}
+        for kind, prefix in order:
+            if kind == "conv":
+                w, b = conv_map[prefix]
+                state[prefix + ".weight"] = w.to(dtype)
+                state[prefix + ".bias"] = b.to(dtype)
+            else:
+                c = dims[prefix]
+                state[prefix + ".running_mean"] = torch.zeros(c, dtype=dtype)
+                state[prefix + ".running_var"] = torch.ones(c, dtype=dtype)
+                state[prefix + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return state
+
+
+# --------------------------------------------------------------------------------------
+# Ops (explicit restatements of the ATen semantics the reference relies on)
+# --------------------------------------------------------------------------------------
+
+def instance_norm_train(x: torch.Tensor, state: dict, prefix: str) -> torch.Tensor:
+    """nn.InstanceNorm3d(affine=False, track_running_stats=True) in train mode
+    (networks3D.py:19).  y = (x − μ_nc)/√(σ²_nc,biased + eps).  Running stats:
+    r ← (1−m)·r + m·mean_n(stat_n) with the UNBIASED variance; num_batches_tracked is
+    left at 0 (InstanceNorm never increments it)."""
+    n = x.shape[2] * x.shape[3] * x.shape[4]
+    if n <= 1:
+        raise ValueError(f"Expected more than 1 spatial element when training, got input size {list(x.shape)}")
+    dims = (2, 3, 4)
+    mean = x.mean(dim=dims, keepdim=True)
+    var = ((x - mean) ** 2).mean(dim=dims, keepdim=True)
+    y = (x - mean) / torch.sqrt(var + IN_EPS)
+    with torch.no_grad():
+        rm = state[prefix + ".running_mean"]
+        rv = state[prefix + ".running_var"]
+        bmean = mean.detach().reshape(x.shape[0], x.shape[1]).to(rm.dtype).mean(0)
+        bvar_unb = (var.detach() * (n / (n - 1))).reshape(x.shape[0], x.shape[1]).to(rv.dtype).mean(0)
+        rm.mul_(1 - IN_MOMENTUM).add_(IN_MOMENTUM * bmean)
+        rv.mul_(1 - IN_MOMENTUM).add_(IN_MOMENTUM * bvar_unb)
+    return y
+
+
+def _act(x, act):
+    if act == "relu":
+        return F.relu(x)
+    if act == "lrelu":
+        return F.leaky_relu(x, LRELU_SLOPE)
+    if act == "tanh":
+        return torch.tanh(x)
+    if act == "sigmoid":
+        return torch.sigmoid(x)
+    return x
+
+
+def _rpad(x, p):
+    return F.pad(x, (p,) * 6, mode="replicate") if p else x   # nn.ReplicationPad3d(p)
+
+
+def generator_forward(state: dict, params: dict, layers: List[dict], x: torch.Tensor) -> torch.Tensor:
+    """ResnetGenerator.forward (networks3D.py:219-220): the Sequential of layers."""
+    h = x
+    for L in layers:
+        if L["kind"] == "conv":
+            h = F.conv3d(_rpad(h, L["prepad"]), params[L["name"] + ".weight"], params[L["name"] + ".bias"],
+                         stride=L["s"], padding=L["p"])
+            if L["norm"]:
+                h = instance_norm_train(h, state, L["norm"])
+            h = _act(h, L["act"])
+        elif L["kind"] == "convT":
+            h = F.conv_transpose3d(h, params[L["name"] + ".weight"], params[L["name"] + ".bias"],
+                                   stride=L["s"], padding=L["p"], output_padding=L["op"])
+            h = instance_norm_train(h, state, L["norm"])
+            h = _act(h, L["act"])
+        else:  # ResnetBlock.forward: x + conv_block(x)   networks3D.py:261-263
+            r = F.conv3d(_rpad(h, 1), params[L["conv1"] + ".weight"], params[L["conv1"] + ".bias"])
+            r = F.relu(instance_norm_train(r, state, L["norm1"]))
+            r = F.conv3d(_rpad(r, 1), params[L["conv2"] + ".weight"], params[L["conv2"] + ".bias"])
+            r = instance_norm_train(r, state, L["norm2"])
+            h = h + r
+    return h
+
+
+discriminator_forward = generator_forward   # same Sequential walk (networks3D.py:424-425)
+
+
+def gan_loss(pred: torch.Tensor, target_is_real: bool, use_lsgan: bool) -> torch.Tensor:
+    """GANLoss.__call__ (networks3D.py:130-150): MSELoss (lsgan) or BCELoss vs a constant
+    target of 1/0.  BCELoss clamps each log at −100 (ATen binary_cross_entropy)."""
+    t = 1.0 if target_is_real else 0.0
+    if use_lsgan:
+        return ((pred - t) ** 2).mean()
+    return F.binary_cross_entropy(pred, torch.full_like(pred, t))
+
+
+def l1_loss(a, b):
+    return (a - b).abs().mean()      # nn.L1Loss (cycle_gan_model.py:104-105)
+
+
+def cor_coe_loss(y_pred, y_target):
+    """Cor_CoeLoss (networks3D.py:156-166): 1 − r²; computed but unused by loss_G."""
+    xv = y_pred - y_pred.mean()
+    yv = y_target - y_target.mean()
+    r = (xv * yv).sum() / (torch.sqrt((xv ** 2).sum()) * torch.sqrt((yv ** 2).sum()))
+    return 1 - r ** 2
+
+
+class ImagePool:
+    """ImagePool (cycle_gan_model.py:8-35).  Uses the Python `random` module."""
+
+    def __init__(self, pool_size: int, rng: random.Random = None):
+        self.pool_size = pool_size
+        self.rng = rng if rng is not None else random
+        self.num_imgs = 0
+        self.images: List[torch.Tensor] = []
+
+    def query(self, images: torch.Tensor) -> torch.Tensor:
+        if self.pool_size == 0:
+            return images
+        out = []
+        for image in images:
+            image = image.detach().unsqueeze(0)
+            if self.num_imgs < self.pool_size:
+                self.num_imgs += 1
+                self.images.append(image)
+                out.append(image)
+            else:
+                if self.rng.uniform(0, 1) > 0.5:
+                    rid = self.rng.randint(0, self.pool_size - 1)
+                    tmp = self.images[rid].clone()
+                    self.images[rid] = image
+                    out.append(tmp)
+                else:
+                    out.append(image)
+        return torch.cat(out, 0)
+
+
+def adam_update(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int,
+                lr: float, beta1: float, beta2: float = 0.999, eps: float = 1e-8) -> None:
+    """torch.optim.Adam single-tensor update (amsgrad=False, weight_decay=0), as used by
+    cycle_gan_model.py:107-110.  m uses lerp (torch's exact form)."""
+    m.lerp_(g, 1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    step_size = lr / bc1
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-step_size)
+
+
+# --------------------------------------------------------------------------------------
+# The step
+# --------------------------------------------------------------------------------------
+
+class CycleGANOracle:
+    """Functional restatement of CycleGANModel (cycle_gan_model.py:38-240) on CPU."""
+
+    LOSS_NAMES = ['D_A', 'G_A', 'cycle_A', 'idt_A', 'D_B', 'G_B', 'cycle_B', 'idt_B']  # :68
+
+    def __init__(self, input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, n_layers_D=3,
+                 use_lsgan=False, lambda_A=10.0, lambda_B=10.0, lambda_identity=0.5,
+                 lr=2e-4, beta1=0.5, pool_size=50, init_gain=0.02, dtype=torch.float32,
+                 states: Dict[str, dict] = None, pool_rng: random.Random = None):
+        self.dtype = dtype
+        self.use_lsgan = use_lsgan
+        self.lambda_A, self.lambda_B, self.lambda_idt = lambda_A, lambda_B, lambda_identity
+        self.lr, self.beta1 = lr, beta1
+        self.layers = {
+            "G_A": resnet_generator_layers(input_nc, output_nc, ngf, n_blocks),
+            "G_B": resnet_generator_layers(output_nc, input_nc, ngf, n_blocks),
+            "D_A": nlayer_discriminator_layers(output_nc, ndf, n_layers_D, not use_lsgan),
+            "D_B": nlayer_discriminator_layers(input_nc, ndf, n_layers_D, not use_lsgan),
+        }
+        if states is None:   # same construction order as CycleGANModel.initialize (:83-96)
+            states = {k: init_net_state(self.layers[k], init_gain) for k in ("G_A", "G_B", "D_A", "D_B")}
+        self.state = {k: OrderedDict((n, t.clone().to(dtype) if t.is_floating_point() else t.clone())
+                                     for n, t in v.items()) for k, v in states.items()}
+        self.params = {k: OrderedDict((n, t) for n, t in self.state[k].items()
+                                      if n.endswith(".weight") or n.endswith(".bias")) for k in self.state}
+        self.adam = {k: {n: (torch.zeros_like(t), torch.zeros_like(t)) for n, t in self.params[k].items()}
+                     for k in self.params}
+        self.step_count = {"G": 0, "D": 0}
+        self.fake_A_pool = ImagePool(pool_size, pool_rng)
+        self.fake_B_pool = ImagePool(pool_size, pool_rng)
+        self.grads: Dict[str, Dict[str, torch.Tensor]] = {}
+
+    # --- helpers -------------------------------------------------------------------
+    def _net(self, name, x, params):
+        return generator_forward(self.state[name], params, self.layers[name], x)
+
+    def _leaf_params(self, names, requires_grad):
+        out = {}
+        for k in names:
+            out[k] = {n: t.detach().clone().requires_grad_(requires_grad) for n, t in self.params[k].items()}
+        return out
+
+    def _adam(self, nets, leaf, group):
+        self.step_count[group] += 1
+        step = self.step_count[group]
+        for k in nets:
+            for n, p in self.params[k].items():
+                g = leaf[k][n].grad
+                if g is None:
+                    continue
+                m, v = self.adam[k][n]
+                adam_update(p, g.detach(), m, v, step, self.lr, self.beta1)
+
+    # --- optimize_parameters (cycle_gan_model.py:227-240) --------------------------
+    def optimize_parameters(self, real_A: torch.Tensor, real_B: torch.Tensor) -> "OrderedDict[str, float]":
+        real_A = real_A.to(self.dtype)
+        real_B = real_B.to(self.dtype)
+        self.real_A, self.real_B = real_A, real_B
+        lp = self._leaf_params(["G_A", "G_B"], True)
+        dp = self._leaf_params(["D_A", "D_B"], False)       # set_requires_grad(D, False) :231
+        # forward (:121-136)
+        fake_B = self._net("G_A", real_A, lp["G_A"])
+        rec_A = self._net("G_B", fake_B, lp["G_B"])
+        fake_A = self._net("G_B", real_B, lp["G_B"])
+        rec_B = self._net("G_A", fake_A, lp["G_A"])
+        # backward_G (:163-225)
+        idt_A = self._net("G_A", real_B, lp["G_A"])
+        loss_idt_A = l1_loss(idt_A, real_B) * self.lambda_B * self.lambda_idt
+        idt_B = self._net("G_B", real_A, lp["G_B"])
+        loss_idt_B = l1_loss(idt_B, real_A) * self.lambda_A * self.lambda_idt
+        loss_G_A = gan_loss(self._net("D_A", fake_B, dp["D_A"]), True, self.use_lsgan)
+        loss_G_B = gan_loss(self._net("D_B", fake_A, dp["D_B"]), True, self.use_lsgan)
+        loss_cycle_A = l1_loss(rec_A, real_A) * self.lambda_A
+        loss_cycle_B = l1_loss(rec_B, real_B) * self.lambda_B
+        loss_G = loss_G_A + loss_G_B + loss_cycle_A + loss_cycle_B + loss_idt_A + loss_idt_B
+        loss_G.backward()
+        self.grads = {k: {n: t.grad.detach().clone() for n, t in lp[k].items()} for k in ("G_A", "G_B")}
+        self._adam(["G_A", "G_B"], lp, "G")
+        # D phase (:236-240)
+        dp = self._leaf_params(["D_A", "D_B"], True)
+        fB = self.fake_B_pool.query(fake_B.detach())
+        loss_D_A = 0.5 * (gan_loss(self._net("D_A", real_B, dp["D_A"]), True, self.use_lsgan)
+                          + gan_loss(self._net("D_A", fB, dp["D_A"]), False, self.use_lsgan))
+        loss_D_A.backward()
+        fA = self.fake_A_pool.query(fake_A.detach())
+        loss_D_B = 0.5 * (gan_loss(self._net("D_B", real_A, dp["D_B"]), True, self.use_lsgan)
+                          + gan_loss(self._net("D_B", fA, dp["D_B"]), False, self.use_lsgan))
+        loss_D_B.backward()
+        self.grads.update({k: {n: t.grad.detach().clone() for n, t in dp[k].items()} for k in ("D_A", "D_B")})
+        self._adam(["D_A", "D_B"], dp, "D")
+        self.fake_B, self.rec_A, self.fake_A, self.rec_B = (t.detach() for t in (fake_B, rec_A, fake_A, rec_B))
+        self.idt_A, self.idt_B = idt_A.detach(), idt_B.detach()
+        vals = dict(D_A=loss_D_A, G_A=loss_G_A, cycle_A=loss_cycle_A, idt_A=loss_idt_A,
+                    D_B=loss_D_B, G_B=loss_G_B, cycle_B=loss_cycle_B, idt_B=loss_idt_B)
+        return OrderedDict((k, float(vals[k].detach())) for k in self.LOSS_NAMES)
+
+
+def synthetic_pair(shape, seed: int):
+    """Synthetic inputs: A then B ~ N(0,1) fp32 from torch.Generator(seed)."""
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(shape, generator=g)
+    b = torch.randn(shape, generator=g)
+    return a, b

@@ -1,0 +1,56 @@
+"""Helpers to read the golden fixtures made by tools/gen_fixtures.py (reference run)."""
+import ast
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# argv flags of each case → oracle / engine constructor kwargs
+CASE_KW = {
+    "step_r9_s32_b1": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
+    "step_r6_s24_b2_nc2_lsgan": dict(input_nc=2, output_nc=2, ngf=8, ndf=8, n_blocks=6, use_lsgan=True),
+    "step_r9_s32_b2_ngf16": dict(input_nc=1, output_nc=1, ngf=16, ndf=16, n_blocks=9, use_lsgan=False),
+}
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    meta = ast.literal_eval(str(z["meta"]))
+    return z, meta
+
+
+def sampled(z, key, t: torch.Tensor):
+    flat = t.detach().reshape(-1).double().cpu()
+    idx = torch.from_numpy(z[key + "/idx"])
+    return flat[idx].numpy(), z[key + "/val"]
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def inputs(meta, step):
+    g = torch.Generator().manual_seed(1000 + meta["seed"] + step)
+    shape = (meta["B"], meta["nc"], meta["S"], meta["S"], meta["S"])
+    return torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+
+
+# Pre-InstanceNorm conv biases have an identically-zero true gradient (IN without affine
+# cancels any per-channel constant).  Their fp32 reference gradient is round-off noise.
+def is_pre_in_bias(net, key, n_layers_D=3):
+    if not key.endswith(".bias"):
+        return False
+    if net.startswith("G"):
+        return "conv_block" in key or not _is_g_head(key)
+    # D: model.0 (no IN) and the final conv have real gradients
+    idx = int(key.split(".")[1])
+    return idx not in (0, 3 * n_layers_D + 2)
+
+
+def _is_g_head(key):
+    # the head conv is the last conv of the generator; its index depends on n_blocks
+    return key in ("model.26.bias", "model.23.bias")
