@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark: 3D patches/sec of one full CycleGAN optimize_parameters() step
+(G_A, G_B, D_A, D_B forward + backward + both Adam steps), BASELINE.json's metric.
+
+Workload (N=1): BASELINE configs[1] — ResNet-9blocks G + 3-layer PatchGAN D, 1ch→1ch,
+64³ patch, batch 2 per GPU, synthetic N(0,1) volumes, random init (seed 0).  Multi-GPU:
+one process per GPU (torch.distributed over RCCL), each rank its own batch (weak scaling),
+gradients all-reduced inside the step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 64] [--batch 2]
+
+Prints ONE JSON line on rank 0 (contract in the task description), with:
+  roofline     — the dominant kernel (res-block 3×3×3 conv, implicit-GEMM f32 MFMA): algorithmic
+                 FLOP per launch ÷ its mean launch duration, timed with HIP events around every
+                 such launch inside the timed region;
+  cpu_baseline — the CPU oracle (oracle/cyclegan_oracle.py, the reference's algorithm restated
+                 in PyTorch-CPU) timed on this host for one step of the same workload.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "mra-gan_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix/vector peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--ngf", type=int, default=32)
+    ap.add_argument("--netG", default="resnet_9blocks")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    return ap.parse_args()
+
+
+def step_flops(S, batch, ngf=32, n_blocks=9, ndf=32, nc=1):
+    """Algorithmic conv FLOPs of one optimize_parameters() step (2 × MAC; forward, dgrad where
+    the reference computes it, wgrad).  Matches SURVEY §0 (1.6045 TFLOP per 64³ patch)."""
+    def conv(cin, cout, k, out_vox):
+        return 2.0 * cin * cout * k ** 3 * out_vox
+    s4 = (S // 4) ** 3
+    g_layers = [conv(nc, ngf, 7, S ** 3), conv(ngf, 2 * ngf, 3, (S // 2) ** 3), conv(2 * ngf, 4 * ngf, 3, s4)]
+    g_layers += [conv(4 * ngf, 4 * ngf, 3, s4)] * (2 * n_blocks)
+    g_layers += [conv(2 * ngf, 4 * ngf, 3, s4), conv(ngf, 2 * ngf, 3, (S // 2) ** 3), conv(ngf, nc, 7, S ** 3)]
+    g_fwd = sum(g_layers)
+    first_g = g_layers[0]
+    d_sp = [S // 2, S // 4, S // 8, S // 8 - 1, S // 8 - 2]
+    d_layers = [conv(nc, ndf, 4, d_sp[0] ** 3), conv(ndf, 2 * ndf, 4, d_sp[1] ** 3), conv(2 * ndf, 4 * ndf, 4, d_sp[2] ** 3),
+                conv(4 * ndf, 8 * ndf, 4, d_sp[3] ** 3), conv(8 * ndf, 1, 4, d_sp[4] ** 3)]
+    d_fwd = sum(d_layers)
+    first_d = d_layers[0]
+    # 6 G passes: fwd + wgrad + dgrad, minus input dgrad for the 4 passes fed real data
+    g = 6 * (3 * g_fwd) - 4 * first_g
+    # D: 2 frozen passes (fwd + dgrad incl. input), 4 trainable passes (fwd + wgrad + dgrad w/o input)
+    d = 2 * (2 * d_fwd) + 4 * (3 * d_fwd - first_d)
+    return batch * (g + d)
+
+
+def cpu_baseline(args):
+    """Oracle step on the host CPU (same workload shape), bounded to a couple of steps."""
+    from oracle.cyclegan_oracle import CycleGANOracle, synthetic_pair
+    torch.set_num_threads(os.cpu_count())
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    orc = CycleGANOracle(ngf=args.ngf, ndf=args.ngf, n_blocks=9 if args.netG == "resnet_9blocks" else 6,
+                         pool_rng=random.Random(0))
+    shape = (args.batch, 1, args.size, args.size, args.size)
+    times = []
+    for i in range(args.cpu_steps):
+        A, B = synthetic_pair(shape, 1000 + i)
+        t0 = time.perf_counter()
+        orc.optimize_parameters(A, B)
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": args.batch / t, "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} optimize_parameters() step(s) of the CPU oracle (PyTorch-CPU fp32) on "
+                      f"{args.batch}x1x{args.size}^3, best {t:.2f} s, {cpu_model}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+
+    from models import create_model
+    from mragan_hip import ops
+    from options.train_options import TrainOptions
+
+    sys_argv = sys.argv
+    sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
+                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch)]
+    opt = TrainOptions().gather_options()
+    sys.argv = sys_argv
+    opt.isTrain, opt.gpu_ids = True, 0
+    torch.manual_seed(0)
+    random.seed(0)
+    model = create_model(opt)
+    model.setup(opt)
+
+    g = torch.Generator().manual_seed(1000 + rank)
+    shape = (args.batch, 1, args.size, args.size, args.size)
+    n_in = args.warmup + args.steps
+    inputs = [(torch.randn(shape, generator=g).cuda(), torch.randn(shape, generator=g).cuda()) for _ in range(n_in)]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        model.set_input(inputs[i])
+        model.optimize_parameters()
+    barrier()
+
+    # dominant kernel: residual-block conv 4ngf→4ngf k3 (forward form) of the batched first G pass
+    c4 = 4 * args.ngf
+    s4 = args.size // 4
+    n_launch = 2 * args.batch
+    ops.TIMER.reset()
+    ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
+                                 not i["transposed"] and i["N"] == n_launch)
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    start.record()
+    for i in range(args.steps):
+        model.set_input(inputs[args.warmup + i])
+        model.optimize_parameters()
+    end.record()
+    barrier()
+    wall = time.perf_counter() - t0
+    ops.TIMER.match = None
+    elapsed = start.elapsed_time(end) / 1e3
+    elapsed = max(elapsed, wall)
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    kern_ms = ops.TIMER.mean_ms()
+    n_kern = len(ops.TIMER.events)
+
+    if rank != 0:
+        dist.destroy_process_group() if dist is not None else None
+        return
+
+    patches = world * args.batch * args.steps
+    value = patches / elapsed
+    flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
+    achieved = flops_launch / (kern_ms / 1e3) / 1e12 if kern_ms else None
+    step_tf = step_flops(args.size, args.batch, args.ngf) / 1e12
+    res = {
+        "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
+        "value": round(value, 3),
+        "unit": "patches/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic N(0,1) volumes, random init (seed 0)",
+        "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, 1ch->1ch, "
+                               f"{args.size}^3 patch, batch {args.batch}/GPU (BASELINE configs[1] shape; fp32)",
+                   "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": f"conv_igemm_f32 res-block conv {c4}->{c4} k3 "
+                                               f"[{n_launch}x{s4}^3] fwd",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": MFMA_F32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4) if achieved else None,
+                     "traffic": None, "launch_ms": round(kern_ms, 4) if kern_ms else None,
+                     "launches_timed": n_kern, "flop_per_launch": flops_launch},
+        "step_tflop": round(step_tf, 4),
+        "step_tflops_achieved": round(step_tf * args.steps / elapsed, 2),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

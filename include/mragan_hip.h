@@ -1,0 +1,114 @@
+/* mragan_hip.h — C ABI of the MI355X (gfx950) kernel library behind the MRA-GAN CycleGAN
+ * training step.  Built as mra-gan_amd/lib/libmragan_hip.so.
+ *
+ * The reference (pedrob37/MRA-GAN) has no FFI: its hot path is PyTorch/ATen called from
+ * models/networks3D.py and models/cycle_gan_model.py.  Each entry point below replaces the
+ * ATen op(s) those reference lines invoke; the Python layer in mra-gan_amd/ (models/,
+ * mragan_hip/) binds them with ctypes.
+ *
+ * Conventions
+ *   - every pointer is a device pointer (hipMalloc / torch caching allocator); kernels never
+ *     allocate, callers pass workspaces sized by the *_workspace() queries;
+ *   - activations are NDHWC fp32 (channels contiguous); "padded" tensors carry a replication
+ *     border of `pad` voxels on every spatial side;
+ *   - packed conv weights are [k³][Nout][Kc] fp32 (tap = (td*k + th)*k + tw), produced from the
+ *     torch layouts by mragan_pack_weight;
+ *   - `stream` is a hipStream_t (NULL = default stream);
+ *   - return value 0 = success, otherwise an error code; mragan_last_error() describes it.
+ */
+#ifndef MRAGAN_HIP_H_
+#define MRAGAN_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRAGAN_ABI_VERSION 1
+
+enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
+enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
+
+int mragan_abi_version(void);
+const char* mragan_last_error(void);
+
+/* ---- convolution --------------------------------------------------------------------------
+ * Forward form:     y[n,o,:] = act(bias + Σ_{j<k³} x[n, o*stride − pad + j, :] · Wp[j])  (zero fill)
+ * Replaces nn.Conv3d.forward (networks3D.py:186, 192, 241, 257, 212, 389, 397, 406, 414) and the
+ * input-gradient of nn.ConvTranspose3d (networks3D.py:203-210).                              */
+int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, const float* bias,
+                      int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream);
+
+/* Transposed form:  y[n,o,:] = act(bias + Σ_{t:(o+pad−t)%stride==0} x[n,(o+pad−t)/stride,:] · Wp[t])
+ * Replaces nn.ConvTranspose3d.forward (networks3D.py:203-210) and the input-gradient of every
+ * nn.Conv3d above (autograd convolution_backward, grad_input branch).                        */
+int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                             const float* bias, int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho,
+                             int Wo, void* stream);
+
+/* Weight gradient:  dw[dn][gn][t] (=|+=) Σ_m dense[m][dn] · gathered[m*stride − pad + t][gn]
+ * Conv3d:          dense = dY (output grid), gathered = X      → dw = torch [Cout][Cin][k][k][k]
+ * ConvTranspose3d: dense = X (input grid),   gathered = dY     → dw = torch [Cin][Cout][k][k][k]
+ * Replaces the grad_weight branch of convolution_backward for the same layers.              */
+size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride);
+int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int Cd, const float* gathered, int Dg, int Hg,
+                        int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                        size_t ws_bytes, void* stream);
+
+/* src[A][B][k³] (torch layout) → dst[k³][A][B] (transpose_ab = 0) or dst[k³][B][A] (= 1). */
+int mragan_pack_weight(const float* src, int A, int B, int T, int transpose_ab, float* dst, void* stream);
+
+/* ---- InstanceNorm3d(affine=False, track_running_stats=True), train mode --------------------
+ * y (replication-padded by ypad) = act((x − μ_nc)·rstd_nc) (+ resid interior of an rpad-padded
+ * tensor).  mean / rstd: [N][C] outputs saved for the backward.  Replaces nn.InstanceNorm3d +
+ * the following nn.ReLU / LeakyReLU / residual add / nn.ReplicationPad3d
+ * (networks3D.py:19, 186-189, 191-197, 203-210, 233-263, 396-409).                           */
+size_t mragan_instnorm_workspace(int N, int D, int H, int W, int C);
+int mragan_instnorm_fwd(const float* x, int N, int D, int H, int W, int C, float* y, int ypad, int act, const float* resid,
+                        int rpad, float* mean, float* rstd, void* ws, size_t ws_bytes, void* stream);
+/* dx = IN-backward( fold(dy, dypad) + dy_add ) through act; the workspace must hold
+ * mragan_instnorm_workspace(...) + 8·N·C bytes.                                              */
+int mragan_instnorm_bwd(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                        const float* dy, int dypad, const float* dy_add, int act, float* dx, void* ws, size_t ws_bytes,
+                        void* stream);
+
+/* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
+ * entry listing the per-instance statistics of the reference's sequential calls in call order. */
+typedef struct mragan_running_seg { const float* mean; const float* rstd; int32_t count; int32_t _pad; } mragan_running_seg;
+typedef struct mragan_running_entry {
+  float* running_mean; float* running_var; const float* bias; int32_t C; int32_t nseg; int64_t S;
+  mragan_running_seg seg[8];
+} mragan_running_entry;
+int mragan_instnorm_running_update(const void* table, int nentries, float momentum, void* stream);
+size_t mragan_running_entry_size(void);
+
+/* ---- replication pad (nn.ReplicationPad3d forward / backward) ---------------------------- */
+int mragan_rpad(const float* x, int N, int D, int H, int W, int C, int pad, float* y, void* stream);
+int mragan_rpad_fold(const float* ypad, int N, int D, int H, int W, int C, int pad, const float* add, float* x, void* stream);
+
+/* ---- element-wise / losses ---------------------------------------------------------------- */
+/* dx = (g0 + g1 + g2) · act'(y)   (ReLU/LeakyReLU from their output, Tanh, Sigmoid)         */
+int mragan_act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx,
+                   void* stream);
+/* nn.L1Loss (cycle_gan_model.py:104-105): loss[0] (=|+=) scale·mean|a−b|; grad (=|+=) scale·sign(a−b)/n.
+ * ws: ≥ 4096 bytes.                                                                            */
+int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_accumulate, float* grad,
+                   int grad_accumulate, void* ws, void* stream);
+/* GANLoss (networks3D.py:130-150) on D's output p: BCE (lsgan = 0, p = sigmoid output) or MSE.
+ * loss[0] (=|+=) scale·loss; dlogit = d(scale·loss)/d(pre-sigmoid logits) (BCE) or d/dp (MSE). */
+int mragan_gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_accumulate,
+                    float* dlogit, void* ws, void* stream);
+/* bias gradient: out[c] (=|+=) Σ_m x[m][c] */
+int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int accumulate, void* stream);
+/* torch.optim.Adam step (amsgrad=False, weight_decay=0) on flat buffers (cycle_gan_model.py:107-110);
+ * the gradient is multiplied by grad_scale first (1/world_size after a SUM all-reduce).      */
+int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+                int step, float grad_scale, void* stream);
+int mragan_fill(float* p, int64_t n, float value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRAGAN_HIP_H_ */

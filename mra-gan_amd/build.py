@@ -1,0 +1,56 @@
+"""Build libmragan_hip.so for gfx950 in-tree (mra-gan_amd/lib/).  No JIT cache, no torch
+extension machinery: plain hipcc, one object per .hip file, parallel compile."""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+OBJ = os.path.join(HERE, "build")
+ARCH = os.environ.get("MRAGAN_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+
+
+def sources():
+    return sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _needs(obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, jobs=None):
+    os.makedirs(LIB, exist_ok=True)
+    os.makedirs(OBJ, exist_ok=True)
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "mragan_hip.h"))
+    objs, cmds = [], []
+    for s in sources():
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s.replace(".hip", ".o"))
+        objs.append(obj)
+        if _needs(obj, [src] + headers):
+            cmds.append(["hipcc", *FLAGS, "-c", src, "-o", obj])
+    with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 1)) as ex:
+        for cmd, r in zip(cmds, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds)):
+            if verbose or r.returncode:
+                sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+            if r.returncode:
+                raise RuntimeError(f"hipcc failed for {cmd[-3]}")
+    so = os.path.join(LIB, "libmragan_hip.so")
+    if cmds or not os.path.exists(so):
+        r = subprocess.run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", so],
+                           capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
+    return so
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

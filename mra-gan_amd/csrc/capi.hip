@@ -1,0 +1,163 @@
+// extern "C" entry points of libmragan_hip.so (declared in include/mragan_hip.h).
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/mragan_hip.h"
+#include "kernels.h"
+
+namespace mragan {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return kLaunch;
+  }
+  return kOk;
+}
+
+static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0; }
+
+static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
+                       int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* stream) {
+  MRAGAN_CHECK_ARG(x && w && y, "conv: null pointer");
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv: bad input shape");
+  MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv: bad output shape");
+  MRAGAN_CHECK_ARG(k >= 1 && stride >= 1 && pad >= 0, "conv: bad k/stride/pad");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (thin_side(cin, cout)) {
+    ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
+    return conv_thin(a, st);
+  }
+  IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1};
+  return conv_igemm(a, st);
+}
+
+static bool thin_wgrad_side(int Cd, int Cg) { return Cd < 8 || Cg < 8; }
+
+}  // namespace mragan
+
+using namespace mragan;
+
+extern "C" {
+
+int mragan_abi_version(void) { return MRAGAN_ABI_VERSION; }
+const char* mragan_last_error(void) { return g_err; }
+
+int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
+                      int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream) {
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 0, stream);
+}
+
+int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias,
+                             int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream) {
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 1, stream);
+}
+
+size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride) {
+  if (thin_wgrad_side(Cd, Cg)) return conv_thin_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k, stride);
+  return conv_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k);
+}
+
+int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int Cd, const float* gathered, int Dg, int Hg,
+                        int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws, size_t ws_bytes,
+                        void* stream) {
+  MRAGAN_CHECK_ARG(dense && gathered && dw && ws, "wgrad: null pointer");
+  MRAGAN_CHECK_ARG(Cd > 0 && Cg > 0 && k >= 1 && stride >= 1 && pad >= 0, "wgrad: bad args");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (thin_wgrad_side(Cd, Cg)) {
+    ThinWgradArgs a{};
+    a.D = dense; a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd;
+    a.G = gathered; a.Dg = Dg; a.Hg = Hg; a.Wg = Wg; a.Cg = Cg; a.k = k; a.s = stride; a.p = pad;
+    return conv_thin_wgrad(a, dw, accumulate, static_cast<float*>(ws), ws_bytes, st);
+  }
+  WgradArgs a{dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0};
+  return conv_wgrad(a, dw, accumulate, ws_bytes, st);
+}
+
+int mragan_pack_weight(const float* src, int A, int B, int T, int tr, float* dst, void* stream) {
+  MRAGAN_CHECK_ARG(src && dst && A > 0 && B > 0 && T > 0, "pack_weight: bad args");
+  return pack_weight(src, A, B, T, tr, dst, static_cast<hipStream_t>(stream));
+}
+
+size_t mragan_instnorm_workspace(int N, int D, int H, int W, int C) {
+  return instnorm_ws_bytes(N, D, H, W, C) + (size_t)N * C * 2 * sizeof(float) + 256;
+}
+
+int mragan_instnorm_fwd(const float* x, int N, int D, int H, int W, int C, float* y, int ypad, int act, const float* resid,
+                        int rpad_, float* mean, float* rstd, void* ws, size_t ws_bytes, void* stream) {
+  MRAGAN_CHECK_ARG(x && y && mean && rstd && ws, "instnorm_fwd: null pointer");
+  return instnorm_fwd(x, InShape{N, D, H, W, C}, y, ypad, act, resid, rpad_, mean, rstd, ws, ws_bytes,
+                      static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_bwd(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                        const float* dy, int dypad, const float* dy_add, int act, float* dx, void* ws, size_t ws_bytes,
+                        void* stream) {
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx && ws, "instnorm_bwd: null pointer");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, dx};
+  return instnorm_bwd(a, InShape{N, D, H, W, C}, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_running_update(const void* table, int nentries, float momentum, void* stream) {
+  return instnorm_running(table, nentries, momentum, static_cast<hipStream_t>(stream));
+}
+
+size_t mragan_running_entry_size(void) { return instnorm_running_entry_bytes(); }
+
+int mragan_rpad(const float* x, int N, int D, int H, int W, int C, int pad, float* y, void* stream) {
+  MRAGAN_CHECK_ARG(x && y && pad >= 0, "rpad: bad args");
+  return rpad(x, N, D, H, W, C, pad, y, static_cast<hipStream_t>(stream));
+}
+
+int mragan_rpad_fold(const float* yp, int N, int D, int H, int W, int C, int pad, const float* add, float* x, void* stream) {
+  MRAGAN_CHECK_ARG(yp && x && pad >= 0, "rpad_fold: bad args");
+  return rpad_fold(yp, N, D, H, W, C, pad, add, x, static_cast<hipStream_t>(stream));
+}
+
+int mragan_act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx,
+                   void* stream) {
+  MRAGAN_CHECK_ARG(dx && n >= 0, "act_bwd: bad args");
+  return act_bwd(y, g0, g1, g2, n, act, dx, static_cast<hipStream_t>(stream));
+}
+
+int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad,
+                   int grad_acc, void* ws, void* stream) {
+  MRAGAN_CHECK_ARG(a && b && loss && ws && n > 0, "l1_loss: bad args");
+  return l1_loss(a, b, n, scale, loss, loss_acc, grad, grad_acc, static_cast<float*>(ws), static_cast<hipStream_t>(stream));
+}
+
+int mragan_gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc,
+                    float* dlogit, void* ws, void* stream) {
+  MRAGAN_CHECK_ARG(p && loss && ws && n > 0, "gan_loss: bad args");
+  return gan_loss(p, n, target, lsgan, scale, loss, loss_acc, dlogit, static_cast<float*>(ws),
+                  static_cast<hipStream_t>(stream));
+}
+
+int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* stream) {
+  MRAGAN_CHECK_ARG(x && out, "channel_sum: bad args");
+  return channel_sum(x, M, C, out, acc, static_cast<hipStream_t>(stream));
+}
+
+int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+                int step, float grad_scale, void* stream) {
+  MRAGAN_CHECK_ARG(p && g && m && v && step >= 1, "adam: bad args");
+  return adam(p, g, m, v, n, lr, beta1, beta2, eps, step, grad_scale, static_cast<hipStream_t>(stream));
+}
+
+int mragan_fill(float* p, int64_t n, float value, void* stream) {
+  MRAGAN_CHECK_ARG(p, "fill: null");
+  return fill(p, n, value, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// Shared helpers for the MRA-GAN MI355X (gfx950) kernel library.
+//
+// Layout conventions:
+//   * activations are NDHWC fp32: element (n, d, h, w, c) at ((((n*D + d)*H + h)*W + w)*C + c)
+//   * packed conv weights are [tap][Nout][Kc] (contraction channels contiguous), tap = (td*k + th)*k + tw
+//   * master weights / gradients keep the reference's torch layouts
+//       Conv3d [Cout][Cin][k][k][k], ConvTranspose3d [Cin][Cout][k][k][k]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace mragan {
+
+// status codes returned through the C ABI
+enum Status : int {
+  kOk = 0,
+  kBadArg = 1,
+  kWorkspace = 2,
+  kLaunch = 3,
+  kUnsupported = 4,
+};
+
+// activation codes shared with include/mragan_hip.h
+enum Act : int { kActNone = 0, kActRelu = 1, kActLrelu = 2, kActTanh = 3, kActSigmoid = 4 };
+
+constexpr float kLreluSlope = 0.2f;   // reference networks3D.py:393
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  switch (act) {
+    case kActRelu: return v > 0.f ? v : 0.f;
+    case kActLrelu: return v > 0.f ? v : v * kLreluSlope;
+    case kActTanh: return tanhf(v);
+    case kActSigmoid: return 1.f / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+struct Vol {   // batch + spatial extents of an NDHWC tensor
+  int n, d, h, w;
+  __host__ __device__ int64_t spatial() const { return (int64_t)d * h * w; }
+  __host__ __device__ int64_t voxels() const { return (int64_t)n * d * h * w; }
+};
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace mragan
+
+#define MRAGAN_CHECK_ARG(cond, ...)           \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::mragan::set_error(__VA_ARGS__);       \
+      return ::mragan::kBadArg;               \
+    }                                         \
+  } while (0)

@@ -1,0 +1,273 @@
+// Generic implicit-GEMM 3D convolution on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// One kernel covers every dense convolution of the hot path (SURVEY §8a A9-A11, A16 and
+// all their data-gradients):
+//
+//   forward form   y[n,o,:] = Σ_{j<k³}  x[n, o*s - p + j, :] · Wp[j]            (zero fill)
+//   transposed form y[n,o,:] = Σ_{t : (o+p-t) % s == 0} x[n, (o+p-t)/s, :] · Wp[t]
+//
+// The transposed form is evaluated per output parity class (o ≡ c mod s, blockIdx.z = class),
+// so every tap a block visits is a real one (sub-pixel decomposition; no masked MACs).
+// It is used for ConvTranspose3d forward (networks3D.py:203-210) and for the data gradient of
+// every forward conv; the forward form also yields the data gradient of ConvTranspose3d.
+//
+// GEMM view per class: rows = output voxels (M), cols = output channels (N = ny),
+// contraction = (tap, input channel) with input channels contiguous (NDHWC) → the A tile is a
+// gather of BM voxel rows × BK channels, the B tile is Wp[t][n0:n0+BN][c0:c0+BK].
+// Both tiles live in LDS as [row][BK+4] (K contiguous, +16 B row pad → conflict-free
+// ds_read_b128), register-staged double buffer, one barrier per K-step.
+// MFMA K-order: lane half h supplies k = 4h+s at step s, so each lane reads ONE float4 of
+// A and of B per 8-deep chunk and feeds 4 MFMAs from it.
+#include "kernels.h"
+
+namespace mragan {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+
+// per-dimension class geometry
+struct DimGeo {
+  int Q;       // number of output positions in the class along this dim
+  int ntap;    // taps visited along this dim
+  int t0, tstep;
+  int a_mul;   // in = a_mul*q + base_add + sign*j
+  int base_add;
+  int sign;
+  int o_mul, o_add;   // output coordinate = o_mul*q + o_add
+};
+
+__device__ __forceinline__ DimGeo dim_geo(int c, int O, int k, int s, int p, int trans) {
+  DimGeo g;
+  if (!trans) {
+    g.Q = O; g.ntap = k; g.t0 = 0; g.tstep = 1;
+    g.a_mul = s; g.base_add = -p; g.sign = 1;
+    g.o_mul = 1; g.o_add = 0;
+  } else {
+    g.Q = (O - c + s - 1) / s;
+    int t0 = (c + p) % s;
+    g.t0 = t0; g.tstep = s;
+    g.ntap = (t0 < k) ? (k - t0 + s - 1) / s : 0;
+    g.a_mul = 1; g.base_add = (c + p - t0) / s; g.sign = -1;
+    g.o_mul = s; g.o_add = c;
+  }
+  return g;
+}
+
+template <int WM, int WN, int TM, int TN, int BK>
+__global__ void __launch_bounds__(256)
+conv_igemm_f32_kernel(IgemmArgs a) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int LDK = BK + 4;               // padded row (floats)
+  constexpr int LPR = BK / 4;               // float4 per row
+  constexpr int A_LOADS = (BM * LPR + 255) / 256;
+  constexpr int B_LOADS = (BN * LPR + 255) / 256;
+  constexpr int ROWS_PER_PASS = 256 / LPR;
+  static_assert(WM * WN == 4, "4 waves");
+
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK + BM];
+  float* As = smem;                          // [2][BM][LDK]
+  float* Bs = smem + 2 * BM * LDK;           // [2][BN][LDK]
+  int* out_off = reinterpret_cast<int*>(smem + 2 * (BM + BN) * LDK);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM * 32;
+  const int wn0 = (wave % WN) * TN * 32;
+
+  // class geometry (wave-uniform)
+  int cls = blockIdx.z;
+  int cw = cls % a.s, ch = (cls / a.s) % a.s, cd = cls / (a.s * a.s);
+  if (a.nclass == 1) { cd = ch = cw = 0; }
+  const DimGeo gd = dim_geo(cd, a.Do, a.k, a.s, a.p, a.trans);
+  const DimGeo gh = dim_geo(ch, a.Ho, a.k, a.s, a.p, a.trans);
+  const DimGeo gw = dim_geo(cw, a.Wo, a.k, a.s, a.p, a.trans);
+  const int64_t Mc = (int64_t)a.N * gd.Q * gh.Q * gw.Q;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  if (m0 >= Mc) return;
+  const int ntaps = gd.ntap * gh.ntap * gw.ntap;
+
+  // output offsets of this tile's rows (for the epilogue)
+  for (int r = tid; r < BM; r += 256) {
+    int64_t m = m0 + r;
+    int off = -1;
+    if (m < Mc) {
+      int qw = (int)(m % gw.Q); int64_t t = m / gw.Q;
+      int qh = (int)(t % gh.Q); t /= gh.Q;
+      int qd = (int)(t % gd.Q); int nb = (int)(t / gd.Q);
+      int od = gd.o_mul * qd + gd.o_add, oh = gh.o_mul * qh + gh.o_add, ow = gw.o_mul * qw + gw.o_add;
+      off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+    }
+    out_off[r] = off;
+  }
+
+  // loader state: input base coordinates of this thread's A rows
+  const int q = tid % LPR;
+  int a_nb[A_LOADS], a_bd[A_LOADS], a_bh[A_LOADS], a_bw[A_LOADS];
+#pragma unroll
+  for (int i = 0; i < A_LOADS; ++i) {
+    int r = tid / LPR + i * ROWS_PER_PASS;
+    int64_t m = m0 + r;
+    if (r < BM && m < Mc) {
+      int qw = (int)(m % gw.Q); int64_t t = m / gw.Q;
+      int qh = (int)(t % gh.Q); t /= gh.Q;
+      int qd = (int)(t % gd.Q); int nb = (int)(t / gd.Q);
+      a_nb[i] = nb;
+      a_bd[i] = gd.a_mul * qd + gd.base_add;
+      a_bh[i] = gh.a_mul * qh + gh.base_add;
+      a_bw[i] = gw.a_mul * qw + gw.base_add;
+    } else {
+      a_nb[i] = -1; a_bd[i] = a_bh[i] = a_bw[i] = 0;
+    }
+  }
+
+  const int kchunks = a.cx / BK;
+  const int nK = ntaps * kchunks;
+
+  float4 ra[A_LOADS], rb[B_LOADS];
+
+  auto load_tiles = [&](int ks) {
+    int tap = ks / kchunks;
+    int c0 = (ks - tap * kchunks) * BK;
+    int jw = tap % gw.ntap; int tt = tap / gw.ntap;
+    int jh = tt % gh.ntap; int jd = tt / gh.ntap;
+    int td = gd.t0 + gd.tstep * jd, th = gh.t0 + gh.tstep * jh, tw = gw.t0 + gw.tstep * jw;
+    int wt = (td * a.k + th) * a.k + tw;
+    int dd = gd.sign * jd, dh = gh.sign * jh, dw = gw.sign * jw;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
+      bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
+                (unsigned)iw < (unsigned)a.Wi;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        const float* src = a.x + ((((int64_t)a_nb[i] * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 + 4 * q;
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      int n = n0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < BN && n < a.ny)
+        v = *reinterpret_cast<const float4*>(a.w + ((int64_t)wt * a.ny + n) * a.cx + c0 + 4 * q);
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      if (r < BM) *reinterpret_cast<float4*>(As + (buf * BM + r) * LDK + 4 * q) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      if (r < BN) *reinterpret_cast<float4*>(Bs + (buf * BN + r) * LDK + 4 * q) = rb[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  if (nK > 0) {
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
+
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nK) load_tiles(ks + 1);
+    const float* Ab = As + buf * BM * LDK;
+    const float* Bb = Bs + buf * BN * LDK;
+#pragma unroll
+    for (int kc = 0; kc < BK / 8; ++kc) {
+      float4 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[i] = *reinterpret_cast<const float4*>(Ab + (wm0 + i * 32 + li) * LDK + kc * 8 + 4 * lh);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = *reinterpret_cast<const float4*>(Bb + (wn0 + j * 32 + li) * LDK + kc * 8 + 4 * lh);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (ks + 1 < nK) store_tiles(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int col = n0 + wn0 + j * 32 + li;
+    if (col >= a.ny) continue;
+    float bsum = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int off = out_off[row];
+        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int BK>
+static int launch_igemm(const IgemmArgs& a, int64_t max_mc, hipStream_t st) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  dim3 grid(ceil_div(max_mc, BM), ceil_div(a.ny, BN), a.nclass);
+  hipLaunchKernelGGL((conv_igemm_f32_kernel<WM, WN, TM, TN, BK>), grid, dim3(256), 0, st, a);
+  return check_launch("conv_igemm_f32");
+}
+
+template <int BK>
+static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  // pick the largest tile that still gives ≥ 2 blocks per CU (256 CUs), else the smallest
+  auto blocks = [&](int bm, int bn) { return (int64_t)ceil_div(total_m, bm) * ceil_div(a.ny, bn); };
+  if (a.ny > 64) {
+    if (blocks(128, 128) >= 512) return launch_igemm<2, 2, 2, 2, BK>(a, max_mc, st);
+    if (blocks(128, 64) >= 512) return launch_igemm<2, 2, 2, 1, BK>(a, max_mc, st);
+    return launch_igemm<2, 2, 1, 1, BK>(a, max_mc, st);
+  }
+  if (a.ny > 32) {
+    if (blocks(128, 64) >= 512) return launch_igemm<2, 2, 2, 1, BK>(a, max_mc, st);
+    return launch_igemm<2, 2, 1, 1, BK>(a, max_mc, st);
+  }
+  if (blocks(256, 32) >= 512) return launch_igemm<4, 1, 2, 1, BK>(a, max_mc, st);
+  return launch_igemm<4, 1, 1, 1, BK>(a, max_mc, st);
+}
+
+int conv_igemm(IgemmArgs a, hipStream_t st) {
+  MRAGAN_CHECK_ARG(a.cx % 8 == 0, "conv_igemm: contraction channels %d not a multiple of 8", a.cx);
+  MRAGAN_CHECK_ARG(a.k >= 1 && a.s >= 1 && a.p >= 0, "conv_igemm: bad k/s/p");
+  a.nclass = (a.trans && a.s > 1) ? a.s * a.s * a.s : 1;
+  // largest class row count (class 0 is the largest along every dim)
+  auto q = [&](int O, int c) { return a.trans ? (O - c + a.s - 1) / a.s : O; };
+  int64_t max_mc = (int64_t)a.N * q(a.Do, 0) * q(a.Ho, 0) * q(a.Wo, 0);
+  int64_t total_m = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  if (max_mc == 0 || a.ny == 0) return kOk;
+  if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);
+  if (a.cx % 16 == 0) return dispatch_tile<16>(a, max_mc, total_m, st);
+  return dispatch_tile<8>(a, max_mc, total_m, st);
+}
+
+}  // namespace mragan

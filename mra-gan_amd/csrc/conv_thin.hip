@@ -1,0 +1,447 @@
+// Thin-channel 3D convolutions (one side has the image channel count nc = 1..2):
+//   * G stem   Conv3d(nc→ngf, k7) on the RPad3 input      (networks3D.py:185-189)  fwd: thin_k
+//   * G head   Conv3d(ngf→nc, k7) + Tanh                   (networks3D.py:211-213)  fwd: thin_n
+//   * D first  Conv3d(nc→ndf, k4 s2 p1) + LeakyReLU        (networks3D.py:389-390)  fwd: thin_k
+//   * D last   Conv3d(8ndf→1, k4 s1 p1) (+ Sigmoid)        (networks3D.py:417-420)  fwd: naive
+// and their data / weight gradients.  On fp32 the VALU FMA rate equals the f32 MFMA rate
+// (157 TF both), and these GEMMs have N or K of 1-2, so they are written as VALU direct
+// convolutions with the input halo staged in LDS and the per-tap weights read as
+// wave-uniform (scalar) loads.
+#include "kernels.h"
+
+namespace mragan {
+
+
+// ---------------------------------------------------------------------------------------
+// thin_k: contraction channels cx ≤ 4, many output channels.  One thread = one output voxel ×
+// 32 output channels (grid.y walks channel groups).  Forward (any stride) or transposed s = 1.
+// ---------------------------------------------------------------------------------------
+constexpr int TK_OD = 4, TK_OH = 8, TK_OW = 8;   // 256 voxels per block
+constexpr int TK_NB = 32;
+
+template <int CX>
+__global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w, int RD, int RH,
+                                                     int RW) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];   // [RD][RH][RW][CX]
+  const int tid = threadIdx.x;
+  int tile = blockIdx.x;
+  const int tw_ = tile % tiles_w; tile /= tiles_w;
+  const int th_ = tile % tiles_h; tile /= tiles_h;
+  const int td_ = tile % tiles_d; const int nb = tile / tiles_d;
+  const int o0d = td_ * TK_OD, o0h = th_ * TK_OH, o0w = tw_ * TK_OW;
+  const int n0 = blockIdx.y * TK_NB;
+  // region origin in input coordinates
+  int r0d, r0h, r0w;
+  if (!a.trans) { r0d = o0d * a.s - a.p; r0h = o0h * a.s - a.p; r0w = o0w * a.s - a.p; }
+  else { r0d = o0d + a.p - (a.k - 1); r0h = o0h + a.p - (a.k - 1); r0w = o0w + a.p - (a.k - 1); }
+  const int R = RD * RH * RW;
+  for (int e = tid; e < R; e += 256) {
+    int rw = e % RW, rh = (e / RW) % RH, rd = e / (RW * RH);
+    int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
+    bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+    const float* src = a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * CX;
+#pragma unroll
+    for (int c = 0; c < CX; ++c) xs[e * CX + c] = ok ? src[c] : 0.f;
+  }
+  __syncthreads();
+  const int ow = tid % TK_OW, oh = (tid / TK_OW) % TK_OH, od = tid / (TK_OW * TK_OH);
+  const int gd = o0d + od, gh = o0h + oh, gw = o0w + ow;
+  float acc[TK_NB];
+#pragma unroll
+  for (int j = 0; j < TK_NB; ++j) acc[j] = 0.f;
+  // local origin of this voxel's window inside the region
+  const int ld = a.trans ? od : od * a.s, lh = a.trans ? oh : oh * a.s, lw = a.trans ? ow : ow * a.s;
+  const int k = a.k;
+  const int nvalid = min(TK_NB, a.ny - n0);
+  for (int jd = 0; jd < k; ++jd)
+    for (int jh = 0; jh < k; ++jh)
+      for (int jw = 0; jw < k; ++jw) {
+        // forward: tap t = j at offset j; transposed (s=1): offset j ↔ tap k-1-j
+        int t = a.trans ? (((k - 1 - jd) * k + (k - 1 - jh)) * k + (k - 1 - jw)) : ((jd * k + jh) * k + jw);
+        const float* xv = xs + (((ld + jd) * RH + (lh + jh)) * RW + (lw + jw)) * CX;
+        const float* wt = a.w + ((int64_t)t * a.ny + n0) * CX;
+        float xr[CX];
+#pragma unroll
+        for (int c = 0; c < CX; ++c) xr[c] = xv[c];
+        if (nvalid == TK_NB) {
+#pragma unroll
+          for (int j = 0; j < TK_NB; ++j)
+#pragma unroll
+            for (int c = 0; c < CX; ++c) acc[j] = fmaf(xr[c], wt[j * CX + c], acc[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < TK_NB; ++j)
+            if (j < nvalid)
+#pragma unroll
+              for (int c = 0; c < CX; ++c) acc[j] = fmaf(xr[c], wt[j * CX + c], acc[j]);
+        }
+      }
+  if (gd < a.Do && gh < a.Ho && gw < a.Wo) {
+    float* dst = a.y + ((((int64_t)nb * a.Do + gd) * a.Ho + gh) * a.Wo + gw) * a.ny + n0;
+#pragma unroll
+    for (int j = 0; j < TK_NB; ++j)
+      if (j < nvalid) dst[j] = act_fwd(acc[j] + (a.bias ? a.bias[n0 + j] : 0.f), a.act);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// thin_n: few output channels (ny ≤ 4), contraction channels a multiple of 2; stride 1.
+// Block = 4×4×64 output voxels, thread = 4 consecutive w outputs; the input halo is staged
+// two channels at a time and each thread holds a (4 + K − 1)-wide window of the row in
+// registers, so each LDS read feeds up to 4·K·NY·2 FMAs.
+// ---------------------------------------------------------------------------------------
+constexpr int TN_OD = 4, TN_OH = 4, TN_OW = 64, TN_VW = 4;
+
+template <int NY, int K>
+__global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w) {
+  extern __shared__ __attribute__((aligned(16))) float2 xs2[];   // [RD][RH][RW] float2
+  constexpr int RD = TN_OD + K - 1, RH = TN_OH + K - 1, RW = TN_OW + K - 1;
+  constexpr int WL = TN_VW + K - 1;
+  const int tid = threadIdx.x;
+  int tile = blockIdx.x;
+  const int tw_ = tile % tiles_w; tile /= tiles_w;
+  const int th_ = tile % tiles_h; tile /= tiles_h;
+  const int td_ = tile % tiles_d; const int nb = tile / tiles_d;
+  const int o0d = td_ * TN_OD, o0h = th_ * TN_OH, o0w = tw_ * TN_OW;
+  int r0d, r0h, r0w;
+  if (!a.trans) { r0d = o0d - a.p; r0h = o0h - a.p; r0w = o0w - a.p; }
+  else { r0d = o0d + a.p - (K - 1); r0h = o0h + a.p - (K - 1); r0w = o0w + a.p - (K - 1); }
+  const int vw = tid % (TN_OW / TN_VW), oh = (tid / (TN_OW / TN_VW)) % TN_OH, od = tid / ((TN_OW / TN_VW) * TN_OH);
+  const int ow0 = vw * TN_VW;
+  float acc[NY][TN_VW];
+#pragma unroll
+  for (int n = 0; n < NY; ++n)
+#pragma unroll
+    for (int v = 0; v < TN_VW; ++v) acc[n][v] = 0.f;
+  constexpr int R = RD * RH * RW;
+  for (int c0 = 0; c0 < a.cx; c0 += 2) {
+    __syncthreads();
+    for (int e = tid; e < R; e += 256) {
+      int rw = e % RW, rh = (e / RW) % RH, rd = e / (RW * RH);
+      int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
+      bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+      float2 v = make_float2(0.f, 0.f);
+      if (ok) v = *reinterpret_cast<const float2*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0);
+      xs2[e] = v;
+    }
+    __syncthreads();
+    for (int jd = 0; jd < K; ++jd)
+      for (int jh = 0; jh < K; ++jh) {
+        const float2* row = xs2 + ((od + jd) * RH + (oh + jh)) * RW + ow0;
+        float2 win[WL];
+#pragma unroll
+        for (int i = 0; i < WL; ++i) win[i] = row[i];
+#pragma unroll
+        for (int jw = 0; jw < K; ++jw) {
+          const int t = a.trans ? (((K - 1 - jd) * K + (K - 1 - jh)) * K + (K - 1 - jw)) : ((jd * K + jh) * K + jw);
+          const float* wt = a.w + (int64_t)t * NY * a.cx + c0;
+#pragma unroll
+          for (int n = 0; n < NY; ++n) {
+            const float w0 = wt[n * a.cx], w1 = wt[n * a.cx + 1];
+#pragma unroll
+            for (int v = 0; v < TN_VW; ++v)
+              acc[n][v] = fmaf(win[v + jw].x, w0, fmaf(win[v + jw].y, w1, acc[n][v]));
+          }
+        }
+      }
+  }
+  const int gd = o0d + od, gh = o0h + oh;
+  if (gd < a.Do && gh < a.Ho) {
+#pragma unroll
+    for (int v = 0; v < TN_VW; ++v) {
+      int gw = o0w + ow0 + v;
+      if (gw >= a.Wo) continue;
+      float* dst = a.y + ((((int64_t)nb * a.Do + gd) * a.Ho + gh) * a.Wo + gw) * NY;
+#pragma unroll
+      for (int n = 0; n < NY; ++n) dst[n] = act_fwd(acc[n][v] + (a.bias ? a.bias[n] : 0.f), a.act);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// naive: one wave per output voxel (lanes split taps × channels), any stride / transposed
+// form.  Used for the tiny D-last convolution and the D-first data gradient.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) thin_naive_kernel(ThinArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  if (o >= total) return;
+  int ow = (int)(o % a.Wo); int64_t u = o / a.Wo;
+  int oh = (int)(u % a.Ho); u /= a.Ho;
+  int od = (int)(u % a.Do); int nb = (int)(u / a.Do);
+  const int k = a.k, T = k * k * k;
+  for (int n = 0; n < a.ny; ++n) {
+    float s = 0.f;
+    for (int e = lane; e < T * a.cx; e += 64) {
+      int c = e % a.cx, t = e / a.cx;
+      int tw = t % k, th = (t / k) % k, td = t / (k * k);
+      int id, ih, iw;
+      if (!a.trans) { id = od * a.s - a.p + td; ih = oh * a.s - a.p + th; iw = ow * a.s - a.p + tw; }
+      else {
+        int nd = od + a.p - td, nh = oh + a.p - th, nw = ow + a.p - tw;
+        if (nd < 0 || nh < 0 || nw < 0 || nd % a.s || nh % a.s || nw % a.s) continue;
+        id = nd / a.s; ih = nh / a.s; iw = nw / a.s;
+      }
+      if ((unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi || (unsigned)iw >= (unsigned)a.Wi) continue;
+      s = fmaf(a.x[((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c], a.w[((int64_t)t * a.ny + n) * a.cx + c], s);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) a.y[o * a.ny + n] = act_fwd(s + (a.bias ? a.bias[n] : 0.f), a.act);
+  }
+}
+
+template <int NY>
+static void launch_thin_n(const ThinArgs& a, dim3 grid, size_t lds, hipStream_t st, int td, int th, int tw) {
+  switch (a.k) {
+    case 3: hipLaunchKernelGGL((thin_n_kernel<NY, 3>), grid, dim3(256), lds, st, a, td, th, tw); break;
+    case 4: hipLaunchKernelGGL((thin_n_kernel<NY, 4>), grid, dim3(256), lds, st, a, td, th, tw); break;
+    default: hipLaunchKernelGGL((thin_n_kernel<NY, 7>), grid, dim3(256), lds, st, a, td, th, tw); break;
+  }
+}
+
+int conv_thin(ThinArgs a, hipStream_t st) {
+  MRAGAN_CHECK_ARG(a.k >= 1 && a.k <= 7, "conv_thin: k=%d unsupported", a.k);
+  if (a.N == 0 || a.ny == 0) return kOk;
+  const bool s1 = a.s == 1;
+  if (a.cx <= 4 && (!a.trans || s1)) {
+    int td = ceil_div(a.Do, TK_OD), th = ceil_div(a.Ho, TK_OH), tw = ceil_div(a.Wo, TK_OW);
+    int RD, RH, RW;
+    if (!a.trans) { RD = (TK_OD - 1) * a.s + a.k; RH = (TK_OH - 1) * a.s + a.k; RW = (TK_OW - 1) * a.s + a.k; }
+    else { RD = TK_OD + a.k - 1; RH = TK_OH + a.k - 1; RW = TK_OW + a.k - 1; }
+    size_t lds = (size_t)RD * RH * RW * a.cx * sizeof(float);
+    dim3 grid(a.N * td * th * tw, ceil_div(a.ny, TK_NB));
+    switch (a.cx) {
+      case 1: hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
+      case 2: hipLaunchKernelGGL(thin_k_kernel<2>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
+      case 3: hipLaunchKernelGGL(thin_k_kernel<3>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
+      default: hipLaunchKernelGGL(thin_k_kernel<4>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
+    }
+    return check_launch("thin_k");
+  }
+  if (a.ny <= 4 && s1 && a.cx % 2 == 0 && (a.k == 3 || a.k == 4 || a.k == 7)) {
+    int td = ceil_div(a.Do, TN_OD), th = ceil_div(a.Ho, TN_OH), tw = ceil_div(a.Wo, TN_OW);
+    size_t lds = (size_t)(TN_OD + a.k - 1) * (TN_OH + a.k - 1) * (TN_OW + a.k - 1) * sizeof(float2);
+    dim3 grid(a.N * td * th * tw);
+    switch (a.ny) {
+      case 1: launch_thin_n<1>(a, grid, lds, st, td, th, tw); break;
+      case 2: launch_thin_n<2>(a, grid, lds, st, td, th, tw); break;
+      case 3: launch_thin_n<3>(a, grid, lds, st, td, th, tw); break;
+      default: launch_thin_n<4>(a, grid, lds, st, td, th, tw); break;
+    }
+    return check_launch("thin_n");
+  }
+  int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  hipLaunchKernelGGL(thin_naive_kernel, dim3(ceil_div(total, 4)), dim3(256), 0, st, a);
+  return check_launch("thin_naive");
+}
+
+// ---------------------------------------------------------------------------------------
+// Thin weight gradient:  dW[dn][gn][t] = Σ_m D[m][dn] · G[m*s − p + t][gn]  (one side ≤ 4 ch)
+// Block = one channel group of the narrow side (grid.y) × a grid-stride walk over 4×4×16
+// tiles of D's grid.  D's tile and G's halo are staged in LDS.  A "role" =
+// (4 channels of the wide side or the narrow channel, td, th) and owns all K taps along w,
+// so per voxel it does one D read, K G reads and 4K FMAs.  When roles < threads the tile's
+// rows are split over RS threads and combined through LDS.  Per-block partials go to a slab
+// that a second kernel sums in fixed order (deterministic).
+// ---------------------------------------------------------------------------------------
+constexpr int TW_D = 4, TW_H = 4, TW_W = 16, TW_M = TW_D * TW_H * TW_W;
+constexpr int TW_MAXR = 2;
+
+
+template <int K>
+__global__ void __launch_bounds__(256) thin_wgrad_kernel(ThinWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int s = a.s;
+  const int RD = (TW_D - 1) * s + K, RH = (TW_H - 1) * s + K, RW = (TW_W - 1) * s + K;
+  const int Rn = RD * RH * RW;
+  const int dch = a.vec_dn ? a.Cd : 1;          // D channels staged
+  const int doff = a.vec_dn ? 0 : 0;
+  const int gch = a.vec_dn ? 1 : 4;             // G channels staged
+  const int goff = a.vec_dn ? blockIdx.y : 4 * blockIdx.y;
+  const int dsel = a.vec_dn ? 0 : -1;           // vec over gn: role picks the dn
+  (void)doff; (void)dsel;
+  float* Dt = sm;                               // [TW_M][Cd]  (all D channels; small or the wide side)
+  float* Gt = sm + TW_M * a.Cd;                 // [Rn][gch]
+  float* red = Gt + Rn * gch;
+  const int T = K * K * K;
+  const int nroles = a.nroles, RS = a.RS;
+  const int tid = threadIdx.x;
+  float acc[TW_MAXR][4][K];
+#pragma unroll
+  for (int r = 0; r < TW_MAXR; ++r)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int t = 0; t < K; ++t) acc[r][v][t] = 0.f;
+
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int tt = tile;
+    const int tw_ = tt % a.tiles_w; tt /= a.tiles_w;
+    const int th_ = tt % a.tiles_h; tt /= a.tiles_h;
+    const int td_ = tt % a.tiles_d; const int nb = tt / a.tiles_d;
+    const int m0d = td_ * TW_D, m0h = th_ * TW_H, m0w = tw_ * TW_W;
+    __syncthreads();
+    for (int e = tid; e < TW_M * a.Cd; e += 256) {
+      int c = e % a.Cd, mi = e / a.Cd;
+      int mw = mi % TW_W, mh = (mi / TW_W) % TW_H, md = mi / (TW_W * TW_H);
+      int gd = m0d + md, gh = m0h + mh, gw = m0w + mw;
+      bool ok = gd < a.Dd && gh < a.Hd && gw < a.Wd;
+      Dt[e] = ok ? a.D[((((int64_t)nb * a.Dd + gd) * a.Hd + gh) * a.Wd + gw) * a.Cd + c] : 0.f;
+    }
+    const int r0d = m0d * s - a.p, r0h = m0h * s - a.p, r0w = m0w * s - a.p;
+    for (int e = tid; e < Rn * gch; e += 256) {
+      int c = e % gch, ri = e / gch;
+      int rw = ri % RW, rh = (ri / RW) % RH, rd = ri / (RW * RH);
+      int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
+      bool ok = (unsigned)id < (unsigned)a.Dg && (unsigned)ih < (unsigned)a.Hg && (unsigned)iw < (unsigned)a.Wg;
+      Gt[e] = ok ? a.G[((((int64_t)nb * a.Dg + id) * a.Hg + ih) * a.Wg + iw) * a.Cg + goff + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rs = 0; rs < TW_MAXR; ++rs) {
+      int role, split;
+      if (RS > 1) {
+        if (rs > 0) continue;
+        role = tid % nroles; split = tid / nroles;
+        if (split >= RS) continue;
+      } else {
+        role = tid + rs * 256; split = 0;
+        if (role >= nroles) continue;
+      }
+      const int th = role % K, td = (role / K) % K, ch = role / (K * K);
+      for (int row = split; row < TW_D * TW_H; row += RS) {
+        const int mh = row % TW_H, md = row / TW_H;
+        for (int mw = 0; mw < TW_W; ++mw) {
+          const int mi = (md * TW_H + mh) * TW_W + mw;
+          const float* grow = Gt + (((md * s + td) * RH + (mh * s + th)) * RW + mw * s) * gch;
+          if (a.vec_dn) {
+            const float4 dv = *reinterpret_cast<const float4*>(Dt + mi * a.Cd + 4 * ch);
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+              const float g = grow[t];
+              acc[rs][0][t] = fmaf(dv.x, g, acc[rs][0][t]);
+              acc[rs][1][t] = fmaf(dv.y, g, acc[rs][1][t]);
+              acc[rs][2][t] = fmaf(dv.z, g, acc[rs][2][t]);
+              acc[rs][3][t] = fmaf(dv.w, g, acc[rs][3][t]);
+            }
+          } else {
+            const float d = Dt[mi * a.Cd + ch];
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+              const float4 g = *reinterpret_cast<const float4*>(grow + 4 * t);
+              acc[rs][0][t] = fmaf(d, g.x, acc[rs][0][t]);
+              acc[rs][1][t] = fmaf(d, g.y, acc[rs][1][t]);
+              acc[rs][2][t] = fmaf(d, g.z, acc[rs][2][t]);
+              acc[rs][3][t] = fmaf(d, g.w, acc[rs][3][t]);
+            }
+          }
+        }
+      }
+    }
+  }
+  float* out = a.slab + (int64_t)blockIdx.x * a.Cd * a.Cg * T;
+  auto out_index = [&](int role, int v, int t) -> int64_t {
+    const int th = role % K, td = (role / K) % K, ch = role / (K * K);
+    int dn, gn;
+    if (a.vec_dn) { dn = 4 * ch + v; gn = goff; } else { dn = ch; gn = goff + v; }
+    return ((int64_t)dn * a.Cg + gn) * T + (td * K + th) * K + t;
+  };
+  if (RS > 1) {
+    __syncthreads();
+    const int role = tid % nroles, split = tid / nroles;
+    if (split < RS) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int t = 0; t < K; ++t) red[((split * nroles + role) * 4 + v) * K + t] = acc[0][v][t];
+    }
+    __syncthreads();
+    for (int e = tid; e < nroles * 4 * K; e += 256) {
+      const int t = e % K, v = (e / K) % 4, rl = e / (4 * K);
+      float sum = 0.f;
+      for (int z = 0; z < RS; ++z) sum += red[((z * nroles + rl) * 4 + v) * K + t];
+      out[out_index(rl, v, t)] = sum;
+    }
+  } else {
+#pragma unroll
+    for (int rs = 0; rs < TW_MAXR; ++rs) {
+      const int role = tid + rs * 256;
+      if (role >= nroles) continue;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int t = 0; t < K; ++t) out[out_index(role, v, t)] = acc[rs][v][t];
+    }
+  }
+}
+
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int64_t E, int nslab,
+                                   int accumulate) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < nslab; ++z) s += slab[(int64_t)z * E + e];
+    out[e] = accumulate ? out[e] + s : s;
+  }
+}
+
+static int thin_wgrad_setup(ThinWgradArgs& a, int* gx, int* gy, size_t* lds) {
+  a.vec_dn = (a.Cd % 4 == 0 && a.Cd >= a.Cg) ? 1 : 0;
+  MRAGAN_CHECK_ARG(a.vec_dn || (a.Cg % 4 == 0 && a.Cd <= 64), "thin_wgrad: unsupported channels (%d,%d)", a.Cd, a.Cg);
+  MRAGAN_CHECK_ARG(a.k == 3 || a.k == 4 || a.k == 7, "thin_wgrad: k=%d unsupported", a.k);
+  const int K = a.k;
+  a.nroles = a.vec_dn ? (a.Cd / 4) * K * K : a.Cd * K * K;
+  MRAGAN_CHECK_ARG(a.nroles <= 256 * TW_MAXR, "thin_wgrad: %d roles > %d", a.nroles, 256 * TW_MAXR);
+  a.RS = 256 / a.nroles;
+  if (a.RS < 1) a.RS = 1;
+  if (a.RS > TW_D * TW_H) a.RS = TW_D * TW_H;
+  a.tiles_d = ceil_div(a.Dd, TW_D); a.tiles_h = ceil_div(a.Hd, TW_H); a.tiles_w = ceil_div(a.Wd, TW_W);
+  a.ntiles = a.N * a.tiles_d * a.tiles_h * a.tiles_w;
+  *gy = a.vec_dn ? a.Cg : a.Cg / 4;
+  int want = 1024 / *gy;
+  if (want < 16) want = 16;
+  *gx = a.ntiles < want ? a.ntiles : want;
+  if (*gx < 1) *gx = 1;
+  const int s = a.s;
+  int RD = (TW_D - 1) * s + K, RH = (TW_H - 1) * s + K, RW = (TW_W - 1) * s + K;
+  int gch = a.vec_dn ? 1 : 4;
+  *lds = ((size_t)TW_M * a.Cd + (size_t)RD * RH * RW * gch + (a.RS > 1 ? (size_t)a.RS * a.nroles * 4 * K : 0)) *
+         sizeof(float);
+  MRAGAN_CHECK_ARG(*lds <= 160 * 1024, "thin_wgrad: LDS %zu too large", *lds);
+  return kOk;
+}
+
+size_t conv_thin_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int s) {
+  ThinWgradArgs a{};
+  a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd; a.Cg = Cg; a.k = k; a.s = s;
+  int gx, gy; size_t lds;
+  if (thin_wgrad_setup(a, &gx, &gy, &lds)) return 0;
+  return (size_t)gx * Cd * Cg * k * k * k * sizeof(float);
+}
+
+int conv_thin_wgrad(ThinWgradArgs a, float* out, int accumulate, float* ws, size_t ws_bytes, hipStream_t st) {
+  int gx, gy; size_t lds;
+  int rc = thin_wgrad_setup(a, &gx, &gy, &lds);
+  if (rc) return rc;
+  const int K = a.k;
+  const int64_t E = (int64_t)a.Cd * a.Cg * K * K * K;
+  size_t need = (size_t)gx * E * sizeof(float);
+  if (need > ws_bytes) { set_error("thin_wgrad: workspace %zu < %zu", ws_bytes, need); return kWorkspace; }
+  if (a.ntiles == 0) return kOk;
+  a.slab = ws;
+  dim3 grid(gx, gy);
+  switch (K) {
+    case 3: hipLaunchKernelGGL(thin_wgrad_kernel<3>, grid, dim3(256), lds, st, a); break;
+    case 4: hipLaunchKernelGGL(thin_wgrad_kernel<4>, grid, dim3(256), lds, st, a); break;
+    default: hipLaunchKernelGGL(thin_wgrad_kernel<7>, grid, dim3(256), lds, st, a); break;
+  }
+  rc = check_launch("thin_wgrad");
+  if (rc) return rc;
+  int blocks = (int)((E + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, out, E, gx, accumulate);
+  return check_launch("thin_wgrad_reduce");
+}
+
+}  // namespace mragan

@@ -1,0 +1,82 @@
+// Internal interface between the C ABI (capi.hip) and the kernel files.
+#pragma once
+#include "common.h"
+
+namespace mragan {
+
+struct IgemmArgs {
+  const float* x;   // [N][Di][Hi][Wi][cx]
+  const float* w;   // [k³][ny][cx]
+  const float* bias;
+  float* y;         // [N][Do][Ho][Wo][ny]
+  int N, Di, Hi, Wi, cx;
+  int Do, Ho, Wo, ny;
+  int k, s, p;
+  int trans;
+  int act;
+  int nclass;       // set by conv_igemm: 1 (forward or s==1) or s³
+};
+int conv_igemm(IgemmArgs a, hipStream_t st);
+
+struct ThinArgs {
+  const float* x; int N, Di, Hi, Wi, cx;
+  const float* w;      // packed [k³][ny][cx]
+  const float* bias;
+  float* y; int Do, Ho, Wo, ny;
+  int k, s, p, trans, act;
+};
+int conv_thin(ThinArgs a, hipStream_t st);
+
+struct WgradArgs {
+  const float* D; int N, Dd, Hd, Wd, Cd;
+  const float* G; int Dg, Hg, Wg, Cg;
+  int k, s, p;
+  float* ws;       // [splits][k³][Cd][Cg]
+  int64_t chunk;   // set by conv_wgrad
+  int splits;
+};
+int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
+size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k);
+
+struct ThinWgradArgs {
+  const float* D; int N, Dd, Hd, Wd, Cd;
+  const float* G; int Dg, Hg, Wg, Cg;
+  int k, s, p;
+  int vec_dn;      // 1: 4-vector over dn (wide side = D), 0: over gn (wide side = G)
+  int tiles_d, tiles_h, tiles_w, ntiles;
+  int nroles, RS;
+  float* slab;     // [gridDim.x][Cd*Cg*k³]
+};
+int conv_thin_wgrad(ThinWgradArgs a, float* out, int accumulate, float* ws, size_t ws_bytes, hipStream_t st);
+size_t conv_thin_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int s);
+
+struct InShape {
+  int N, D, H, W, C;
+  __host__ __device__ int64_t S() const { return (int64_t)D * H * W; }
+};
+struct InBwdArgs {
+  const float* x; const float* mean; const float* rstd;
+  const float* dy; int dypad; const float* dy_add; int act;
+  float* dx;
+};
+int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
+                 float* rstd, void* ws, size_t ws_bytes, hipStream_t st);
+int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st);
+size_t instnorm_ws_bytes(int N, int D, int H, int W, int C);
+int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st);
+size_t instnorm_running_entry_bytes();
+
+int rpad(const float* x, int N, int D, int H, int W, int C, int p, float* y, hipStream_t st);
+int rpad_fold(const float* yp, int N, int D, int H, int W, int C, int p, const float* add, float* x, hipStream_t st);
+int act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx, hipStream_t st);
+int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad, int grad_acc,
+            float* ws, hipStream_t st);
+int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc, float* dlogit,
+             float* ws, hipStream_t st);
+int channel_sum(const float* x, int64_t M, int C, float* out, int acc, hipStream_t st);
+int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
+         float grad_scale, hipStream_t st);
+int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);
+int fill(float* p, int64_t n, float v, hipStream_t st);
+
+}  // namespace mragan

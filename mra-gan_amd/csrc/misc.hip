@@ -1,0 +1,245 @@
+// Element-wise / reduction kernels of the CycleGAN step:
+//   ReplicationPad3d forward + backward fold   (networks3D.py:185, 211, 233, 249)
+//   activation backward (ReLU/LeakyReLU from the output, Tanh, Sigmoid)
+//   L1Loss (cycle_gan_model.py:104-105), GANLoss BCE-on-sigmoid / MSE (networks3D.py:130-150)
+//   bias gradients (channel sums), torch.optim.Adam (cycle_gan_model.py:107-110),
+//   weight packing torch layout → [tap][Nout][Kc].
+#include "kernels.h"
+
+namespace mragan {
+
+static int grid_cap(int64_t work, int cap = 8192) {
+  int64_t b = (work + 255) / 256;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+// ---- replication pad ---------------------------------------------------------------------
+__global__ void rpad_kernel(const float* __restrict__ x, int N, int D, int H, int W, int C, int p, float* __restrict__ y) {
+  const int Dp = D + 2 * p, Hp = H + 2 * p, Wp = W + 2 * p;
+  const int64_t total = (int64_t)N * Dp * Hp * Wp * C;
+  GRID_STRIDE(e, total) {
+    const int c = (int)(e % C); int64_t u = e / C;
+    const int w = (int)(u % Wp); u /= Wp;
+    const int h = (int)(u % Hp); u /= Hp;
+    const int d = (int)(u % Dp); const int n = (int)(u / Dp);
+    const int sd = min(max(d - p, 0), D - 1), sh = min(max(h - p, 0), H - 1), sw = min(max(w - p, 0), W - 1);
+    y[e] = x[((((int64_t)n * D + sd) * H + sh) * W + sw) * C + c];
+  }
+}
+
+// `add` may alias `x` (in-place accumulate): each element is read before it is written by the
+// same thread, so neither carries __restrict__.
+__global__ void rpad_fold_kernel(const float* __restrict__ yp, int N, int D, int H, int W, int C, int p,
+                                 const float* add, float* x) {
+  const int Dp = D + 2 * p, Hp = H + 2 * p, Wp = W + 2 * p;
+  const int64_t total = (int64_t)N * D * H * W * C;
+  GRID_STRIDE(e, total) {
+    const int c = (int)(e % C); int64_t u = e / C;
+    const int w = (int)(u % W); u /= W;
+    const int h = (int)(u % H); u /= H;
+    const int d = (int)(u % D); const int n = (int)(u / D);
+    const int d0 = d == 0 ? 0 : d + p, d1 = d == D - 1 ? D - 1 + 2 * p : d + p;
+    const int h0 = h == 0 ? 0 : h + p, h1 = h == H - 1 ? H - 1 + 2 * p : h + p;
+    const int w0 = w == 0 ? 0 : w + p, w1 = w == W - 1 ? W - 1 + 2 * p : w + p;
+    float s = add ? add[e] : 0.f;
+    for (int a = d0; a <= d1; ++a)
+      for (int b = h0; b <= h1; ++b)
+        for (int cc = w0; cc <= w1; ++cc) s += yp[((((int64_t)n * Dp + a) * Hp + b) * Wp + cc) * C + c];
+    x[e] = s;
+  }
+}
+
+// ---- activation backward: dx = (dy0 + dy1 + dy2) · act'(y) --------------------------------
+__global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restrict__ g0, const float* __restrict__ g1,
+                               const float* __restrict__ g2, int64_t n, int act, float* __restrict__ dx) {
+  GRID_STRIDE(i, n) {
+    float g = g0 ? g0[i] : 0.f;
+    if (g1) g += g1[i];
+    if (g2) g += g2[i];
+    const float v = y ? y[i] : 0.f;
+    float d;
+    switch (act) {
+      case kActRelu: d = v > 0.f ? 1.f : 0.f; break;
+      case kActLrelu: d = v > 0.f ? 1.f : kLreluSlope; break;
+      case kActTanh: d = 1.f - v * v; break;
+      case kActSigmoid: d = v * (1.f - v); break;
+      default: d = 1.f;
+    }
+    dx[i] = g * d;
+  }
+}
+
+// ---- block reduction helper --------------------------------------------------------------
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double sh[4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  return t;
+}
+
+// ---- L1 loss: loss += scale·mean|a−b| ; grad (=|+=) scale·sign(a−b)/n ---------------------
+__global__ void __launch_bounds__(256) l1_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                                 float scale, float* loss_partial, float* __restrict__ grad, int acc) {
+  double s = 0;
+  const float gs = scale / (float)n;
+  GRID_STRIDE(i, n) {
+    const float d = a[i] - b[i];
+    s += fabsf(d);
+    if (grad) {
+      const float g = d > 0.f ? gs : (d < 0.f ? -gs : 0.f);
+      grad[i] = acc ? grad[i] + g : g;
+    }
+  }
+  const double t = block_sum(s);
+  if (threadIdx.x == 0) loss_partial[blockIdx.x] = (float)(t * (double)scale / (double)n);
+}
+
+// ---- GAN loss on D's output map ------------------------------------------------------------
+// BCE (default, pred = sigmoid output p): loss = −mean(t·max(ln p,−100) + (1−t)·max(ln(1−p),−100));
+//   dlogit = scale/n · (p−t)/max(p(1−p),1e-12) · p(1−p)       (ATen binary_cross_entropy_backward
+//   followed by sigmoid_backward)
+// MSE (--no_lsgan given → LSGAN): loss = mean((x−t)²); dlogit = scale/n · 2(x−t)
+__global__ void __launch_bounds__(256) gan_kernel(const float* __restrict__ p, int64_t n, float t, int lsgan, float scale,
+                                                  float* loss_partial, float* __restrict__ dlogit) {
+  double s = 0;
+  GRID_STRIDE(i, n) {
+    const float v = p[i];
+    float g;
+    if (lsgan) {
+      const float d = v - t;
+      s += (double)d * d;
+      g = 2.f * d;
+    } else {
+      const float lp = fmaxf(logf(v), -100.f), l1p = fmaxf(logf(1.f - v), -100.f);
+      s += -(t * lp + (1.f - t) * l1p);
+      const float pp = (1.f - v) * v;
+      g = (v - t) / fmaxf(pp, 1e-12f) * pp;
+    }
+    if (dlogit) dlogit[i] = g * (scale / (float)n);
+  }
+  const double tt = block_sum(s);
+  if (threadIdx.x == 0) loss_partial[blockIdx.x] = (float)(tt * (double)scale / (double)n);
+}
+
+__global__ void partial_sum_kernel(const float* __restrict__ part, int nb, float* __restrict__ out, int acc) {
+  double s = 0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  const double t = block_sum(s);
+  if (threadIdx.x == 0) out[0] = acc ? out[0] + (float)t : (float)t;
+}
+
+// ---- channel sums (bias gradients): out[c] (=|+=) Σ_m x[m][c] ------------------------------
+__global__ void __launch_bounds__(256) channel_sum_kernel(const float* __restrict__ x, int64_t M, int C, float* __restrict__ out,
+                                                          int acc) {
+  const int c = blockIdx.x;
+  double s = 0;
+  for (int64_t m = threadIdx.x; m < M; m += blockDim.x) s += x[m * C + c];
+  const double t = block_sum(s);
+  if (threadIdx.x == 0) out[c] = acc ? out[c] + (float)t : (float)t;
+}
+
+// ---- Adam (torch.optim.Adam, amsgrad=False, weight_decay=0, single-tensor formula) ---------
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                            int64_t n, float step_size, float beta1, float beta2, float eps, float bc2_sqrt,
+                            float grad_scale) {
+  const float w1 = 1.f - beta1;
+  GRID_STRIDE(i, n) {
+    const float gi = g[i] * grad_scale;
+    float mi = m[i];
+    // torch lerp: weight < 0.5 ? self + w·(end−self) : end − (end−self)·(1−w)
+    mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+// ---- weight packing: src[A][B][T] → dst[T][A][B] (transpose_ab=0) or dst[T][B][A] (=1) ----
+__global__ void pack_kernel(const float* __restrict__ src, int A, int B, int T, int tr, float* __restrict__ dst) {
+  const int64_t total = (int64_t)A * B * T;
+  GRID_STRIDE(e, total) {
+    // e enumerates dst
+    const int t = (int)(e / ((int64_t)A * B));
+    const int r = (int)(e % ((int64_t)A * B));
+    int a, b;
+    if (!tr) { a = r / B; b = r % B; } else { b = r / A; a = r % A; }
+    dst[e] = src[((int64_t)a * B + b) * T + t];
+  }
+}
+
+__global__ void fill_kernel(float* __restrict__ p, int64_t n, float v) {
+  GRID_STRIDE(i, n) p[i] = v;
+}
+
+// ---- host wrappers -------------------------------------------------------------------------
+int rpad(const float* x, int N, int D, int H, int W, int C, int p, float* y, hipStream_t st) {
+  const int64_t total = (int64_t)N * (D + 2 * p) * (H + 2 * p) * (W + 2 * p) * C;
+  hipLaunchKernelGGL(rpad_kernel, dim3(grid_cap(total)), dim3(256), 0, st, x, N, D, H, W, C, p, y);
+  return check_launch("rpad");
+}
+int rpad_fold(const float* yp, int N, int D, int H, int W, int C, int p, const float* add, float* x, hipStream_t st) {
+  const int64_t total = (int64_t)N * D * H * W * C;
+  hipLaunchKernelGGL(rpad_fold_kernel, dim3(grid_cap(total)), dim3(256), 0, st, yp, N, D, H, W, C, p, add, x);
+  return check_launch("rpad_fold");
+}
+int act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx, hipStream_t st) {
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, st, y, g0, g1, g2, n, act, dx);
+  return check_launch("act_bwd");
+}
+int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad, int grad_acc,
+            float* ws, hipStream_t st) {
+  const int nb = grid_cap(n, 1024);
+  hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(256), 0, st, a, b, n, scale, ws, grad, grad_acc);
+  int rc = check_launch("l1_loss");
+  if (rc) return rc;
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, ws, nb, loss, loss_acc);
+  return check_launch("l1_loss_sum");
+}
+int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc, float* dlogit,
+             float* ws, hipStream_t st) {
+  const int nb = grid_cap(n, 1024);
+  hipLaunchKernelGGL(gan_kernel, dim3(nb), dim3(256), 0, st, p, n, target, lsgan, scale, ws, dlogit);
+  int rc = check_launch("gan_loss");
+  if (rc) return rc;
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, ws, nb, loss, loss_acc);
+  return check_launch("gan_loss_sum");
+}
+int channel_sum(const float* x, int64_t M, int C, float* out, int acc, hipStream_t st) {
+  if (C <= 0) return kOk;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(C), dim3(256), 0, st, x, M, C, out, acc);
+  return check_launch("channel_sum");
+}
+int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
+         float grad_scale, hipStream_t st) {
+  // bias corrections and step size in double on the host, as torch does with python floats
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  const float step_size = (float)((double)lr / bc1);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, step_size, beta1, beta2, eps,
+                     (float)sqrt(bc2), grad_scale);
+  return check_launch("adam");
+}
+int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(pack_kernel, dim3(grid_cap((int64_t)A * B * T)), dim3(256), 0, st, src, A, B, T, tr, dst);
+  return check_launch("pack_weight");
+}
+int fill(float* p, int64_t n, float v, hipStream_t st) {
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, n, v);
+  return check_launch("fill");
+}
+
+}  // namespace mragan

@@ -1,0 +1,324 @@
+"""CycleGANModel — drop-in for the reference's models/cycle_gan_model.py (lines 38-240).
+
+Same options, attributes (netG_A/netG_B/netD_A/netD_B, real_A/fake_B/rec_A/idt_A/...,
+loss_* , optimizers) and method names.  `optimize_parameters()` computes the same step —
+6 generator and 6 discriminator forward/backward passes, both Adam updates, the image pools
+and the InstanceNorm running statistics — but as a fused schedule on the HIP engine:
+
+  G passes batched where the reference makes independent calls (InstanceNorm is per
+  instance, so this is exact):   G_A([real_A; real_B]) → [fake_B; idt_A]
+                                 G_B([real_B; real_A]) → [fake_A; idt_B]
+                                 G_B(fake_B) → rec_A,  G_A(fake_A) → rec_B
+  D passes batched:              D_A([real_B; pool(fake_B)]), D_B([real_A; pool(fake_A)])
+  running stats:                 applied afterwards in the reference's call order.
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): each rank takes its own patch
+batch; the G gradient all-reduce is launched right after backward_G and overlaps the whole D
+phase (which only needs pre-update G outputs and D weights), then both optimizers step.
+Reordering "G step, then D phase" → "D phase, then G step" is exact for the same reason.
+"""
+import itertools
+import random
+from collections import OrderedDict
+
+import torch
+
+from . import networks3D
+from .base_model import BaseModel
+
+device = networks3D.device
+
+
+class ImagePool():
+    """cycle_gan_model.py:8-35: history of generated images (Python `random`, like the
+    reference).  Images are kept as NDHWC device tensors."""
+
+    def __init__(self, pool_size):
+        self.pool_size = pool_size
+        if self.pool_size > 0:
+            self.num_imgs = 0
+            self.images = []
+
+    def query(self, images):
+        if self.pool_size == 0:
+            return images
+        out = []
+        for image in images:
+            image = image.detach().unsqueeze(0)
+            if self.num_imgs < self.pool_size:
+                self.num_imgs += 1
+                self.images.append(image.clone())
+                out.append(image)
+            else:
+                if random.uniform(0, 1) > 0.5:
+                    rid = random.randint(0, self.pool_size - 1)
+                    tmp = self.images[rid]
+                    self.images[rid] = image.clone()
+                    out.append(tmp)
+                else:
+                    out.append(image)
+        return out
+
+
+def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
+    return x.float().permute(0, 2, 3, 4, 1).contiguous()
+
+
+def _to_ncdhw(x: torch.Tensor) -> torch.Tensor:
+    return x.permute(0, 4, 1, 2, 3)
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam semantics (amsgrad=False, weight_decay=0) as one HIP kernel per flat
+    parameter buffer.  Subclasses torch.optim.Optimizer so LambdaLR & co. drive `lr`."""
+
+    def __init__(self, nets, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.nets = list(nets)
+        params = list(itertools.chain(*[n.parameters() for n in self.nets]))
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False))
+        self._m = {}
+        self._v = {}
+        self.step_count = 0
+        self.grad_scale = 1.0
+
+    def zero_grad(self, set_to_none: bool = True):
+        from mragan_hip import ops
+        for n in self.nets:
+            networks3D.ensure_flat(n)
+            ops.fill(n._flat_grad, 0.0)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from mragan_hip import ops
+        self.step_count += 1
+        g = self.param_groups[0]
+        beta1, beta2 = g['betas']
+        for n in self.nets:
+            networks3D.ensure_flat(n)
+            key = id(n)
+            if key not in self._m or self._m[key].numel() != n._flat_param.numel():
+                self._m[key] = torch.zeros_like(n._flat_param)
+                self._v[key] = torch.zeros_like(n._flat_param)
+            ops.adam(n._flat_param, n._flat_grad, self._m[key], self._v[key], g['lr'], beta1, beta2, g['eps'],
+                     self.step_count, self.grad_scale)
+            n.mark_params_dirty()
+
+
+class CycleGANModel(BaseModel):
+    def name(self):
+        return 'CycleGANModel'
+
+    @staticmethod
+    def modify_commandline_options(parser, is_train=True):
+        parser.set_defaults(no_dropout=True)
+        if is_train:
+            parser.add_argument('--lambda_A', type=float, default=10.0, help='weight for cycle loss (A -> B -> A)')
+            parser.add_argument('--lambda_B', type=float, default=10.0, help='weight for cycle loss (B -> A -> B)')
+            parser.add_argument('--lambda_identity', type=float, default=0.5,
+                                help='weight of the identity mapping loss, relative to the reconstruction loss')
+            parser.add_argument('--lambda_co_A', type=float, default=2,
+                                help='weight for correlation coefficient loss (A -> B)')
+            parser.add_argument('--lambda_co_B', type=float, default=2,
+                                help='weight for correlation coefficient loss (B -> A )')
+        return parser
+
+    def initialize(self, opt):
+        BaseModel.initialize(self, opt)
+        self.loss_names = ['D_A', 'G_A', 'cycle_A', 'idt_A', 'D_B', 'G_B', 'cycle_B', 'idt_B']
+        visual_names_A = ['real_A', 'fake_B', 'rec_A']
+        visual_names_B = ['real_B', 'fake_A', 'rec_B']
+        if self.isTrain and self.opt.lambda_identity > 0.0:
+            visual_names_A.append('idt_A')
+            visual_names_B.append('idt_B')
+        self.visual_names = visual_names_A + visual_names_B
+        self.model_names = ['G_A', 'G_B', 'D_A', 'D_B'] if self.isTrain else ['G_A', 'G_B']
+
+        self.netG_A = networks3D.define_G(opt.input_nc, opt.output_nc, opt.ngf, opt.netG, opt.norm,
+                                          not opt.no_dropout, opt.init_type, opt.init_gain, self.gpu_ids)
+        self.netG_B = networks3D.define_G(opt.output_nc, opt.input_nc, opt.ngf, opt.netG, opt.norm,
+                                          not opt.no_dropout, opt.init_type, opt.init_gain, self.gpu_ids)
+        if self.isTrain:
+            use_sigmoid = opt.no_lsgan
+            self.netD_A = networks3D.define_D(opt.output_nc, opt.ndf, opt.netD, opt.n_layers_D, opt.norm, use_sigmoid,
+                                              opt.init_type, opt.init_gain, self.gpu_ids)
+            self.netD_B = networks3D.define_D(opt.input_nc, opt.ndf, opt.netD, opt.n_layers_D, opt.norm, use_sigmoid,
+                                              opt.init_type, opt.init_gain, self.gpu_ids)
+            self.fake_A_pool = ImagePool(opt.pool_size)
+            self.fake_B_pool = ImagePool(opt.pool_size)
+            self.use_lsgan = not opt.no_lsgan
+            self.criterionGAN = networks3D.GANLoss(use_lsgan=self.use_lsgan).to(self.device)
+            self.criterionCycle = torch.nn.L1Loss()
+            self.criterionIdt = torch.nn.L1Loss()
+            self.optimizer_G = FusedAdam([self.netG_A, self.netG_B], lr=opt.lr, betas=(opt.beta1, 0.999))
+            self.optimizer_D = FusedAdam([self.netD_A, self.netD_B], lr=opt.lr, betas=(opt.beta1, 0.999))
+            self.optimizers = [self.optimizer_G, self.optimizer_D]
+            self._loss_buf = torch.zeros(8, device=self.device, dtype=torch.float32)
+            for i, n in enumerate(self.loss_names):
+                setattr(self, 'loss_' + n, self._loss_buf[i])
+        self._dist = None
+
+    # ------------------------------------------------------------------ inputs / visuals
+    def set_input(self, input):
+        AtoB = self.opt.which_direction == 'AtoB'
+        self.real_A = input[0 if AtoB else 1].to(self.device, non_blocking=True)
+        self.real_B = input[1 if AtoB else 0].to(self.device, non_blocking=True)
+
+    def _publish(self, **ndhwc):
+        for k, v in ndhwc.items():
+            setattr(self, k, _to_ncdhw(v))
+
+    @property
+    def loss_cor_coe_GA(self):      # computed-but-unused in the reference (cycle_gan_model.py:217)
+        return networks3D.Cor_CoeLoss(self.fake_B, self.real_A) * self.opt.lambda_co_A
+
+    @property
+    def loss_cor_coe_GB(self):      # cycle_gan_model.py:218
+        return networks3D.Cor_CoeLoss(self.fake_A, self.real_B) * self.opt.lambda_co_B
+
+    # ------------------------------------------------------------------ plain forward (test)
+    def forward(self):
+        """cycle_gan_model.py:121-136 (used by test()): the four generator passes."""
+        A, B = _to_ndhwc(self.real_A), _to_ndhwc(self.real_B)
+        pGA, pGB = self.netG_A.plan, self.netG_B.plan
+        from mragan_hip import engine
+        c1 = pGA.forward(A)
+        c2 = pGB.forward(c1.out)
+        c3 = pGB.forward(B)
+        c4 = pGA.forward(c3.out)
+        keep = [engine.apply_running_updates(pGA.running_entries([(c1, 0, c1.N), (c4, 0, c4.N)]), A.device),
+                engine.apply_running_updates(pGB.running_entries([(c2, 0, c2.N), (c3, 0, c3.N)]), A.device)]
+        self._publish(fake_B=c1.out, rec_A=c2.out, fake_A=c3.out, rec_B=c4.out)
+        del keep
+
+    # ------------------------------------------------------------------ training step
+    def _dist_info(self):
+        if self._dist is None:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                self._dist = (dist, dist.get_world_size())
+            else:
+                self._dist = (None, 1)
+        return self._dist
+
+    def forward_train(self):
+        """The four cycle passes plus the two identity passes, batched (see module doc)."""
+        for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+            networks3D.ensure_flat(n)
+        A, B = _to_ndhwc(self.real_A), _to_ndhwc(self.real_B)
+        b = A.shape[0]
+        self._A, self._B, self._b = A, B, b
+        pGA, pGB = self.netG_A.plan, self.netG_B.plan
+        self._cGA1 = pGA.forward(torch.cat([A, B], 0))       # [fake_B; idt_A]
+        self._cGB1 = pGB.forward(torch.cat([B, A], 0))       # [fake_A; idt_B]
+        fake_B, idt_A = self._cGA1.out[:b], self._cGA1.out[b:]
+        fake_A, idt_B = self._cGB1.out[:b], self._cGB1.out[b:]
+        self._cGB2 = pGB.forward(fake_B)                     # rec_A
+        self._cGA2 = pGA.forward(fake_A)                     # rec_B
+        self._fake_B, self._fake_A = fake_B, fake_A
+        self._publish(fake_B=fake_B, idt_A=idt_A, fake_A=fake_A, idt_B=idt_B, rec_A=self._cGB2.out,
+                      rec_B=self._cGA2.out)
+
+    def backward_G(self):
+        """cycle_gan_model.py:163-225: identity, GAN and cycle losses; backward through the 6
+        generator passes and (data gradient only) the 2 frozen discriminator passes."""
+        from mragan_hip import ops
+        b, A, B = self._b, self._A, self._B
+        lA, lB, li = self.opt.lambda_A, self.opt.lambda_B, self.opt.lambda_identity
+        L = self._loss_buf
+        pDA, pDB = self.netD_A.plan, self.netD_B.plan
+        self._cDA1 = pDA.forward(self._fake_B)
+        self._cDB1 = pDB.forward(self._fake_A)
+        dlogA = torch.empty_like(self._cDA1.out)
+        dlogB = torch.empty_like(self._cDB1.out)
+        ops.gan_loss(self._cDA1.out, 1.0, self.use_lsgan, 1.0, L[1:2], dlogA)          # loss_G_A
+        ops.gan_loss(self._cDB1.out, 1.0, self.use_lsgan, 1.0, L[5:6], dlogB)          # loss_G_B
+        dGA1 = torch.empty_like(self._cGA1.out)     # d/d[fake_B; idt_A]
+        dGB1 = torch.empty_like(self._cGB1.out)     # d/d[fake_A; idt_B]
+        d_recA = torch.empty_like(self._cGB2.out)
+        d_recB = torch.empty_like(self._cGA2.out)
+        ops.l1_loss(self._cGB2.out, A, lA, L[2:3], d_recA)                             # loss_cycle_A
+        ops.l1_loss(self._cGA2.out, B, lB, L[6:7], d_recB)                             # loss_cycle_B
+        if li > 0:
+            ops.l1_loss(self._cGA1.out[b:], B, lB * li, L[3:4], dGA1[b:])              # loss_idt_A
+            ops.l1_loss(self._cGB1.out[b:], A, lA * li, L[7:8], dGB1[b:])              # loss_idt_B
+        else:
+            ops.fill(dGA1[b:], 0.0)
+            ops.fill(dGB1[b:], 0.0)
+            ops.fill(L[3:4], 0.0)
+            ops.fill(L[7:8], 0.0)
+        # frozen D: data gradients only, written into the fake halves
+        pDA.backward(self._cDA1, [dlogA], need_wgrad=False, need_input_grad=True, dx_out=dGA1[:b])
+        pDB.backward(self._cDB1, [dlogB], need_wgrad=False, need_input_grad=True, dx_out=dGB1[:b])
+        # cycle passes: weight gradients + data gradient into the fakes
+        pGA, pGB = self.netG_A.plan, self.netG_B.plan
+        pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b])
+        pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b])
+        pGA.backward(self._cGA1, [dGA1])
+        pGB.backward(self._cGB1, [dGB1])
+
+    def backward_D_basic(self, netD, real, fake, loss_slot):
+        """cycle_gan_model.py:138-149 with real and (pooled, detached) fake batched."""
+        from mragan_hip import ops
+        b = real.shape[0]
+        plan = netD.plan
+        x = torch.empty((2 * b,) + tuple(real.shape[1:]), device=real.device, dtype=torch.float32)
+        x[:b].copy_(real)
+        for i, f in enumerate(fake):
+            x[b + i:b + i + 1].copy_(f)
+        ctx = plan.forward(x)
+        dlog = torch.empty_like(ctx.out)
+        ops.gan_loss(ctx.out[:b], 1.0, self.use_lsgan, 0.5, loss_slot, dlog[:b])
+        ops.gan_loss(ctx.out[b:], 0.0, self.use_lsgan, 0.5, loss_slot, dlog[b:], loss_accumulate=True)
+        plan.backward(ctx, [dlog], need_wgrad=True, need_input_grad=False)
+        return ctx
+
+    def backward_D_A(self):
+        fake_B = self.fake_B_pool.query(self._fake_B)
+        self._cDA2 = self.backward_D_basic(self.netD_A, self._B, fake_B, self._loss_buf[0:1])
+
+    def backward_D_B(self):
+        fake_A = self.fake_A_pool.query(self._fake_A)
+        self._cDB2 = self.backward_D_basic(self.netD_B, self._A, fake_A, self._loss_buf[4:5])
+
+    def _running_stats(self):
+        from mragan_hip import engine
+        b = self._b
+        dev = self._A.device
+        keep = []
+        keep.append(engine.apply_running_updates(self.netG_A.plan.running_entries(
+            [(self._cGA1, 0, b), (self._cGA2, 0, b), (self._cGA1, b, b)]), dev))
+        keep.append(engine.apply_running_updates(self.netG_B.plan.running_entries(
+            [(self._cGB2, 0, b), (self._cGB1, 0, b), (self._cGB1, b, b)]), dev))
+        keep.append(engine.apply_running_updates(self.netD_A.plan.running_entries(
+            [(self._cDA1, 0, b), (self._cDA2, 0, b), (self._cDA2, b, b)]), dev))
+        keep.append(engine.apply_running_updates(self.netD_B.plan.running_entries(
+            [(self._cDB1, 0, b), (self._cDB2, 0, b), (self._cDB2, b, b)]), dev))
+        self._keep = keep
+
+    def optimize_parameters(self):
+        dist, world = self._dist_info()
+        self.forward_train()
+        self.set_requires_grad([self.netD_A, self.netD_B], False)
+        self.optimizer_G.zero_grad()
+        self.backward_G()
+        work_G = None
+        if dist is not None:
+            work_G = [dist.all_reduce(n._flat_grad, async_op=True) for n in (self.netG_A, self.netG_B)]
+        self.set_requires_grad([self.netD_A, self.netD_B], True)
+        self.optimizer_D.zero_grad()
+        self.backward_D_A()
+        self.backward_D_B()
+        if dist is not None:
+            work_D = [dist.all_reduce(n._flat_grad, async_op=True) for n in (self.netD_A, self.netD_B)]
+            for w in work_G:
+                w.wait()
+            self.optimizer_G.grad_scale = 1.0 / world
+            self.optimizer_D.grad_scale = 1.0 / world
+            self.optimizer_G.step()
+            for w in work_D:
+                w.wait()
+            self.optimizer_D.step()
+        else:
+            self.optimizer_G.step()
+            self.optimizer_D.step()
+        self._running_stats()

@@ -1,0 +1,94 @@
+"""ctypes binding of libmragan_hip.so (C ABI declared in include/mragan_hip.h).
+
+The library is the only compute path of this package: there is no CPU or eager-PyTorch
+fallback.  If the shared object is missing, `lib()` raises; if a kernel call returns a
+non-zero status, the wrapper raises RuntimeError with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamdhip64 against torch's copy)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
+
+ABI_VERSION = 1
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_int64
+f32 = C.c_float
+sz = C.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "mragan_abi_version": (i32, []),
+    "mragan_last_error": (C.c_char_p, []),
+    "mragan_conv3d_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
+    "mragan_conv3d_transposed": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
+    "mragan_conv3d_wgrad_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),
+    "mragan_conv3d_wgrad": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
+    "mragan_pack_weight": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "mragan_instnorm_workspace": (sz, [i32, i32, i32, i32, i32]),
+    "mragan_instnorm_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, vp, vp, vp, sz, vp]),
+    "mragan_instnorm_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, sz, vp]),
+    "mragan_instnorm_running_update": (i32, [vp, i32, f32, vp]),
+    "mragan_running_entry_size": (sz, []),
+    "mragan_rpad": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "mragan_rpad_fold": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "mragan_act_bwd": (i32, [vp, vp, vp, vp, i64, i32, vp, vp]),
+    "mragan_l1_loss": (i32, [vp, vp, i64, f32, vp, i32, vp, i32, vp, vp]),
+    "mragan_gan_loss": (i32, [vp, i64, f32, i32, f32, vp, i32, vp, vp, vp]),
+    "mragan_channel_sum": (i32, [vp, i64, i32, vp, i32, vp]),
+    "mragan_adam": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, f32, vp]),
+    "mragan_fill": (i32, [vp, i64, f32, vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class MraganError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes library handle.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise MraganError(f"libmragan_hip.so not found at {LIB_PATH}: build it with "
+                              f"`python mra-gan_amd/build.py` (or __graft_entry__.build())")
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = h.mragan_abi_version()
+        if v != ABI_VERSION:
+            raise MraganError(f"libmragan_hip ABI {v} != expected {ABI_VERSION}")
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().mragan_last_error().decode(errors="replace")
+        raise MraganError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name: str, *args):
+    return getattr(lib(), name)(*args)

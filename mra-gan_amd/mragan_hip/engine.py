@@ -1,0 +1,382 @@
+"""Explicit forward/backward plans for the CycleGAN networks on the HIP kernel library.
+
+The reference runs ResnetGenerator / NLayerDiscriminator through torch.nn + autograd
+(networks3D.py:173-263, 381-425).  Here each network is compiled once into a list of
+*stages* (conv or transposed conv → InstanceNorm → activation, or a whole ResnetBlock) and
+run by hand-written forward and backward passes on NDHWC fp32 tensors:
+
+* the ReplicationPad3d in front of a conv is produced by the previous stage's InstanceNorm
+  kernel writing a padded output (no separate pad pass), and folded back inside the next
+  InstanceNorm-backward kernel;
+* conv biases that feed an InstanceNorm are mathematically cancelled by it (affine=False), so
+  they are not added in the forward and their gradient is exactly 0 (the reference's fp32
+  gradient for them is round-off noise); they still enter the running_mean;
+* weight gradients are written straight into the net's flat gradient buffer (torch layout),
+  so the optimizer is one fused kernel per buffer.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from . import ops
+from ._lib import call
+
+IN_MOMENTUM = 0.1
+
+
+# --------------------------------------------------------------------------------------
+# Layers
+# --------------------------------------------------------------------------------------
+
+class ConvLayer:
+    """A Conv3d (forward form) or ConvTranspose3d (transposed form) with packed weights."""
+
+    def __init__(self, module, transposed: bool):
+        self.m = module
+        self.transposed = transposed
+        self.k = module.kernel_size
+        self.s = module.stride
+        self.p = module.padding
+        self.op = getattr(module, "output_padding", 0)
+        self.cin = module.in_channels
+        self.cout = module.out_channels
+        self.wp_fwd: Optional[torch.Tensor] = None
+        self.wp_bwd: Optional[torch.Tensor] = None
+
+    def repack(self):
+        w = self.m.weight.data
+        T = self.k ** 3
+        if self.wp_fwd is None or self.wp_fwd.device != w.device:
+            self.wp_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+            self.wp_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+        if not self.transposed:     # torch [Cout][Cin][t]
+            ops.pack_weight(w, self.cout, self.cin, T, False, self.wp_fwd)   # [t][Cout][Cin]
+            ops.pack_weight(w, self.cout, self.cin, T, True, self.wp_bwd)    # [t][Cin][Cout]
+        else:                       # torch [Cin][Cout][t]
+            ops.pack_weight(w, self.cin, self.cout, T, True, self.wp_fwd)    # [t][Cout][Cin]
+            ops.pack_weight(w, self.cin, self.cout, T, False, self.wp_bwd)   # [t][Cin][Cout]
+
+    def out_spatial(self, d, h, w):
+        if self.transposed:
+            f = lambda n: ops.convT_out_size(n, self.k, self.s, self.p, self.op)
+        else:
+            f = lambda n: ops.conv_out_size(n, self.k, self.s, self.p)
+        return f(d), f(h), f(w)
+
+    def forward(self, x, bias=None, act=None):
+        N, D, H, W, _ = x.shape
+        return ops.conv3d(x, self.wp_fwd, self.cout, self.k, self.s, self.p, self.out_spatial(D, H, W),
+                          bias=bias, act=act, transposed=self.transposed)
+
+    def dgrad(self, dy, in_spatial):
+        """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
+        return ops.conv3d(dy, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial,
+                          transposed=not self.transposed)
+
+    def wgrad(self, x, dy, accumulate=True):
+        g = self.m.weight.grad
+        if not self.transposed:
+            ops.conv3d_wgrad(dy, x, self.k, self.s, self.p, g, accumulate)     # dW[Cout][Cin][t]
+        else:
+            ops.conv3d_wgrad(x, dy, self.k, self.s, self.p, g, accumulate)     # dW[Cin][Cout][t]
+
+
+@dataclass
+class Stage:
+    kind: str                       # "conv" | "block"
+    conv: Optional[ConvLayer] = None
+    norm: object = None             # InstanceNorm3d container or None
+    act: Optional[str] = None
+    prepad: int = 0                 # ReplicationPad3d applied to this stage's input
+    use_bias: bool = False          # bias actually added (no norm after the conv)
+    # block
+    conv1: Optional[ConvLayer] = None
+    norm1: object = None
+    conv2: Optional[ConvLayer] = None
+    norm2: object = None
+
+
+@dataclass
+class StageCtx:
+    inp: torch.Tensor = None        # stage input (padded by prepad)
+    h: torch.Tensor = None          # conv output
+    mean: torch.Tensor = None
+    rstd: torch.Tensor = None
+    out: torch.Tensor = None        # stage output as produced (padded by next prepad)
+    h1: torch.Tensor = None
+    mean1: torch.Tensor = None
+    rstd1: torch.Tensor = None
+    z1: torch.Tensor = None         # block: relu(IN(h1)) padded by 1
+
+
+@dataclass
+class NetCtx:
+    N: int
+    spatial: tuple
+    stages: List[StageCtx] = field(default_factory=list)
+    out: torch.Tensor = None
+
+
+# --------------------------------------------------------------------------------------
+# Network plan
+# --------------------------------------------------------------------------------------
+
+class NetPlan:
+    """Stage list compiled from a ResnetGenerator / NLayerDiscriminator module tree."""
+
+    def __init__(self, stages: List[Stage], in_channels: int, out_channels: int):
+        self.stages = stages
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.dirty = True
+
+    # ---- parameters --------------------------------------------------------------------
+    def conv_layers(self):
+        for st in self.stages:
+            if st.kind == "block":
+                yield st.conv1
+                yield st.conv2
+            else:
+                yield st.conv
+
+    def repack(self):
+        for c in self.conv_layers():
+            c.repack()
+        self.dirty = False
+
+    def ensure_packed(self):
+        if self.dirty:
+            self.repack()
+
+    def norms_in_order(self):
+        for st in self.stages:
+            if st.kind == "block":
+                yield st, st.norm1, st.conv1
+                yield st, st.norm2, st.conv2
+            elif st.norm is not None:
+                yield st, st.norm, st.conv
+
+    # ---- forward -----------------------------------------------------------------------
+    def _next_prepad(self, i):
+        if i + 1 >= len(self.stages):
+            return 0
+        nxt = self.stages[i + 1]
+        return 1 if nxt.kind == "block" else nxt.prepad
+
+    def forward(self, x: torch.Tensor) -> NetCtx:
+        """x: NDHWC [N, D, H, W, in_channels].  Returns the context holding every tensor the
+        backward needs; ctx.out is the network output (NDHWC)."""
+        self.ensure_packed()
+        N, D, H, W, Cin = x.shape
+        if Cin != self.in_channels:
+            raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
+        ctx = NetCtx(N=N, spatial=(D, H, W))
+        first = self.stages[0]
+        cur = ops.rpad(x, first.prepad) if first.prepad else x
+        for i, st in enumerate(self.stages):
+            sc = StageCtx(inp=cur)
+            ypad = self._next_prepad(i)
+            if st.kind == "block":
+                sc.h1 = st.conv1.forward(cur)
+                sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd(sc.h1, act="relu", ypad=1)
+                sc.h = st.conv2.forward(sc.z1)
+                sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1)
+            else:
+                bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
+                if st.norm is not None:
+                    sc.h = st.conv.forward(cur)
+                    sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad)
+                else:
+                    sc.h = st.conv.forward(cur, bias=bias, act=st.act)     # activated output
+                    sc.out = ops.rpad(sc.h, ypad) if ypad else sc.h
+            ctx.stages.append(sc)
+            cur = sc.out
+        ctx.out = cur
+        return ctx
+
+    # ---- backward ----------------------------------------------------------------------
+    def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,
+                 need_input_grad: bool = False, dx_out: Optional[torch.Tensor] = None,
+                 dx_add: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """dout: up to 3 gradient sources w.r.t. ctx.out (summed).  Weight gradients are
+        accumulated into the parameters' flat grad buffers.  Returns dL/dx (NDHWC) when
+        need_input_grad (written to dx_out, plus dx_add if given)."""
+        g, gpad, gadd = None, 0, None
+        last = len(self.stages) - 1
+        for i in range(last, -1, -1):
+            st, sc = self.stages[i], ctx.stages[i]
+            want_dgrad = i > 0 or need_input_grad
+            if st.kind == "block":
+                G = g if (gpad == 0 and gadd is None) else ops.rpad_fold(g, gpad, add=gadd)
+                dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                if need_wgrad:
+                    st.conv2.wgrad(sc.z1, dh2)
+                dz1 = st.conv2.dgrad(dh2, sc.z1.shape[1:4])
+                dh1 = ops.instnorm_bwd(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
+                if need_wgrad:
+                    st.conv1.wgrad(sc.inp, dh1)
+                g = st.conv1.dgrad(dh1, sc.inp.shape[1:4])
+                gpad, gadd = 1, G
+                continue
+            conv = st.conv
+            if st.norm is not None:
+                dh = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
+            else:
+                if i == last:
+                    srcs = [t for t in dout if t is not None]
+                elif gpad:
+                    srcs = [ops.rpad_fold(g, gpad, add=gadd)]
+                else:
+                    srcs = [g, gadd]
+                dh = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
+                ops.act_bwd(sc.h, srcs, st.act, dh)
+            if need_wgrad:
+                conv.wgrad(sc.inp, dh)
+                if st.use_bias and conv.m.bias is not None:
+                    ops.channel_sum(dh, conv.m.bias.grad, accumulate=True)
+            if want_dgrad:
+                g = conv.dgrad(dh, sc.inp.shape[1:4])
+                gpad, gadd = st.prepad, None
+        if not need_input_grad:
+            return None
+        first = self.stages[0]
+        if first.prepad:
+            return ops.rpad_fold(g, first.prepad, add=dx_add, out=dx_out)
+        if dx_add is not None or dx_out is not None:
+            out = dx_out if dx_out is not None else torch.empty_like(g)
+            ops.act_bwd(None, [g, dx_add], None, out)
+            return out
+        return g
+
+    # ---- running statistics ------------------------------------------------------------
+    def running_entries(self, segments):
+        """segments: list of (NetCtx, row0, count) in the reference's call order.  Returns
+        (norm, bias, C, S, [(mean_ptr, rstd_ptr, count)]) per IN layer."""
+        entries = []
+        si = 0
+        layer_list = list(self.norms_in_order())
+        for li, (st, norm, conv) in enumerate(layer_list):
+            segs = []
+            for ctx, row0, count in segments:
+                sc, which = _locate(self, ctx, li)
+                mean = sc.mean1 if which == 1 else sc.mean
+                rstd = sc.rstd1 if which == 1 else sc.rstd
+                h = sc.h1 if which == 1 else sc.h
+                C_ = mean.shape[1]
+                S = h.shape[1] * h.shape[2] * h.shape[3]
+                segs.append((mean.data_ptr() + 4 * row0 * C_, rstd.data_ptr() + 4 * row0 * C_, count))
+            bias = conv.m.bias
+            entries.append((norm, bias, conv.cout, S, segs))
+            si += 1
+        return entries
+
+
+def _locate(plan: NetPlan, ctx: NetCtx, norm_index: int):
+    """Map the n-th InstanceNorm of the plan to (StageCtx, 1 for a block's first IN else 2/0)."""
+    k = 0
+    for st, sc in zip(plan.stages, ctx.stages):
+        if st.kind == "block":
+            if k == norm_index:
+                return sc, 1
+            if k + 1 == norm_index:
+                return sc, 2
+            k += 2
+        elif st.norm is not None:
+            if k == norm_index:
+                return sc, 0
+            k += 1
+    raise IndexError(norm_index)
+
+
+class _Seg(C.Structure):
+    _fields_ = [("mean", C.c_void_p), ("rstd", C.c_void_p), ("count", C.c_int32), ("_pad", C.c_int32)]
+
+
+class _Entry(C.Structure):
+    _fields_ = [("rm", C.c_void_p), ("rv", C.c_void_p), ("bias", C.c_void_p), ("C", C.c_int32),
+                ("nseg", C.c_int32), ("S", C.c_int64), ("seg", _Seg * 8)]
+
+
+def apply_running_updates(entries, device):
+    """Launch the running-stat update for a list of entries from NetPlan.running_entries."""
+    if not entries:
+        return
+    arr = (_Entry * len(entries))()
+    for e, (norm, bias, C_, S, segs) in zip(arr, entries):
+        if len(segs) > 8:
+            raise ValueError("more than 8 IN calls per step for one layer")
+        e.rm = norm.running_mean.data_ptr()
+        e.rv = norm.running_var.data_ptr()
+        e.bias = bias.data_ptr() if bias is not None else None
+        e.C = C_
+        e.nseg = len(segs)
+        e.S = S
+        for j, (mp, rp, cnt) in enumerate(segs):
+            e.seg[j].mean = mp
+            e.seg[j].rstd = rp
+            e.seg[j].count = cnt
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    dev = host.to(device, non_blocking=False)
+    call("mragan_instnorm_running_update", dev.data_ptr(), len(entries), C.c_float(IN_MOMENTUM),
+         torch.cuda.current_stream().cuda_stream)
+    return dev   # keep alive until the stream consumed it (caller holds the reference)
+
+
+# --------------------------------------------------------------------------------------
+# Plan compilation from the module trees in models/networks3D.py
+# --------------------------------------------------------------------------------------
+
+def compile_resnet_generator(net) -> NetPlan:
+    from models import networks3D as N3
+    stages: List[Stage] = []
+    pending_pad = 0
+    for m in net.model:
+        if isinstance(m, N3.ReplicationPad3d):
+            pending_pad = m.padding
+        elif isinstance(m, N3.Conv3d):
+            stages.append(Stage(kind="conv", conv=ConvLayer(m, False), prepad=pending_pad))
+            pending_pad = 0
+        elif isinstance(m, N3.ConvTranspose3d):
+            stages.append(Stage(kind="conv", conv=ConvLayer(m, True), prepad=pending_pad))
+            pending_pad = 0
+        elif isinstance(m, N3.InstanceNorm3d):
+            stages[-1].norm = m
+        elif isinstance(m, (N3.ReLU, N3.LeakyReLU, N3.Tanh, N3.Sigmoid)):
+            stages[-1].act = m.act_name
+        elif isinstance(m, N3.ResnetBlock):
+            cb = list(m.conv_block)
+            convs = [c for c in cb if isinstance(c, N3.Conv3d)]
+            norms = [c for c in cb if isinstance(c, N3.InstanceNorm3d)]
+            if len(convs) != 2 or len(norms) != 2:
+                raise NotImplementedError("ResnetBlock without two conv+InstanceNorm pairs")
+            stages.append(Stage(kind="block", conv1=ConvLayer(convs[0], False), norm1=norms[0],
+                                conv2=ConvLayer(convs[1], False), norm2=norms[1]))
+        elif isinstance(m, N3.Dropout):
+            raise NotImplementedError("dropout inside the generator is not supported by the HIP engine")
+        else:
+            raise NotImplementedError(f"generator layer {type(m).__name__} not supported by the HIP engine")
+    for st in stages:
+        if st.kind == "conv":
+            st.use_bias = st.norm is None
+    return NetPlan(stages, net.input_nc, net.output_nc)
+
+
+def compile_nlayer_discriminator(net) -> NetPlan:
+    from models import networks3D as N3
+    stages: List[Stage] = []
+    for m in net.model:
+        if isinstance(m, N3.Conv3d):
+            stages.append(Stage(kind="conv", conv=ConvLayer(m, False)))
+        elif isinstance(m, N3.InstanceNorm3d):
+            stages[-1].norm = m
+        elif isinstance(m, (N3.ReLU, N3.LeakyReLU, N3.Tanh, N3.Sigmoid)):
+            stages[-1].act = m.act_name
+        else:
+            raise NotImplementedError(f"discriminator layer {type(m).__name__} not supported by the HIP engine")
+    for st in stages:
+        st.use_bias = st.norm is None
+    return NetPlan(stages, stages[0].conv.cin, stages[-1].conv.cout)

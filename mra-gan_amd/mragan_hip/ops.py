@@ -1,0 +1,229 @@
+"""Tensor-level wrappers around the C ABI.  All tensors are CUDA (HIP) fp32, contiguous.
+Activations are NDHWC tensors of shape [N, D, H, W, C].  Every call runs on the current
+torch stream; no call allocates inside the library (workspaces come from `Workspace`)."""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from ._lib import call, query
+
+ACT = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4}
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(t: torch.Tensor, name: str, ndim: int = 5):
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor (HIP); got {t.device}")
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    if ndim and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-d NDHWC tensor, got shape {tuple(t.shape)}")
+
+
+class Workspace:
+    """Grow-only scratch buffer per device (sized by the first step; reused afterwards)."""
+
+    def __init__(self):
+        self._buf = {}
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        dev = torch.cuda.current_device()
+        b = self._buf.get(dev)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes * 1.25), 1 << 20), dtype=torch.uint8, device=f"cuda:{dev}")
+            self._buf[dev] = b
+        return b
+
+
+WS = Workspace()
+
+
+class KernelTimer:
+    """Optional per-launch HIP-event timing of selected conv launches (used by bench.py to
+    measure the dominant kernel inside the timed region, on the stream it runs on)."""
+
+    def __init__(self):
+        self.match = None       # callable(info: dict) -> bool
+        self.events = []
+
+    def begin(self, info):
+        if self.match is None or not self.match(info):
+            return None
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        return (s, e)
+
+    def end(self, pair):
+        if pair is not None:
+            pair[1].record()
+            self.events.append(pair)
+
+    def reset(self):
+        self.events = []
+
+    def mean_ms(self):
+        if not self.events:
+            return None
+        torch.cuda.synchronize()
+        return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
+
+
+TIMER = KernelTimer()
+
+
+def conv_out_size(n: int, k: int, s: int, p: int) -> int:
+    return (n + 2 * p - k) // s + 1
+
+
+def convT_out_size(n: int, k: int, s: int, p: int, op: int = 0) -> int:
+    return (n - 1) * s - 2 * p + k + op
+
+
+def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
+           bias: Optional[torch.Tensor] = None, act=None, transposed: bool = False,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Forward-form (transposed=False) or transposed-form convolution; see include/mragan_hip.h."""
+    _check(x, "conv3d.x")
+    N, Di, Hi, Wi, cin = x.shape
+    Do, Ho, Wo = out_spatial
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    if out is None:
+        out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
+    elif tuple(out.shape) != (N, Do, Ho, Wo, cout):
+        raise ValueError(f"conv3d: out shape {tuple(out.shape)} != {(N, Do, Ho, Wo, cout)}")
+    name = "mragan_conv3d_transposed" if transposed else "mragan_conv3d_fwd"
+    tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
+                          in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo))) if TIMER.match else None
+    call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo,
+         _stream())
+    TIMER.end(tm)
+    return out
+
+
+def conv3d_wgrad(dense: torch.Tensor, gathered: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
+                 accumulate: bool) -> torch.Tensor:
+    _check(dense, "wgrad.dense")
+    _check(gathered, "wgrad.gathered")
+    N, Dd, Hd, Wd, Cd = dense.shape
+    Ng, Dg, Hg, Wg, Cg = gathered.shape
+    if Ng != N:
+        raise ValueError("wgrad: batch mismatch")
+    if dw.numel() != Cd * Cg * k ** 3 or not dw.is_contiguous():
+        raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
+    nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
+    ws = WS.get(nbytes)
+    call("mragan_conv3d_wgrad", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered), Dg, Hg, Wg, Cg, k, s, p, _ptr(dw),
+         int(accumulate), _ptr(ws), ws.numel(), _stream())
+    return dw
+
+
+def pack_weight(src: torch.Tensor, A: int, B: int, T: int, transpose_ab: bool, out: torch.Tensor) -> torch.Tensor:
+    call("mragan_pack_weight", _ptr(src), A, B, T, int(transpose_ab), _ptr(out), _stream())
+    return out
+
+
+def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch.Tensor] = None, rpad: int = 0,
+                 out: Optional[torch.Tensor] = None, mean: Optional[torch.Tensor] = None,
+                 rstd: Optional[torch.Tensor] = None):
+    _check(x, "instnorm.x")
+    N, D, H, W, C = x.shape
+    shp = (N, D + 2 * ypad, H + 2 * ypad, W + 2 * ypad, C)
+    if out is None:
+        out = torch.empty(shp, device=x.device, dtype=torch.float32)
+    if mean is None:
+        mean = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    if rstd is None:
+        rstd = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    if resid is not None:
+        _check(resid, "instnorm.resid")
+        if tuple(resid.shape) != (N, D + 2 * rpad, H + 2 * rpad, W + 2 * rpad, C):
+            raise ValueError("instnorm: residual shape mismatch")
+    nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+    ws = WS.get(nbytes)
+    call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad, _ptr(mean),
+         _ptr(rstd), _ptr(ws), ws.numel(), _stream())
+    return out, mean, rstd
+
+
+def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int = 0,
+                 dy_add: Optional[torch.Tensor] = None, act=None, out: Optional[torch.Tensor] = None):
+    _check(x, "instnorm_bwd.x")
+    N, D, H, W, C = x.shape
+    if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
+        raise ValueError(f"instnorm_bwd: dy shape {tuple(dy.shape)} does not match pad {dypad}")
+    if out is None:
+        out = torch.empty_like(x)
+    nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+    ws = WS.get(nbytes)
+    call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
+         ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
+    return out
+
+
+def rpad(x: torch.Tensor, p: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, "rpad.x")
+    N, D, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((N, D + 2 * p, H + 2 * p, W + 2 * p, C), device=x.device, dtype=torch.float32)
+    call("mragan_rpad", _ptr(x), N, D, H, W, C, p, _ptr(out), _stream())
+    return out
+
+
+def rpad_fold(yp: torch.Tensor, p: int, add: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(yp, "rpad_fold.y")
+    N, Dp, Hp, Wp, C = yp.shape
+    D, H, W = Dp - 2 * p, Hp - 2 * p, Wp - 2 * p
+    if out is None:
+        out = torch.empty((N, D, H, W, C), device=yp.device, dtype=torch.float32)
+    call("mragan_rpad_fold", _ptr(yp), N, D, H, W, C, p, _ptr(add), _ptr(out), _stream())
+    return out
+
+
+def act_bwd(y: Optional[torch.Tensor], grads: Sequence[Optional[torch.Tensor]], act, out: torch.Tensor) -> torch.Tensor:
+    g = list(grads) + [None] * (3 - len(grads))
+    call("mragan_act_bwd", _ptr(y), _ptr(g[0]), _ptr(g[1]), _ptr(g[2]), out.numel(), ACT[act], _ptr(out), _stream())
+    return out
+
+
+def l1_loss(a: torch.Tensor, b: torch.Tensor, scale: float, loss_slot: torch.Tensor, grad: Optional[torch.Tensor],
+            loss_accumulate=False, grad_accumulate=False):
+    ws = WS.get(1 << 14)
+    call("mragan_l1_loss", _ptr(a), _ptr(b), a.numel(), float(scale), _ptr(loss_slot), int(loss_accumulate), _ptr(grad),
+         int(grad_accumulate), _ptr(ws), _stream())
+
+
+def gan_loss(p: torch.Tensor, target: float, lsgan: bool, scale: float, loss_slot: torch.Tensor,
+             dlogit: Optional[torch.Tensor], loss_accumulate=False):
+    ws = WS.get(1 << 14)
+    call("mragan_gan_loss", _ptr(p), p.numel(), float(target), int(lsgan), float(scale), _ptr(loss_slot),
+         int(loss_accumulate), _ptr(dlogit), _ptr(ws), _stream())
+
+
+def channel_sum(x: torch.Tensor, out: torch.Tensor, accumulate=False):
+    C = x.shape[-1]
+    call("mragan_channel_sum", _ptr(x), x.numel() // C, C, _ptr(out), int(accumulate), _stream())
+    return out
+
+
+def adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, lr: float, beta1: float, beta2: float,
+         eps: float, step: int, grad_scale: float = 1.0):
+    call("mragan_adam", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
+         int(step), float(grad_scale), _stream())
+
+
+def fill(t: torch.Tensor, value: float):
+    call("mragan_fill", _ptr(t), t.numel(), float(value), _stream())

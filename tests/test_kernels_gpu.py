@@ -1,0 +1,263 @@
+"""Per-kernel parity: every HIP entry point (through the C ABI) against a float64 PyTorch-CPU
+evaluation of the same op.  Tolerances are relative L2 errors; fp32 kernels reach ~1e-6, the
+gate is 1e-5 (SURVEY §8c per-op gate)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def ndhwc(t):          # NCDHW → NDHWC contiguous
+    return t.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def ncdhw(t):
+    return t.permute(0, 4, 1, 2, 3)
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mragan_hip import ops as _ops
+    return _ops
+
+
+def pack(ops, w, transposed_layer, for_dgrad):
+    """Pack a torch-layout weight the way engine.ConvLayer does."""
+    w = w.float().cuda().contiguous()
+    k = w.shape[2]
+    out = torch.empty(w.numel(), device="cuda")
+    A, B = w.shape[0], w.shape[1]
+    tr = (not transposed_layer) == for_dgrad
+    ops.pack_weight(w, A, B, k ** 3, tr, out)
+    return out
+
+
+CONV_CASES = [
+    # N, cin, cout, S, k, s, p     (generic MFMA path: cin % 8 == 0, cout > 4)
+    (2, 32, 64, 12, 3, 2, 1),
+    (1, 64, 128, 8, 3, 2, 1),
+    (2, 128, 128, 6, 3, 1, 0),
+    (1, 32, 64, 10, 4, 2, 1),
+    (2, 128, 256, 5, 4, 1, 1),
+    (1, 8, 16, 9, 3, 2, 1),
+    (3, 16, 24, 7, 3, 1, 1),
+    (1, 24, 40, 6, 4, 2, 1),
+    # thin paths
+    (2, 1, 32, 14, 7, 1, 0),
+    (1, 2, 32, 12, 7, 1, 0),
+    (2, 32, 1, 14, 7, 1, 0),
+    (1, 32, 2, 12, 7, 1, 0),
+    (2, 1, 32, 16, 4, 2, 1),
+    (1, 2, 16, 12, 4, 2, 1),
+    (2, 256, 1, 7, 4, 1, 1),
+    (1, 64, 1, 6, 4, 1, 1),
+]
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", CONV_CASES)
+@pytest.mark.parametrize("act", [None, "lrelu"])
+def test_conv3d_fwd(ops, N, cin, cout, S, k, s, p, act):
+    g = torch.Generator().manual_seed(N * 1000 + cin * 7 + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    ref = F.conv3d(x, w, b, stride=s, padding=p)
+    if act == "lrelu":
+        ref = F.leaky_relu(ref, 0.2)
+    wp = pack(ops, w, False, False)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), wp, cout, k, s, p, ref.shape[2:], bias=b.float().cuda(), act=act)
+    assert rel(ncdhw(out), ref) < TOL
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", CONV_CASES)
+def test_conv3d_dgrad(ops, N, cin, cout, S, k, s, p):
+    """Input gradient of a forward conv = transposed-form kernel with the dgrad packing."""
+    g = torch.Generator().manual_seed(7 + N * 100 + cin + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv3d(x, w, stride=s, padding=p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    wp = pack(ops, w, False, True)
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), wp, cin, k, s, p, x.shape[2:], transposed=True)
+    assert rel(ncdhw(dx), dx_ref) < TOL
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", CONV_CASES)
+def test_conv3d_wgrad(ops, N, cin, cout, S, k, s, p):
+    g = torch.Generator().manual_seed(11 + N * 10 + cin + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv3d(x, w, stride=s, padding=p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw = torch.full((cout, cin, k, k, k), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=False)
+    assert rel(dw, dw_ref) < TOL
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=True)
+    assert rel(dw, 2 * dw_ref) < TOL
+
+
+CONVT_CASES = [
+    # N, cin, cout, S, k, s, p, op
+    (2, 128, 64, 6, 3, 2, 1, 1),
+    (1, 64, 32, 8, 3, 2, 1, 1),
+    (1, 16, 8, 5, 3, 2, 1, 1),
+    (2, 32, 16, 4, 4, 2, 1, 0),
+    (1, 24, 32, 5, 3, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
+def test_conv_transpose3d_fwd_dgrad_wgrad(ops, N, cin, cout, S, k, s, p, op):
+    g = torch.Generator().manual_seed(N + cin + 3 * cout)
+    x = torch.randn(N, cin, S, S + 1, S, generator=g, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=op)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dx_ref, dw_ref = torch.autograd.grad(y, (x, w), dy)
+    xg = ndhwc(x.detach().float()).cuda()
+    out = ops.conv3d(xg, pack(ops, w.detach(), True, False), cout, k, s, p, y.shape[2:], transposed=True)
+    assert rel(ncdhw(out), y.detach()) < TOL
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w.detach(), True, True), cin, k, s, p, x.shape[2:])
+    assert rel(ncdhw(dx), dx_ref) < TOL
+    dw = torch.empty(cin, cout, k, k, k, device="cuda")
+    ops.conv3d_wgrad(xg, ndhwc(dy.float()).cuda(), k, s, p, dw, accumulate=False)
+    assert rel(dw, dw_ref) < TOL
+
+
+def _in_ref(x, act):
+    m = x.mean(dim=(2, 3, 4), keepdim=True)
+    v = ((x - m) ** 2).mean(dim=(2, 3, 4), keepdim=True)
+    y = (x - m) / torch.sqrt(v + 1e-5)
+    if act == "relu":
+        y = F.relu(y)
+    elif act == "lrelu":
+        y = F.leaky_relu(y, 0.2)
+    return y
+
+
+@pytest.mark.parametrize("N,C,S", [(2, 32, 9), (1, 128, 6), (3, 8, 5), (1, 256, 3)])
+@pytest.mark.parametrize("act", [None, "relu", "lrelu"])
+@pytest.mark.parametrize("ypad", [0, 1, 3])
+def test_instnorm_fwd(ops, N, C, S, act, ypad):
+    g = torch.Generator().manual_seed(N * C + S)
+    x = torch.randn(N, C, S, S + 1, S + 2, generator=g, dtype=torch.float64) * 3 + 1.5
+    resid = torch.randn(N, C, S, S + 1, S + 2, generator=g, dtype=torch.float64) if act is None else None
+    ref = _in_ref(x, act)
+    if resid is not None:
+        ref = ref + resid
+    ref = F.pad(ref, (ypad,) * 6, mode="replicate") if ypad else ref
+    rg = None
+    if resid is not None:
+        rg = ndhwc(F.pad(resid, (1,) * 6, mode="replicate").float()).cuda()
+    out, mean, rstd = ops.instnorm_fwd(ndhwc(x.float()).cuda(), act=act, ypad=ypad, resid=rg, rpad=1)
+    assert rel(ncdhw(out), ref) < TOL
+    assert rel(mean, x.mean(dim=(2, 3, 4))) < 1e-6
+
+
+@pytest.mark.parametrize("N,C,S", [(2, 32, 7), (1, 128, 5), (2, 8, 6)])
+@pytest.mark.parametrize("act", [None, "relu", "lrelu"])
+@pytest.mark.parametrize("dypad", [0, 1, 3])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_instnorm_bwd(ops, N, C, S, act, dypad, with_add):
+    g = torch.Generator().manual_seed(N + C + S + dypad)
+    x = (torch.randn(N, C, S, S + 1, S, generator=g, dtype=torch.float64) * 2 - 0.5).requires_grad_()
+    y = _in_ref(x, act)
+    yp = F.pad(y, (dypad,) * 6, mode="replicate") if dypad else y
+    dyp = torch.randn(yp.shape, generator=g, dtype=torch.float64)
+    add = torch.randn(y.shape, generator=g, dtype=torch.float64) if with_add else None
+    loss = (yp * dyp).sum() + ((y * add).sum() if with_add else 0)
+    (dx_ref,) = torch.autograd.grad(loss, x)
+    xg = ndhwc(x.detach().float()).cuda()
+    _, mean, rstd = ops.instnorm_fwd(xg, act=act)
+    dx = ops.instnorm_bwd(xg, mean, rstd, ndhwc(dyp.float()).cuda(), dypad,
+                          ndhwc(add.float()).cuda() if with_add else None, act=act)
+    assert rel(ncdhw(dx), dx_ref) < 5e-5
+
+
+def test_instnorm_single_voxel_raises(ops):
+    from mragan_hip import MraganError
+    with pytest.raises(MraganError, match="more than 1 spatial element"):
+        ops.instnorm_fwd(torch.zeros(1, 1, 1, 1, 8, device="cuda"))
+
+
+@pytest.mark.parametrize("C,p", [(1, 3), (32, 1), (2, 3)])
+def test_rpad_and_fold(ops, C, p):
+    g = torch.Generator().manual_seed(C + p)
+    x = torch.randn(2, C, 5, 6, 7, generator=g, dtype=torch.float64, requires_grad=True)
+    y = F.pad(x, (p,) * 6, mode="replicate")
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    out = ops.rpad(ndhwc(x.detach().float()).cuda(), p)
+    assert rel(ncdhw(out), y.detach()) < 1e-7
+    add = torch.randn(x.shape, generator=g, dtype=torch.float64)
+    dx = ops.rpad_fold(ndhwc(dy.float()).cuda(), p, add=ndhwc(add.float()).cuda())
+    assert rel(ncdhw(dx), dx_ref + add) < 1e-6
+
+
+@pytest.mark.parametrize("lsgan", [False, True])
+@pytest.mark.parametrize("target", [0.0, 1.0])
+def test_gan_loss(ops, lsgan, target):
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(2, 1, 6, 6, 6, generator=g, dtype=torch.float64, requires_grad=True)
+    if lsgan:
+        p = z
+        loss = ((p - target) ** 2).mean()
+    else:
+        p = torch.sigmoid(z)
+        loss = F.binary_cross_entropy(p, torch.full_like(p, target))
+    (dz,) = torch.autograd.grad(0.5 * loss, z)
+    slot = torch.zeros(1, device="cuda")
+    dlog = torch.empty(p.numel(), device="cuda")
+    ops.gan_loss(p.detach().float().cuda().reshape(-1), target, lsgan, 0.5, slot, dlog)
+    assert abs(float(slot) - 0.5 * float(loss)) < 1e-6 * max(1.0, abs(float(loss)))
+    assert rel(dlog, dz.reshape(-1)) < 1e-5
+
+
+def test_l1_loss(ops):
+    g = torch.Generator().manual_seed(4)
+    a = torch.randn(3, 5, 7, 9, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(3, 5, 7, 9, generator=g, dtype=torch.float64)
+    loss = (a - b).abs().mean() * 5.0
+    (da,) = torch.autograd.grad(loss, a)
+    slot = torch.zeros(1, device="cuda")
+    grad = torch.empty(a.numel(), device="cuda")
+    ops.l1_loss(a.detach().float().cuda(), b.float().cuda(), 5.0, slot, grad)
+    assert abs(float(slot) - float(loss)) < 1e-5
+    assert rel(grad, da.reshape(-1)) < 1e-6
+
+
+def test_adam_matches_torch_formula(ops):
+    from oracle.cyclegan_oracle import adam_update
+    g = torch.Generator().manual_seed(5)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    m0, v0 = torch.zeros(n), torch.zeros(n)
+    pd, md, vd = p0.cuda(), m0.cuda(), v0.cuda()
+    p, m, v = p0.clone(), m0.clone(), v0.clone()
+    for step in range(1, 4):
+        gr = torch.randn(n, generator=g)
+        adam_update(p, gr, m, v, step, 2e-4, 0.5)
+        ops.adam(pd, gr.cuda(), md, vd, 2e-4, 0.5, 0.999, 1e-8, step)
+    assert rel(pd, p) < 1e-7
+    assert rel(md, m) < 1e-6
+
+
+def test_channel_sum(ops):
+    x = torch.randn(1000, 12)
+    out = torch.empty(12, device="cuda")
+    ops.channel_sum(x.cuda(), out)
+    assert rel(out, x.sum(0)) < 1e-6
