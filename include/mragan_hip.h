@@ -97,11 +97,14 @@ int mragan_act_bwd(const float* y, const float* g0, const float* g1, const float
 int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_accumulate, float* grad,
                    int grad_accumulate, void* ws, void* stream);
 /* GANLoss (networks3D.py:130-150) on D's output p: BCE (lsgan = 0, p = sigmoid output) or MSE.
- * loss[0] (=|+=) scale·loss; dlogit = d(scale·loss)/d(pre-sigmoid logits) (BCE) or d/dp (MSE). */
+ * loss[0] (=|+=) scale·loss; dp = d(scale·loss)/dp (the Sigmoid backward belongs to D's last
+ * layer, see mragan_act_bwd).                                                                 */
 int mragan_gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_accumulate,
-                    float* dlogit, void* ws, void* stream);
-/* bias gradient: out[c] (=|+=) Σ_m x[m][c] */
-int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int accumulate, void* stream);
+                    float* dp, void* ws, void* stream);
+/* bias gradient: out[c] (=|+=) Σ_m x[m][c]  (deterministic two-pass reduction) */
+size_t mragan_channel_sum_workspace(int64_t M, int C);
+int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int accumulate, void* ws, size_t ws_bytes,
+                       void* stream);
 /* torch.optim.Adam step (amsgrad=False, weight_decay=0) on flat buffers (cycle_gan_model.py:107-110);
  * the gradient is multiplied by grad_scale first (1/world_size after a SUM all-reduce).      */
 int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,

@@ -144,9 +144,10 @@ int mragan_gan_loss(const float* p, int64_t n, float target, int lsgan, float sc
                   static_cast<hipStream_t>(stream));
 }
 
-int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* stream) {
-  MRAGAN_CHECK_ARG(x && out, "channel_sum: bad args");
-  return channel_sum(x, M, C, out, acc, static_cast<hipStream_t>(stream));
+size_t mragan_channel_sum_workspace(int64_t M, int C) { return channel_sum_ws_bytes(M, C); }
+int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* ws, size_t ws_bytes, void* stream) {
+  MRAGAN_CHECK_ARG(x && out && ws, "channel_sum: bad args");
+  return channel_sum(x, M, C, out, acc, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,

@@ -34,7 +34,7 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
     case kActRelu: return v > 0.f ? v : 0.f;
     case kActLrelu: return v > 0.f ? v : v * kLreluSlope;
     case kActTanh: return tanhf(v);
-    case kActSigmoid: return 1.f / (1.f + __expf(-v));
+    case kActSigmoid: return 1.f / (1.f + expf(-v));
     default: return v;
   }
 }

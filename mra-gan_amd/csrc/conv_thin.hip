@@ -85,77 +85,143 @@ __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, in
 }
 
 // ---------------------------------------------------------------------------------------
-// thin_n: few output channels (ny ≤ 4), contraction channels a multiple of 2; stride 1.
-// Block = 4×4×64 output voxels, thread = 4 consecutive w outputs; the input halo is staged
-// two channels at a time and each thread holds a (4 + K − 1)-wide window of the row in
-// registers, so each LDS read feeds up to 4·K·NY·2 FMAs.
+// thin_n: few output channels (ny ≤ 4), contraction channels a multiple of 8; stride 1
+// (G head Conv3d(ngf→nc, k7) forward, G stem data gradient).
+// Block = one output plane d × 16 rows h × 64 columns w; thread = 4 consecutive w outputs of
+// one row.  The kernel sweeps td (plane offset) and 8-channel chunks: each stage fills LDS
+// with the (16+K−1) × (64+K−1) × 8-channel input slab of plane d+td (float4 loads, two per
+// position), then every thread slides a (4+K−1)-wide register window along its row for each
+// th, K taps each: 4·K·8·NY FMAs per 2(4+K−1) ds_read_b128.  Weights of a (t, chunk) are
+// wave-uniform (scalar loads).
 // ---------------------------------------------------------------------------------------
-constexpr int TN_OD = 4, TN_OH = 4, TN_OW = 64, TN_VW = 4;
+constexpr int TN_TH = 16, TN_OW = 64, TN_VW = 4, TN_CC = 8;
 
 template <int NY, int K>
-__global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w) {
-  extern __shared__ __attribute__((aligned(16))) float2 xs2[];   // [RD][RH][RW] float2
-  constexpr int RD = TN_OD + K - 1, RH = TN_OH + K - 1, RW = TN_OW + K - 1;
+__global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, int tiles_w) {
+  extern __shared__ __attribute__((aligned(16))) float4 slab[];   // [RH][RW][2] float4
+  constexpr int RH = TN_TH + K - 1, RW = TN_OW + K - 1;
   constexpr int WL = TN_VW + K - 1;
   const int tid = threadIdx.x;
   int tile = blockIdx.x;
   const int tw_ = tile % tiles_w; tile /= tiles_w;
   const int th_ = tile % tiles_h; tile /= tiles_h;
-  const int td_ = tile % tiles_d; const int nb = tile / tiles_d;
-  const int o0d = td_ * TN_OD, o0h = th_ * TN_OH, o0w = tw_ * TN_OW;
-  int r0d, r0h, r0w;
-  if (!a.trans) { r0d = o0d - a.p; r0h = o0h - a.p; r0w = o0w - a.p; }
-  else { r0d = o0d + a.p - (K - 1); r0h = o0h + a.p - (K - 1); r0w = o0w + a.p - (K - 1); }
-  const int vw = tid % (TN_OW / TN_VW), oh = (tid / (TN_OW / TN_VW)) % TN_OH, od = tid / ((TN_OW / TN_VW) * TN_OH);
+  const int od = tile % a.Do; const int nb = tile / a.Do;
+  const int o0h = th_ * TN_TH, o0w = tw_ * TN_OW;
+  // input coordinate of local offset j along a dim: fwd o - p + j (tap j); trans o + p - (K-1) + j (tap K-1-j)
+  const int sh = a.trans ? a.p - (K - 1) : -a.p;
+  const int r0h = o0h + sh, r0w = o0w + sh;
+  const int vw = tid % (TN_OW / TN_VW), hr = tid / (TN_OW / TN_VW);
   const int ow0 = vw * TN_VW;
   float acc[NY][TN_VW];
 #pragma unroll
   for (int n = 0; n < NY; ++n)
 #pragma unroll
     for (int v = 0; v < TN_VW; ++v) acc[n][v] = 0.f;
-  constexpr int R = RD * RH * RW;
-  for (int c0 = 0; c0 < a.cx; c0 += 2) {
-    __syncthreads();
-    for (int e = tid; e < R; e += 256) {
-      int rw = e % RW, rh = (e / RW) % RH, rd = e / (RW * RH);
-      int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
-      bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-      float2 v = make_float2(0.f, 0.f);
-      if (ok) v = *reinterpret_cast<const float2*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0);
-      xs2[e] = v;
-    }
-    __syncthreads();
-    for (int jd = 0; jd < K; ++jd)
+  constexpr int R = RH * RW * 2;   // float4 pieces per stage
+  for (int jd = 0; jd < K; ++jd) {
+    const int id = od + sh + jd;
+    if ((unsigned)id >= (unsigned)a.Di) continue;           // whole plane is zero padding
+    const int td = a.trans ? K - 1 - jd : jd;
+    for (int c0 = 0; c0 < a.cx; c0 += TN_CC) {
+      __syncthreads();
+      for (int e = tid; e < R; e += 256) {
+        const int half = e & 1, pos = e >> 1;
+        const int rw = pos % RW, rh = pos / RW;
+        const int ih = r0h + rh, iw = r0w + rw;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
+          v = *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 +
+                                               4 * half);
+        slab[e] = v;
+      }
+      __syncthreads();
       for (int jh = 0; jh < K; ++jh) {
-        const float2* row = xs2 + ((od + jd) * RH + (oh + jh)) * RW + ow0;
-        float2 win[WL];
+        const int th = a.trans ? K - 1 - jh : jh;
+        const float4* row = slab + ((hr + jh) * RW + ow0) * 2;
+        float4 lo[WL], hi[WL];
 #pragma unroll
-        for (int i = 0; i < WL; ++i) win[i] = row[i];
+        for (int i = 0; i < WL; ++i) { lo[i] = row[2 * i]; hi[i] = row[2 * i + 1]; }
 #pragma unroll
         for (int jw = 0; jw < K; ++jw) {
-          const int t = a.trans ? (((K - 1 - jd) * K + (K - 1 - jh)) * K + (K - 1 - jw)) : ((jd * K + jh) * K + jw);
-          const float* wt = a.w + (int64_t)t * NY * a.cx + c0;
+          const int tw = a.trans ? K - 1 - jw : jw;
+          const float* wt = a.w + ((int64_t)((td * K + th) * K + tw) * NY) * a.cx + c0;
 #pragma unroll
           for (int n = 0; n < NY; ++n) {
-            const float w0 = wt[n * a.cx], w1 = wt[n * a.cx + 1];
+            const float* wn = wt + n * a.cx;
+            const float w0 = wn[0], w1 = wn[1], w2 = wn[2], w3 = wn[3], w4 = wn[4], w5 = wn[5], w6 = wn[6], w7 = wn[7];
 #pragma unroll
-            for (int v = 0; v < TN_VW; ++v)
-              acc[n][v] = fmaf(win[v + jw].x, w0, fmaf(win[v + jw].y, w1, acc[n][v]));
+            for (int v = 0; v < TN_VW; ++v) {
+              const float4 a0 = lo[v + jw], a1 = hi[v + jw];
+              float s = acc[n][v];
+              s = fmaf(a0.x, w0, s); s = fmaf(a0.y, w1, s); s = fmaf(a0.z, w2, s); s = fmaf(a0.w, w3, s);
+              s = fmaf(a1.x, w4, s); s = fmaf(a1.y, w5, s); s = fmaf(a1.z, w6, s); s = fmaf(a1.w, w7, s);
+              acc[n][v] = s;
+            }
           }
         }
       }
+    }
   }
-  const int gd = o0d + od, gh = o0h + oh;
-  if (gd < a.Do && gh < a.Ho) {
+  const int gh = o0h + hr;
+  if (gh < a.Ho) {
 #pragma unroll
     for (int v = 0; v < TN_VW; ++v) {
-      int gw = o0w + ow0 + v;
+      const int gw = o0w + ow0 + v;
       if (gw >= a.Wo) continue;
-      float* dst = a.y + ((((int64_t)nb * a.Do + gd) * a.Ho + gh) * a.Wo + gw) * NY;
+      float* dst = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + gh) * a.Wo + gw) * NY;
 #pragma unroll
       for (int n = 0; n < NY; ++n) dst[n] = act_fwd(acc[n][v] + (a.bias ? a.bias[n] : 0.f), a.act);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// thin_n_class: few output channels, transposed form with stride s > 1 (D-first data
+// gradient, k4 s2 p1): one parity class per blockIdx.y, so the (≤ ceil(k/s)³) taps of a block
+// are uniform; one thread per output voxel reads each tap's channel row with float4 loads.
+// ---------------------------------------------------------------------------------------
+template <int NY>
+__global__ void __launch_bounds__(256) thin_n_class_kernel(ThinArgs a) {
+  const int s = a.s, k = a.k;
+  const int cls = blockIdx.y;
+  const int cw = cls % s, ch = (cls / s) % s, cd = cls / (s * s);
+  const int Qd = (a.Do - cd + s - 1) / s, Qh = (a.Ho - ch + s - 1) / s, Qw = (a.Wo - cw + s - 1) / s;
+  const int64_t M = (int64_t)a.N * Qd * Qh * Qw;
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  int qw = (int)(m % Qw); int64_t u = m / Qw;
+  int qh = (int)(u % Qh); u /= Qh;
+  int qd = (int)(u % Qd); int nb = (int)(u / Qd);
+  const int od = qd * s + cd, oh = qh * s + ch, ow = qw * s + cw;
+  const int t0d = (cd + a.p) % s, t0h = (ch + a.p) % s, t0w = (cw + a.p) % s;
+  float acc[NY];
+#pragma unroll
+  for (int n = 0; n < NY; ++n) acc[n] = 0.f;
+  for (int td = t0d; td < k; td += s) {
+    const int id = (od + a.p - td) / s;
+    if ((unsigned)id >= (unsigned)a.Di) continue;
+    for (int th = t0h; th < k; th += s) {
+      const int ih = (oh + a.p - th) / s;
+      if ((unsigned)ih >= (unsigned)a.Hi) continue;
+      for (int tw = t0w; tw < k; tw += s) {
+        const int iw = (ow + a.p - tw) / s;
+        if ((unsigned)iw >= (unsigned)a.Wi) continue;
+        const float* xr = a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx;
+        const float* wt = a.w + (int64_t)((td * k + th) * k + tw) * NY * a.cx;
+        for (int c = 0; c < a.cx; c += 4) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + c);
+#pragma unroll
+          for (int n = 0; n < NY; ++n) {
+            const float* wn = wt + n * a.cx + c;
+            acc[n] = fmaf(xv.x, wn[0], fmaf(xv.y, wn[1], fmaf(xv.z, wn[2], fmaf(xv.w, wn[3], acc[n]))));
+          }
+        }
+      }
+    }
+  }
+  float* dst = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * NY;
+#pragma unroll
+  for (int n = 0; n < NY; ++n) dst[n] = act_fwd(acc[n] + (a.bias ? a.bias[n] : 0.f), a.act);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -193,11 +259,11 @@ __global__ void __launch_bounds__(256) thin_naive_kernel(ThinArgs a) {
 }
 
 template <int NY>
-static void launch_thin_n(const ThinArgs& a, dim3 grid, size_t lds, hipStream_t st, int td, int th, int tw) {
+static void launch_thin_n(const ThinArgs& a, dim3 grid, size_t lds, hipStream_t st, int th, int tw) {
   switch (a.k) {
-    case 3: hipLaunchKernelGGL((thin_n_kernel<NY, 3>), grid, dim3(256), lds, st, a, td, th, tw); break;
-    case 4: hipLaunchKernelGGL((thin_n_kernel<NY, 4>), grid, dim3(256), lds, st, a, td, th, tw); break;
-    default: hipLaunchKernelGGL((thin_n_kernel<NY, 7>), grid, dim3(256), lds, st, a, td, th, tw); break;
+    case 3: hipLaunchKernelGGL((thin_n_kernel<NY, 3>), grid, dim3(256), lds, st, a, th, tw); break;
+    case 4: hipLaunchKernelGGL((thin_n_kernel<NY, 4>), grid, dim3(256), lds, st, a, th, tw); break;
+    default: hipLaunchKernelGGL((thin_n_kernel<NY, 7>), grid, dim3(256), lds, st, a, th, tw); break;
   }
 }
 
@@ -220,19 +286,30 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     }
     return check_launch("thin_k");
   }
-  if (a.ny <= 4 && s1 && a.cx % 2 == 0 && (a.k == 3 || a.k == 4 || a.k == 7)) {
-    int td = ceil_div(a.Do, TN_OD), th = ceil_div(a.Ho, TN_OH), tw = ceil_div(a.Wo, TN_OW);
-    size_t lds = (size_t)(TN_OD + a.k - 1) * (TN_OH + a.k - 1) * (TN_OW + a.k - 1) * sizeof(float2);
-    dim3 grid(a.N * td * th * tw);
+  const int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  if (a.ny <= 4 && s1 && a.cx % TN_CC == 0 && (a.k == 3 || a.k == 4 || a.k == 7) && total >= 4096) {
+    int th = ceil_div(a.Ho, TN_TH), tw = ceil_div(a.Wo, TN_OW);
+    size_t lds = (size_t)(TN_TH + a.k - 1) * (TN_OW + a.k - 1) * 2 * sizeof(float4);
+    dim3 grid(a.N * a.Do * th * tw);
     switch (a.ny) {
-      case 1: launch_thin_n<1>(a, grid, lds, st, td, th, tw); break;
-      case 2: launch_thin_n<2>(a, grid, lds, st, td, th, tw); break;
-      case 3: launch_thin_n<3>(a, grid, lds, st, td, th, tw); break;
-      default: launch_thin_n<4>(a, grid, lds, st, td, th, tw); break;
+      case 1: launch_thin_n<1>(a, grid, lds, st, th, tw); break;
+      case 2: launch_thin_n<2>(a, grid, lds, st, th, tw); break;
+      case 3: launch_thin_n<3>(a, grid, lds, st, th, tw); break;
+      default: launch_thin_n<4>(a, grid, lds, st, th, tw); break;
     }
     return check_launch("thin_n");
   }
-  int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0) {
+    const int64_t maxq = (int64_t)a.N * ceil_div(a.Do, a.s) * ceil_div(a.Ho, a.s) * ceil_div(a.Wo, a.s);
+    dim3 grid(ceil_div(maxq, 256), a.s * a.s * a.s);
+    switch (a.ny) {
+      case 1: hipLaunchKernelGGL(thin_n_class_kernel<1>, grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(thin_n_class_kernel<2>, grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(thin_n_class_kernel<3>, grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(thin_n_class_kernel<4>, grid, dim3(256), 0, st, a); break;
+    }
+    return check_launch("thin_n_class");
+  }
   hipLaunchKernelGGL(thin_naive_kernel, dim3(ceil_div(total, 4)), dim3(256), 0, st, a);
   return check_launch("thin_naive");
 }
@@ -250,18 +327,15 @@ constexpr int TW_D = 4, TW_H = 4, TW_W = 16, TW_M = TW_D * TW_H * TW_W;
 constexpr int TW_MAXR = 2;
 
 
-template <int K>
+template <int K, int S>
 __global__ void __launch_bounds__(256) thin_wgrad_kernel(ThinWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int s = a.s;
-  const int RD = (TW_D - 1) * s + K, RH = (TW_H - 1) * s + K, RW = (TW_W - 1) * s + K;
-  const int Rn = RD * RH * RW;
-  const int dch = a.vec_dn ? a.Cd : 1;          // D channels staged
-  const int doff = a.vec_dn ? 0 : 0;
+  constexpr int s = S;
+  constexpr int RD = (TW_D - 1) * S + K, RH = (TW_H - 1) * S + K, RW = (TW_W - 1) * S + K;
+  constexpr int WLEN = (TW_W - 1) * S + K;      // G row window of one tile row
+  constexpr int Rn = RD * RH * RW;
   const int gch = a.vec_dn ? 1 : 4;             // G channels staged
   const int goff = a.vec_dn ? blockIdx.y : 4 * blockIdx.y;
-  const int dsel = a.vec_dn ? 0 : -1;           // vec over gn: role picks the dn
-  (void)doff; (void)dsel;
   float* Dt = sm;                               // [TW_M][Cd]  (all D channels; small or the wide side)
   float* Gt = sm + TW_M * a.Cd;                 // [Rn][gch]
   float* red = Gt + Rn * gch;
@@ -313,24 +387,47 @@ __global__ void __launch_bounds__(256) thin_wgrad_kernel(ThinWgradArgs a) {
       const int th = role % K, td = (role / K) % K, ch = role / (K * K);
       for (int row = split; row < TW_D * TW_H; row += RS) {
         const int mh = row % TW_H, md = row / TW_H;
-        for (int mw = 0; mw < TW_W; ++mw) {
-          const int mi = (md * TW_H + mh) * TW_W + mw;
-          const float* grow = Gt + (((md * s + td) * RH + (mh * s + th)) * RW + mw * s) * gch;
-          if (a.vec_dn) {
-            const float4 dv = *reinterpret_cast<const float4*>(Dt + mi * a.Cd + 4 * ch);
+        const int mi0 = (md * TW_H + mh) * TW_W;
+        const float* grow = Gt + (((md * S + td) * RH + (mh * S + th)) * RW) * gch;
+        if (a.vec_dn) {
+          // the whole G row window in registers (gch == 1): one LDS read per voxel
+          float gw[WLEN];
+#pragma unroll
+          for (int i = 0; i < WLEN; ++i) gw[i] = grow[i];
+#pragma unroll
+          for (int mw = 0; mw < TW_W; ++mw) {
+            const float4 dv = *reinterpret_cast<const float4*>(Dt + (mi0 + mw) * a.Cd + 4 * ch);
 #pragma unroll
             for (int t = 0; t < K; ++t) {
-              const float g = grow[t];
+              const float g = gw[mw * S + t];
               acc[rs][0][t] = fmaf(dv.x, g, acc[rs][0][t]);
               acc[rs][1][t] = fmaf(dv.y, g, acc[rs][1][t]);
               acc[rs][2][t] = fmaf(dv.z, g, acc[rs][2][t]);
               acc[rs][3][t] = fmaf(dv.w, g, acc[rs][3][t]);
             }
-          } else {
-            const float d = Dt[mi * a.Cd + ch];
+          }
+        } else if constexpr (S == 1) {
+          float4 gw[WLEN];
+#pragma unroll
+          for (int i = 0; i < WLEN; ++i) gw[i] = *reinterpret_cast<const float4*>(grow + 4 * i);
+#pragma unroll
+          for (int mw = 0; mw < TW_W; ++mw) {
+            const float d = Dt[(mi0 + mw) * a.Cd + ch];
 #pragma unroll
             for (int t = 0; t < K; ++t) {
-              const float4 g = *reinterpret_cast<const float4*>(grow + 4 * t);
+              const float4 g = gw[mw + t];
+              acc[rs][0][t] = fmaf(d, g.x, acc[rs][0][t]);
+              acc[rs][1][t] = fmaf(d, g.y, acc[rs][1][t]);
+              acc[rs][2][t] = fmaf(d, g.z, acc[rs][2][t]);
+              acc[rs][3][t] = fmaf(d, g.w, acc[rs][3][t]);
+            }
+          }
+        } else {
+          for (int mw = 0; mw < TW_W; ++mw) {
+            const float d = Dt[(mi0 + mw) * a.Cd + ch];
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+              const float4 g = *reinterpret_cast<const float4*>(grow + 4 * (mw * S + t));
               acc[rs][0][t] = fmaf(d, g.x, acc[rs][0][t]);
               acc[rs][1][t] = fmaf(d, g.y, acc[rs][1][t]);
               acc[rs][2][t] = fmaf(d, g.z, acc[rs][2][t]);
@@ -431,10 +528,14 @@ int conv_thin_wgrad(ThinWgradArgs a, float* out, int accumulate, float* ws, size
   if (a.ntiles == 0) return kOk;
   a.slab = ws;
   dim3 grid(gx, gy);
-  switch (K) {
-    case 3: hipLaunchKernelGGL(thin_wgrad_kernel<3>, grid, dim3(256), lds, st, a); break;
-    case 4: hipLaunchKernelGGL(thin_wgrad_kernel<4>, grid, dim3(256), lds, st, a); break;
-    default: hipLaunchKernelGGL(thin_wgrad_kernel<7>, grid, dim3(256), lds, st, a); break;
+  const int ks = K * 10 + a.s;
+  switch (ks) {
+    case 31: hipLaunchKernelGGL((thin_wgrad_kernel<3, 1>), grid, dim3(256), lds, st, a); break;
+    case 32: hipLaunchKernelGGL((thin_wgrad_kernel<3, 2>), grid, dim3(256), lds, st, a); break;
+    case 41: hipLaunchKernelGGL((thin_wgrad_kernel<4, 1>), grid, dim3(256), lds, st, a); break;
+    case 42: hipLaunchKernelGGL((thin_wgrad_kernel<4, 2>), grid, dim3(256), lds, st, a); break;
+    case 71: hipLaunchKernelGGL((thin_wgrad_kernel<7, 1>), grid, dim3(256), lds, st, a); break;
+    default: set_error("thin_wgrad: k=%d stride=%d unsupported", K, a.s); return kUnsupported;
   }
   rc = check_launch("thin_wgrad");
   if (rc) return rc;

@@ -73,7 +73,8 @@ int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss,
             float* ws, hipStream_t st);
 int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc, float* dlogit,
              float* ws, hipStream_t st);
-int channel_sum(const float* x, int64_t M, int C, float* out, int acc, hipStream_t st);
+int channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* ws, size_t ws_bytes, hipStream_t st);
+size_t channel_sum_ws_bytes(int64_t M, int C);
 int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
          float grad_scale, hipStream_t st);
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);

@@ -108,9 +108,9 @@ __global__ void __launch_bounds__(256) l1_kernel(const float* __restrict__ a, co
 
 // ---- GAN loss on D's output map ------------------------------------------------------------
 // BCE (default, pred = sigmoid output p): loss = −mean(t·max(ln p,−100) + (1−t)·max(ln(1−p),−100));
-//   dlogit = scale/n · (p−t)/max(p(1−p),1e-12) · p(1−p)       (ATen binary_cross_entropy_backward
-//   followed by sigmoid_backward)
-// MSE (--no_lsgan given → LSGAN): loss = mean((x−t)²); dlogit = scale/n · 2(x−t)
+//   dp = scale/n · (p−t)/max(p(1−p),1e-12)     (ATen binary_cross_entropy_backward; the sigmoid
+//   backward is applied by the discriminator's last stage)
+// MSE (--no_lsgan given → LSGAN): loss = mean((x−t)²); dp = scale/n · 2(x−t)
 __global__ void __launch_bounds__(256) gan_kernel(const float* __restrict__ p, int64_t n, float t, int lsgan, float scale,
                                                   float* loss_partial, float* __restrict__ dlogit) {
   double s = 0;
@@ -124,8 +124,7 @@ __global__ void __launch_bounds__(256) gan_kernel(const float* __restrict__ p, i
     } else {
       const float lp = fmaxf(logf(v), -100.f), l1p = fmaxf(logf(1.f - v), -100.f);
       s += -(t * lp + (1.f - t) * l1p);
-      const float pp = (1.f - v) * v;
-      g = (v - t) / fmaxf(pp, 1e-12f) * pp;
+      g = (v - t) / fmaxf((1.f - v) * v, 1e-12f);
     }
     if (dlogit) dlogit[i] = g * (scale / (float)n);
   }
@@ -141,11 +140,23 @@ __global__ void partial_sum_kernel(const float* __restrict__ part, int nb, float
 }
 
 // ---- channel sums (bias gradients): out[c] (=|+=) Σ_m x[m][c] ------------------------------
-__global__ void __launch_bounds__(256) channel_sum_kernel(const float* __restrict__ x, int64_t M, int C, float* __restrict__ out,
-                                                          int acc) {
+// pass 1: grid (chunks, C); each block sums a contiguous chunk of rows of one channel
+__global__ void __launch_bounds__(256) channel_sum_kernel(const float* __restrict__ x, int64_t M, int C, int chunks,
+                                                          double* __restrict__ part) {
+  const int c = blockIdx.y;
+  const int64_t per = (M + chunks - 1) / chunks;
+  const int64_t m0 = blockIdx.x * per, m1 = min(M, m0 + per);
+  double s = 0;
+  for (int64_t m = m0 + threadIdx.x; m < m1; m += blockDim.x) s += x[m * C + c];
+  const double t = block_sum(s);
+  if (threadIdx.x == 0) part[(int64_t)c * chunks + blockIdx.x] = t;
+}
+
+// pass 2: one block per channel adds the chunk partials in a fixed order (deterministic)
+__global__ void channel_sum_final_kernel(const double* __restrict__ part, int chunks, float* __restrict__ out, int acc) {
   const int c = blockIdx.x;
   double s = 0;
-  for (int64_t m = threadIdx.x; m < M; m += blockDim.x) s += x[m * C + c];
+  for (int i = threadIdx.x; i < chunks; i += blockDim.x) s += part[(int64_t)c * chunks + i];
   const double t = block_sum(s);
   if (threadIdx.x == 0) out[c] = acc ? out[c] + (float)t : (float)t;
 }
@@ -218,10 +229,23 @@ int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, fl
   hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, ws, nb, loss, loss_acc);
   return check_launch("gan_loss_sum");
 }
-int channel_sum(const float* x, int64_t M, int C, float* out, int acc, hipStream_t st) {
+static int channel_sum_chunks(int64_t M, int C) {
+  int64_t ch = (M + 4095) / 4096;
+  int64_t cap = (2048 + C - 1) / C;
+  if (ch > cap) ch = cap;
+  return ch < 1 ? 1 : (int)ch;
+}
+size_t channel_sum_ws_bytes(int64_t M, int C) { return (size_t)channel_sum_chunks(M, C) * C * sizeof(double); }
+int channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* ws, size_t ws_bytes, hipStream_t st) {
   if (C <= 0) return kOk;
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(C), dim3(256), 0, st, x, M, C, out, acc);
-  return check_launch("channel_sum");
+  const int chunks = channel_sum_chunks(M, C);
+  if (channel_sum_ws_bytes(M, C) > ws_bytes) { set_error("channel_sum: workspace too small"); return kWorkspace; }
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(chunks, C), dim3(256), 0, st, x, M, C, chunks, part);
+  int rc = check_launch("channel_sum");
+  if (rc) return rc;
+  hipLaunchKernelGGL(channel_sum_final_kernel, dim3(C), dim3(256), 0, st, part, chunks, out, acc);
+  return check_launch("channel_sum_final");
 }
 int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
          float grad_scale, hipStream_t st) {

@@ -42,7 +42,8 @@ SIGNATURES = {
     "mragan_act_bwd": (i32, [vp, vp, vp, vp, i64, i32, vp, vp]),
     "mragan_l1_loss": (i32, [vp, vp, i64, f32, vp, i32, vp, i32, vp, vp]),
     "mragan_gan_loss": (i32, [vp, i64, f32, i32, f32, vp, i32, vp, vp, vp]),
-    "mragan_channel_sum": (i32, [vp, i64, i32, vp, i32, vp]),
+    "mragan_channel_sum_workspace": (sz, [i64, i32]),
+    "mragan_channel_sum": (i32, [vp, i64, i32, vp, i32, vp, sz, vp]),
     "mragan_adam": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, f32, vp]),
     "mragan_fill": (i32, [vp, i64, f32, vp]),
 }

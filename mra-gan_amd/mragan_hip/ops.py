@@ -215,7 +215,9 @@ def gan_loss(p: torch.Tensor, target: float, lsgan: bool, scale: float, loss_slo
 
 def channel_sum(x: torch.Tensor, out: torch.Tensor, accumulate=False):
     C = x.shape[-1]
-    call("mragan_channel_sum", _ptr(x), x.numel() // C, C, _ptr(out), int(accumulate), _stream())
+    M = x.numel() // C
+    ws = WS.get(query("mragan_channel_sum_workspace", M, C))
+    call("mragan_channel_sum", _ptr(x), M, C, _ptr(out), int(accumulate), _ptr(ws), ws.numel(), _stream())
     return out
 
 

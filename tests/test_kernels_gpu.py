@@ -63,11 +63,16 @@ CONV_CASES = [
     (1, 2, 16, 12, 4, 2, 1),
     (2, 256, 1, 7, 4, 1, 1),
     (1, 64, 1, 6, 4, 1, 1),
+    # large enough for the row-sweep thin_n kernel (fwd: ≥ 4096 output voxels; dgrad likewise)
+    (1, 32, 1, 22, 7, 1, 0),
+    (1, 16, 2, 21, 7, 1, 0),
+    (1, 8, 1, 20, 4, 1, 1),
+    (2, 2, 32, 20, 7, 1, 0),
 ]
 
 
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p", CONV_CASES)
-@pytest.mark.parametrize("act", [None, "lrelu"])
+@pytest.mark.parametrize("act", [None, "lrelu", "tanh", "sigmoid"])
 def test_conv3d_fwd(ops, N, cin, cout, S, k, s, p, act):
     g = torch.Generator().manual_seed(N * 1000 + cin * 7 + cout)
     x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
@@ -76,6 +81,10 @@ def test_conv3d_fwd(ops, N, cin, cout, S, k, s, p, act):
     ref = F.conv3d(x, w, b, stride=s, padding=p)
     if act == "lrelu":
         ref = F.leaky_relu(ref, 0.2)
+    elif act == "tanh":
+        ref = torch.tanh(ref)
+    elif act == "sigmoid":
+        ref = torch.sigmoid(ref)
     wp = pack(ops, w, False, False)
     out = ops.conv3d(ndhwc(x.float()).cuda(), wp, cout, k, s, p, ref.shape[2:], bias=b.float().cuda(), act=act)
     assert rel(ncdhw(out), ref) < TOL
@@ -211,20 +220,20 @@ def test_rpad_and_fold(ops, C, p):
 @pytest.mark.parametrize("lsgan", [False, True])
 @pytest.mark.parametrize("target", [0.0, 1.0])
 def test_gan_loss(ops, lsgan, target):
+    """Loss value and d(loss)/d(D output) — the Sigmoid backward is D's last layer's job."""
     g = torch.Generator().manual_seed(3)
-    z = torch.randn(2, 1, 6, 6, 6, generator=g, dtype=torch.float64, requires_grad=True)
+    z = torch.randn(2, 1, 6, 6, 6, generator=g, dtype=torch.float64)
+    p = (z if lsgan else torch.sigmoid(z)).requires_grad_()
     if lsgan:
-        p = z
         loss = ((p - target) ** 2).mean()
     else:
-        p = torch.sigmoid(z)
         loss = F.binary_cross_entropy(p, torch.full_like(p, target))
-    (dz,) = torch.autograd.grad(0.5 * loss, z)
+    (dp,) = torch.autograd.grad(0.5 * loss, p)
     slot = torch.zeros(1, device="cuda")
-    dlog = torch.empty(p.numel(), device="cuda")
-    ops.gan_loss(p.detach().float().cuda().reshape(-1), target, lsgan, 0.5, slot, dlog)
-    assert abs(float(slot) - 0.5 * float(loss)) < 1e-6 * max(1.0, abs(float(loss)))
-    assert rel(dlog, dz.reshape(-1)) < 1e-5
+    dout = torch.empty(p.numel(), device="cuda")
+    ops.gan_loss(p.detach().float().cuda().reshape(-1), target, lsgan, 0.5, slot, dout)
+    assert abs(float(slot) - 0.5 * float(loss.detach())) < 1e-6 * max(1.0, abs(float(loss.detach())))
+    assert rel(dout, dp.reshape(-1)) < 1e-5
 
 
 def test_l1_loss(ops):

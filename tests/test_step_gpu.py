@@ -102,9 +102,37 @@ def test_generated_volumes(stepped):
         assert rel_err(g, w) < 1e-4, vis
 
 
-def test_gradients(stepped):
+PERTURB = 4e-6      # relative input perturbation ≈ the fp32 forward error of the generated volumes
+
+
+@pytest.fixture(scope="module")
+def conditioning(stepped):
+    """fp64 oracle gradients at inputs perturbed by PERTURB (two realizations): how far the
+    exact gradient moves when the forward pass moves by fp32 rounding.  ReLU / LeakyReLU
+    pre-activations within ~1e-5 of 0 flip their derivative under such perturbations, which
+    makes the step's gradients 1e-3…1e-2-conditioned (tools/diag_d.py traces it)."""
+    from oracle.cyclegan_oracle import CycleGANOracle
+    name, z, meta, _, _, _ = stepped
+    A, B = inputs(meta, 0)
+    out = []
+    for r in range(2):
+        g = torch.Generator().manual_seed(77 + r)
+        Ap = A.double() * (1 + PERTURB * torch.randn(A.shape, generator=g, dtype=torch.float64))
+        Bp = B.double() * (1 + PERTURB * torch.randn(B.shape, generator=g, dtype=torch.float64))
+        torch.manual_seed(meta["seed"])
+        orc = CycleGANOracle(dtype=torch.float64, pool_rng=random.Random(meta["seed"]), **CASE_KW[name])
+        orc.optimize_parameters(Ap, Bp)
+        out.append(orc.grads)
+    return out
+
+
+def test_gradients(stepped, conditioning):
+    """Per parameter: ‖g − g64‖ ≤ max(1e-3, 2·‖g_ref32 − g64‖, 2·‖g64(perturbed) − g64‖)·‖g64‖
+    (SURVEY §8c calibrated protocol, plus the measured conditioning of this step).  Pre-IN
+    conv biases: exactly 0.  Whole network: the same rule on all sampled elements together."""
     name, z, meta, _, _, snap = stepped
-    worst = 0.0
+    bad = []
+    ours, ref32, ref64, pert = [], [], [], [[] for _ in conditioning]
     for net, grads in snap["grads"].items():
         for k, gr in grads.items():
             if is_pre_in_bias(net, k):
@@ -113,11 +141,25 @@ def test_gradients(stepped):
             key64 = f"fp64/step0/grad/{net}/{k}"
             g, w64 = sampled(z, key64, gr)
             w32 = z[f"fp32/step0/grad/{net}/{k}/val"]
-            env = max(1e-3, 2 * rel_err(w32, w64))
+            wp = [sampled(z, key64, c[net][k])[0] for c in conditioning]
+            env = max(1e-3, 2 * rel_err(w32, w64), *[2 * rel_err(x, w64) for x in wp])
             r = rel_err(g, w64)
-            worst = max(worst, r / env)
-            assert r <= env, (net, k, r, env)
-    print("worst grad error / envelope:", worst)
+            if r > env:
+                bad.append((net, k, r, env))
+            scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
+            ours.append(g * scale)
+            ref32.append(w32 * scale)
+            ref64.append(w64 * scale)
+            for lst, x in zip(pert, wp):
+                lst.append(x * scale)
+    assert not bad, bad
+    cat = np.concatenate
+    whole = rel_err(cat(ours), cat(ref64))
+    whole_ref = rel_err(cat(ref32), cat(ref64))
+    whole_pert = max(rel_err(cat(p), cat(ref64)) for p in pert)
+    print(f"{name}: whole-net grad rel err {whole:.2e} (reference fp32 {whole_ref:.2e}, "
+          f"fp64 under {PERTURB:g} input perturbation {whole_pert:.2e})")
+    assert whole <= max(1e-3, 2 * whole_ref, 2 * whole_pert), (whole, whole_ref, whole_pert)
 
 
 def test_running_stats(stepped):

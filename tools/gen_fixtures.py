@@ -50,7 +50,10 @@ def synthetic_pair(shape, seed):
 
 def sample(t: torch.Tensor, key: str, out: dict, n=N_SAMPLES):
     flat = t.detach().reshape(-1).double()
-    rng = np.random.default_rng(zlib.crc32(key.encode()))
+    # the sample positions depend on the tensor's name only (not on the fp32/fp64 prefix), so
+    # the fp32 and fp64 runs are sampled at identical indices and can be compared directly
+    name = key.split("/", 1)[1] if key.startswith(("fp32/", "fp64/")) else key
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
     idx = np.sort(rng.choice(flat.numel(), size=min(n, flat.numel()), replace=False))
     out[key + "/idx"] = idx.astype(np.int64)
     out[key + "/val"] = flat[torch.from_numpy(idx)].numpy()
