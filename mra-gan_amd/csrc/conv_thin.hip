@@ -43,6 +43,13 @@ __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, in
 #pragma unroll
     for (int c = 0; c < CX; ++c) xs[e * CX + c] = ok ? src[c] : 0.f;
   }
+  // the block's weight slice for every tap, [t][32][CX], zero beyond ny (broadcast reads)
+  const int T = a.k * a.k * a.k;
+  float* wsl = xs + ((R * CX + 3) & ~3);
+  for (int e = tid; e < T * TK_NB * CX; e += 256) {
+    const int c = e % CX, j = (e / CX) % TK_NB, t = e / (CX * TK_NB);
+    wsl[e] = (n0 + j < a.ny) ? a.w[((int64_t)t * a.ny + n0 + j) * CX + c] : 0.f;
+  }
   __syncthreads();
   const int ow = tid % TK_OW, oh = (tid / TK_OW) % TK_OH, od = tid / (TK_OW * TK_OH);
   const int gd = o0d + od, gh = o0h + oh, gw = o0w + ow;
@@ -59,22 +66,14 @@ __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, in
         // forward: tap t = j at offset j; transposed (s=1): offset j ↔ tap k-1-j
         int t = a.trans ? (((k - 1 - jd) * k + (k - 1 - jh)) * k + (k - 1 - jw)) : ((jd * k + jh) * k + jw);
         const float* xv = xs + (((ld + jd) * RH + (lh + jh)) * RW + (lw + jw)) * CX;
-        const float* wt = a.w + ((int64_t)t * a.ny + n0) * CX;
+        const float* wt = wsl + t * TK_NB * CX;
         float xr[CX];
 #pragma unroll
         for (int c = 0; c < CX; ++c) xr[c] = xv[c];
-        if (nvalid == TK_NB) {
 #pragma unroll
-          for (int j = 0; j < TK_NB; ++j)
+        for (int j = 0; j < TK_NB; ++j)
 #pragma unroll
-            for (int c = 0; c < CX; ++c) acc[j] = fmaf(xr[c], wt[j * CX + c], acc[j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < TK_NB; ++j)
-            if (j < nvalid)
-#pragma unroll
-              for (int c = 0; c < CX; ++c) acc[j] = fmaf(xr[c], wt[j * CX + c], acc[j]);
-        }
+          for (int c = 0; c < CX; ++c) acc[j] = fmaf(xr[c], wt[j * CX + c], acc[j]);
       }
   if (gd < a.Do && gh < a.Ho && gw < a.Wo) {
     float* dst = a.y + ((((int64_t)nb * a.Do + gd) * a.Ho + gh) * a.Wo + gw) * a.ny + n0;
@@ -96,10 +95,18 @@ __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, in
 // ---------------------------------------------------------------------------------------
 constexpr int TN_TH = 16, TN_OW = 64, TN_VW = 4, TN_CC = 8;
 
+// LDS image of one slab row: position p's two float4 at p*2 + p/4 (+half); one 16-B pad after
+// every 4 positions makes the 16 lanes of a ds_read_b128 group (positions 4·vw + i) land on
+// slots 9·vw mod 16 — all distinct — and the row stride is a multiple of 256 B so lanes of
+// neighbouring rows inside a group stay distinct too.
+__host__ __device__ constexpr int tn_row_stride(int rw) { return ((rw * 2 + rw / 4 + 1) + 15) / 16 * 16; }
+__device__ __forceinline__ int tn_slot(int p) { return p * 2 + (p >> 2); }
+
 template <int NY, int K>
 __global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, int tiles_w) {
-  extern __shared__ __attribute__((aligned(16))) float4 slab[];   // [RH][RW][2] float4
+  extern __shared__ __attribute__((aligned(16))) float4 slab[];   // [RH][RS] float4
   constexpr int RH = TN_TH + K - 1, RW = TN_OW + K - 1;
+  constexpr int RS = tn_row_stride(RW);
   constexpr int WL = TN_VW + K - 1;
   const int tid = threadIdx.x;
   int tile = blockIdx.x;
@@ -118,12 +125,21 @@ __global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, in
 #pragma unroll
     for (int v = 0; v < TN_VW; ++v) acc[n][v] = 0.f;
   constexpr int R = RH * RW * 2;   // float4 pieces per stage
+  // this stage's weights [jh][jw][n][8] (broadcast reads), after the input slab
+  float4* wsl = slab + RH * RS;
   for (int jd = 0; jd < K; ++jd) {
     const int id = od + sh + jd;
     if ((unsigned)id >= (unsigned)a.Di) continue;           // whole plane is zero padding
     const int td = a.trans ? K - 1 - jd : jd;
     for (int c0 = 0; c0 < a.cx; c0 += TN_CC) {
       __syncthreads();
+      for (int e = tid; e < K * K * NY * 2; e += 256) {
+        const int half = e & 1, n = (e >> 1) % NY, jj = (e >> 1) / NY;
+        const int jw = jj % K, jh = jj / K;
+        const int th = a.trans ? K - 1 - jh : jh, tw = a.trans ? K - 1 - jw : jw;
+        wsl[e] = *reinterpret_cast<const float4*>(a.w + ((int64_t)((td * K + th) * K + tw) * NY + n) * a.cx + c0 +
+                                                  4 * half);
+      }
       for (int e = tid; e < R; e += 256) {
         const int half = e & 1, pos = e >> 1;
         const int rw = pos % RW, rh = pos / RW;
@@ -132,23 +148,24 @@ __global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, in
         if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
           v = *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 +
                                                4 * half);
-        slab[e] = v;
+        slab[rh * RS + tn_slot(rw) + half] = v;
       }
       __syncthreads();
       for (int jh = 0; jh < K; ++jh) {
-        const int th = a.trans ? K - 1 - jh : jh;
-        const float4* row = slab + ((hr + jh) * RW + ow0) * 2;
+        const float4* row = slab + (hr + jh) * RS;
         float4 lo[WL], hi[WL];
 #pragma unroll
-        for (int i = 0; i < WL; ++i) { lo[i] = row[2 * i]; hi[i] = row[2 * i + 1]; }
+        for (int i = 0; i < WL; ++i) {
+          const int sl = tn_slot(ow0 + i);
+          lo[i] = row[sl];
+          hi[i] = row[sl + 1];
+        }
 #pragma unroll
         for (int jw = 0; jw < K; ++jw) {
-          const int tw = a.trans ? K - 1 - jw : jw;
-          const float* wt = a.w + ((int64_t)((td * K + th) * K + tw) * NY) * a.cx + c0;
 #pragma unroll
           for (int n = 0; n < NY; ++n) {
-            const float* wn = wt + n * a.cx;
-            const float w0 = wn[0], w1 = wn[1], w2 = wn[2], w3 = wn[3], w4 = wn[4], w5 = wn[5], w6 = wn[6], w7 = wn[7];
+            const float4 wa = wsl[((jh * K + jw) * NY + n) * 2], wb = wsl[((jh * K + jw) * NY + n) * 2 + 1];
+            const float w0 = wa.x, w1 = wa.y, w2 = wa.z, w3 = wa.w, w4 = wb.x, w5 = wb.y, w6 = wb.z, w7 = wb.w;
 #pragma unroll
             for (int v = 0; v < TN_VW; ++v) {
               const float4 a0 = lo[v + jw], a1 = hi[v + jw];
@@ -276,7 +293,9 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     int RD, RH, RW;
     if (!a.trans) { RD = (TK_OD - 1) * a.s + a.k; RH = (TK_OH - 1) * a.s + a.k; RW = (TK_OW - 1) * a.s + a.k; }
     else { RD = TK_OD + a.k - 1; RH = TK_OH + a.k - 1; RW = TK_OW + a.k - 1; }
-    size_t lds = (size_t)RD * RH * RW * a.cx * sizeof(float);
+    size_t lds = ((((size_t)RD * RH * RW * a.cx + 3) & ~(size_t)3) + (size_t)a.k * a.k * a.k * TK_NB * a.cx) *
+                 sizeof(float);
+    MRAGAN_CHECK_ARG(lds <= 160 * 1024, "thin_k: LDS %zu too large", lds);
     dim3 grid(a.N * td * th * tw, ceil_div(a.ny, TK_NB));
     switch (a.cx) {
       case 1: hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
@@ -289,7 +308,8 @@ int conv_thin(ThinArgs a, hipStream_t st) {
   const int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
   if (a.ny <= 4 && s1 && a.cx % TN_CC == 0 && (a.k == 3 || a.k == 4 || a.k == 7) && total >= 4096) {
     int th = ceil_div(a.Ho, TN_TH), tw = ceil_div(a.Wo, TN_OW);
-    size_t lds = (size_t)(TN_TH + a.k - 1) * (TN_OW + a.k - 1) * 2 * sizeof(float4);
+    size_t lds = ((size_t)(TN_TH + a.k - 1) * tn_row_stride(TN_OW + a.k - 1) + (size_t)a.k * a.k * a.ny * 2) *
+                 sizeof(float4);
     dim3 grid(a.N * a.Do * th * tw);
     switch (a.ny) {
       case 1: launch_thin_n<1>(a, grid, lds, st, th, tw); break;
@@ -316,39 +336,40 @@ int conv_thin(ThinArgs a, hipStream_t st) {
 
 // ---------------------------------------------------------------------------------------
 // Thin weight gradient:  dW[dn][gn][t] = Σ_m D[m][dn] · G[m*s − p + t][gn]  (one side ≤ 4 ch)
+// Used for the G stem / head, D first / last layers (dn or gn = image channels).
 // Block = one channel group of the narrow side (grid.y) × a grid-stride walk over 4×4×16
-// tiles of D's grid.  D's tile and G's halo are staged in LDS.  A "role" =
-// (4 channels of the wide side or the narrow channel, td, th) and owns all K taps along w,
-// so per voxel it does one D read, K G reads and 4K FMAs.  When roles < threads the tile's
-// rows are split over RS threads and combined through LDS.  Per-block partials go to a slab
-// that a second kernel sums in fixed order (deterministic).
+// tiles of D's grid; D's tile and G's halo are staged in LDS.  A "role" = (4 channels of the
+// wide side, or one channel of D when the vector runs over G, td, th) owns all K taps along w.
+// Per tile row a role loads the G row window into registers once and sweeps the 16 voxels:
+// one LDS read of D per voxel feeding 4K FMAs.  One role per thread (block = roles rounded up
+// to 64, ≤ 512 threads); with fewer roles than 256 threads the tile rows are split over RS
+// threads and combined through LDS.  Per-block partials go to a slab that a second kernel sums
+// in fixed order (deterministic).
 // ---------------------------------------------------------------------------------------
 constexpr int TW_D = 4, TW_H = 4, TW_W = 16, TW_M = TW_D * TW_H * TW_W;
-constexpr int TW_MAXR = 2;
 
-
-template <int K, int S>
-__global__ void __launch_bounds__(256) thin_wgrad_kernel(ThinWgradArgs a) {
+template <int K, int S, bool VDN>
+__global__ void __launch_bounds__(512) thin_wgrad_kernel(ThinWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  constexpr int s = S;
   constexpr int RD = (TW_D - 1) * S + K, RH = (TW_H - 1) * S + K, RW = (TW_W - 1) * S + K;
   constexpr int WLEN = (TW_W - 1) * S + K;      // G row window of one tile row
   constexpr int Rn = RD * RH * RW;
-  const int gch = a.vec_dn ? 1 : 4;             // G channels staged
-  const int goff = a.vec_dn ? blockIdx.y : 4 * blockIdx.y;
-  float* Dt = sm;                               // [TW_M][Cd]  (all D channels; small or the wide side)
-  float* Gt = sm + TW_M * a.Cd;                 // [Rn][gch]
-  float* red = Gt + Rn * gch;
+  constexpr int GCH = VDN ? 1 : 4;              // G channels staged
+  const int goff = VDN ? blockIdx.y : 4 * blockIdx.y;
+  float* Dt = sm;                               // [TW_M][Cd]
+  float* Gt = sm + TW_M * a.Cd;                 // [Rn][GCH]
+  float* red = Gt + Rn * GCH;
   const int T = K * K * K;
   const int nroles = a.nroles, RS = a.RS;
-  const int tid = threadIdx.x;
-  float acc[TW_MAXR][4][K];
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int role = tid % nroles, split = tid / nroles;
+  const bool active = split < RS;
+  const int th = role % K, td = (role / K) % K, ch = role / (K * K);
+  float acc[4][K];
 #pragma unroll
-  for (int r = 0; r < TW_MAXR; ++r)
+  for (int v = 0; v < 4; ++v)
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-#pragma unroll
-      for (int t = 0; t < K; ++t) acc[r][v][t] = 0.f;
+    for (int t = 0; t < K; ++t) acc[v][t] = 0.f;
 
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int tt = tile;
@@ -357,120 +378,101 @@ __global__ void __launch_bounds__(256) thin_wgrad_kernel(ThinWgradArgs a) {
     const int td_ = tt % a.tiles_d; const int nb = tt / a.tiles_d;
     const int m0d = td_ * TW_D, m0h = th_ * TW_H, m0w = tw_ * TW_W;
     __syncthreads();
-    for (int e = tid; e < TW_M * a.Cd; e += 256) {
-      int c = e % a.Cd, mi = e / a.Cd;
-      int mw = mi % TW_W, mh = (mi / TW_W) % TW_H, md = mi / (TW_W * TW_H);
-      int gd = m0d + md, gh = m0h + mh, gw = m0w + mw;
-      bool ok = gd < a.Dd && gh < a.Hd && gw < a.Wd;
+    for (int e = tid; e < TW_M * a.Cd; e += nthr) {
+      const int c = e % a.Cd, mi = e / a.Cd;
+      const int mw = mi % TW_W, mh = (mi / TW_W) % TW_H, md = mi / (TW_W * TW_H);
+      const int gd = m0d + md, gh = m0h + mh, gw = m0w + mw;
+      const bool ok = gd < a.Dd && gh < a.Hd && gw < a.Wd;
       Dt[e] = ok ? a.D[((((int64_t)nb * a.Dd + gd) * a.Hd + gh) * a.Wd + gw) * a.Cd + c] : 0.f;
     }
-    const int r0d = m0d * s - a.p, r0h = m0h * s - a.p, r0w = m0w * s - a.p;
-    for (int e = tid; e < Rn * gch; e += 256) {
-      int c = e % gch, ri = e / gch;
-      int rw = ri % RW, rh = (ri / RW) % RH, rd = ri / (RW * RH);
-      int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
-      bool ok = (unsigned)id < (unsigned)a.Dg && (unsigned)ih < (unsigned)a.Hg && (unsigned)iw < (unsigned)a.Wg;
+    const int r0d = m0d * S - a.p, r0h = m0h * S - a.p, r0w = m0w * S - a.p;
+    for (int e = tid; e < Rn * GCH; e += nthr) {
+      const int c = e % GCH, ri = e / GCH;
+      const int rw = ri % RW, rh = (ri / RW) % RH, rd = ri / (RW * RH);
+      const int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
+      const bool ok = (unsigned)id < (unsigned)a.Dg && (unsigned)ih < (unsigned)a.Hg && (unsigned)iw < (unsigned)a.Wg;
       Gt[e] = ok ? a.G[((((int64_t)nb * a.Dg + id) * a.Hg + ih) * a.Wg + iw) * a.Cg + goff + c] : 0.f;
     }
     __syncthreads();
+    if (!active) continue;
+    for (int row = split; row < TW_D * TW_H; row += RS) {
+      const int mh = row % TW_H, md = row / TW_H;
+      const int mi0 = (md * TW_H + mh) * TW_W;
+      const float* grow = Gt + (((md * S + td) * RH + (mh * S + th)) * RW) * GCH;
+      if constexpr (VDN) {
+        float gw[WLEN];
 #pragma unroll
-    for (int rs = 0; rs < TW_MAXR; ++rs) {
-      int role, split;
-      if (RS > 1) {
-        if (rs > 0) continue;
-        role = tid % nroles; split = tid / nroles;
-        if (split >= RS) continue;
+        for (int i = 0; i < WLEN; ++i) gw[i] = grow[i];
+#pragma unroll
+        for (int mw = 0; mw < TW_W; ++mw) {
+          const float4 dv = *reinterpret_cast<const float4*>(Dt + (mi0 + mw) * a.Cd + 4 * ch);
+#pragma unroll
+          for (int t = 0; t < K; ++t) {
+            const float g = gw[mw * S + t];
+            acc[0][t] = fmaf(dv.x, g, acc[0][t]);
+            acc[1][t] = fmaf(dv.y, g, acc[1][t]);
+            acc[2][t] = fmaf(dv.z, g, acc[2][t]);
+            acc[3][t] = fmaf(dv.w, g, acc[3][t]);
+          }
+        }
+      } else if constexpr (S == 1) {
+        float4 gw[WLEN];
+#pragma unroll
+        for (int i = 0; i < WLEN; ++i) gw[i] = *reinterpret_cast<const float4*>(grow + 4 * i);
+#pragma unroll
+        for (int mw = 0; mw < TW_W; ++mw) {
+          const float d = Dt[(mi0 + mw) * a.Cd + ch];
+#pragma unroll
+          for (int t = 0; t < K; ++t) {
+            const float4 g = gw[mw + t];
+            acc[0][t] = fmaf(d, g.x, acc[0][t]);
+            acc[1][t] = fmaf(d, g.y, acc[1][t]);
+            acc[2][t] = fmaf(d, g.z, acc[2][t]);
+            acc[3][t] = fmaf(d, g.w, acc[3][t]);
+          }
+        }
       } else {
-        role = tid + rs * 256; split = 0;
-        if (role >= nroles) continue;
-      }
-      const int th = role % K, td = (role / K) % K, ch = role / (K * K);
-      for (int row = split; row < TW_D * TW_H; row += RS) {
-        const int mh = row % TW_H, md = row / TW_H;
-        const int mi0 = (md * TW_H + mh) * TW_W;
-        const float* grow = Gt + (((md * S + td) * RH + (mh * S + th)) * RW) * gch;
-        if (a.vec_dn) {
-          // the whole G row window in registers (gch == 1): one LDS read per voxel
-          float gw[WLEN];
+        for (int mw = 0; mw < TW_W; ++mw) {
+          const float d = Dt[(mi0 + mw) * a.Cd + ch];
 #pragma unroll
-          for (int i = 0; i < WLEN; ++i) gw[i] = grow[i];
-#pragma unroll
-          for (int mw = 0; mw < TW_W; ++mw) {
-            const float4 dv = *reinterpret_cast<const float4*>(Dt + (mi0 + mw) * a.Cd + 4 * ch);
-#pragma unroll
-            for (int t = 0; t < K; ++t) {
-              const float g = gw[mw * S + t];
-              acc[rs][0][t] = fmaf(dv.x, g, acc[rs][0][t]);
-              acc[rs][1][t] = fmaf(dv.y, g, acc[rs][1][t]);
-              acc[rs][2][t] = fmaf(dv.z, g, acc[rs][2][t]);
-              acc[rs][3][t] = fmaf(dv.w, g, acc[rs][3][t]);
-            }
-          }
-        } else if constexpr (S == 1) {
-          float4 gw[WLEN];
-#pragma unroll
-          for (int i = 0; i < WLEN; ++i) gw[i] = *reinterpret_cast<const float4*>(grow + 4 * i);
-#pragma unroll
-          for (int mw = 0; mw < TW_W; ++mw) {
-            const float d = Dt[(mi0 + mw) * a.Cd + ch];
-#pragma unroll
-            for (int t = 0; t < K; ++t) {
-              const float4 g = gw[mw + t];
-              acc[rs][0][t] = fmaf(d, g.x, acc[rs][0][t]);
-              acc[rs][1][t] = fmaf(d, g.y, acc[rs][1][t]);
-              acc[rs][2][t] = fmaf(d, g.z, acc[rs][2][t]);
-              acc[rs][3][t] = fmaf(d, g.w, acc[rs][3][t]);
-            }
-          }
-        } else {
-          for (int mw = 0; mw < TW_W; ++mw) {
-            const float d = Dt[(mi0 + mw) * a.Cd + ch];
-#pragma unroll
-            for (int t = 0; t < K; ++t) {
-              const float4 g = *reinterpret_cast<const float4*>(grow + 4 * (mw * S + t));
-              acc[rs][0][t] = fmaf(d, g.x, acc[rs][0][t]);
-              acc[rs][1][t] = fmaf(d, g.y, acc[rs][1][t]);
-              acc[rs][2][t] = fmaf(d, g.z, acc[rs][2][t]);
-              acc[rs][3][t] = fmaf(d, g.w, acc[rs][3][t]);
-            }
+          for (int t = 0; t < K; ++t) {
+            const float4 g = *reinterpret_cast<const float4*>(grow + 4 * (mw * S + t));
+            acc[0][t] = fmaf(d, g.x, acc[0][t]);
+            acc[1][t] = fmaf(d, g.y, acc[1][t]);
+            acc[2][t] = fmaf(d, g.z, acc[2][t]);
+            acc[3][t] = fmaf(d, g.w, acc[3][t]);
           }
         }
       }
     }
   }
   float* out = a.slab + (int64_t)blockIdx.x * a.Cd * a.Cg * T;
-  auto out_index = [&](int role, int v, int t) -> int64_t {
-    const int th = role % K, td = (role / K) % K, ch = role / (K * K);
+  auto out_index = [&](int rl, int v, int t) -> int64_t {
+    const int th_ = rl % K, td_ = (rl / K) % K, ch_ = rl / (K * K);
     int dn, gn;
-    if (a.vec_dn) { dn = 4 * ch + v; gn = goff; } else { dn = ch; gn = goff + v; }
-    return ((int64_t)dn * a.Cg + gn) * T + (td * K + th) * K + t;
+    if (VDN) { dn = 4 * ch_ + v; gn = goff; } else { dn = ch_; gn = goff + v; }
+    return ((int64_t)dn * a.Cg + gn) * T + (td_ * K + th_) * K + t;
   };
   if (RS > 1) {
     __syncthreads();
-    const int role = tid % nroles, split = tid / nroles;
-    if (split < RS) {
+    if (active) {
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int t = 0; t < K; ++t) red[((split * nroles + role) * 4 + v) * K + t] = acc[0][v][t];
+        for (int t = 0; t < K; ++t) red[((split * nroles + role) * 4 + v) * K + t] = acc[v][t];
     }
     __syncthreads();
-    for (int e = tid; e < nroles * 4 * K; e += 256) {
+    for (int e = tid; e < nroles * 4 * K; e += nthr) {
       const int t = e % K, v = (e / K) % 4, rl = e / (4 * K);
       float sum = 0.f;
       for (int z = 0; z < RS; ++z) sum += red[((z * nroles + rl) * 4 + v) * K + t];
       out[out_index(rl, v, t)] = sum;
     }
-  } else {
+  } else if (active) {
 #pragma unroll
-    for (int rs = 0; rs < TW_MAXR; ++rs) {
-      const int role = tid + rs * 256;
-      if (role >= nroles) continue;
+    for (int v = 0; v < 4; ++v)
 #pragma unroll
-      for (int v = 0; v < 4; ++v)
-#pragma unroll
-        for (int t = 0; t < K; ++t) out[out_index(role, v, t)] = acc[rs][v][t];
-    }
+      for (int t = 0; t < K; ++t) out[out_index(role, v, t)] = acc[v][t];
   }
 }
 
@@ -483,65 +485,77 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, float* __rest
   }
 }
 
-static int thin_wgrad_setup(ThinWgradArgs& a, int* gx, int* gy, size_t* lds) {
+struct ThinWgradPlan { int gx, gy, threads; size_t lds; };
+
+static int thin_wgrad_setup(ThinWgradArgs& a, ThinWgradPlan* pl) {
   a.vec_dn = (a.Cd % 4 == 0 && a.Cd >= a.Cg) ? 1 : 0;
   MRAGAN_CHECK_ARG(a.vec_dn || (a.Cg % 4 == 0 && a.Cd <= 64), "thin_wgrad: unsupported channels (%d,%d)", a.Cd, a.Cg);
   MRAGAN_CHECK_ARG(a.k == 3 || a.k == 4 || a.k == 7, "thin_wgrad: k=%d unsupported", a.k);
+  MRAGAN_CHECK_ARG(a.s == 1 || (a.s == 2 && a.k != 7), "thin_wgrad: stride %d with k=%d unsupported", a.s, a.k);
   const int K = a.k;
   a.nroles = a.vec_dn ? (a.Cd / 4) * K * K : a.Cd * K * K;
-  MRAGAN_CHECK_ARG(a.nroles <= 256 * TW_MAXR, "thin_wgrad: %d roles > %d", a.nroles, 256 * TW_MAXR);
-  a.RS = 256 / a.nroles;
-  if (a.RS < 1) a.RS = 1;
-  if (a.RS > TW_D * TW_H) a.RS = TW_D * TW_H;
+  MRAGAN_CHECK_ARG(a.nroles <= 512, "thin_wgrad: %d roles > 512", a.nroles);
+  if (a.nroles <= 256) {
+    pl->threads = 256;
+    a.RS = 256 / a.nroles;
+    if (a.RS > TW_D * TW_H) a.RS = TW_D * TW_H;
+  } else {
+    pl->threads = (a.nroles + 63) / 64 * 64;
+    a.RS = 1;
+  }
   a.tiles_d = ceil_div(a.Dd, TW_D); a.tiles_h = ceil_div(a.Hd, TW_H); a.tiles_w = ceil_div(a.Wd, TW_W);
   a.ntiles = a.N * a.tiles_d * a.tiles_h * a.tiles_w;
-  *gy = a.vec_dn ? a.Cg : a.Cg / 4;
-  int want = 1024 / *gy;
+  pl->gy = a.vec_dn ? a.Cg : a.Cg / 4;
+  int want = 1024 / pl->gy;
   if (want < 16) want = 16;
-  *gx = a.ntiles < want ? a.ntiles : want;
-  if (*gx < 1) *gx = 1;
+  pl->gx = a.ntiles < want ? a.ntiles : want;
+  if (pl->gx < 1) pl->gx = 1;
   const int s = a.s;
-  int RD = (TW_D - 1) * s + K, RH = (TW_H - 1) * s + K, RW = (TW_W - 1) * s + K;
-  int gch = a.vec_dn ? 1 : 4;
-  *lds = ((size_t)TW_M * a.Cd + (size_t)RD * RH * RW * gch + (a.RS > 1 ? (size_t)a.RS * a.nroles * 4 * K : 0)) *
-         sizeof(float);
-  MRAGAN_CHECK_ARG(*lds <= 160 * 1024, "thin_wgrad: LDS %zu too large", *lds);
+  const int RD = (TW_D - 1) * s + K, RH = (TW_H - 1) * s + K, RW = (TW_W - 1) * s + K;
+  const int gch = a.vec_dn ? 1 : 4;
+  pl->lds = ((size_t)TW_M * a.Cd + (size_t)RD * RH * RW * gch + (a.RS > 1 ? (size_t)a.RS * a.nroles * 4 * K : 0)) *
+            sizeof(float);
+  MRAGAN_CHECK_ARG(pl->lds <= 160 * 1024, "thin_wgrad: LDS %zu too large", pl->lds);
   return kOk;
 }
 
 size_t conv_thin_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int s) {
   ThinWgradArgs a{};
   a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd; a.Cg = Cg; a.k = k; a.s = s;
-  int gx, gy; size_t lds;
-  if (thin_wgrad_setup(a, &gx, &gy, &lds)) return 0;
-  return (size_t)gx * Cd * Cg * k * k * k * sizeof(float);
+  ThinWgradPlan pl;
+  if (thin_wgrad_setup(a, &pl)) return 0;
+  return (size_t)pl.gx * Cd * Cg * k * k * k * sizeof(float);
+}
+
+template <int K, int S>
+static void launch_thin_wgrad(const ThinWgradArgs& a, const ThinWgradPlan& pl, hipStream_t st) {
+  dim3 grid(pl.gx, pl.gy);
+  if (a.vec_dn) hipLaunchKernelGGL((thin_wgrad_kernel<K, S, true>), grid, dim3(pl.threads), pl.lds, st, a);
+  else hipLaunchKernelGGL((thin_wgrad_kernel<K, S, false>), grid, dim3(pl.threads), pl.lds, st, a);
 }
 
 int conv_thin_wgrad(ThinWgradArgs a, float* out, int accumulate, float* ws, size_t ws_bytes, hipStream_t st) {
-  int gx, gy; size_t lds;
-  int rc = thin_wgrad_setup(a, &gx, &gy, &lds);
+  ThinWgradPlan pl;
+  int rc = thin_wgrad_setup(a, &pl);
   if (rc) return rc;
   const int K = a.k;
   const int64_t E = (int64_t)a.Cd * a.Cg * K * K * K;
-  size_t need = (size_t)gx * E * sizeof(float);
+  size_t need = (size_t)pl.gx * E * sizeof(float);
   if (need > ws_bytes) { set_error("thin_wgrad: workspace %zu < %zu", ws_bytes, need); return kWorkspace; }
   if (a.ntiles == 0) return kOk;
   a.slab = ws;
-  dim3 grid(gx, gy);
-  const int ks = K * 10 + a.s;
-  switch (ks) {
-    case 31: hipLaunchKernelGGL((thin_wgrad_kernel<3, 1>), grid, dim3(256), lds, st, a); break;
-    case 32: hipLaunchKernelGGL((thin_wgrad_kernel<3, 2>), grid, dim3(256), lds, st, a); break;
-    case 41: hipLaunchKernelGGL((thin_wgrad_kernel<4, 1>), grid, dim3(256), lds, st, a); break;
-    case 42: hipLaunchKernelGGL((thin_wgrad_kernel<4, 2>), grid, dim3(256), lds, st, a); break;
-    case 71: hipLaunchKernelGGL((thin_wgrad_kernel<7, 1>), grid, dim3(256), lds, st, a); break;
-    default: set_error("thin_wgrad: k=%d stride=%d unsupported", K, a.s); return kUnsupported;
+  switch (K * 10 + a.s) {
+    case 31: launch_thin_wgrad<3, 1>(a, pl, st); break;
+    case 32: launch_thin_wgrad<3, 2>(a, pl, st); break;
+    case 41: launch_thin_wgrad<4, 1>(a, pl, st); break;
+    case 42: launch_thin_wgrad<4, 2>(a, pl, st); break;
+    default: launch_thin_wgrad<7, 1>(a, pl, st); break;
   }
   rc = check_launch("thin_wgrad");
   if (rc) return rc;
   int blocks = (int)((E + 255) / 256);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, out, E, gx, accumulate);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, out, E, pl.gx, accumulate);
   return check_launch("thin_wgrad_reduce");
 }
 

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmark at the 64³ / batch-2 bench shapes (GPU box), for rocprofv3
+kernel traces and PMC counter passes.  Each selected op runs `--reps` times.
+
+    python tools/kbench.py [--ops head_fwd,stem_fwd,...] [--reps 20] [--S 64] [--N 4]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mra-gan_amd"))
+
+import torch  # noqa: E402
+
+from mragan_hip import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="all")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--S", type=int, default=64)
+    ap.add_argument("--N", type=int, default=4)
+    ap.add_argument("--ngf", type=int, default=32)
+    args = ap.parse_args()
+    S, N, ngf = args.S, args.N, args.ngf
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*shape):
+        return torch.randn(shape, device=dev, generator=g)
+
+    c4 = 4 * ngf
+    s4 = S // 4
+    x_head = rnd(N, S + 6, S + 6, S + 6, ngf)           # padded up2 output
+    w_head = rnd(343 * 1 * ngf) * 0.01
+    x_stem = rnd(N, S + 6, S + 6, S + 6, 1)
+    w_stem = rnd(343 * ngf) * 0.01
+    x_res = rnd(N, s4 + 2, s4 + 2, s4 + 2, c4)
+    w_res = rnd(27 * c4 * c4) * 0.01
+    dy_res = rnd(N, s4, s4, s4, c4)
+    dz = rnd(N, S, S, S, 1)
+    dh1 = rnd(N, S, S, S, ngf)
+    x_in = rnd(N, S, S, S, ngf)
+    dy_in = rnd(N, S + 6, S + 6, S + 6, ngf)
+    gw_res = torch.empty(c4 * c4 * 27, device=dev)
+    gw_head = torch.empty(343 * ngf, device=dev)
+
+    table = {
+        "head_fwd": lambda: ops.conv3d(x_head, w_head, 1, 7, 1, 0, (S, S, S), act="tanh"),
+        "stem_dgrad": lambda: ops.conv3d(dh1, w_head, 1, 7, 1, 0, (S + 6,) * 3, transposed=True),
+        "stem_fwd": lambda: ops.conv3d(x_stem, w_stem, ngf, 7, 1, 0, (S, S, S)),
+        "head_dgrad": lambda: ops.conv3d(dz, w_stem, ngf, 7, 1, 0, (S + 6,) * 3, transposed=True),
+        "head_wgrad": lambda: ops.conv3d_wgrad(dz, x_head, 7, 1, 0, gw_head, False),
+        "stem_wgrad": lambda: ops.conv3d_wgrad(dh1, x_stem, 7, 1, 0, gw_head, False),
+        "res_fwd": lambda: ops.conv3d(x_res, w_res, c4, 3, 1, 0, (s4, s4, s4)),
+        "res_dgrad": lambda: ops.conv3d(dy_res, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, transposed=True),
+        "res_wgrad": lambda: ops.conv3d_wgrad(dy_res, x_res, 3, 1, 0, gw_res, False),
+        "in_fwd": lambda: ops.instnorm_fwd(x_in, act="relu", ypad=3),
+        "in_bwd": lambda: ops.instnorm_bwd(x_in, *ops.instnorm_fwd(x_in, act="relu")[1:], dy_in, 3, None, act="relu"),
+    }
+    names = list(table) if args.ops == "all" else args.ops.split(",")
+    for name in names:
+        fn = table[name]
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            fn()
+        torch.cuda.synchronize()
+        print(f"{name:12s} {1e6 * (time.perf_counter() - t0) / args.reps:9.1f} us/call (wall, incl. launch)")
+
+
+if __name__ == "__main__":
+    main()
