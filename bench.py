@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--netG", default="resnet_9blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
     return ap.parse_args()
 
 
@@ -70,10 +74,20 @@ def step_flops(S, batch, ngf=32, n_blocks=9, ndf=32, nc=1):
     return batch * (g + d)
 
 
+def host_threads():
+    """CPU threads this job may use: the affinity mask, capped by OMP_NUM_THREADS when set
+    (os.cpu_count() reports the whole machine on the GPU box, not this job's share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args):
     """Oracle step on the host CPU (same workload shape), bounded to a couple of steps."""
     from oracle.cyclegan_oracle import CycleGANOracle, synthetic_pair
-    torch.set_num_threads(os.cpu_count())
+    torch.set_num_threads(host_threads())
     threads = torch.get_num_threads()
     torch.manual_seed(0)
     orc = CycleGANOracle(ngf=args.ngf, ndf=args.ngf, n_blocks=9 if args.netG == "resnet_9blocks" else 6,
@@ -99,16 +113,40 @@ def cpu_baseline(args):
                       f"{args.batch}x1x{args.size}^3, best {t:.2f} s, {cpu_model}"}
 
 
+def cpu_baseline_child(args, timeout_s=240):
+    """Run cpu_baseline() in a child process (the GPU process only waits), bounded in time."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--size", str(args.size),
+           "--batch", str(args.batch), "--ngf", str(args.ngf), "--netG", args.netG, "--cpu-steps", str(args.cpu_steps)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+        for line in r.stdout.splitlines():
+            if line.startswith("{"):
+                return json.loads(line)
+        return {"value": None, "unit": "patches/s", "cores": host_threads(), "kind": "port",
+                "sample": f"CPU baseline child failed (rc {r.returncode}): {r.stderr[-300:]}"}
+    except subprocess.TimeoutExpired:
+        return {"value": None, "unit": "patches/s", "cores": host_threads(), "kind": "port",
+                "sample": f"CPU oracle step exceeded {timeout_s} s on this host; not reported"}
+
+
 def main():
     args = parse()
+    if args.cpu_baseline_only:
+        print(json.dumps(cpu_baseline(args)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dev = 0 if args.same_device else local
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
 
@@ -206,7 +244,7 @@ def main():
         "step_tflops_achieved": round(step_tf * args.steps / elapsed, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args)
+        res["cpu_baseline"] = cpu_baseline_child(args)
     print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -191,15 +191,6 @@ class CycleGANModel(BaseModel):
         del keep
 
     # ------------------------------------------------------------------ training step
-    def _dist_info(self):
-        if self._dist is None:
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-                self._dist = (dist, dist.get_world_size())
-            else:
-                self._dist = (None, 1)
-        return self._dist
-
     def forward_train(self):
         """The four cycle passes plus the two identity passes, batched (see module doc)."""
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
@@ -296,29 +287,29 @@ class CycleGANModel(BaseModel):
         self._keep = keep
 
     def optimize_parameters(self):
-        dist, world = self._dist_info()
+        """cycle_gan_model.py:227-240.  Single GPU: the reference's order.  Data parallel:
+        G all-reduce overlapped with the D phase (see mragan_hip/dist.py)."""
+        from mragan_hip.dist import GradSync, default_sync
+        if self._dist is None:
+            self._dist = default_sync() or False
         self.forward_train()
         self.set_requires_grad([self.netD_A, self.netD_B], False)
         self.optimizer_G.zero_grad()
         self.backward_G()
-        work_G = None
-        if dist is not None:
-            work_G = [dist.all_reduce(n._flat_grad, async_op=True) for n in (self.netG_A, self.netG_B)]
+        if not self._dist:
+            self.optimizer_G.step()
+        else:
+            sync_G = GradSync(self._dist.dist, self._dist.group)
+            sync_G.start([self.netG_A._flat_grad, self.netG_B._flat_grad])
         self.set_requires_grad([self.netD_A, self.netD_B], True)
         self.optimizer_D.zero_grad()
         self.backward_D_A()
         self.backward_D_B()
-        if dist is not None:
-            work_D = [dist.all_reduce(n._flat_grad, async_op=True) for n in (self.netD_A, self.netD_B)]
-            for w in work_G:
-                w.wait()
-            self.optimizer_G.grad_scale = 1.0 / world
-            self.optimizer_D.grad_scale = 1.0 / world
+        if self._dist:
+            sync_D = GradSync(self._dist.dist, self._dist.group)
+            sync_D.start([self.netD_A._flat_grad, self.netD_B._flat_grad])
+            self.optimizer_G.grad_scale = sync_G.finish()
             self.optimizer_G.step()
-            for w in work_D:
-                w.wait()
-            self.optimizer_D.step()
-        else:
-            self.optimizer_G.step()
-            self.optimizer_D.step()
+            self.optimizer_D.grad_scale = sync_D.finish()
+        self.optimizer_D.step()
         self._running_stats()
