@@ -130,6 +130,18 @@ def cpu_baseline_child(args, timeout_s=240):
                 "sample": f"CPU oracle step exceeded {timeout_s} s on this host; not reported"}
 
 
+def measured_traffic(key):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (profiles/traffic.json, written by tools/pmc_traffic.py: (2·FETCH_SIZE + WRITE_SIZE)·1 KiB,
+    the gfx950 correction); None when no pass was recorded for this configuration."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh)[key]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
@@ -217,6 +229,7 @@ def main():
     flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
     achieved = flops_launch / (kern_ms / 1e3) / 1e12 if kern_ms else None
     step_tf = step_flops(args.size, args.batch, args.ngf) / 1e12
+    traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}")
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
         "value": round(value, 3),
@@ -238,7 +251,7 @@ def main():
                                                f"[{n_launch}x{s4}^3] fwd",
                      "achieved": round(achieved, 2) if achieved else None, "peak": MFMA_F32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4) if achieved else None,
-                     "traffic": None, "launch_ms": round(kern_ms, 4) if kern_ms else None,
+                     "traffic": traffic, "launch_ms": round(kern_ms, 4) if kern_ms else None,
                      "launches_timed": n_kern, "flop_per_launch": flops_launch},
         "step_tflop": round(step_tf, 4),
         "step_tflops_achieved": round(step_tf * args.steps / elapsed, 2),

@@ -95,6 +95,31 @@ def test_state_dict_keys_and_counts():
     assert sum(p.numel() for p in model.netD_A.parameters()) == 2771425   # A16
 
 
+def test_checkpoint_roundtrip(tmp_path):
+    """save_networks/load_networks (reference base_model.py:89-148): '{epoch}_net_{name}.pth' files
+    holding CPU state_dicts with the reference's keys; loading restores the weights in place (the
+    flat-buffer parameter views stay valid) and fills num_batches_tracked like the reference's
+    InstanceNorm patching does."""
+    z, meta, model = _build("step_r6_s24_b2_nc2_lsgan")
+    model.save_dir = str(tmp_path)
+    model.save_networks("latest")
+    ref_keys = {f.split("/")[2] for f in z.files if f.startswith("init/G_A/")}
+    sd = torch.load(tmp_path / "latest_net_G_A.pth", weights_only=True)
+    assert ref_keys <= set(sd) and all(v.device.type == "cpu" for v in sd.values())
+    torch.manual_seed(123)
+    _, _, other = _build("step_r6_s24_b2_nc2_lsgan")
+    other.save_dir = str(tmp_path)
+    ptr = other.netG_A.model[1].weight.data_ptr()
+    other.load_networks("latest")
+    assert other.netG_A.model[1].weight.data_ptr() == ptr
+    for net in ("G_A", "G_B", "D_A", "D_B"):
+        a = getattr(model, "net" + net).state_dict()
+        b = getattr(other, "net" + net).state_dict()
+        assert a.keys() == b.keys()
+        for k in a:
+            assert torch.equal(a[k].cpu(), b[k].cpu()), (net, k)
+
+
 def test_options_defaults_and_quirks():
     from options.train_options import TrainOptions
     argv = sys.argv
