@@ -31,6 +31,7 @@ for p in (ROOT, os.path.join(ROOT, "mra-gan_amd")):
 import torch  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix/vector peak
+MFMA_BF16_PEAK_TFLOPS = 2516.6   # 16 × the f32 MFMA rate (dense bf16, no sparsity)
 
 
 def parse():
@@ -43,6 +44,8 @@ def parse():
     ap.add_argument("--ngf", type=int, default=32)
     ap.add_argument("--netG", default="resnet_9blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="f32", choices=["f32", "bf16x3"],
+                    help="dense-conv contraction: exact f32 MFMA or split-bf16 (bf16x3) MFMA, fp32 accumulate")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
@@ -168,7 +171,8 @@ def main():
 
     sys_argv = sys.argv
     sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
-                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch)]
+                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
+                "--conv_precision", args.precision]
     opt = TrainOptions().gather_options()
     sys.argv = sys_argv
     opt.isTrain, opt.gpu_ids = True, 0
@@ -229,7 +233,12 @@ def main():
     flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
     achieved = flops_launch / (kern_ms / 1e3) / 1e12 if kern_ms else None
     step_tf = step_flops(args.size, args.batch, args.ngf) / 1e12
-    traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}")
+    x3 = args.precision == "bf16x3"
+    # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic (fp32) FLOPs is
+    # the bf16 dense peak / 3
+    peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
+    kname = "conv_igemm_x3 (bf16x3 split MFMA)" if x3 else "conv_igemm_f32"
+    traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
         "value": round(value, 3),
@@ -241,16 +250,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if not x3 else "f32 (bf16x3 split products, f32 accumulate)",
         "data": "synthetic N(0,1) volumes, random init (seed 0)",
         "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, 1ch->1ch, "
-                               f"{args.size}^3 patch, batch {args.batch}/GPU (BASELINE configs[1] shape; fp32)",
+                               f"{args.size}^3 patch, batch {args.batch}/GPU (BASELINE configs[1] shape; fp32 tensors)",
+                   "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"conv_igemm_f32 res-block conv {c4}->{c4} k3 "
-                                               f"[{n_launch}x{s4}^3] fwd",
-                     "achieved": round(achieved, 2) if achieved else None, "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4) if achieved else None,
+        "roofline": {"bound": "mfma", "kernel": f"{kname} res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "launch_ms": round(kern_ms, 4) if kern_ms else None,
                      "launches_timed": n_kern, "flop_per_launch": flops_launch},
         "step_tflop": round(step_tf, 4),

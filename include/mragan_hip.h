@@ -34,6 +34,17 @@ enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2
 int mragan_abi_version(void);
 const char* mragan_last_error(void);
 
+/* Contraction precision of the dense (MFMA) convolutions, process-wide.  The reference computes
+ * in fp32 (ATen conv); both modes take and return fp32 tensors.
+ *   MRAGAN_PREC_F32    exact fp32 products (v_mfma_f32_32x32x2_f32), 157 TF peak;
+ *   MRAGAN_PREC_BF16X3 each operand split into bf16 hi + lo, a·b ≈ lo·hi + hi·lo + hi·hi with fp32
+ *                      accumulation (3 × v_mfma_f32_32x32x16_bf16), ≤ 3·2⁻¹⁸ relative error per
+ *                      product, up to 5.3× the exact rate.
+ * Thin (VALU) convolutions and weight gradients are exact fp32 in both modes.              */
+enum mragan_precision { MRAGAN_PREC_F32 = 0, MRAGAN_PREC_BF16X3 = 1 };
+int mragan_set_conv_precision(int mode);
+int mragan_get_conv_precision(void);
+
 /* ---- convolution --------------------------------------------------------------------------
  * Forward form:     y[n,o,:] = act(bias + Σ_{j<k³} x[n, o*stride − pad + j, :] · Wp[j])  (zero fill)
  * Replaces nn.Conv3d.forward (networks3D.py:186, 192, 241, 257, 212, 389, 397, 406, 414) and the

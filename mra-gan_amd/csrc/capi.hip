@@ -26,6 +26,9 @@ int check_launch(const char* what) {
   return kOk;
 }
 
+// contraction precision of the dense (MFMA) convolutions: kPrecF32 or kPrecBf16x3
+static int g_conv_precision = MRAGAN_PREC_F32;
+
 static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0; }
 
 static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
@@ -39,7 +42,8 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
     return conv_thin(a, st);
   }
-  IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1};
+  IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
+              g_conv_precision == MRAGAN_PREC_BF16X3};
   return conv_igemm(a, st);
 }
 
@@ -53,6 +57,13 @@ extern "C" {
 
 int mragan_abi_version(void) { return MRAGAN_ABI_VERSION; }
 const char* mragan_last_error(void) { return g_err; }
+
+int mragan_set_conv_precision(int mode) {
+  MRAGAN_CHECK_ARG(mode == MRAGAN_PREC_F32 || mode == MRAGAN_PREC_BF16X3, "set_conv_precision: unknown mode %d", mode);
+  g_conv_precision = mode;
+  return kOk;
+}
+int mragan_get_conv_precision(void) { return g_conv_precision; }
 
 int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
                       int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream) {

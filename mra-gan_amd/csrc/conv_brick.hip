@@ -1,0 +1,347 @@
+// 3×3×3 stride-1 convolution with an LDS-resident input halo ("brick" implicit GEMM), gfx950.
+//
+// Used for the residual-block convolutions (networks3D.py:241-243, 256-257: Conv3d(4ngf,4ngf,k3)
+// on a ReplicationPad3d(1) input, 18 of the 26 dense convs of a ResNet-9 generator) and their
+// data gradients (the transposed form with s = 1 is the forward form with pad k−1−p and the taps
+// flipped).  Together they are ~⅓ of the step's FLOPs.
+//
+// A block owns an output brick of BD×BH×BW voxels (≤ BM GEMM rows) × BN output channels.  For
+// each 32-channel chunk of the contraction it keeps the brick's input halo
+// (BD+2)×(BH+2)×(BW+2) × 32 channels in LDS and runs all 27 taps from it, so every input element
+// is fetched from L2 once per chunk instead of once per tap (8.6× fewer gathers for a 2×8×8
+// brick).  Per K-step (one tap × 32 channels) only the weight tile Wp[tap][n0:n0+BN][c0:c0+32]
+// is staged (prefetch distance 2, register-staged, LDS double buffer); the next chunk's halo is
+// streamed in one float4 per thread per step during taps 1…NH of the current chunk, so no step
+// waits on a whole-halo load.
+//
+// Inner product: X3 = 0 → exact fp32 v_mfma_f32_32x32x2_f32 (K-permuted float4 fragments, as in
+// conv_igemm.hip); X3 = 1 → bf16x3 split (see conv_igemm_x3.hip): LDS rows hold
+// [hi 32 × bf16][lo 32 × bf16], split once when staged.  Both row formats are 144 B (36 dwords:
+// 16 consecutive rows of a ds_read_b128 phase land on distinct bank quads).
+#include "conv_geo.h"
+#include "kernels.h"
+
+namespace mragan {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kBrickBK = 32;          // contraction channels per chunk
+constexpr int kRowBytes = 144;        // one LDS row (both formats)
+constexpr int kTaps = 27;
+
+__device__ __forceinline__ void brick_split4(const float4& v, uint2& hi, uint2& lo) {
+  bf16x2 h0 = __builtin_convertvector((f32x2){v.x, v.y}, bf16x2);
+  bf16x2 h1 = __builtin_convertvector((f32x2){v.z, v.w}, bf16x2);
+  f32x2 f0 = __builtin_convertvector(h0, f32x2);
+  f32x2 f1 = __builtin_convertvector(h1, f32x2);
+  bf16x2 l0 = __builtin_convertvector((f32x2){v.x - f0.x, v.y - f0.y}, bf16x2);
+  bf16x2 l1 = __builtin_convertvector((f32x2){v.z - f1.x, v.w - f1.y}, bf16x2);
+  hi.x = __builtin_bit_cast(uint32_t, h0);
+  hi.y = __builtin_bit_cast(uint32_t, h1);
+  lo.x = __builtin_bit_cast(uint32_t, l0);
+  lo.y = __builtin_bit_cast(uint32_t, l1);
+}
+
+// write float4 #q (channels 4q..4q+3 of the chunk) of one LDS row
+template <int X3>
+__device__ __forceinline__ void row_store(char* row, int q, const float4& v) {
+  if constexpr (X3) {
+    uint2 hi, lo;
+    brick_split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(row + 8 * q) = hi;
+    *reinterpret_cast<uint2*>(row + 64 + 8 * q) = lo;
+  } else {
+    // component-wise (a whole-float4 copy lets the optimizer turn the register set into a
+    // private-memory temporary)
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<f32x4v*>(row + 16 * q) = f32x4v{v.x, v.y, v.z, v.w};
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int X3, int HMAX>
+__global__ void __launch_bounds__(256)
+conv_brick_kernel(BrickArgs a) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int NB = BN * (kBrickBK / 4) / 256;      // weight float4 per thread per step
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(NB >= 1 && BN * (kBrickBK / 4) % 256 == 0, "weight tile / thread mismatch");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* halo_buf = smem;                                   // [2][HMAX][144 B]
+  char* b_buf = smem + 2 * HMAX * kRowBytes;               // [2][BN][144 B]
+  int* out_off = reinterpret_cast<int*>(b_buf + 2 * BN * kRowBytes);   // [BM], then hoff [HMAX]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // tile → (instance, brick, n-block); XCD-aware order (n fastest, then bricks)
+  int L = blockIdx.x, tile = L;
+  if ((a.ntiles & 7) == 0) tile = (L & 7) * (a.ntiles >> 3) + (L >> 3);
+  const int nbk = tile % a.gn;
+  int rest = tile / a.gn;
+  const int bw_i = rest % a.nbw; rest /= a.nbw;
+  const int bh_i = rest % a.nbh; rest /= a.nbh;
+  const int bd_i = rest % a.nbd;
+  const int nb = rest / a.nbd;
+  const int od0 = bd_i * a.BD, oh0 = bh_i * a.BH, ow0 = bw_i * a.BW;
+  const int n0 = nbk * BN;
+  const int HP = a.HD * a.HH * a.HW;
+
+  // output offsets of the brick rows
+  for (int r = tid; r < BM; r += 256) {
+    int off = -1;
+    int bd = r / (a.BH * a.BW), bh = (r / a.BW) % a.BH, bw = r % a.BW;
+    if (bd < a.BD) {
+      int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+    }
+    out_off[r] = off;
+  }
+  // halo row of each fragment row (tap 0)
+  int hrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int r = wm0 + i * 32 + li;
+    int bd = r / (a.BH * a.BW), bh = (r / a.BW) % a.BH, bw = r % a.BW;
+    hrow[i] = bd < a.BD ? (bd * a.HH + bh) * a.HW + bw : 0;
+  }
+
+  const int nchunks = a.C / kBrickBK;
+  const int nK = nchunks * kTaps;
+  const int NH = (HP + 31) / 32;               // steps that stream the next chunk's halo (32 positions each)
+
+  // halo position → element offset inside this instance (or -1: outside the input, zero fill);
+  // computed once, so the pipelined loop does no index arithmetic beyond adds
+  int* hoff = out_off + BM;                    // [HMAX]
+  for (int pos = tid; pos < HP; pos += 256) {
+    int hw = pos % a.HW, hh = (pos / a.HW) % a.HH, hd = pos / (a.HW * a.HH);
+    int id = od0 - a.p + hd, ih = oh0 - a.p + hh, iw = ow0 - a.p + hw;
+    bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+    hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C : -1;
+  }
+  const float* xb = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C;
+  const int q8 = tid & 7, p32 = tid >> 3;        // this thread's quad / position within a 32-position slab
+  int woff[NB];                                  // weight rows of this thread (tap 0, chunk 0)
+#pragma unroll
+  for (int i = 0; i < NB; ++i) woff[i] = (n0 + (tid >> 3) + i * 32) * a.C + 4 * q8;
+  const int tap_stride = a.ny * a.C;
+  __syncthreads();
+
+  // Every load of the pipelined loop is issued unconditionally (clamped offset, result selected
+  // to 0 afterwards): the count of outstanding vector-memory ops per step is static, so the
+  // compiler's s_waitcnt vmcnt(N) drains only the step being stored, never the one just issued.
+  auto halo_load = [&](int chunk, int pos) __attribute__((always_inline)) -> float4 {
+    const int o = pos < HP ? hoff[pos] : -1;
+    const float4 v = *reinterpret_cast<const float4*>(xb + (o < 0 ? 0 : o) + chunk * kBrickBK + 4 * q8);
+    return o < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+  };
+  auto b_load = [&](int chunk, int t, float4 (&rb)[NB]) __attribute__((always_inline)) {
+    const int tap = a.flip ? kTaps - 1 - t : t;
+    const float* wt = a.w + tap * tap_stride + chunk * kBrickBK;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const float4*>(wt + woff[i]);
+  };
+  auto b_store = [&](int buf, const float4 (&rb)[NB]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) row_store<X3>(b_buf + (buf * BN + (tid >> 3) + i * 32) * kRowBytes, q8, rb[i]);
+  };
+
+  // prologue: whole halo of chunk 0 (32 positions per pass); weights of steps 0 and 1; the
+  // halo slab streamed with step 1
+  for (int pos0 = 0; pos0 < HP; pos0 += 32) {
+    const int pos = pos0 + p32;
+    if (pos < HP) row_store<X3>(halo_buf + pos * kRowBytes, q8, halo_load(0, pos));
+  }
+  float4 rb0[NB], rb1[NB];
+  float4 rh0 = make_float4(0.f, 0.f, 0.f, 0.f), rh1;
+  b_load(0, 0, rb0);
+  b_load(nK > 1 ? 1 / kTaps : 0, nK > 1 ? 1 % kTaps : 0, rb1);
+  // streamed slab of step u (chunk c, tap t): taps 1..NH carry positions 32(t−1)… of chunk c+1
+  auto slab_pos = [&](int c, int t) -> int {
+    return (t >= 1 && t <= NH && c + 1 < nchunks) ? (t - 1) * 32 + p32 : HMAX;   // HMAX: none
+  };
+  {
+    const int sp = slab_pos(0, 1);
+    rh1 = halo_load(1 < nchunks ? 1 : 0, sp);
+  }
+  b_store(0, rb0);
+  __syncthreads();
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  // one K-step (chunk c, tap t); `rb_mine/rh_mine` receive step +2, `rb_other/rh_other` hold step +1
+  auto step = [&](int c, int t, float4 (&rb_mine)[NB], float4& rh_mine, const float4 (&rb_other)[NB],
+                  const float4& rh_other) __attribute__((always_inline)) {
+    // (c2, t2) = step + 2, (c1, t1) = step + 1, clamped to the last step
+    int t1 = t + 1, c1 = c;
+    if (t1 == kTaps) { t1 = 0; ++c1; }
+    int t2 = t1 + 1, c2 = c1;
+    if (t2 == kTaps) { t2 = 0; ++c2; }
+    const int cl2 = c2 < nchunks ? c2 : nchunks - 1, tl2 = c2 < nchunks ? t2 : kTaps - 1;
+    b_load(cl2, tl2, rb_mine);
+    {
+      const int sp = c2 < nchunks ? slab_pos(c2, t2) : HMAX;
+      rh_mine = halo_load(c2 + 1 < nchunks ? c2 + 1 : nchunks - 1, sp);
+    }
+    const int tap_row = ((t / 9) * a.HH + (t / 3) % 3) * a.HW + t % 3;
+    const char* H = halo_buf + (c & 1) * HMAX * kRowBytes;
+    const char* Bb = b_buf + ((c * kTaps + t) & 1) * BN * kRowBytes;
+    if constexpr (X3) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const char* row = H + (hrow[i] + tap_row) * kRowBytes + kk * 32 + lh * 16;
+          ah[i] = *reinterpret_cast<const bf16x8*>(row);
+          al[i] = *reinterpret_cast<const bf16x8*>(row + 64);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const char* row = Bb + (wn0 + j * 32 + li) * kRowBytes + kk * 32 + lh * 16;
+          bh[j] = *reinterpret_cast<const bf16x8*>(row);
+          bl[j] = *reinterpret_cast<const bf16x8*>(row + 64);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < kBrickBK / 8; ++kc) {
+        float4 av[TM], bv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[i] = *reinterpret_cast<const float4*>(H + (hrow[i] + tap_row) * kRowBytes + kc * 32 + lh * 16);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[j] = *reinterpret_cast<const float4*>(Bb + (wn0 + j * 32 + li) * kRowBytes + kc * 32 + lh * 16);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+          }
+      }
+    }
+    // drain step +1 (past the last step: a clamped duplicate into the idle buffer, harmless)
+    b_store((c1 * kTaps + t1) & 1, rb_other);
+    {
+      const int sp = c1 < nchunks ? slab_pos(c1, t1) : HMAX;
+      if (sp < HP) row_store<X3>(halo_buf + (((c1 + 1) & 1) * HMAX + sp) * kRowBytes, q8, rh_other);
+    }
+    __syncthreads();
+  };
+
+  // register sets alternate with the step parity (compile-time indices: no scratch)
+  int c = 0, t = 0, ks = 0;
+  for (; ks + 1 < nK; ks += 2) {
+    step(c, t, rb0, rh0, rb1, rh1);
+    if (++t == kTaps) { t = 0; ++c; }
+    step(c, t, rb1, rh1, rb0, rh0);
+    if (++t == kTaps) { t = 0; ++c; }
+  }
+  if (ks < nK) step(c, t, rb0, rh0, rb1, rh1);
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int col = n0 + wn0 + j * 32 + li;
+    if (col >= a.ny) continue;
+    float bsum = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int off = out_off[row];
+        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int X3, int HMAX>
+static int launch_brick(BrickArgs a, hipStream_t st) {
+  constexpr int BN = WN * TN * 32, BM = WM * TM * 32;
+  size_t lds = (size_t)2 * HMAX * kRowBytes + (size_t)2 * BN * kRowBytes + (BM + HMAX) * sizeof(int);
+  auto kern = conv_brick_kernel<WM, WN, TM, TN, X3, HMAX>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.ntiles), dim3(256), lds, st, a);
+  return check_launch("conv_brick");
+}
+
+struct BrickChoice {
+  int bm, bn, bd, bh, bw;
+  int64_t blocks;
+  double cost;
+};
+
+// candidate bricks per GEMM-row budget; the host picks the cheapest (rounds of 256 blocks ×
+// block work, then fewer blocks)
+static BrickChoice choose_brick(int N, int Do, int Ho, int Wo, int ny) {
+  // halos: (bd+2)(bh+2)(bw+2) ≤ 400 for the 128-row shapes, ≤ 300 for the 64-row shapes
+  static const int shapes128[][3] = {{2, 8, 8}, {2, 6, 9}, {3, 6, 6}, {2, 9, 6}, {4, 4, 8}};
+  static const int shapes64[][3] = {{1, 8, 8}, {1, 6, 9}, {1, 9, 6}, {2, 4, 8}};
+  BrickChoice best{0, 0, 0, 0, 0, 0, 1e30};
+  auto consider = [&](int bm, int bn, const int* s) {
+    if (ny % bn != 0) return;
+    int64_t bricks = (int64_t)N * ceil_div(Do, s[0]) * ceil_div(Ho, s[1]) * ceil_div(Wo, s[2]);
+    int64_t blocks = bricks * ceil_div(ny, bn);
+    double rounds = (double)((blocks + 255) / 256);
+    double cost = rounds * bm * bn;
+    if (cost < best.cost * 0.999 || (cost < best.cost * 1.001 && blocks < best.blocks))
+      best = BrickChoice{bm, bn, s[0], s[1], s[2], blocks, cost};
+  };
+  for (auto& s : shapes128) consider(128, 64, s);
+  for (auto& s : shapes64) consider(64, 128, s);
+  for (auto& s : shapes64) consider(64, 64, s);
+  return best;
+}
+
+bool conv_brick_applicable(const IgemmArgs& a) {
+  return a.k == 3 && a.s == 1 && a.cx % kBrickBK == 0 && a.ny % 64 == 0 && a.Di > 0;
+}
+
+int conv_brick(const IgemmArgs& g, hipStream_t st) {
+  BrickArgs a{};
+  a.x = g.x; a.N = g.N; a.Di = g.Di; a.Hi = g.Hi; a.Wi = g.Wi; a.C = g.cx;
+  a.w = g.w; a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
+  a.act = g.act;
+  // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
+  a.flip = g.trans ? 1 : 0;
+  a.p = g.trans ? g.k - 1 - g.p : g.p;
+  BrickChoice c = choose_brick(g.N, g.Do, g.Ho, g.Wo, g.ny);
+  a.BD = c.bd; a.BH = c.bh; a.BW = c.bw;
+  a.HD = c.bd + 2; a.HH = c.bh + 2; a.HW = c.bw + 2;
+  a.nbd = ceil_div(g.Do, c.bd); a.nbh = ceil_div(g.Ho, c.bh); a.nbw = ceil_div(g.Wo, c.bw);
+  a.gn = ceil_div(g.ny, c.bn);
+  a.ntiles = (int)c.blocks;
+  if (a.ntiles == 0) return kOk;
+  const bool x3 = g.x3 != 0;
+  if (c.bm == 128) return x3 ? launch_brick<2, 2, 2, 1, 1, 400>(a, st) : launch_brick<2, 2, 2, 1, 0, 400>(a, st);
+  if (c.bn == 128) return x3 ? launch_brick<2, 2, 1, 2, 1, 300>(a, st) : launch_brick<2, 2, 1, 2, 0, 300>(a, st);
+  return x3 ? launch_brick<2, 2, 1, 1, 1, 300>(a, st) : launch_brick<2, 2, 1, 1, 0, 300>(a, st);
+}
+
+}  // namespace mragan

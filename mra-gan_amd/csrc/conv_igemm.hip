@@ -19,39 +19,14 @@
 // MFMA K-order: lane half h supplies k = 4h+s at step s, so each lane reads ONE float4 of
 // A and of B per 8-deep chunk and feeds 4 MFMAs from it.
 #include "kernels.h"
+#include "conv_geo.h"
+
+#include <cstdlib>
 
 namespace mragan {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-
-// per-dimension class geometry
-struct DimGeo {
-  int Q;       // number of output positions in the class along this dim
-  int ntap;    // taps visited along this dim
-  int t0, tstep;
-  int a_mul;   // in = a_mul*q + base_add + sign*j
-  int base_add;
-  int sign;
-  int o_mul, o_add;   // output coordinate = o_mul*q + o_add
-};
-
-__device__ __forceinline__ DimGeo dim_geo(int c, int O, int k, int s, int p, int trans) {
-  DimGeo g;
-  if (!trans) {
-    g.Q = O; g.ntap = k; g.t0 = 0; g.tstep = 1;
-    g.a_mul = s; g.base_add = -p; g.sign = 1;
-    g.o_mul = 1; g.o_add = 0;
-  } else {
-    g.Q = (O - c + s - 1) / s;
-    int t0 = (c + p) % s;
-    g.t0 = t0; g.tstep = s;
-    g.ntap = (t0 < k) ? (k - t0 + s - 1) / s : 0;
-    g.a_mul = 1; g.base_add = (c + p - t0) / s; g.sign = -1;
-    g.o_mul = s; g.o_add = c;
-  }
-  return g;
-}
 
 template <int WM, int WN, int TM, int TN, int BK>
 __global__ void __launch_bounds__(256)
@@ -265,6 +240,9 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   int64_t max_mc = (int64_t)a.N * q(a.Do, 0) * q(a.Ho, 0) * q(a.Wo, 0);
   int64_t total_m = (int64_t)a.N * a.Do * a.Ho * a.Wo;
   if (max_mc == 0 || a.ny == 0) return kOk;
+  static const bool brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
+  if (!brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+  if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3(a, max_mc, total_m, st);
   if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);
   if (a.cx % 16 == 0) return dispatch_tile<16>(a, max_mc, total_m, st);
   return dispatch_tile<8>(a, max_mc, total_m, st);

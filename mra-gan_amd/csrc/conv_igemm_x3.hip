@@ -1,0 +1,277 @@
+// Implicit-GEMM 3D convolution on gfx950 bf16 MFMA with a three-term fp32 split ("bf16x3").
+//
+// Same GEMM view, geometry and epilogue as conv_igemm.hip (forward form, transposed form per
+// output parity class); only the inner product differs.  Every fp32 operand x is split once,
+// when its tile is staged into LDS, into x = hi + lo + r with hi = bf16(x), lo = bf16(x − hi)
+// (x − hi is exact in fp32, |r| ≤ 2⁻¹⁸|x|), and
+//
+//     a·b ≈ lo_a·hi_b + hi_a·lo_b + hi_a·hi_b
+//
+// is accumulated in fp32 by three v_mfma_f32_32x32x16_bf16 (the dropped lo·lo term and the
+// residuals are ≤ 3·2⁻¹⁸ of |a·b|; bf16×bf16 products are exact in the fp32 accumulator).
+// Three bf16 MFMAs cost 96 cycles per 32×32×16 block versus 512 for eight f32 32x32x2 MFMAs,
+// so the contraction runs at up to 5.3× the exact-f32 MFMA rate.  Error measured against fp64
+// is of the same order as fp32 accumulation over the K = 27·Cin taps (tests/test_kernels_gpu.py).
+//
+// LDS: hi and lo planes of the A tile [BM][BK] and B tile [BN][BK] in bf16, rows padded by
+// 16 B (BK = 32 → 80-B rows, BK = 16 → 48-B rows: the 16 lanes of each ds_read_b128 phase hit
+// disjoint bank quads); register-staged double buffer, one barrier per K-step.  Fragment of
+// lane l for k-slice kk: row l&31, k = 16kk + 8(l>>5) … +7 — one ds_read_b128 per plane.
+// Grid: 1-D, XCD-aware — consecutive tiles (the n-blocks sharing an A row-block, then the
+// neighbouring row-blocks sharing input halo) are placed on the same XCD's L2.
+#include "conv_geo.h"
+#include "kernels.h"
+
+namespace mragan {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// split 4 floats into bf16 hi / lo quads (packed as 2 dwords each)
+__device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
+  bf16x2 h0 = __builtin_convertvector((f32x2){v.x, v.y}, bf16x2);
+  bf16x2 h1 = __builtin_convertvector((f32x2){v.z, v.w}, bf16x2);
+  f32x2 f0 = __builtin_convertvector(h0, f32x2);
+  f32x2 f1 = __builtin_convertvector(h1, f32x2);
+  bf16x2 l0 = __builtin_convertvector((f32x2){v.x - f0.x, v.y - f0.y}, bf16x2);
+  bf16x2 l1 = __builtin_convertvector((f32x2){v.z - f1.x, v.w - f1.y}, bf16x2);
+  hi.x = __builtin_bit_cast(uint32_t, h0);
+  hi.y = __builtin_bit_cast(uint32_t, h1);
+  lo.x = __builtin_bit_cast(uint32_t, l0);
+  lo.y = __builtin_bit_cast(uint32_t, l1);
+}
+
+template <int WM, int WN, int TM, int TN, int BK>
+__global__ void __launch_bounds__(256)
+conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int LDK = BK + 8;               // bf16 per padded row
+  constexpr int LPR = BK / 4;               // float4 per row (global side)
+  constexpr int A_LOADS = (BM * LPR + 255) / 256;
+  constexpr int B_LOADS = (BN * LPR + 255) / 256;
+  constexpr int ROWS_PER_PASS = 256 / LPR;
+  constexpr int PLANE_A = BM * LDK, PLANE_B = BN * LDK;   // bf16 elements per plane
+  constexpr int STAGE = 2 * (PLANE_A + PLANE_B);          // hi+lo of A and B
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(BK % 16 == 0, "bf16 MFMA consumes K in 16s");
+
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  __shared__ int out_off[BM];
+
+  // XCD-aware tile order: hardware puts block L on XCD L % 8; give each XCD a contiguous range
+  int L = blockIdx.x, tile = L;
+  if ((ntiles & 7) == 0) tile = (L & 7) * (ntiles >> 3) + (L >> 3);
+  const int nb_idx = tile % gn;
+  int rest = tile / gn;
+  const int mb_idx = rest % gm;
+  const int cls = rest / gm;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM * 32;
+  const int wn0 = (wave % WN) * TN * 32;
+
+  int cw = cls % a.s, ch = (cls / a.s) % a.s, cd = cls / (a.s * a.s);
+  if (a.nclass == 1) { cd = ch = cw = 0; }
+  const DimGeo gd = dim_geo(cd, a.Do, a.k, a.s, a.p, a.trans);
+  const DimGeo gh = dim_geo(ch, a.Ho, a.k, a.s, a.p, a.trans);
+  const DimGeo gw = dim_geo(cw, a.Wo, a.k, a.s, a.p, a.trans);
+  const int64_t Mc = (int64_t)a.N * gd.Q * gh.Q * gw.Q;
+  const int64_t m0 = (int64_t)mb_idx * BM;
+  const int n0 = nb_idx * BN;
+  if (m0 >= Mc) return;
+  const int ntaps = gd.ntap * gh.ntap * gw.ntap;
+
+  for (int r = tid; r < BM; r += 256) {
+    int64_t m = m0 + r;
+    int off = -1;
+    if (m < Mc) {
+      int qw = (int)(m % gw.Q); int64_t t = m / gw.Q;
+      int qh = (int)(t % gh.Q); t /= gh.Q;
+      int qd = (int)(t % gd.Q); int nb = (int)(t / gd.Q);
+      int od = gd.o_mul * qd + gd.o_add, oh = gh.o_mul * qh + gh.o_add, ow = gw.o_mul * qw + gw.o_add;
+      off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+    }
+    out_off[r] = off;
+  }
+
+  const int q = tid % LPR;
+  int a_nb[A_LOADS], a_bd[A_LOADS], a_bh[A_LOADS], a_bw[A_LOADS];
+#pragma unroll
+  for (int i = 0; i < A_LOADS; ++i) {
+    int r = tid / LPR + i * ROWS_PER_PASS;
+    int64_t m = m0 + r;
+    if (r < BM && m < Mc) {
+      int qw = (int)(m % gw.Q); int64_t t = m / gw.Q;
+      int qh = (int)(t % gh.Q); t /= gh.Q;
+      int qd = (int)(t % gd.Q); int nb = (int)(t / gd.Q);
+      a_nb[i] = nb;
+      a_bd[i] = gd.a_mul * qd + gd.base_add;
+      a_bh[i] = gh.a_mul * qh + gh.base_add;
+      a_bw[i] = gw.a_mul * qw + gw.base_add;
+    } else {
+      a_nb[i] = -1; a_bd[i] = a_bh[i] = a_bw[i] = 0;
+    }
+  }
+
+  const int kchunks = a.cx / BK;
+  const int nK = ntaps * kchunks;
+  float4 ra[A_LOADS], rb[B_LOADS];
+
+  auto load_tiles = [&](int ks) {
+    int tap = ks / kchunks;
+    int c0 = (ks - tap * kchunks) * BK;
+    int jw = tap % gw.ntap; int tt = tap / gw.ntap;
+    int jh = tt % gh.ntap; int jd = tt / gh.ntap;
+    int td = gd.t0 + gd.tstep * jd, th = gh.t0 + gh.tstep * jh, tw = gw.t0 + gw.tstep * jw;
+    int wt = (td * a.k + th) * a.k + tw;
+    int dd = gd.sign * jd, dh = gh.sign * jh, dw = gw.sign * jw;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
+      bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
+                (unsigned)iw < (unsigned)a.Wi;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        const float* src = a.x + ((((int64_t)a_nb[i] * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 + 4 * q;
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      int n = n0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < BN && n < a.ny)
+        v = *reinterpret_cast<const float4*>(a.w + ((int64_t)wt * a.ny + n) * a.cx + c0 + 4 * q);
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    __bf16* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      if (r < BM) {
+        uint2 hi, lo;
+        split4(ra[i], hi, lo);
+        *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
+        *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      int r = tid / LPR + i * ROWS_PER_PASS;
+      if (r < BN) {
+        uint2 hi, lo;
+        split4(rb[i], hi, lo);
+        *reinterpret_cast<uint2*>(st + 2 * PLANE_A + r * LDK + 4 * q) = hi;
+        *reinterpret_cast<uint2*>(st + 2 * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  if (nK > 0) {
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
+
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nK) load_tiles(ks + 1);
+    const __bf16* Ah = smem + buf * STAGE;
+    const __bf16* Al = Ah + PLANE_A;
+    const __bf16* Bh = Ah + 2 * PLANE_A;
+    const __bf16* Bl = Bh + PLANE_B;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int o = (wm0 + i * 32 + li) * LDK + kk * 16 + 8 * lh;
+        ah[i] = *reinterpret_cast<const bf16x8*>(Ah + o);
+        al[i] = *reinterpret_cast<const bf16x8*>(Al + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int o = (wn0 + j * 32 + li) * LDK + kk * 16 + 8 * lh;
+        bh[j] = *reinterpret_cast<const bf16x8*>(Bh + o);
+        bl[j] = *reinterpret_cast<const bf16x8*>(Bl + o);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (ks + 1 < nK) store_tiles(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int col = n0 + wn0 + j * 32 + li;
+    if (col >= a.ny) continue;
+    float bsum = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int off = out_off[row];
+        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int BK>
+static int launch_x3(const IgemmArgs& a, int64_t max_mc, hipStream_t st) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
+  int ntiles = gm * gn * a.nclass;
+  hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK>), dim3(ntiles), dim3(256), 0, st, a, gm, gn, ntiles);
+  return check_launch("conv_igemm_x3");
+}
+
+template <int BK>
+static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  // largest tile that still gives one block per CU (256 CUs), else the smallest
+  auto blocks = [&](int bm, int bn) { return (int64_t)ceil_div(total_m, bm) * ceil_div(a.ny, bn); };
+  if (a.ny > 64) {
+    if (blocks(128, 128) >= 256) return launch_x3<2, 2, 2, 2, BK>(a, max_mc, st);
+    if (blocks(128, 64) >= 256) return launch_x3<2, 2, 2, 1, BK>(a, max_mc, st);
+    return launch_x3<2, 2, 1, 1, BK>(a, max_mc, st);
+  }
+  if (a.ny > 32) {
+    if (blocks(128, 64) >= 256) return launch_x3<2, 2, 2, 1, BK>(a, max_mc, st);
+    return launch_x3<2, 2, 1, 1, BK>(a, max_mc, st);
+  }
+  if (blocks(256, 32) >= 256) return launch_x3<4, 1, 2, 1, BK>(a, max_mc, st);
+  return launch_x3<4, 1, 1, 1, BK>(a, max_mc, st);
+}
+
+int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  if (a.cx % 32 == 0) return dispatch_x3<32>(a, max_mc, total_m, st);
+  return dispatch_x3<16>(a, max_mc, total_m, st);
+}
+
+}  // namespace mragan

@@ -15,13 +15,15 @@ namespace mragan {
 constexpr float kInEps = 1e-5f;
 
 
+// voxel chunks per instance: ≈2048 blocks per launch, but ≥ 4 voxel rows per thread
 static int in_chunks(const InShape& s) {
-  int64_t S = s.S();
-  int want = (1024 + s.N - 1) / s.N;
-  int64_t max_chunks = (S + 255) / 256;
-  if (want > max_chunks) want = (int)max_chunks;
+  const int CQ = s.C / 4;
+  const int R = CQ >= 256 ? 1 : 256 / CQ;
+  int64_t want = (2048 + s.N - 1) / s.N;
+  int64_t cap = s.S() / (4 * R);
+  if (want > cap) want = cap;
   if (want < 1) want = 1;
-  return want;
+  return (int)want;
 }
 
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
@@ -71,16 +73,37 @@ __global__ void __launch_bounds__(256) in_stats_kernel(const float* __restrict__
   }
 }
 
-__global__ void in_finalize_kernel(const double* __restrict__ part, InShape s, int chunks, float* __restrict__ mean,
-                                   float* __restrict__ rstd) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= s.N * s.C) return;
-  const int n = i / s.C, c = i % s.C;
-  double a = 0, b = 0;
-  for (int k = 0; k < chunks; ++k) {
-    const double* p = part + (((int64_t)n * chunks + k) * s.C + c) * 2;
-    a += p[0]; b += p[1];
+// Σ over chunks of partials[n][chunk][C][2], fixed order (deterministic).  Block: 64-channel
+// group × (256/CW) chunk rows; grid (ceil(C/64), N).  mode 0: mean/rstd, mode 1: bwd coefficients.
+__device__ __forceinline__ void in_reduce_chunks(const double* __restrict__ part, const InShape& s, int chunks,
+                                                 double& a, double& b, int& c, bool& valid) {
+  __shared__ double red[2][256];
+  const int CW = s.C < 64 ? s.C : 64;
+  const int rows = 256 / CW;
+  const int tid = threadIdx.x, cl = tid % CW, row = tid / CW;
+  const int n = blockIdx.y;
+  c = blockIdx.x * 64 + cl;
+  double sa = 0, sb = 0;
+  if (row < rows && c < s.C) {
+    for (int k = row; k < chunks; k += rows) {
+      const double* p = part + (((int64_t)n * chunks + k) * s.C + c) * 2;
+      sa += p[0]; sb += p[1];
+    }
   }
+  red[0][tid] = sa; red[1][tid] = sb;
+  __syncthreads();
+  valid = row == 0 && c < s.C;
+  a = 0; b = 0;
+  if (valid)
+    for (int r = 0; r < rows; ++r) { a += red[0][r * CW + cl]; b += red[1][r * CW + cl]; }
+}
+
+__global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
+                                                          float* __restrict__ mean, float* __restrict__ rstd) {
+  double a, b; int c; bool valid;
+  in_reduce_chunks(part, s, chunks, a, b, c, valid);
+  if (!valid) return;
+  const int i = blockIdx.y * s.C + c;
   const double S = (double)s.S();
   const double mu = a / S;
   double var = b / S - mu * mu;
@@ -183,15 +206,12 @@ __global__ void __launch_bounds__(256) in_bwd_stats_kernel(InBwdArgs a, InShape 
   }
 }
 
-__global__ void in_bwd_finalize_kernel(double* __restrict__ part, InShape s, int chunks, float* __restrict__ coef) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= s.N * s.C) return;
-  const int n = i / s.C, c = i % s.C;
-  double a = 0, b = 0;
-  for (int k = 0; k < chunks; ++k) {
-    const double* p = part + (((int64_t)n * chunks + k) * s.C + c) * 2;
-    a += p[0]; b += p[1];
-  }
+__global__ void __launch_bounds__(256) in_bwd_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
+                                                              float* __restrict__ coef) {
+  double a, b; int c; bool valid;
+  in_reduce_chunks(part, s, chunks, a, b, c, valid);
+  if (!valid) return;
+  const int i = blockIdx.y * s.C + c;
   const double S = (double)s.S();
   coef[2 * i] = (float)(a / S);
   coef[2 * i + 1] = (float)(b / S);
@@ -273,7 +293,7 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, x, s, chunks, part);
   int rc = check_launch("in_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div((int64_t)s.N * s.C, 256)), dim3(256), 0, st, part, s, chunks, mean, rstd);
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 64), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
   if ((rc = check_launch("in_finalize"))) return rc;
   const int64_t total = (int64_t)s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad) * (s.W + 2 * ypad) * (s.C / 4);
   hipLaunchKernelGGL(in_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad);
@@ -290,7 +310,7 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, a, s, chunks, part);
   int rc = check_launch("in_bwd_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div((int64_t)s.N * s.C, 256)), dim3(256), 0, st, part, s, chunks, coef);
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 64), s.N), dim3(256), 0, st, part, s, chunks, coef);
   if ((rc = check_launch("in_bwd_finalize"))) return rc;
   const int64_t total = (int64_t)s.N * s.S() * (s.C / 4);
   hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, a, s, coef);

@@ -15,8 +15,24 @@ struct IgemmArgs {
   int trans;
   int act;
   int nclass;       // set by conv_igemm: 1 (forward or s==1) or s³
+  int x3;           // 1: bf16x3 split MFMA (conv_igemm_x3.hip), 0: exact f32 MFMA
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
+int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st);
+
+// k3 s1 convolutions with an LDS-resident input halo (conv_brick.hip)
+struct BrickArgs {
+  const float* x; int N, Di, Hi, Wi, C;
+  const float* w;   // packed [27][ny][C]
+  const float* bias;
+  float* y; int Do, Ho, Wo, ny;
+  int p, flip, act;
+  int BD, BH, BW;   // output brick
+  int HD, HH, HW;   // its input halo
+  int nbd, nbh, nbw, gn, ntiles;
+};
+bool conv_brick_applicable(const IgemmArgs& a);
+int conv_brick(const IgemmArgs& a, hipStream_t st);
 
 struct ThinArgs {
   const float* x; int N, Di, Hi, Wi, cx;

@@ -27,6 +27,8 @@ sz = C.c_size_t
 SIGNATURES = {
     "mragan_abi_version": (i32, []),
     "mragan_last_error": (C.c_char_p, []),
+    "mragan_set_conv_precision": (i32, [i32]),
+    "mragan_get_conv_precision": (i32, []),
     "mragan_conv3d_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
     "mragan_conv3d_transposed": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
     "mragan_conv3d_wgrad_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),

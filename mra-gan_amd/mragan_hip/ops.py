@@ -83,6 +83,23 @@ class KernelTimer:
 TIMER = KernelTimer()
 
 
+PRECISION = {"f32": 0, "bf16x3": 1}
+
+
+def set_conv_precision(mode: str) -> None:
+    """Contraction precision of the dense MFMA convolutions ('f32' exact, 'bf16x3' split);
+    see include/mragan_hip.h.  Process-wide."""
+    if mode not in PRECISION:
+        raise ValueError(f"conv precision must be one of {sorted(PRECISION)}, got {mode!r}")
+    call("mragan_set_conv_precision", PRECISION[mode])
+
+
+def get_conv_precision() -> str:
+    from ._lib import lib
+    code = lib().mragan_get_conv_precision()
+    return {v: k for k, v in PRECISION.items()}[code]
+
+
 def conv_out_size(n: int, k: int, s: int, p: int) -> int:
     return (n + 2 * p - k) // s + 1
 

@@ -44,6 +44,9 @@ BASE_FLAGS = [
     ('--init_gain', dict(type=float, default=0.02, help='scaling factor for normal, xavier and orthogonal.')),
     ('--verbose', dict(action='store_true', help='if specified, print more debugging information')),
     ('--suffix', dict(default='', type=str, help='customized suffix: opt.name = opt.name + suffix')),
+    # engine-only flag (not in the reference): contraction precision of the dense MFMA convolutions
+    ('--conv_precision', dict(type=str, default='f32', choices=['f32', 'bf16x3'],
+                              help='f32: exact fp32 MFMA; bf16x3: split-bf16 MFMA with fp32 accumulation')),
 ]
 
 

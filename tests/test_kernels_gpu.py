@@ -54,6 +54,7 @@ CONV_CASES = [
     (1, 8, 16, 9, 3, 2, 1),
     (3, 16, 24, 7, 3, 1, 1),
     (1, 24, 40, 6, 4, 2, 1),
+    (2, 64, 128, 13, 3, 1, 1),      # k3 s1 halo-brick path (conv_brick.hip), zero pad, 2 chunks
     # thin paths
     (2, 1, 32, 14, 7, 1, 0),
     (1, 2, 32, 12, 7, 1, 0),
@@ -145,6 +146,68 @@ def test_conv_transpose3d_fwd_dgrad_wgrad(ops, N, cin, cout, S, k, s, p, op):
     dw = torch.empty(cin, cout, k, k, k, device="cuda")
     ops.conv3d_wgrad(xg, ndhwc(dy.float()).cuda(), k, s, p, dw, accumulate=False)
     assert rel(dw, dw_ref) < TOL
+
+
+X3_TOL = 2e-5     # bf16x3: ≤ 3·2⁻¹⁸ relative per product, random → ~5e-6 rel-L2 measured scale
+
+X3_CASES = [
+    # N, cin, cout, S, k, s, p   (every tile shape of conv_igemm_x3.hip's dispatch)
+    (2, 128, 128, 6, 3, 1, 0),
+    (8, 128, 128, 18, 3, 1, 0),     # 128x128 tiles
+    (4, 128, 128, 16, 3, 1, 0),     # 128x64 tiles
+    (2, 32, 64, 12, 3, 2, 1),
+    (4, 64, 128, 16, 3, 2, 1),
+    (2, 128, 256, 5, 4, 1, 1),
+    (3, 16, 24, 7, 3, 1, 1),        # BK = 16
+    (2, 64, 32, 20, 4, 2, 1),       # ny = 32 tiles
+]
+
+
+@pytest.fixture
+def x3(ops):
+    ops.set_conv_precision("bf16x3")
+    assert ops.get_conv_precision() == "bf16x3"
+    yield ops
+    ops.set_conv_precision("f32")
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES)
+def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
+    ops = x3
+    g = torch.Generator().manual_seed(5 + N * 100 + cin + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    y = F.conv3d(x, w, b, stride=s, padding=p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    out = ops.conv3d(ndhwc(x.detach().float()).cuda(), pack(ops, w, False, False), cout, k, s, p, y.shape[2:],
+                     bias=b.float().cuda(), act="lrelu")
+    assert rel(ncdhw(out), F.leaky_relu(y.detach(), 0.2)) < X3_TOL
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w, False, True), cin, k, s, p, x.shape[2:], transposed=True)
+    assert rel(ncdhw(dx), dx_ref) < X3_TOL
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
+def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
+    ops = x3
+    g = torch.Generator().manual_seed(N + cin + 3 * cout)
+    x = torch.randn(N, cin, S, S + 1, S, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=op)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    out = ops.conv3d(ndhwc(x.detach().float()).cuda(), pack(ops, w, True, False), cout, k, s, p, y.shape[2:],
+                     transposed=True)
+    assert rel(ncdhw(out), y.detach()) < X3_TOL
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w, True, True), cin, k, s, p, x.shape[2:])
+    assert rel(ncdhw(dx), dx_ref) < X3_TOL
+
+
+def test_conv_precision_modes(ops):
+    assert ops.get_conv_precision() == "f32"
+    with pytest.raises(ValueError):
+        ops.set_conv_precision("fp8")
 
 
 def _in_ref(x, act):

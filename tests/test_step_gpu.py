@@ -23,12 +23,12 @@ pytestmark = pytest.mark.gpu
 CASES = list(CASE_KW)
 
 
-def build_model(meta, ckdir):
+def build_model(meta, ckdir, precision="f32"):
     from models import create_model
     from options.train_options import TrainOptions
     argv = sys.argv
     try:
-        sys.argv = ["train.py", "--checkpoints_dir", str(ckdir)] + meta["argv"].split()
+        sys.argv = ["train.py", "--checkpoints_dir", str(ckdir), "--conv_precision", precision] + meta["argv"].split()
         opt = TrainOptions().gather_options()
     finally:
         sys.argv = argv
@@ -41,13 +41,17 @@ def build_model(meta, ckdir):
     return model
 
 
-@pytest.fixture(scope="module", params=CASES)
+# every case in both contraction precisions of the dense convolutions (include/mragan_hip.h)
+PARAMS = [(c, p) for p in ("f32", "bf16x3") for c in CASES]
+
+
+@pytest.fixture(scope="module", params=PARAMS, ids=[f"{c}-{p}" for c, p in PARAMS])
 def stepped(request, tmp_path_factory):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    name = request.param
+    name, precision = request.param
     z, meta = load(name)
-    model = build_model(meta, tmp_path_factory.mktemp(name))
+    model = build_model(meta, tmp_path_factory.mktemp(name), precision)
     init = {}
     for net in ("G_A", "G_B", "D_A", "D_B"):
         for k, v in getattr(model, "net" + net).state_dict().items():
@@ -71,6 +75,8 @@ def stepped(request, tmp_path_factory):
                           if "running" in k} for n in ("G_A", "G_B", "D_A", "D_B")},
             )
     torch.cuda.synchronize()
+    from mragan_hip import ops
+    ops.set_conv_precision("f32")
     return name, z, meta, init, history, snap
 
 

@@ -24,7 +24,9 @@ def main():
     ap.add_argument("--S", type=int, default=64)
     ap.add_argument("--N", type=int, default=4)
     ap.add_argument("--ngf", type=int, default=32)
+    ap.add_argument("--precision", default="f32")
     args = ap.parse_args()
+    ops.set_conv_precision(args.precision)
     S, N, ngf = args.S, args.N, args.ngf
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
