@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--ngf", type=int, default=32)
     ap.add_argument("--netG", default="resnet_9blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="f32", choices=["f32", "bf16x3"],
+    ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3"],
                     help="dense-conv contraction: exact f32 MFMA or split-bf16 (bf16x3) MFMA, fp32 accumulate")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
@@ -237,7 +237,7 @@ def main():
     # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic (fp32) FLOPs is
     # the bf16 dense peak / 3
     peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
-    kname = "conv_igemm_x3 (bf16x3 split MFMA)" if x3 else "conv_igemm_f32"
+    kname = "conv_brick_kernel (LDS-halo implicit GEMM, " + ("bf16x3 split MFMA)" if x3 else "f32 MFMA)")
     traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",

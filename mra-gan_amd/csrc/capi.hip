@@ -92,7 +92,8 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
     a.G = gathered; a.Dg = Dg; a.Hg = Hg; a.Wg = Wg; a.Cg = Cg; a.k = k; a.s = stride; a.p = pad;
     return conv_thin_wgrad(a, dw, accumulate, static_cast<float*>(ws), ws_bytes, st);
   }
-  WgradArgs a{dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0};
+  WgradArgs a{dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0,
+              g_conv_precision == MRAGAN_PREC_BF16X3};
   return conv_wgrad(a, dw, accumulate, ws_bytes, st);
 }
 

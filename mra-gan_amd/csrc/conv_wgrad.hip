@@ -135,6 +135,170 @@ conv_wgrad_f32_kernel(WgradArgs a) {
   }
 }
 
+// ---- bf16x3 variant ------------------------------------------------------------------------
+// Same split-K structure; the contraction (voxels) becomes the MFMA K.  Tiles are staged
+// TRANSPOSED into LDS, one row per channel holding 32 voxels as [hi 32 × bf16][lo 32 × bf16]
+// (144-B rows, the brick/igemm_x3 format), so the 32x32x16 fragments are plain ds_read_b128.
+// Staging unit = 4 voxels × 4 channels per thread: lanes run over voxel quads first, so the
+// 16 lanes of a ds_write_b64 group cover two rows 4 apart (144 dwords ≡ 16 mod 32 banks) and
+// 8 consecutive 8-byte slots: conflict-free.  Every load is unconditional (clamped address,
+// selected to 0) so vmcnt stays static across the register-staged double buffer.
+typedef float f32x2w __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2w __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4w __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef float f32x4w __attribute__((ext_vector_type(4)));
+constexpr int kWRow = 144;
+
+// hi/lo of 4 voxel values of one channel → two 8-byte quads
+__device__ __forceinline__ void wsplit4(float a, float b, float c, float d, uint2& hi, uint2& lo) {
+  bf16x2w h0 = __builtin_convertvector((f32x2w){a, b}, bf16x2w);
+  bf16x2w h1 = __builtin_convertvector((f32x2w){c, d}, bf16x2w);
+  f32x2w f0 = __builtin_convertvector(h0, f32x2w);
+  f32x2w f1 = __builtin_convertvector(h1, f32x2w);
+  bf16x2w l0 = __builtin_convertvector((f32x2w){a - f0.x, b - f0.y}, bf16x2w);
+  bf16x2w l1 = __builtin_convertvector((f32x2w){c - f1.x, d - f1.y}, bf16x2w);
+  hi.x = __builtin_bit_cast(uint32_t, h0); hi.y = __builtin_bit_cast(uint32_t, h1);
+  lo.x = __builtin_bit_cast(uint32_t, l0); lo.y = __builtin_bit_cast(uint32_t, l1);
+}
+
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(256)
+conv_wgrad_x3_kernel(WgradArgs a) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int BKm = 32;
+  constexpr int UD = BM / 4 * 8, UG = BN / 4 * 8;          // staging units (4 voxels × 4 channels)
+  static_assert(UD <= 256 && UG <= 256, "one unit per thread");
+  constexpr int STAGE = (BM + BN) * kWRow;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (a.Cg + BN - 1) / BN;
+  const int dn0 = (blockIdx.x / ntn) * BM, gn0 = (blockIdx.x % ntn) * BN;
+  const int t = blockIdx.y;
+  const int tw = t % a.k, th = (t / a.k) % a.k, td = t / (a.k * a.k);
+  const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
+  const int64_t mb = (int64_t)blockIdx.z * a.chunk;
+  const int64_t me = min(M, mb + a.chunk);
+  const int nK = (int)((me - mb + BKm - 1) / BKm);
+
+  // this thread's staging unit: voxel quad vq (4 voxels), channel quad cq
+  const int vq = tid & 7, cq = tid >> 3;
+  const bool do_d = tid < UD, do_g = tid < UG;
+  const int cd = dn0 + 4 * (do_d ? cq : 0), cg = gn0 + 4 * (do_g ? cq : 0);
+  const bool cd_ok = do_d && cd < a.Cd, cg_ok = do_g && cg < a.Cg;
+
+  float4 rd[4], rg[4];
+  auto load = [&](int ks) __attribute__((always_inline)) {
+    const int64_t m_base = mb + (int64_t)ks * BKm + 4 * vq;
+    // voxel coordinates of m_base, then +1 with carry for the next three
+    int64_t mm = m_base < M ? m_base : M - 1;
+    int mw = (int)(mm % a.Wd); int64_t u = mm / a.Wd;
+    int mh = (int)(u % a.Hd); u /= a.Hd;
+    int md = (int)(u % a.Dd); int nb = (int)(u / a.Dd);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t m = m_base + s;
+      const bool m_ok = m < me;
+      const float4 dv = *reinterpret_cast<const float4*>(a.D + (m_ok ? m : mb) * a.Cd + (cd_ok ? cd : 0));
+      rd[s] = (m_ok && cd_ok) ? dv : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int gd = md * a.s - a.p + td, gh = mh * a.s - a.p + th, gw = mw * a.s - a.p + tw;
+      const bool g_in = m_ok && cg_ok && (unsigned)gd < (unsigned)a.Dg && (unsigned)gh < (unsigned)a.Hg &&
+                        (unsigned)gw < (unsigned)a.Wg;
+      const int64_t goff = g_in ? ((((int64_t)nb * a.Dg + gd) * a.Hg + gh) * a.Wg + gw) * a.Cg + cg : 0;
+      const float4 gv = *reinterpret_cast<const float4*>(a.G + goff);
+      rg[s] = g_in ? gv : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (++mw == a.Wd) { mw = 0; if (++mh == a.Hd) { mh = 0; if (++md == a.Dd) { md = 0; ++nb; } } }
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    char* A = smem + buf * STAGE;
+    char* B = A + BM * kWRow;
+    uint2 hi, lo;
+    if (do_d) {
+      const int r = 4 * cq;
+      wsplit4(rd[0].x, rd[1].x, rd[2].x, rd[3].x, hi, lo);
+      *reinterpret_cast<uint2*>(A + (r + 0) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 0) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rd[0].y, rd[1].y, rd[2].y, rd[3].y, hi, lo);
+      *reinterpret_cast<uint2*>(A + (r + 1) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 1) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rd[0].z, rd[1].z, rd[2].z, rd[3].z, hi, lo);
+      *reinterpret_cast<uint2*>(A + (r + 2) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 2) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rd[0].w, rd[1].w, rd[2].w, rd[3].w, hi, lo);
+      *reinterpret_cast<uint2*>(A + (r + 3) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 3) * kWRow + 64 + 8 * vq) = lo;
+    }
+    if (do_g) {
+      const int r = 4 * cq;
+      wsplit4(rg[0].x, rg[1].x, rg[2].x, rg[3].x, hi, lo);
+      *reinterpret_cast<uint2*>(B + (r + 0) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 0) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rg[0].y, rg[1].y, rg[2].y, rg[3].y, hi, lo);
+      *reinterpret_cast<uint2*>(B + (r + 1) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 1) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rg[0].z, rg[1].z, rg[2].z, rg[3].z, hi, lo);
+      *reinterpret_cast<uint2*>(B + (r + 2) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 2) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4(rg[0].w, rg[1].w, rg[2].w, rg[3].w, hi, lo);
+      *reinterpret_cast<uint2*>(B + (r + 3) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 3) * kWRow + 64 + 8 * vq) = lo;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    load(ks + 1 < nK ? ks + 1 : ks);          // unconditional (last step reloads itself, unused)
+    const char* A = smem + buf * STAGE;
+    const char* B = A + BM * kWRow;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8w ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const char* row = A + (wm0 + i * 32 + li) * kWRow + kk * 32 + lh * 16;
+        ah[i] = *reinterpret_cast<const bf16x8w*>(row);
+        al[i] = *reinterpret_cast<const bf16x8w*>(row + 64);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const char* row = B + (wn0 + j * 32 + li) * kWRow + kk * 32 + lh * 16;
+        bh[j] = *reinterpret_cast<const bf16x8w*>(row);
+        bl[j] = *reinterpret_cast<const bf16x8w*>(row + 64);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (ks + 1 < nK) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  const int T = a.k * a.k * a.k;
+  float* slab = a.ws + ((int64_t)blockIdx.z * T + t) * a.Cd * a.Cg;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    int col = gn0 + wn0 + j * 32 + li;
+    if (col >= a.Cg) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = dn0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < a.Cd) slab[(int64_t)row * a.Cg + col] = acc[i][j][r];
+      }
+  }
+}
+
 // out[dn][gn][t] (=|+=) Σ_z ws[z][t][dn][gn]
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int Cd, int Cg, int T,
                                     int splits, int accumulate) {
@@ -183,7 +347,17 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
     set_error("conv_wgrad: workspace %zu < %zu", ws_bytes, need);
     return kWorkspace;
   }
-  if (big) {
+  if (a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0) {
+    auto grid_of = [&](int bm, int bn) { return dim3(ceil_div(a.Cd, bm) * ceil_div(a.Cg, bn), T, a.splits); };
+    if (a.Cd >= 128 && a.Cg >= 128)
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 2>), grid_of(128, 128), dim3(256), 0, st, a);
+    else if (a.Cd >= 128)
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 1>), grid_of(128, 64), dim3(256), 0, st, a);
+    else if (a.Cg >= 128)
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 2>), grid_of(64, 128), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 1>), grid_of(64, 64), dim3(256), 0, st, a);
+  } else if (big) {
     dim3 grid(ceil_div(a.Cd, 128) * ceil_div(a.Cg, 128), T, a.splits);
     hipLaunchKernelGGL((conv_wgrad_f32_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
   } else {

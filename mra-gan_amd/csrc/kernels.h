@@ -50,6 +50,7 @@ struct WgradArgs {
   float* ws;       // [splits][k³][Cd][Cg]
   int64_t chunk;   // set by conv_wgrad
   int splits;
+  int x3;          // bf16x3 split MFMA (needs Cd, Cg multiples of 32)
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
 size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k);

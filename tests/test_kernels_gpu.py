@@ -188,6 +188,22 @@ def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
     assert rel(ncdhw(dx), dx_ref) < X3_TOL
 
 
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1)])
+def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
+    ops = x3
+    g = torch.Generator().manual_seed(13 + N * 10 + cin + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv3d(x, w, stride=s, padding=p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw = torch.full((cout, cin, k, k, k), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=False)
+    assert rel(dw, dw_ref) < X3_TOL
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=True)
+    assert rel(dw, 2 * dw_ref) < X3_TOL
+
+
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
 def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
     ops = x3

@@ -51,6 +51,7 @@ def stepped(request, tmp_path_factory):
         pytest.skip("no HIP device")
     name, precision = request.param
     z, meta = load(name)
+    meta = dict(meta, precision=precision)
     model = build_model(meta, tmp_path_factory.mktemp(name), precision)
     init = {}
     for net in ("G_A", "G_B", "D_A", "D_B"):
@@ -91,11 +92,16 @@ def test_init_bit_exact(stepped):
     assert n > 20
 
 
+# forward-value gates: exact-f32 MFMA 1e-4 (measured 1e-6…2e-5); bf16x3 split MFMA (≤ 3·2⁻¹⁸ per
+# product) the north star's 1e-3 (measured ≤ 1.5e-4)
+VALUE_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
+
+
 def test_losses(stepped):
     name, z, meta, _, history, _ = stepped
     got = history[0]
     want = z["fp64/step0/losses"]
-    assert rel_err(got, want) < 1e-4, (got, want)
+    assert rel_err(got, want) < VALUE_TOL[meta["precision"]], (got, want)
     for step in range(1, meta["steps"]):
         w = z[f"fp64/step{step}/losses"]
         assert rel_err(history[step], w) < 1e-2, (step, history[step], w)
@@ -105,10 +111,12 @@ def test_generated_volumes(stepped):
     name, z, meta, _, _, snap = stepped
     for vis, t in snap["vis"].items():
         g, w = sampled(z, f"fp64/step0/{vis}", t)
-        assert rel_err(g, w) < 1e-4, vis
+        assert rel_err(g, w) < VALUE_TOL[meta["precision"]], vis
 
 
-PERTURB = 4e-6      # relative input perturbation ≈ the fp32 forward error of the generated volumes
+# relative input perturbation ≈ the forward error of the generated volumes in each precision
+# (exact f32: ≈2e-5 volume error → 4e-6; bf16x3: ≈1.5e-4 → 4e-5)
+PERTURB = {"f32": 4e-6, "bf16x3": 4e-5}
 
 
 @pytest.fixture(scope="module")
@@ -120,11 +128,12 @@ def conditioning(stepped):
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
     A, B = inputs(meta, 0)
+    eps = PERTURB[meta["precision"]]
     out = []
     for r in range(2):
         g = torch.Generator().manual_seed(77 + r)
-        Ap = A.double() * (1 + PERTURB * torch.randn(A.shape, generator=g, dtype=torch.float64))
-        Bp = B.double() * (1 + PERTURB * torch.randn(B.shape, generator=g, dtype=torch.float64))
+        Ap = A.double() * (1 + eps * torch.randn(A.shape, generator=g, dtype=torch.float64))
+        Bp = B.double() * (1 + eps * torch.randn(B.shape, generator=g, dtype=torch.float64))
         torch.manual_seed(meta["seed"])
         orc = CycleGANOracle(dtype=torch.float64, pool_rng=random.Random(meta["seed"]), **CASE_KW[name])
         orc.optimize_parameters(Ap, Bp)
@@ -164,7 +173,7 @@ def test_gradients(stepped, conditioning):
     whole_ref = rel_err(cat(ref32), cat(ref64))
     whole_pert = max(rel_err(cat(p), cat(ref64)) for p in pert)
     print(f"{name}: whole-net grad rel err {whole:.2e} (reference fp32 {whole_ref:.2e}, "
-          f"fp64 under {PERTURB:g} input perturbation {whole_pert:.2e})")
+          f"fp64 under {PERTURB[meta['precision']]:g} input perturbation {whole_pert:.2e})")
     assert whole <= max(1e-3, 2 * whole_ref, 2 * whole_pert), (whole, whole_ref, whole_pert)
 
 
@@ -173,7 +182,7 @@ def test_running_stats(stepped):
     for net, bufs in snap["bufs"].items():
         for k, b in bufs.items():
             g, w = sampled(z, f"fp64/step0/buf/{net}/{k}", b)
-            assert rel_err(g, w) < 1e-4, (net, k)
+            assert rel_err(g, w) < VALUE_TOL[meta["precision"]], (net, k)
 
 
 def test_params_after_adam(stepped):

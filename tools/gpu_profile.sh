@@ -17,11 +17,11 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/tr
     -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/trace.log" 2>&1
 echo "[gpu_profile] pmc FETCH_SIZE"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run \
-    -- python3 "$R/tools/kbench.py" --ops res_fwd --reps 10 > "$O/pmc_fetch.log" 2>&1
+    -- python3 "$R/tools/kbench.py" --ops res_fwd --reps 10 --precision bf16x3 > "$O/pmc_fetch.log" 2>&1
 echo "[gpu_profile] pmc WRITE_SIZE"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run \
-    -- python3 "$R/tools/kbench.py" --ops res_fwd --reps 10 > "$O/pmc_write.log" 2>&1
+    -- python3 "$R/tools/kbench.py" --ops res_fwd --reps 10 --precision bf16x3 > "$O/pmc_write.log" 2>&1
 # res conv fwd at 64^3 b2 (N=4 instances): padded input 4*18^3*128*4 + weights 27*128*128*4 + output 4*16^3*128*4
-python3 "$R/tools/pmc_traffic.py" --fetch "$O/pmc_fetch" --write "$O/pmc_write" --kernel conv_igemm \
-    --key res_fwd:S64:N4:ngf32 --algorithmic-bytes 22102016 --out "$O/traffic.json"
+python3 "$R/tools/pmc_traffic.py" --fetch "$O/pmc_fetch" --write "$O/pmc_write" --kernel conv_brick \
+    --key res_fwd:S64:N4:ngf32:bf16x3 --algorithmic-bytes 22102016 --out "$O/traffic.json"
 echo "[gpu_profile] done"
