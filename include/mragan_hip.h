@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 1
+#define MRAGAN_ABI_VERSION 2
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -50,14 +50,21 @@ int mragan_get_conv_precision(void);
  * Replaces nn.Conv3d.forward (networks3D.py:186, 192, 241, 257, 212, 389, 397, 406, 414) and the
  * input-gradient of nn.ConvTranspose3d (networks3D.py:203-210).                              */
 int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, const float* bias,
-                      int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream);
+                      int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* Transposed form:  y[n,o,:] = act(bias + Σ_{t:(o+pad−t)%stride==0} x[n,(o+pad−t)/stride,:] · Wp[t])
  * Replaces nn.ConvTranspose3d.forward (networks3D.py:203-210) and the input-gradient of every
  * nn.Conv3d above (autograd convolution_backward, grad_input branch).                        */
 int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
                              const float* bias, int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho,
-                             int Wo, void* stream);
+                             int Wo, void* ws, size_t ws_bytes, void* stream);
+
+/* Workspace (bytes) the two calls above need for these shapes in the current precision mode:
+ * split-K partial tiles of small-M / large-K dense convolutions (PatchGAN layers 2-4 and their
+ * data gradients), summed in a fixed order by a second kernel; 0 when no split is used. */
+size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad,
+                               int Do, int Ho, int Wo, int transposed);
 
 /* Weight gradient:  dw[dn][gn][t] (=|+=) Σ_m dense[m][dn] · gathered[m*stride − pad + t][gn]
  * Conv3d:          dense = dY (output grid), gathered = X      → dw = torch [Cout][Cin][k][k][k]

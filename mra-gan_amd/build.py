@@ -45,7 +45,7 @@ def build(verbose=False, jobs=None):
                 raise RuntimeError(f"hipcc failed for {cmd[-3]}")
     so = os.path.join(LIB, "libmragan_hip.so")
     if cmds or not os.path.exists(so):
-        r = subprocess.run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", so],
+        r = subprocess.run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,--no-undefined", *objs, "-o", so],
                            capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)

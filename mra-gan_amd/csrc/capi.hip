@@ -32,7 +32,8 @@ static int g_conv_precision = MRAGAN_PREC_F32;
 static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0; }
 
 static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
-                       int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* stream) {
+                       int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* ws,
+                       size_t ws_bytes, void* stream) {
   MRAGAN_CHECK_ARG(x && w && y, "conv: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv: bad input shape");
   MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv: bad output shape");
@@ -43,7 +44,7 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
-              g_conv_precision == MRAGAN_PREC_BF16X3};
+              g_conv_precision == MRAGAN_PREC_BF16X3, static_cast<float*>(ws), ws_bytes};
   return conv_igemm(a, st);
 }
 
@@ -66,13 +67,23 @@ int mragan_set_conv_precision(int mode) {
 int mragan_get_conv_precision(void) { return g_conv_precision; }
 
 int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
-                      int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream) {
-  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 0, stream);
+                      int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* ws, size_t ws_bytes,
+                      void* stream) {
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 0, ws, ws_bytes, stream);
 }
 
 int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias,
-                             int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* stream) {
-  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 1, stream);
+                             int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* ws,
+                             size_t ws_bytes, void* stream) {
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 1, ws, ws_bytes, stream);
+}
+
+size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,
+                               int Ho, int Wo, int transposed) {
+  if (thin_side(cin, cout)) return 0;
+  IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, 0, 1,
+              g_conv_precision == MRAGAN_PREC_BF16X3, nullptr, 0};
+  return conv_igemm_ws_bytes(a);
 }
 
 size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride) {

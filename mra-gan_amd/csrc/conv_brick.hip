@@ -299,21 +299,26 @@ struct BrickChoice {
 
 // candidate bricks per GEMM-row budget; the host picks the cheapest (rounds of 256 blocks ×
 // block work, then fewer blocks)
-static BrickChoice choose_brick(int N, int Do, int Ho, int Wo, int ny) {
+static BrickChoice choose_brick(int N, int Do, int Ho, int Wo, int ny, bool x3) {
   // halos: (bd+2)(bh+2)(bw+2) ≤ 400 for the 128-row shapes, ≤ 300 for the 64-row shapes
   static const int shapes128[][3] = {{2, 8, 8}, {2, 6, 9}, {3, 6, 6}, {2, 9, 6}, {4, 4, 8}};
   static const int shapes64[][3] = {{1, 8, 8}, {1, 6, 9}, {1, 9, 6}, {2, 4, 8}};
+  // time model (one block per CU): rounds of 256 blocks × per-step cost, where a step costs a
+  // fixed ~1500 cycles (barrier, staging, halo slab) plus per 32×32 wave tile 6 bf16 MFMAs
+  // (≈200 cycles, bf16x3) or 16 f32 MFMAs (≈1024 cycles)
+  const double c0 = 1500.0, c1 = x3 ? 200.0 : 1024.0;
   BrickChoice best{0, 0, 0, 0, 0, 0, 1e30};
   auto consider = [&](int bm, int bn, const int* s) {
     if (ny % bn != 0) return;
     int64_t bricks = (int64_t)N * ceil_div(Do, s[0]) * ceil_div(Ho, s[1]) * ceil_div(Wo, s[2]);
     int64_t blocks = bricks * ceil_div(ny, bn);
     double rounds = (double)((blocks + 255) / 256);
-    double cost = rounds * bm * bn;
+    double cost = rounds * (c0 + c1 * (bm / 32) * (bn / 32) / 4.0);
     if (cost < best.cost * 0.999 || (cost < best.cost * 1.001 && blocks < best.blocks))
       best = BrickChoice{bm, bn, s[0], s[1], s[2], blocks, cost};
   };
   for (auto& s : shapes128) consider(128, 64, s);
+  for (auto& s : shapes128) consider(128, 128, s);
   for (auto& s : shapes64) consider(64, 128, s);
   for (auto& s : shapes64) consider(64, 64, s);
   return best;
@@ -331,14 +336,16 @@ int conv_brick(const IgemmArgs& g, hipStream_t st) {
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
   a.flip = g.trans ? 1 : 0;
   a.p = g.trans ? g.k - 1 - g.p : g.p;
-  BrickChoice c = choose_brick(g.N, g.Do, g.Ho, g.Wo, g.ny);
+  const bool x3 = g.x3 != 0;
+  BrickChoice c = choose_brick(g.N, g.Do, g.Ho, g.Wo, g.ny, x3);
   a.BD = c.bd; a.BH = c.bh; a.BW = c.bw;
   a.HD = c.bd + 2; a.HH = c.bh + 2; a.HW = c.bw + 2;
   a.nbd = ceil_div(g.Do, c.bd); a.nbh = ceil_div(g.Ho, c.bh); a.nbw = ceil_div(g.Wo, c.bw);
   a.gn = ceil_div(g.ny, c.bn);
   a.ntiles = (int)c.blocks;
   if (a.ntiles == 0) return kOk;
-  const bool x3 = g.x3 != 0;
+  if (c.bm == 128 && c.bn == 128)
+    return x3 ? launch_brick<2, 2, 2, 2, 1, 400>(a, st) : launch_brick<2, 2, 2, 2, 0, 400>(a, st);
   if (c.bm == 128) return x3 ? launch_brick<2, 2, 2, 1, 1, 400>(a, st) : launch_brick<2, 2, 2, 1, 0, 400>(a, st);
   if (c.bn == 128) return x3 ? launch_brick<2, 2, 1, 2, 1, 300>(a, st) : launch_brick<2, 2, 1, 2, 0, 300>(a, st);
   return x3 ? launch_brick<2, 2, 1, 1, 1, 300>(a, st) : launch_brick<2, 2, 1, 1, 0, 300>(a, st);

@@ -231,17 +231,32 @@ static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hi
   return launch_igemm<4, 1, 1, 1, BK>(a, max_mc, st);
 }
 
+static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
+
+// class count and row counts (class 0 is the largest along every dim)
+static void igemm_geometry(IgemmArgs& a, int64_t& max_mc, int64_t& total_m) {
+  a.nclass = (a.trans && a.s > 1) ? a.s * a.s * a.s : 1;
+  auto q = [&](int O, int c) { return a.trans ? (O - c + a.s - 1) / a.s : O; };
+  max_mc = (int64_t)a.N * q(a.Do, 0) * q(a.Ho, 0) * q(a.Wo, 0);
+  total_m = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+}
+
+size_t conv_igemm_ws_bytes(IgemmArgs a) {
+  int64_t max_mc, total_m;
+  igemm_geometry(a, max_mc, total_m);
+  if (max_mc == 0 || a.ny == 0) return 0;
+  if (!g_brick_off && conv_brick_applicable(a)) return 0;
+  if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_ws_bytes(a, max_mc, total_m);
+  return 0;
+}
+
 int conv_igemm(IgemmArgs a, hipStream_t st) {
   MRAGAN_CHECK_ARG(a.cx % 8 == 0, "conv_igemm: contraction channels %d not a multiple of 8", a.cx);
   MRAGAN_CHECK_ARG(a.k >= 1 && a.s >= 1 && a.p >= 0, "conv_igemm: bad k/s/p");
-  a.nclass = (a.trans && a.s > 1) ? a.s * a.s * a.s : 1;
-  // largest class row count (class 0 is the largest along every dim)
-  auto q = [&](int O, int c) { return a.trans ? (O - c + a.s - 1) / a.s : O; };
-  int64_t max_mc = (int64_t)a.N * q(a.Do, 0) * q(a.Ho, 0) * q(a.Wo, 0);
-  int64_t total_m = (int64_t)a.N * a.Do * a.Ho * a.Wo;
+  int64_t max_mc, total_m;
+  igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return kOk;
-  static const bool brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
-  if (!brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+  if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3(a, max_mc, total_m, st);
   if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);
   if (a.cx % 16 == 0) return dispatch_tile<16>(a, max_mc, total_m, st);

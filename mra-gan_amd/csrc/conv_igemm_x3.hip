@@ -45,7 +45,7 @@ __device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
 
 template <int WM, int WN, int TM, int TN, int BK>
 __global__ void __launch_bounds__(256)
-conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
+conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int LDK = BK + 8;               // bf16 per padded row
@@ -62,7 +62,8 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
   __shared__ int out_off[BM];
 
   // XCD-aware tile order: hardware puts block L on XCD L % 8; give each XCD a contiguous range
-  int L = blockIdx.x, tile = L;
+  const int kz = blockIdx.x / ntiles;                 // split-K slice
+  int L = blockIdx.x - kz * ntiles, tile = L;
   if ((ntiles & 7) == 0) tile = (L & 7) * (ntiles >> 3) + (L >> 3);
   const int nb_idx = tile % gn;
   int rest = tile / gn;
@@ -119,10 +120,14 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
   }
 
   const int kchunks = a.cx / BK;
-  const int nK = ntaps * kchunks;
+  const int nK_all = ntaps * kchunks;
+  const int kper = (nK_all + ksplit - 1) / ksplit;
+  const int ks0 = min(nK_all, kz * kper);
+  const int nK = min(nK_all, ks0 + kper) - ks0;       // steps of this slice: ks0 … ks0+nK−1
   float4 ra[A_LOADS], rb[B_LOADS];
 
-  auto load_tiles = [&](int ks) {
+  auto load_tiles = [&](int ksl) {
+    const int ks = ks0 + ksl;
     int tap = ks / kchunks;
     int c0 = (ks - tap * kchunks) * BK;
     int jw = tap % gw.ntap; int tt = tap / gw.ntap;
@@ -225,7 +230,24 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
     __syncthreads();
   }
 
-  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Split-K slices write raw partial tiles to their slab; conv_splitk_reduce applies bias/act.
+  if (ksplit > 1) {
+    float* slab = a.ws + (int64_t)kz * ((int64_t)a.N * a.Do * a.Ho * a.Wo * a.ny);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int col = n0 + wn0 + j * 32 + li;
+      if (col >= a.ny) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int off = out_off[wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
+          if (off >= 0) slab[(int64_t)off * a.ny + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     int col = n0 + wn0 + j * 32 + li;
@@ -243,35 +265,92 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles) {
   }
 }
 
+// y[e] = act(bias[col] + Σ_z slab[z][e]), fixed order (deterministic)
+__global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(const float* __restrict__ ws, int64_t E, int ny,
+                                                                 int splits, const float* __restrict__ bias, int act,
+                                                                 float* __restrict__ y) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    float v = bias ? bias[e % ny] : 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[(int64_t)z * E + e];
+    y[e] = act_fwd(v, act);
+  }
+}
+
+// tile configurations of the dispatch, in preference order per output-channel class
+struct X3Cfg { int bm, bn; };
+static const X3Cfg kX3Cfg[] = {{128, 128}, {128, 64}, {64, 64}, {256, 32}, {128, 32}};
+
+struct X3Plan { int cfg; int splits; };
+
+// largest tile that still gives one block per CU (256 CUs), else the smallest; when even that
+// leaves the chip under-filled and the contraction is long (PatchGAN layers: M ≤ 4k rows,
+// K = 16·Cin), split K across ≤ 16 slices.
+static X3Plan x3_plan(const IgemmArgs& a, int64_t total_m) {
+  auto blocks = [&](int c) {
+    return (int64_t)ceil_div(total_m, kX3Cfg[c].bm) * ceil_div(a.ny, kX3Cfg[c].bn);
+  };
+  int cfg;
+  if (a.ny > 64) cfg = blocks(0) >= 256 ? 0 : blocks(1) >= 256 ? 1 : 2;
+  else if (a.ny > 32) cfg = blocks(1) >= 256 ? 1 : 2;
+  else cfg = blocks(3) >= 256 ? 3 : 4;
+  X3Plan pl{cfg, 1};
+  const int64_t b = blocks(cfg);
+  const int bk = a.cx % 32 == 0 ? 32 : 16;
+  const int nk = (a.k * a.k * a.k + a.nclass - 1) / a.nclass * (a.cx / bk);   // K-steps per class (average)
+  if (b < 256 && nk >= 32) {
+    int64_t sp = (512 + b - 1) / b;
+    if (sp > nk / 16) sp = nk / 16;
+    if (sp > 16) sp = 16;
+    if (sp > 1) pl.splits = (int)sp;
+  }
+  return pl;
+}
+
+size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_m) {
+  (void)max_mc;
+  X3Plan pl = x3_plan(a, total_m);
+  return pl.splits > 1 ? (size_t)pl.splits * total_m * a.ny * sizeof(float) : 0;
+}
+
 template <int WM, int WN, int TM, int TN, int BK>
-static int launch_x3(const IgemmArgs& a, int64_t max_mc, hipStream_t st) {
+static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
   int ntiles = gm * gn * a.nclass;
-  hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK>), dim3(ntiles), dim3(256), 0, st, a, gm, gn, ntiles);
+  hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK>), dim3(ntiles * splits), dim3(256), 0, st, a, gm, gn,
+                     ntiles, splits);
   return check_launch("conv_igemm_x3");
 }
 
 template <int BK>
-static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hipStream_t st) {
-  // largest tile that still gives one block per CU (256 CUs), else the smallest
-  auto blocks = [&](int bm, int bn) { return (int64_t)ceil_div(total_m, bm) * ceil_div(a.ny, bn); };
-  if (a.ny > 64) {
-    if (blocks(128, 128) >= 256) return launch_x3<2, 2, 2, 2, BK>(a, max_mc, st);
-    if (blocks(128, 64) >= 256) return launch_x3<2, 2, 2, 1, BK>(a, max_mc, st);
-    return launch_x3<2, 2, 1, 1, BK>(a, max_mc, st);
+static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int cfg, int splits, hipStream_t st) {
+  switch (cfg) {
+    case 0: return launch_x3<2, 2, 2, 2, BK>(a, max_mc, splits, st);
+    case 1: return launch_x3<2, 2, 2, 1, BK>(a, max_mc, splits, st);
+    case 2: return launch_x3<2, 2, 1, 1, BK>(a, max_mc, splits, st);
+    case 3: return launch_x3<4, 1, 2, 1, BK>(a, max_mc, splits, st);
+    default: return launch_x3<4, 1, 1, 1, BK>(a, max_mc, splits, st);
   }
-  if (a.ny > 32) {
-    if (blocks(128, 64) >= 256) return launch_x3<2, 2, 2, 1, BK>(a, max_mc, st);
-    return launch_x3<2, 2, 1, 1, BK>(a, max_mc, st);
-  }
-  if (blocks(256, 32) >= 256) return launch_x3<4, 1, 2, 1, BK>(a, max_mc, st);
-  return launch_x3<4, 1, 1, 1, BK>(a, max_mc, st);
 }
 
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {
-  if (a.cx % 32 == 0) return dispatch_x3<32>(a, max_mc, total_m, st);
-  return dispatch_x3<16>(a, max_mc, total_m, st);
+  X3Plan pl = x3_plan(a, total_m);
+  if (pl.splits > 1) {
+    const size_t need = (size_t)pl.splits * total_m * a.ny * sizeof(float);
+    if (a.ws == nullptr || a.ws_bytes < need) {
+      set_error("conv: split-K workspace %zu < %zu bytes (query mragan_conv3d_workspace)", a.ws_bytes, need);
+      return kWorkspace;
+    }
+  }
+  int rc = a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
+                          : dispatch_x3<16>(a, max_mc, pl.cfg, pl.splits, st);
+  if (rc || pl.splits == 1) return rc;
+  const int64_t E = total_m * a.ny;
+  int blocks = (int)((E + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.ws, E, a.ny, pl.splits, a.bias, a.act,
+                     a.y);
+  return check_launch("conv_splitk_reduce");
 }
 
 }  // namespace mragan

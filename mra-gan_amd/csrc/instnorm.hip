@@ -31,6 +31,43 @@ size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
   return (size_t)N * in_chunks(s) * C * 2 * sizeof(double) + 16;
 }
 
+// Σ over chunks of partials[n][chunk][C][2] in fixed order (deterministic).  Block = 16
+// channels × 16 chunk rows; grid (ceil(C/16), N), so each thread sums ≤ chunks/16 partials.
+// mode 0: mean / rstd (out0, out1); mode 1: backward coefficients (out0 = coef[2C]).
+__device__ void in_finalize_group(const double* __restrict__ part, const InShape& s, int chunks, int n, int cgroup,
+                                  int mode, float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ double fr[2][256];
+  constexpr int CW = 16, ROWS = 16;
+  const int tid = threadIdx.x, cl = tid % CW, row = tid / CW;
+  const int c = cgroup * CW + cl;
+  double sa = 0, sb = 0;
+  if (c < s.C) {
+#pragma unroll 4
+    for (int k = row; k < chunks; k += ROWS) {
+      const double2 p = *reinterpret_cast<const double2*>(part + (((int64_t)n * chunks + k) * s.C + c) * 2);
+      sa += p.x; sb += p.y;
+    }
+  }
+  fr[0][tid] = sa; fr[1][tid] = sb;
+  __syncthreads();
+  if (row == 0 && c < s.C) {
+    double a = 0, b = 0;
+    for (int r = 0; r < ROWS; ++r) { a += fr[0][r * CW + cl]; b += fr[1][r * CW + cl]; }
+    const double S = (double)s.S();
+    const int i = n * s.C + c;
+    if (mode == 0) {
+      const double mu = a / S;
+      double var = b / S - mu * mu;
+      if (var < 0) var = 0;
+      out0[i] = (float)mu;
+      out1[i] = (float)(1.0 / sqrt(var + (double)kInEps));
+    } else {
+      out0[2 * i] = (float)(a / S);
+      out0[2 * i + 1] = (float)(b / S);
+    }
+  }
+}
+
 __device__ __forceinline__ float4 f4_act(float4 v, int act) {
   return make_float4(act_fwd(v.x, act), act_fwd(v.y, act), act_fwd(v.z, act), act_fwd(v.w, act));
 }
@@ -73,43 +110,11 @@ __global__ void __launch_bounds__(256) in_stats_kernel(const float* __restrict__
   }
 }
 
-// Σ over chunks of partials[n][chunk][C][2], fixed order (deterministic).  Block: 64-channel
-// group × (256/CW) chunk rows; grid (ceil(C/64), N).  mode 0: mean/rstd, mode 1: bwd coefficients.
-__device__ __forceinline__ void in_reduce_chunks(const double* __restrict__ part, const InShape& s, int chunks,
-                                                 double& a, double& b, int& c, bool& valid) {
-  __shared__ double red[2][256];
-  const int CW = s.C < 64 ? s.C : 64;
-  const int rows = 256 / CW;
-  const int tid = threadIdx.x, cl = tid % CW, row = tid / CW;
-  const int n = blockIdx.y;
-  c = blockIdx.x * 64 + cl;
-  double sa = 0, sb = 0;
-  if (row < rows && c < s.C) {
-    for (int k = row; k < chunks; k += rows) {
-      const double* p = part + (((int64_t)n * chunks + k) * s.C + c) * 2;
-      sa += p[0]; sb += p[1];
-    }
-  }
-  red[0][tid] = sa; red[1][tid] = sb;
-  __syncthreads();
-  valid = row == 0 && c < s.C;
-  a = 0; b = 0;
-  if (valid)
-    for (int r = 0; r < rows; ++r) { a += red[0][r * CW + cl]; b += red[1][r * CW + cl]; }
-}
-
+// one block per instance (kernel boundary = coherence point for the partials of all XCDs; an
+// in-kernel last-block reduction needs agent-scope release fences, i.e. L2 write-backs, per block)
 __global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
                                                           float* __restrict__ mean, float* __restrict__ rstd) {
-  double a, b; int c; bool valid;
-  in_reduce_chunks(part, s, chunks, a, b, c, valid);
-  if (!valid) return;
-  const int i = blockIdx.y * s.C + c;
-  const double S = (double)s.S();
-  const double mu = a / S;
-  double var = b / S - mu * mu;
-  if (var < 0) var = 0;
-  mean[i] = (float)mu;
-  rstd[i] = (float)(1.0 / sqrt(var + (double)kInEps));
+  in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 0, mean, rstd);
 }
 
 // ---- forward apply: y (padded by ypad) = act((x − μ)·rstd) + resid(interior of rpad-padded) --
@@ -208,13 +213,7 @@ __global__ void __launch_bounds__(256) in_bwd_stats_kernel(InBwdArgs a, InShape 
 
 __global__ void __launch_bounds__(256) in_bwd_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
                                                               float* __restrict__ coef) {
-  double a, b; int c; bool valid;
-  in_reduce_chunks(part, s, chunks, a, b, c, valid);
-  if (!valid) return;
-  const int i = blockIdx.y * s.C + c;
-  const double S = (double)s.S();
-  coef[2 * i] = (float)(a / S);
-  coef[2 * i + 1] = (float)(b / S);
+  in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 1, coef, nullptr);
 }
 
 __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape s, const float* __restrict__ coef) {
@@ -293,7 +292,7 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, x, s, chunks, part);
   int rc = check_launch("in_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 64), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 16), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
   if ((rc = check_launch("in_finalize"))) return rc;
   const int64_t total = (int64_t)s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad) * (s.W + 2 * ypad) * (s.C / 4);
   hipLaunchKernelGGL(in_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad);
@@ -310,7 +309,7 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, a, s, chunks, part);
   int rc = check_launch("in_bwd_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 64), s.N), dim3(256), 0, st, part, s, chunks, coef);
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 16), s.N), dim3(256), 0, st, part, s, chunks, coef);
   if ((rc = check_launch("in_bwd_finalize"))) return rc;
   const int64_t total = (int64_t)s.N * s.S() * (s.C / 4);
   hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, a, s, coef);

@@ -16,9 +16,13 @@ struct IgemmArgs {
   int act;
   int nclass;       // set by conv_igemm: 1 (forward or s==1) or s³
   int x3;           // 1: bf16x3 split MFMA (conv_igemm_x3.hip), 0: exact f32 MFMA
+  float* ws;        // split-K partial tiles (conv_igemm_ws_bytes)
+  size_t ws_bytes;
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
+size_t conv_igemm_ws_bytes(IgemmArgs a);
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st);
+size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_m);
 
 // k3 s1 convolutions with an LDS-resident input halo (conv_brick.hip)
 struct BrickArgs {

@@ -124,8 +124,10 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     name = "mragan_conv3d_transposed" if transposed else "mragan_conv3d_fwd"
     tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
                           in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo))) if TIMER.match else None
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
     call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo,
-         _stream())
+         _ptr(ws), nbytes, _stream())
     TIMER.end(tm)
     return out
 

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
     assert set(header_functions()) == set(mragan_hip.exported_symbols())
-    assert lib.mragan_abi_version() == 1
+    assert lib.mragan_abi_version() == 2
 
 
 def test_library_built_for_gfx950():
@@ -49,7 +49,7 @@ def test_bad_args_reported_without_gpu():
     import mragan_hip
     from mragan_hip._lib import MraganError, call
     with pytest.raises(MraganError, match="null pointer"):
-        call("mragan_conv3d_fwd", None, 1, 4, 4, 4, 8, None, None, 8, 3, 1, 1, 0, None, 4, 4, 4, None)
+        call("mragan_conv3d_fwd", None, 1, 4, 4, 4, 8, None, None, 8, 3, 1, 1, 0, None, 4, 4, 4, None, 0, None)
 
 
 def _build(name):

@@ -160,6 +160,8 @@ X3_CASES = [
     (2, 128, 256, 5, 4, 1, 1),
     (3, 16, 24, 7, 3, 1, 1),        # BK = 16
     (2, 64, 32, 20, 4, 2, 1),       # ny = 32 tiles
+    (4, 64, 128, 16, 4, 2, 1),      # PatchGAN layer 3 shape: split-K + deterministic reduce
+    (4, 128, 256, 8, 4, 1, 1),      # PatchGAN layer 4 shape: split-K
 ]
 
 
