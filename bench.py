@@ -54,15 +54,36 @@ def parse():
     return ap.parse_args()
 
 
-def step_flops(S, batch, ngf=32, n_blocks=9, ndf=32, nc=1):
-    """Algorithmic conv FLOPs of one optimize_parameters() step (2 × MAC; forward, dgrad where
-    the reference computes it, wgrad).  Matches SURVEY §0 (1.6045 TFLOP per 64³ patch)."""
-    def conv(cin, cout, k, out_vox):
-        return 2.0 * cin * cout * k ** 3 * out_vox
+def g_layer_flops(netG, S, ngf=32, nc=1):
+    """Forward conv FLOPs (2 × MAC) of each generator layer, stem first.  Transposed convs are
+    priced on their input voxels (every input scatters k³ taps), like torch's flop counter."""
+    def conv(cin, cout, k, vox):
+        return 2.0 * cin * cout * k ** 3 * vox
+    if netG.startswith("unet"):
+        nd = 5 if netG == "unet_custom" else 8
+        chans = [(nc, ngf, nc), (ngf, 2 * ngf, ngf), (2 * ngf, 4 * ngf, 2 * ngf), (4 * ngf, 8 * ngf, 4 * ngf)]
+        chans += [(8 * ngf, 8 * ngf, 8 * ngf)] * (nd - 4)        # middle blocks + innermost
+        downs, ups = [], []
+        for L, (outer, inner, cin) in enumerate(chans):
+            vox = (S >> (L + 1)) ** 3                           # down output = up input voxels
+            downs.append(conv(cin, inner, 4, vox))
+            ups.append(conv(inner if L == len(chans) - 1 else 2 * inner, outer, 4, vox))
+        return downs + ups[::-1]
+    n_blocks = 9 if netG == "resnet_9blocks" else 6
     s4 = (S // 4) ** 3
     g_layers = [conv(nc, ngf, 7, S ** 3), conv(ngf, 2 * ngf, 3, (S // 2) ** 3), conv(2 * ngf, 4 * ngf, 3, s4)]
     g_layers += [conv(4 * ngf, 4 * ngf, 3, s4)] * (2 * n_blocks)
     g_layers += [conv(2 * ngf, 4 * ngf, 3, s4), conv(ngf, 2 * ngf, 3, (S // 2) ** 3), conv(ngf, nc, 7, S ** 3)]
+    return g_layers
+
+
+def step_flops(S, batch, ngf=32, netG="resnet_9blocks", ndf=32, nc=1):
+    """Algorithmic conv FLOPs of one optimize_parameters() step (2 × MAC; forward, dgrad where
+    the reference computes it, wgrad).  Matches SURVEY §0 (1.6045 TFLOP per 64³ resnet_9blocks
+    patch)."""
+    def conv(cin, cout, k, out_vox):
+        return 2.0 * cin * cout * k ** 3 * out_vox
+    g_layers = g_layer_flops(netG, S, ngf, nc)
     g_fwd = sum(g_layers)
     first_g = g_layers[0]
     d_sp = [S // 2, S // 4, S // 8, S // 8 - 1, S // 8 - 2]
@@ -93,8 +114,7 @@ def cpu_baseline(args):
     torch.set_num_threads(host_threads())
     threads = torch.get_num_threads()
     torch.manual_seed(0)
-    orc = CycleGANOracle(ngf=args.ngf, ndf=args.ngf, n_blocks=9 if args.netG == "resnet_9blocks" else 6,
-                         pool_rng=random.Random(0))
+    orc = CycleGANOracle(ngf=args.ngf, ndf=args.ngf, netG=args.netG, pool_rng=random.Random(0))
     shape = (args.batch, 1, args.size, args.size, args.size)
     times = []
     for i in range(args.cpu_steps):
@@ -196,13 +216,20 @@ def main():
         model.optimize_parameters()
     barrier()
 
-    # dominant kernel: residual-block conv 4ngf→4ngf k3 (forward form) of the batched first G pass
+    # dominant kernel of the batched first G pass: resnet — residual-block conv 4ngf→4ngf k3
+    # (forward form); unet — the level-1 upconv ConvTranspose3d(4ngf → ngf, k4 s2) (the largest
+    # conv of the net)
+    unet = args.netG.startswith("unet")
     c4 = 4 * args.ngf
     s4 = args.size // 4
     n_launch = 2 * args.batch
     ops.TIMER.reset()
-    ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
-                                 not i["transposed"] and i["N"] == n_launch)
+    if unet:
+        ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == args.ngf and i["k"] == 4 and i["transposed"]
+                                     and i["N"] == n_launch)
+    else:
+        ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
+                                     not i["transposed"] and i["N"] == n_launch)
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     barrier()
@@ -230,15 +257,24 @@ def main():
 
     patches = world * args.batch * args.steps
     value = patches / elapsed
-    flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
+    if unet:
+        flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * args.ngf * 64
+    else:
+        flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
     achieved = flops_launch / (kern_ms / 1e3) / 1e12 if kern_ms else None
-    step_tf = step_flops(args.size, args.batch, args.ngf) / 1e12
+    step_tf = step_flops(args.size, args.batch, args.ngf, args.netG) / 1e12
     x3 = args.precision == "bf16x3"
     # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic (fp32) FLOPs is
     # the bf16 dense peak / 3
     peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
-    kname = "conv_brick_kernel (LDS-halo implicit GEMM, " + ("bf16x3 split MFMA)" if x3 else "f32 MFMA)")
-    traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
+    prec = "bf16x3 split MFMA" if x3 else "f32 MFMA"
+    if unet:
+        kname = (f"conv_igemm_kernel ({prec}, parity classes) level-1 upconv ConvTranspose3d {c4}->{args.ngf} k4 s2 "
+                 f"[{n_launch}x{s4}^3 in]")
+        traffic = measured_traffic(f"unet_up1:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
+    else:
+        kname = f"conv_brick_kernel (LDS-halo implicit GEMM, {prec}) res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd"
+        traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
         "value": round(value, 3),
@@ -253,11 +289,13 @@ def main():
         "dtype": "f32" if not x3 else "f32 (bf16x3 split products, f32 accumulate)",
         "data": "synthetic N(0,1) volumes, random init (seed 0)",
         "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, 1ch->1ch, "
-                               f"{args.size}^3 patch, batch {args.batch}/GPU (BASELINE configs[1] shape; fp32 tensors)",
+                               f"{args.size}^3 patch, batch {args.batch}/GPU ("
+                               + ("BASELINE configs[3] generator family" if args.netG.startswith("unet")
+                                  else "BASELINE configs[1] shape") + "; fp32 tensors)",
                    "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"{kname} res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd",
+        "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "launch_ms": round(kern_ms, 4) if kern_ms else None,

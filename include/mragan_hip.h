@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 2
+#define MRAGAN_ABI_VERSION 3
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -110,6 +110,15 @@ int mragan_rpad_fold(const float* ypad, int N, int D, int H, int W, int C, int p
 /* dx = (g0 + g1 + g2) · act'(y)   (ReLU/LeakyReLU from their output, Tanh, Sigmoid)         */
 int mragan_act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx,
                    void* stream);
+/* UnetSkipConnectionBlock skip concatenation (networks3D.py:340-343, torch.cat([x, model(x)], 1)
+ * followed by the parent's in-place ReLU, :318-320), NDHWC over M voxels:
+ *   concat: out[m] = [act_a(a[m][0:Ca]) | act_b(b[m][0:Cb])]
+ *   split (its backward): da[m] = g[m][0:Ca]·act_a'(ya[m]), db[m] = g[m][Ca:]·act_b'(yb[m])
+ *   (derivatives from the activation outputs; null ya/yb = identity, null da/db = skipped). */
+int mragan_channel_concat(const float* a, int Ca, int act_a, const float* b, int Cb, int act_b, int64_t M, float* out,
+                          void* stream);
+int mragan_channel_split(const float* g, int Ca, int Cb, int64_t M, const float* ya, int act_a, float* da,
+                         const float* yb, int act_b, float* db, void* stream);
 /* nn.L1Loss (cycle_gan_model.py:104-105): loss[0] (=|+=) scale·mean|a−b|; grad (=|+=) scale·sign(a−b)/n.
  * ws: ≥ 4096 bytes.                                                                            */
 int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_accumulate, float* grad,

@@ -154,6 +154,18 @@ int mragan_act_bwd(const float* y, const float* g0, const float* g1, const float
   return act_bwd(y, g0, g1, g2, n, act, dx, static_cast<hipStream_t>(stream));
 }
 
+int mragan_channel_concat(const float* a, int Ca, int act_a, const float* b, int Cb, int act_b, int64_t M, float* out,
+                          void* stream) {
+  MRAGAN_CHECK_ARG(a && b && out && Ca > 0 && Cb > 0 && M >= 0, "channel_concat: bad args");
+  return channel_concat(a, Ca, act_a, b, Cb, act_b, M, out, static_cast<hipStream_t>(stream));
+}
+
+int mragan_channel_split(const float* g, int Ca, int Cb, int64_t M, const float* ya, int act_a, float* da,
+                         const float* yb, int act_b, float* db, void* stream) {
+  MRAGAN_CHECK_ARG(g && Ca > 0 && Cb > 0 && M >= 0 && (da || db), "channel_split: bad args");
+  return channel_split(g, Ca, Cb, M, ya, act_a, da, yb, act_b, db, static_cast<hipStream_t>(stream));
+}
+
 int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad,
                    int grad_acc, void* ws, void* stream) {
   MRAGAN_CHECK_ARG(a && b && loss && ws && n > 0, "l1_loss: bad args");

@@ -89,6 +89,10 @@ size_t instnorm_running_entry_bytes();
 
 int rpad(const float* x, int N, int D, int H, int W, int C, int p, float* y, hipStream_t st);
 int rpad_fold(const float* yp, int N, int D, int H, int W, int C, int p, const float* add, float* x, hipStream_t st);
+int channel_concat(const float* a, int Ca, int act_a, const float* b, int Cb, int act_b, int64_t M, float* out,
+                   hipStream_t st);
+int channel_split(const float* g, int Ca, int Cb, int64_t M, const float* ya, int act_a, float* da, const float* yb,
+                  int act_b, float* db, hipStream_t st);
 int act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx, hipStream_t st);
 int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad, int grad_acc,
             float* ws, hipStream_t st);

@@ -74,6 +74,65 @@ __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restr
   }
 }
 
+// ---- channel concatenation (UnetSkipConnectionBlock, networks3D.py:340-343) ----------------
+// out[m] = [act_a(a[m][0:Ca]) | act_b(b[m][0:Cb])]: torch.cat([x, model(x)], 1) followed by the
+// parent's in-place uprelu, in NDHWC (m = voxel).  Channel-pair granularity keeps the loads and
+// stores of a wave contiguous.
+__global__ void concat_kernel(const float* __restrict__ a, int Ca, int act_a, const float* __restrict__ b, int Cb,
+                              int act_b, int64_t M, float* __restrict__ out) {
+  const int Co = Ca + Cb;
+  GRID_STRIDE(e, M * Co) {
+    const int64_t m = e / Co;
+    const int c = (int)(e - m * Co);
+    out[e] = c < Ca ? act_fwd(a[m * Ca + c], act_a) : act_fwd(b[m * Cb + (c - Ca)], act_b);
+  }
+}
+
+// backward of concat: da = g[:, :Ca]·act_a'(ya), db = g[:, Ca:]·act_b'(yb) (derivatives from the
+// activation outputs, as act_bwd; a null y means identity).  da may accumulate into itself.
+__device__ __forceinline__ float act_deriv_from_y(float v, int act) {
+  switch (act) {
+    case kActRelu: return v > 0.f ? 1.f : 0.f;
+    case kActLrelu: return v > 0.f ? 1.f : kLreluSlope;
+    case kActTanh: return 1.f - v * v;
+    case kActSigmoid: return v * (1.f - v);
+    default: return 1.f;
+  }
+}
+
+__global__ void split_kernel(const float* __restrict__ g, int Ca, int Cb, int64_t M, const float* __restrict__ ya,
+                             int act_a, float* __restrict__ da, const float* __restrict__ yb, int act_b,
+                             float* __restrict__ db) {
+  const int Co = Ca + Cb;
+  GRID_STRIDE(e, M * Co) {
+    const int64_t m = e / Co;
+    const int c = (int)(e - m * Co);
+    const float v = g[e];
+    if (c < Ca) {
+      const int64_t i = m * Ca + c;
+      if (da) da[i] = ya ? v * act_deriv_from_y(ya[i], act_a) : v;
+    } else {
+      const int64_t i = m * Cb + (c - Ca);
+      if (db) db[i] = yb ? v * act_deriv_from_y(yb[i], act_b) : v;
+    }
+  }
+}
+
+int channel_concat(const float* a, int Ca, int act_a, const float* b, int Cb, int act_b, int64_t M, float* out,
+                   hipStream_t st) {
+  if (M == 0) return kOk;
+  hipLaunchKernelGGL(concat_kernel, dim3(grid_cap(M * (Ca + Cb))), dim3(256), 0, st, a, Ca, act_a, b, Cb, act_b, M, out);
+  return check_launch("concat");
+}
+
+int channel_split(const float* g, int Ca, int Cb, int64_t M, const float* ya, int act_a, float* da, const float* yb,
+                  int act_b, float* db, hipStream_t st) {
+  if (M == 0) return kOk;
+  hipLaunchKernelGGL(split_kernel, dim3(grid_cap(M * (Ca + Cb))), dim3(256), 0, st, g, Ca, Cb, M, ya, act_a, da, yb,
+                     act_b, db);
+  return check_launch("split");
+}
+
 // ---- block reduction helper --------------------------------------------------------------
 __device__ __forceinline__ double block_sum(double v) {
   __shared__ double sh[4];

@@ -280,9 +280,10 @@ def define_G(input_nc, output_nc, ngf, netG, norm='batch', use_dropout=False, in
         net = ResnetGenerator(input_nc, output_nc, ngf, norm_layer=norm_layer, use_dropout=use_dropout, n_blocks=9)
     elif netG == 'resnet_6blocks':
         net = ResnetGenerator(input_nc, output_nc, ngf, norm_layer=norm_layer, use_dropout=use_dropout, n_blocks=6)
-    elif netG in ('unet_custom', 'unet_256'):
-        raise NotImplementedError('Generator model [%s] (UnetGenerator) is not implemented by the HIP engine yet '
-                                  '(see DESIGN.md §8, row A18)' % netG)
+    elif netG == 'unet_custom':
+        net = UnetGenerator(input_nc, output_nc, 5, ngf, norm_layer=norm_layer, use_dropout=use_dropout)
+    elif netG == 'unet_256':
+        net = UnetGenerator(input_nc, output_nc, 8, ngf, norm_layer=norm_layer, use_dropout=use_dropout)
     elif netG == 'Dynet':
         raise NotImplementedError('Generator model [Dynet] needs MONAI DynUNet (out of scope, SURVEY §2 row 1)')
     else:
@@ -504,3 +505,64 @@ class NLayerDiscriminator(_EngineNet):
     def _compile(self):
         from mragan_hip.engine import compile_nlayer_discriminator
         return compile_nlayer_discriminator(self)
+
+
+class UnetGenerator(_EngineNet):
+    """networks3D.py:270-293.  `num_downs` stride-2 k4 convolutions; the innermost block is
+    built first, so parameter init consumes the RNG innermost-out like the reference, and
+    the nested `model.model.1.model.3...` state_dict keys are identical."""
+
+    def __init__(self, input_nc, output_nc, num_downs, ngf=64, norm_layer=InstanceNorm3d, use_dropout=False):
+        super().__init__()
+        if num_downs < 5:
+            raise ValueError("UnetGenerator needs num_downs >= 5 (networks3D.py:278-283)")
+        if norm_layer is None:
+            raise NotImplementedError("norm='none' generator is not supported by the HIP engine")
+        self.input_nc, self.output_nc, self.ngf, self.num_downs = input_nc, output_nc, ngf, num_downs
+        blk = UnetSkipConnectionBlock(ngf * 8, ngf * 8, submodule=None, norm_layer=norm_layer, innermost=True)
+        for _ in range(num_downs - 5):
+            blk = UnetSkipConnectionBlock(ngf * 8, ngf * 8, submodule=blk, norm_layer=norm_layer,
+                                          use_dropout=use_dropout)
+        for outer, inner in ((ngf * 4, ngf * 8), (ngf * 2, ngf * 4), (ngf, ngf * 2)):
+            blk = UnetSkipConnectionBlock(outer, inner, submodule=blk, norm_layer=norm_layer)
+        self.model = UnetSkipConnectionBlock(output_nc, ngf, input_nc=input_nc, submodule=blk, outermost=True,
+                                             norm_layer=norm_layer)
+
+    def _compile(self):
+        from mragan_hip.engine import compile_unet_generator
+        return compile_unet_generator(self)
+
+
+class UnetSkipConnectionBlock(nn.Module):
+    """networks3D.py:298-343: X → [down → submodule → up] → cat(X, ·) (outermost: no cat).
+    The reference's in-place LeakyReLU/ReLU also rewrite the skip tensor; the engine
+    reproduces that (the skip carries LeakyReLU(X)).  Executed by the generator's engine."""
+
+    def __init__(self, outer_nc, inner_nc, input_nc=None, submodule=None, outermost=False, innermost=False,
+                 norm_layer=InstanceNorm3d, use_dropout=False):
+        super().__init__()
+        self.outermost, self.innermost = outermost, innermost
+        if type(norm_layer) == functools.partial:
+            use_bias = norm_layer.func == nn.InstanceNorm2d      # False for the 3-D norms (reference quirk)
+        else:
+            use_bias = norm_layer == nn.InstanceNorm2d
+        if input_nc is None:
+            input_nc = outer_nc
+        downconv = Conv3d(input_nc, inner_nc, kernel_size=4, stride=2, padding=1, bias=use_bias)
+        downrelu, uprelu = LeakyReLU(0.2, True), ReLU(True)
+        downnorm, upnorm = norm_layer(inner_nc), norm_layer(outer_nc)
+        if outermost:
+            upconv = ConvTranspose3d(inner_nc * 2, outer_nc, kernel_size=4, stride=2, padding=1)
+            seq = [downconv, submodule, uprelu, upconv, Tanh()]
+        elif innermost:
+            upconv = ConvTranspose3d(inner_nc, outer_nc, kernel_size=4, stride=2, padding=1, bias=use_bias)
+            seq = [downrelu, downconv, uprelu, upconv, upnorm]
+        else:
+            upconv = ConvTranspose3d(inner_nc * 2, outer_nc, kernel_size=4, stride=2, padding=1, bias=use_bias)
+            seq = [downrelu, downconv, downnorm, submodule, uprelu, upconv, upnorm]
+            if use_dropout:
+                seq.append(Dropout(0.5))
+        self.model = nn.Sequential(*seq)
+
+    def forward(self, x):
+        raise NotImplementedError("UnetSkipConnectionBlock runs inside its UnetGenerator's HIP engine")

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -45,6 +45,8 @@ SIGNATURES = {
     "mragan_rpad": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
     "mragan_rpad_fold": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "mragan_act_bwd": (i32, [vp, vp, vp, vp, i64, i32, vp, vp]),
+    "mragan_channel_concat": (i32, [vp, i32, i32, vp, i32, i32, i64, vp, vp]),
+    "mragan_channel_split": (i32, [vp, i32, i32, i64, vp, i32, vp, vp, i32, vp, vp]),
     "mragan_l1_loss": (i32, [vp, vp, i64, f32, vp, i32, vp, i32, vp, vp]),
     "mragan_gan_loss": (i32, [vp, i64, f32, i32, f32, vp, i32, vp, vp, vp]),
     "mragan_channel_sum_workspace": (sz, [i64, i32]),

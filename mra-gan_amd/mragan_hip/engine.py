@@ -380,3 +380,214 @@ def compile_nlayer_discriminator(net) -> NetPlan:
     for st in stages:
         st.use_bias = st.norm is None
     return NetPlan(stages, stages[0].conv.cin, stages[-1].conv.cout)
+
+
+# --------------------------------------------------------------------------------------
+# UnetGenerator (networks3D.py:270-343)
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class UnetLevel:
+    """One UnetSkipConnectionBlock: `down` = Conv3d k4 s2 p1, `up` = ConvTranspose3d k4 s2 p1.
+    kind "outer" (no norms, up has bias + Tanh), "mid" (down → IN, up → IN) or "inner"
+    (down without norm, up → IN)."""
+    kind: str
+    down: ConvLayer
+    up: ConvLayer
+    down_norm: object = None
+    up_norm: object = None
+
+
+@dataclass
+class UnetLevelCtx:
+    inp: torch.Tensor = None        # level input: the image (outer) or LeakyReLU(x) = the skip tensor
+    h: torch.Tensor = None          # down-conv output (mid: pre-IN; inner: ReLU'd)
+    dmean: torch.Tensor = None
+    drstd: torch.Tensor = None
+    nxt: torch.Tensor = None        # input of the next level (LeakyReLU applied), outer/mid only
+    r: torch.Tensor = None          # up-conv input: ReLU(cat(skip, sub)) (inner: ReLU(h))
+    g: torch.Tensor = None          # up-conv output (pre-IN; outer: Tanh output)
+    umean: torch.Tensor = None
+    urstd: torch.Tensor = None
+    ru: torch.Tensor = None         # ReLU(IN(g)): the sub-block half of the parent's cat, ReLU'd
+
+
+class UnetPlan:
+    """Explicit forward/backward of a UnetGenerator on NDHWC tensors.
+
+    The reference's in-place activations define what every tensor holds
+    (networks3D.py:318-343): a block's `downrelu` (LeakyReLU, inplace) rewrites its input x,
+    which is also the tensor `torch.cat([x, model(x)], 1)` keeps as the skip, and the parent's
+    `uprelu` (ReLU, inplace) acts on the concatenation.  So, level by level:
+
+        a_{L+1} = LeakyReLU(IN(conv_down_L(a_L)))      (outer level: no IN, a_1 = LReLU(conv(x)))
+        r_L     = cat(ReLU(a_{L+1}), ReLU(u_{L+1}))    u = IN(conv_up(r)) of the level below
+        inner:  r = ReLU(conv_down(a));  u = IN(conv_up(r))
+        outer:  out = Tanh(conv_up(r_0) + b)
+
+    Activations are fused into the producing conv / InstanceNorm kernel; the concatenation
+    and its backward are `channel_concat` / `channel_split`."""
+
+    def __init__(self, levels: List[UnetLevel], in_channels: int, out_channels: int):
+        self.levels = levels
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.dirty = True
+
+    def conv_layers(self):
+        for lv in self.levels:
+            yield lv.down
+            yield lv.up
+
+    def repack(self):
+        for c in self.conv_layers():
+            c.repack()
+        self.dirty = False
+
+    def ensure_packed(self):
+        if self.dirty:
+            self.repack()
+
+    def _norms(self):
+        """(norm, conv, ctx getter) for every InstanceNorm, in module order."""
+        out = []
+        for i, lv in enumerate(self.levels):
+            if lv.down_norm is not None:
+                out.append((lv.down_norm, lv.down, i, "down"))
+            if lv.up_norm is not None:
+                out.append((lv.up_norm, lv.up, i, "up"))
+        return out
+
+    @staticmethod
+    def _check_spatial(x_shape, levels):
+        """The reference fails on these inputs too: a conv with an empty output, or an
+        InstanceNorm over a single voxel (torch's message)."""
+        d, h, w = x_shape[1:4]
+        for lv in levels:
+            d, h, w = lv.down.out_spatial(d, h, w)
+            if min(d, h, w) < 1:
+                raise RuntimeError("UnetGenerator: input too small for its number of downsamplings "
+                                   f"(a Conv3d k4 s2 output would be {d}x{h}x{w})")
+            if lv.down_norm is not None and d * h * w == 1:
+                raise ValueError("Expected more than 1 spatial element when training, got input size "
+                                 f"[{x_shape[0]}, {lv.down.cout}, 1, 1, 1]")
+
+    def forward(self, x: torch.Tensor) -> NetCtx:
+        self.ensure_packed()
+        N, D, H, W, Cin = x.shape
+        if Cin != self.in_channels:
+            raise ValueError(f"expected {self.in_channels} input channels, got {Cin}")
+        self._check_spatial(x.shape, self.levels)
+        ctx = NetCtx(N=N, spatial=(D, H, W))
+        cur = x
+        for lv in self.levels:                      # encoder
+            lc = UnetLevelCtx(inp=cur)
+            sp = lv.down.out_spatial(*cur.shape[1:4])
+            if lv.kind == "outer":
+                lc.nxt = lv.down.forward(cur, act="lrelu")
+            elif lv.kind == "mid":
+                lc.h = lv.down.forward(cur)
+                lc.nxt, lc.dmean, lc.drstd = ops.instnorm_fwd(lc.h, act="lrelu")
+            else:
+                lc.h = lv.down.forward(cur, act="relu")
+                lc.r = lc.h
+            assert tuple(sp) == tuple((lc.nxt if lc.nxt is not None else lc.h).shape[1:4])
+            ctx.stages.append(lc)
+            cur = lc.nxt
+        for i in range(len(self.levels) - 1, -1, -1):   # decoder
+            lv, lc = self.levels[i], ctx.stages[i]
+            if lv.kind != "inner":
+                below = ctx.stages[i + 1]
+                lc.r = ops.channel_concat(below.inp, "relu", below.ru, None)
+            lc.g = lv.up.forward(lc.r, bias=lv.up.m.bias if lv.kind == "outer" else None,
+                                 act="tanh" if lv.kind == "outer" else None)
+            if lv.kind != "outer":
+                lc.ru, lc.umean, lc.urstd = ops.instnorm_fwd(lc.g, act="relu")
+        ctx.out = ctx.stages[0].g
+        return ctx
+
+    def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,
+                 need_input_grad: bool = False, dx_out: Optional[torch.Tensor] = None,
+                 dx_add: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """Same contract as NetPlan.backward."""
+        n = len(self.levels)
+        skip = [None] * (n + 1)        # gradient w.r.t. level i's input through the skip half of the cat
+        du = [None] * (n + 1)          # gradient w.r.t. ReLU(u_i) (raw, the IN backward applies ReLU')
+        for i, (lv, lc) in enumerate(zip(self.levels, ctx.stages)):    # decoder, top-down
+            if lv.kind == "outer":
+                srcs = [t for t in dout if t is not None]
+                dg = torch.empty_like(lc.g)
+                ops.act_bwd(lc.g, srcs, "tanh", dg)
+                if need_wgrad and lv.up.m.bias is not None:
+                    ops.channel_sum(dg, lv.up.m.bias.grad, accumulate=True)
+            else:
+                dg = ops.instnorm_bwd(lc.g, lc.umean, lc.urstd, du[i], 0, None, act="relu")
+            if need_wgrad:
+                lv.up.wgrad(lc.r, dg)
+            dr = lv.up.dgrad(dg, lc.r.shape[1:4])
+            if lv.kind == "inner":
+                dh = torch.empty_like(lc.h)
+                ops.act_bwd(lc.h, [dr], "relu", dh)
+                ctx_inner_dh = dh
+            else:
+                below = ctx.stages[i + 1]
+                skip[i + 1], du[i + 1] = ops.channel_split(dr, below.inp.shape[4], below.inp, "relu", None, None)
+        g_in = None                    # gradient w.r.t. the current level's input through its down conv
+        for i in range(n - 1, -1, -1):                                  # encoder, bottom-up
+            lv, lc = self.levels[i], ctx.stages[i]
+            if lv.kind == "inner":
+                dh = ctx_inner_dh
+            elif lv.kind == "mid":
+                dh = ops.instnorm_bwd(lc.h, lc.dmean, lc.drstd, g_in, 0, skip[i + 1], act="lrelu")
+            else:
+                dh = torch.empty_like(lc.nxt)
+                ops.act_bwd(lc.nxt, [g_in, skip[i + 1]], "lrelu", dh)
+            if need_wgrad:
+                lv.down.wgrad(lc.inp, dh)
+            if i > 0 or need_input_grad:
+                g_in = lv.down.dgrad(dh, lc.inp.shape[1:4])
+        if not need_input_grad:
+            return None
+        if dx_add is not None or dx_out is not None:
+            out = dx_out if dx_out is not None else torch.empty_like(g_in)
+            ops.act_bwd(None, [g_in, dx_add], None, out)
+            return out
+        return g_in
+
+    def running_entries(self, segments):
+        entries = []
+        for norm, conv, i, which in self._norms():
+            segs = []
+            for ctx, row0, count in segments:
+                lc = ctx.stages[i]
+                mean, rstd, h = (lc.dmean, lc.drstd, lc.h) if which == "down" else (lc.umean, lc.urstd, lc.g)
+                C_ = mean.shape[1]
+                S = h.shape[1] * h.shape[2] * h.shape[3]
+                segs.append((mean.data_ptr() + 4 * row0 * C_, rstd.data_ptr() + 4 * row0 * C_, count))
+            entries.append((norm, conv.m.bias, conv.cout, S, segs))
+        return entries
+
+
+def compile_unet_generator(net) -> UnetPlan:
+    from models import networks3D as N3
+    levels: List[UnetLevel] = []
+    blk = net.model
+    while blk is not None:
+        seq = list(blk.model)
+        if any(isinstance(m, N3.Dropout) for m in seq):
+            raise NotImplementedError("dropout inside the generator is not supported by the HIP engine")
+        down = next(m for m in seq if isinstance(m, N3.Conv3d))
+        up = next(m for m in seq if isinstance(m, N3.ConvTranspose3d))
+        norms = [m for m in seq if isinstance(m, N3.InstanceNorm3d)]
+        kind = "outer" if blk.outermost else ("inner" if blk.innermost else "mid")
+        lv = UnetLevel(kind=kind, down=ConvLayer(down, False), up=ConvLayer(up, True))
+        if kind == "mid":
+            lv.down_norm, lv.up_norm = norms
+        elif kind == "inner":
+            lv.up_norm = norms[0]
+        levels.append(lv)
+        sub = [m for m in seq if isinstance(m, N3.UnetSkipConnectionBlock)]
+        blk = sub[0] if sub else None
+    if levels[0].kind != "outer" or levels[-1].kind != "inner":
+        raise NotImplementedError("UnetGenerator must run outermost → innermost")
+    return UnetPlan(levels, net.input_nc, net.output_nc)

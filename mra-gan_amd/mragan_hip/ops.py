@@ -218,6 +218,40 @@ def act_bwd(y: Optional[torch.Tensor], grads: Sequence[Optional[torch.Tensor]], 
     return out
 
 
+def channel_concat(a: torch.Tensor, act_a, b: torch.Tensor, act_b, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NDHWC channel concatenation [act_a(a) | act_b(b)] (UNet skip, networks3D.py:340-343)."""
+    _check(a, "concat.a")
+    _check(b, "concat.b")
+    if a.shape[:4] != b.shape[:4]:
+        raise ValueError(f"concat: spatial mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    Ca, Cb = a.shape[4], b.shape[4]
+    if out is None:
+        out = torch.empty(tuple(a.shape[:4]) + (Ca + Cb,), device=a.device, dtype=torch.float32)
+    M = a.numel() // Ca
+    call("mragan_channel_concat", _ptr(a), Ca, ACT[act_a], _ptr(b), Cb, ACT[act_b], M, _ptr(out), _stream())
+    return out
+
+
+def channel_split(g: torch.Tensor, Ca: int, ya: Optional[torch.Tensor], act_a, yb: Optional[torch.Tensor], act_b,
+                  da: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
+    """Backward of channel_concat: (g[..., :Ca]·act_a'(ya), g[..., Ca:]·act_b'(yb))."""
+    _check(g, "split.g")
+    Co = g.shape[4]
+    Cb = Co - Ca
+    sp = tuple(g.shape[:4])
+    if da is None:
+        da = torch.empty(sp + (Ca,), device=g.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(sp + (Cb,), device=g.device, dtype=torch.float32)
+    for t, c in ((ya, Ca), (yb, Cb)):
+        if t is not None and tuple(t.shape) != sp + (c,):
+            raise ValueError("split: activation shape mismatch")
+    M = g.numel() // Co
+    call("mragan_channel_split", _ptr(g), Ca, Cb, M, _ptr(ya), ACT[act_a], _ptr(da), _ptr(yb), ACT[act_b], _ptr(db),
+         _stream())
+    return da, db
+
+
 def l1_loss(a: torch.Tensor, b: torch.Tensor, scale: float, loss_slot: torch.Tensor, grad: Optional[torch.Tensor],
             loss_accumulate=False, grad_accumulate=False):
     ws = WS.get(1 << 14)

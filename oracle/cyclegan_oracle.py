@@ -5,6 +5,7 @@ functional restatement, in PyTorch-CPU (fp32 or fp64), of the reference's
 ``CycleGANModel.optimize_parameters()`` step and everything under it:
 
 * ResnetGenerator / ResnetBlock      (reference models/networks3D.py:173-263)
+* UnetGenerator / UnetSkipConnectionBlock (reference models/networks3D.py:270-343)
 * NLayerDiscriminator                (reference models/networks3D.py:381-425)
 * InstanceNorm3d(affine=False, track_running_stats=True) in train mode
                                      (reference models/networks3D.py:15-24)
@@ -300,6 +301,97 @@ def adam_update(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tens
 
 
 # --------------------------------------------------------------------------------------
+# UnetGenerator (networks3D.py:270-343) — --netG unet_custom / unet_256
+# --------------------------------------------------------------------------------------
+
+def unet_generator_levels(input_nc: int, output_nc: int, ngf: int, num_downs: int) -> dict:
+    """UnetSkipConnectionBlocks outermost → innermost (networks3D.py:276-287) with their
+    state_dict prefixes.  Sequential indices (networks3D.py:316-338): outermost
+    [down 0, sub 1, uprelu 2, up 3, tanh 4]; middle [downrelu 0, down 1, downnorm 2, sub 3,
+    uprelu 4, up 5, upnorm 6]; innermost [downrelu 0, down 1, uprelu 2, up 3, upnorm 4]."""
+    chans = [(output_nc, ngf, input_nc), (ngf, 2 * ngf, ngf), (2 * ngf, 4 * ngf, 2 * ngf), (4 * ngf, 8 * ngf, 4 * ngf)]
+    chans += [(8 * ngf, 8 * ngf, 8 * ngf)] * (num_downs - 5)
+    chans += [(8 * ngf, 8 * ngf, 8 * ngf)]
+    levels = []
+    prefix = "model"
+    for i, (outer, inner, cin) in enumerate(chans):
+        kind = "outer" if i == 0 else ("inner" if i == len(chans) - 1 else "mid")
+        p = prefix + ".model"
+        idx = {"outer": (0, None, 1, 3, None), "mid": (1, 2, 3, 5, 6), "inner": (1, None, None, 3, 4)}[kind]
+        down, dnorm, sub, up, unorm = idx
+        levels.append(dict(kind=kind, down=f"{p}.{down}", up=f"{p}.{up}",
+                           dnorm=f"{p}.{dnorm}" if dnorm is not None else None,
+                           unorm=f"{p}.{unorm}" if unorm is not None else None,
+                           cin=cin, inner=inner, outer=outer, up_cin=inner if kind == "inner" else 2 * inner,
+                           up_bias=kind == "outer"))
+        prefix = f"{p}.{sub}"
+    return dict(kind="unet", levels=levels)
+
+
+def init_unet_state(spec: dict, init_gain: float = 0.02, dtype=torch.float32) -> "OrderedDict[str, torch.Tensor]":
+    """RNG consumption of UnetGenerator construction + init_weights: the blocks are built
+    innermost first, each drawing kaiming_uniform_ for its downconv then its upconv (+ bias for
+    the outermost upconv, the only conv with a bias: use_bias compares against
+    nn.InstanceNorm2d, networks3D.py:302-305); init_weights then redraws normal_(0, gain) in
+    net.apply order = the downconvs outer → inner, then the upconvs inner → outer."""
+    levels = spec["levels"]
+    w = {}
+    for lv in reversed(levels):
+        wd = torch.empty((lv["inner"], lv["cin"], 4, 4, 4), dtype=torch.float32)
+        init.kaiming_uniform_(wd, a=math.sqrt(5))
+        wu = torch.empty((lv["up_cin"], lv["outer"], 4, 4, 4), dtype=torch.float32)
+        init.kaiming_uniform_(wu, a=math.sqrt(5))
+        w[lv["down"]] = [wd, None]
+        w[lv["up"]] = [wu, None]
+        if lv["up_bias"]:
+            b = torch.empty(lv["outer"], dtype=torch.float32)
+            fan_in, _ = init._calculate_fan_in_and_fan_out(wu)
+            init.uniform_(b, -1.0 / math.sqrt(fan_in), 1.0 / math.sqrt(fan_in))
+            w[lv["up"]][1] = b
+    for key in [lv["down"] for lv in levels] + [lv["up"] for lv in reversed(levels)]:
+        init.normal_(w[key][0], 0.0, init_gain)
+        if w[key][1] is not None:
+            w[key][1].zero_()
+    state: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    for key in sorted(w):
+        state[key + ".weight"] = w[key][0].to(dtype)
+        if w[key][1] is not None:
+            state[key + ".bias"] = w[key][1].to(dtype)
+    for lv in levels:
+        for nk, c in ((lv["dnorm"], lv["inner"]), (lv["unorm"], lv["outer"])):
+            if nk:
+                state[nk + ".running_mean"] = torch.zeros(c, dtype=dtype)
+                state[nk + ".running_var"] = torch.ones(c, dtype=dtype)
+                state[nk + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return state
+
+
+def unet_forward(state: dict, params: dict, spec: dict, x: torch.Tensor) -> torch.Tensor:
+    """UnetGenerator.forward with the reference's in-place activations made explicit: a
+    non-outermost block's `downrelu` (inplace) rewrites its input, so the skip half of
+    torch.cat([x, model(x)], 1) is LeakyReLU(x) (networks3D.py:340-343)."""
+    levels = spec["levels"]
+
+    def block(i, h):
+        lv = levels[i]
+        wd, wu = params[lv["down"] + ".weight"], params[lv["up"] + ".weight"]
+        if lv["kind"] == "outer":
+            s = block(i + 1, F.conv3d(h, wd, None, stride=2, padding=1))
+            y = F.conv_transpose3d(F.relu(s), wu, params[lv["up"] + ".bias"], stride=2, padding=1)
+            return torch.tanh(y)
+        a = F.leaky_relu(h, LRELU_SLOPE)
+        d = F.conv3d(a, wd, None, stride=2, padding=1)
+        if lv["kind"] == "mid":
+            r = F.relu(block(i + 1, instance_norm_train(d, state, lv["dnorm"])))
+        else:
+            r = F.relu(d)
+        u = instance_norm_train(F.conv_transpose3d(r, wu, None, stride=2, padding=1), state, lv["unorm"])
+        return torch.cat([a, u], 1)
+
+    return block(0, x)
+
+
+# --------------------------------------------------------------------------------------
 # The step
 # --------------------------------------------------------------------------------------
 
@@ -308,7 +400,7 @@ class CycleGANOracle:
 
     LOSS_NAMES = ['D_A', 'G_A', 'cycle_A', 'idt_A', 'D_B', 'G_B', 'cycle_B', 'idt_B']  # :68
 
-    def __init__(self, input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, n_layers_D=3,
+    def __init__(self, input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, n_layers_D=3, netG=None,
                  use_lsgan=False, lambda_A=10.0, lambda_B=10.0, lambda_identity=0.5,
                  lr=2e-4, beta1=0.5, pool_size=50, init_gain=0.02, dtype=torch.float32,
                  states: Dict[str, dict] = None, pool_rng: random.Random = None):
@@ -316,14 +408,24 @@ class CycleGANOracle:
         self.use_lsgan = use_lsgan
         self.lambda_A, self.lambda_B, self.lambda_idt = lambda_A, lambda_B, lambda_identity
         self.lr, self.beta1 = lr, beta1
+        if netG in ("unet_custom", "unet_256"):      # define_G, networks3D.py:84-102
+            nd = 5 if netG == "unet_custom" else 8
+            gA = unet_generator_levels(input_nc, output_nc, ngf, nd)
+            gB = unet_generator_levels(output_nc, input_nc, ngf, nd)
+        else:
+            if netG is not None:
+                n_blocks = {"resnet_9blocks": 9, "resnet_6blocks": 6}[netG]
+            gA = resnet_generator_layers(input_nc, output_nc, ngf, n_blocks)
+            gB = resnet_generator_layers(output_nc, input_nc, ngf, n_blocks)
         self.layers = {
-            "G_A": resnet_generator_layers(input_nc, output_nc, ngf, n_blocks),
-            "G_B": resnet_generator_layers(output_nc, input_nc, ngf, n_blocks),
+            "G_A": gA,
+            "G_B": gB,
             "D_A": nlayer_discriminator_layers(output_nc, ndf, n_layers_D, not use_lsgan),
             "D_B": nlayer_discriminator_layers(input_nc, ndf, n_layers_D, not use_lsgan),
         }
         if states is None:   # same construction order as CycleGANModel.initialize (:83-96)
-            states = {k: init_net_state(self.layers[k], init_gain) for k in ("G_A", "G_B", "D_A", "D_B")}
+            states = {k: (init_unet_state(self.layers[k], init_gain) if isinstance(self.layers[k], dict)
+                          else init_net_state(self.layers[k], init_gain)) for k in ("G_A", "G_B", "D_A", "D_B")}
         self.state = {k: OrderedDict((n, t.clone().to(dtype) if t.is_floating_point() else t.clone())
                                      for n, t in v.items()) for k, v in states.items()}
         self.params = {k: OrderedDict((n, t) for n, t in self.state[k].items()
@@ -337,7 +439,10 @@ class CycleGANOracle:
 
     # --- helpers -------------------------------------------------------------------
     def _net(self, name, x, params):
-        return generator_forward(self.state[name], params, self.layers[name], x)
+        spec = self.layers[name]
+        if isinstance(spec, dict):
+            return unet_forward(self.state[name], params, spec, x)
+        return generator_forward(self.state[name], params, spec, x)
 
     def _leaf_params(self, names, requires_grad):
         out = {}

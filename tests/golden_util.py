@@ -12,6 +12,7 @@ CASE_KW = {
     "step_r9_s32_b1": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
     "step_r6_s24_b2_nc2_lsgan": dict(input_nc=2, output_nc=2, ngf=8, ndf=8, n_blocks=6, use_lsgan=True),
     "step_r9_s32_b2_ngf16": dict(input_nc=1, output_nc=1, ngf=16, ndf=16, n_blocks=9, use_lsgan=False),
+    "step_unet_s32_b2_ngf8": dict(input_nc=1, output_nc=1, ngf=8, ndf=8, netG="unet_custom", use_lsgan=False),
 }
 
 
@@ -45,6 +46,8 @@ def is_pre_in_bias(net, key, n_layers_D=3):
     if not key.endswith(".bias"):
         return False
     if net.startswith("G"):
+        if key.startswith("model.model"):    # UnetGenerator: only the outermost upconv has a bias
+            return False
         return "conv_block" in key or not _is_g_head(key)
     # D: model.0 (no IN) and the final conv have real gradients
     idx = int(key.split(".")[1])

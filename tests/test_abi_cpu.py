@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
     assert set(header_functions()) == set(mragan_hip.exported_symbols())
-    assert lib.mragan_abi_version() == 2
+    assert lib.mragan_abi_version() == 3
 
 
 def test_library_built_for_gfx950():
@@ -159,3 +159,33 @@ def test_engine_refuses_cpu_tensors():
     z, meta, model = _build("step_r6_s24_b2_nc2_lsgan")
     with pytest.raises(RuntimeError, match="HIP device only"):
         model.netG_A(torch.zeros(1, 2, 8, 8, 8))
+
+
+def test_unet_state_dict_and_plan():
+    """UnetGenerator (networks3D.py:270-343): the reference's nested keys (every weight the
+    reference fixture sampled exists here), only the outermost upconv has a bias, and the plan
+    runs outermost → innermost with the norms where the reference puts them."""
+    from mragan_hip.engine import compile_unet_generator
+    z, meta, model = _build("step_unet_s32_b2_ngf8")
+    sd = model.netG_A.state_dict()
+    ref_keys = {f.split("/")[2] for f in z.files if f.startswith("init/G_A/") and f.endswith("/idx")}
+    assert ref_keys and ref_keys <= set(sd)
+    assert [k for k in sd if k.endswith(".bias")] == ["model.model.3.bias"]
+    plan = compile_unet_generator(model.netG_A)
+    assert [lv.kind for lv in plan.levels] == ["outer", "mid", "mid", "mid", "inner"]
+    assert [lv.down.cout for lv in plan.levels] == [8, 16, 32, 64, 64]
+    assert [lv.up.cin for lv in plan.levels] == [16, 32, 64, 128, 64]
+    assert all(lv.down_norm is not None for lv in plan.levels[1:4])
+    assert plan.levels[-1].up_norm is not None and plan.levels[0].up_norm is None
+
+
+def test_unet_256_too_small_raises():
+    """unet_256 (8 downsamplings) cannot run on a 64³ patch in the reference either (SURVEY §8a
+    A18: an InstanceNorm over one voxel raises ValueError)."""
+    from mragan_hip.engine import UnetPlan, compile_unet_generator
+    from models import networks3D
+    net = networks3D.UnetGenerator(1, 1, 8, 8, norm_layer=networks3D.get_norm_layer('instance'))
+    plan = compile_unet_generator(net)
+    with pytest.raises(ValueError, match="more than 1 spatial element"):
+        UnetPlan._check_spatial((1, 64, 64, 64, 1), plan.levels)
+    UnetPlan._check_spatial((1, 256, 256, 256, 1), plan.levels)

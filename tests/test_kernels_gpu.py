@@ -69,6 +69,10 @@ CONV_CASES = [
     (1, 16, 2, 21, 7, 1, 0),
     (1, 8, 1, 20, 4, 1, 1),
     (2, 2, 32, 20, 7, 1, 0),
+    # UnetGenerator downconvs (k4 s2 p1): stem nc→ngf, down to a 1³ innermost output
+    (2, 1, 8, 16, 4, 2, 1),
+    (1, 64, 64, 2, 4, 2, 1),
+    (2, 16, 32, 8, 4, 2, 1),
 ]
 
 
@@ -127,6 +131,11 @@ CONVT_CASES = [
     (1, 16, 8, 5, 3, 2, 1, 1),
     (2, 32, 16, 4, 4, 2, 1, 0),
     (1, 24, 32, 5, 3, 1, 1, 0),
+    # UnetGenerator upconvs (k4 s2 p1): innermost 1³ → 2³, middle, outermost 2ngf → nc (thin)
+    (2, 64, 64, 1, 4, 2, 1, 0),
+    (1, 128, 32, 4, 4, 2, 1, 0),
+    (2, 16, 1, 8, 4, 2, 1, 0),
+    (1, 16, 2, 6, 4, 2, 1, 0),
 ]
 
 
@@ -351,3 +360,32 @@ def test_channel_sum(ops):
     out = torch.empty(12, device="cuda")
     ops.channel_sum(x.cuda(), out)
     assert rel(out, x.sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("N,cin,cout,S", [(2, 16, 1, 8), (1, 16, 2, 6)])
+def test_conv_transpose3d_thin_bias_tanh(ops, N, cin, cout, S):
+    """UnetGenerator outermost upconv: ConvTranspose3d(2ngf → nc, k4 s2 p1) + bias + Tanh fused."""
+    g = torch.Generator().manual_seed(cin + cout + S)
+    x = torch.randn(N, cin, S, S + 1, S, generator=g, dtype=torch.float64)
+    w = torch.randn(cin, cout, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    ref = torch.tanh(F.conv_transpose3d(x, w, b, stride=2, padding=1))
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, True, False), cout, 4, 2, 1, ref.shape[2:],
+                     bias=b.float().cuda(), act="tanh", transposed=True)
+    assert rel(ncdhw(out), ref) < TOL
+
+
+@pytest.mark.parametrize("Ca,Cb", [(8, 8), (16, 16), (3, 5)])
+def test_channel_concat_split(ops, Ca, Cb):
+    """UNet skip: relu(cat([lrelu(x), u], 1)) forward and its backward."""
+    g = torch.Generator().manual_seed(Ca * 10 + Cb)
+    a = torch.randn(2, Ca, 3, 4, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    u = torch.randn(2, Cb, 3, 4, 5, generator=g, dtype=torch.float64, requires_grad=True)
+    r = torch.relu(torch.cat([a, u], 1))
+    out = ops.channel_concat(ndhwc(a.detach().float()).cuda(), "relu", ndhwc(u.detach().float()).cuda(), None)
+    assert rel(ncdhw(out), torch.cat([torch.relu(a), u], 1).detach()) < 1e-7
+    dr = torch.randn(r.shape, generator=g, dtype=torch.float64)
+    da_ref, du_ref = torch.autograd.grad(r, (a, u), dr)
+    da, du = ops.channel_split(ndhwc(dr.float()).cuda(), Ca, ndhwc(a.detach().float()).cuda(), "relu", None, None)
+    assert rel(ncdhw(da), da_ref) < 1e-7
+    assert rel(ncdhw(du), dr[:, Ca:]) < 1e-7      # raw: the IN backward applies ReLU'

@@ -31,6 +31,8 @@ CASES = {
                                   "--ngf", "8", "--ndf", "8", "--no_lsgan"], 24, 2, 2, ["fp32", "fp64"], 2, 1),
     "step_r9_s32_b2_ngf16": (["--netG", "resnet_9blocks", "--ngf", "16", "--ndf", "16"], 32, 2, 1,
                              ["fp32", "fp64"], 3, 2),
+    # UnetGenerator (BASELINE configs[3] generator family; unet_custom = 5 downsamplings)
+    "step_unet_s32_b2_ngf8": (["--netG", "unet_custom", "--ngf", "8", "--ndf", "8"], 32, 2, 1, ["fp32", "fp64"], 2, 3),
 }
 N_SAMPLES = 256
 
