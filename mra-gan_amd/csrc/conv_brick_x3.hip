@@ -1,0 +1,307 @@
+// bf16x3 3×3×3 stride-1 convolution: LDS-resident input halo, weights streamed from L2 straight
+// into registers (gfx950).
+//
+// Same problem as conv_brick.hip (ResnetBlock convs networks3D.py:241-243, 256-257 and their
+// data gradients), re-organised around one measurement: the staged kernel spends ~1,500 cycles
+// per (tap × 32-channel) K-step of which the MFMAs are ~400 — it is bound by the per-step
+// barrier + staging round trip, not by the matrix pipe (rocprofv3: SQ_WAIT_ANY 42 % of wave
+// cycles, MFMA busy 25 %).  Here:
+//
+//   * the A operand (input voxels) comes from an LDS halo of the output brick, (BD+2)(BH+2)(BW+2)
+//     positions × 32 channels, split once into [hi 32 × bf16][lo 32 × bf16] 144-B rows; the next
+//     channel chunk's halo is streamed into the second buffer while the current chunk runs;
+//   * the B operand is NOT staged: the weights are pre-split once per call (brick_x3_pack) into
+//     bf16 hi/lo fragment order [tap][chunk][16-ch half][hi|lo][n][8-ch group][8], so each lane's
+//     MFMA fragment is one 16-B load and the 64 lanes of a wave read 1 KB contiguous; fragments
+//     are loaded kPF K-steps ahead into a register ring;
+//   * so the only barrier is one per 32-channel chunk (4 per 128-channel conv instead of 108),
+//     and every wave runs its 54 (tap, 16-channel) steps independently.
+//
+// Products: a·b ≈ a_hi·b_hi + a_hi·b_lo + a_lo·b_hi (three v_mfma_f32_32x32x16_bf16, fp32
+// accumulate; see conv_igemm_x3.hip for the error bound).
+#include "conv_geo.h"
+#include "kernels.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 32;                 // channels per chunk
+constexpr int kRow = 144;               // LDS row bytes: hi 64 B, lo 64 B, 16 B pad
+constexpr int kTaps = 27;
+constexpr int kSteps = 2 * kTaps;       // (tap, 16-channel half) steps per chunk
+
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
+  const f32x8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  hi = __builtin_convertvector(v, bf16x8);
+  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+}
+
+// packed weights [27][ny][C] fp32 → fragment order (see the file comment); one thread per 8
+// channels of one (tap, n)
+__global__ void brick_x3_pack_kernel(const float* __restrict__ wp, int ny, int C, __bf16* __restrict__ out) {
+  const int nch = C / kBK;
+  const int64_t total = (int64_t)kTaps * ny * (C / 8);
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(e % (C / 8));
+    const int64_t tn = e / (C / 8);
+    const int n = (int)(tn % ny), tap = (int)(tn / ny);
+    const float* src = wp + tn * C + g * 8;
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    bf16x8 hi, lo;
+    split8(a, b, hi, lo);
+    const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
+    const int64_t base = ((((int64_t)tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + (int64_t)n * 16 + lh * 8;
+    *reinterpret_cast<bf16x8*>(out + base) = hi;
+    *reinterpret_cast<bf16x8*>(out + base + (int64_t)ny * 16) = lo;
+  }
+}
+
+__device__ __forceinline__ void split4_store(char* row, int q, const float4& v) {
+  const f32x4 f = {v.x, v.y, v.z, v.w};
+  const bf16x4 h = __builtin_convertvector(f, bf16x4);
+  const bf16x4 l = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
+  *reinterpret_cast<bf16x4*>(row + 8 * q) = h;
+  *reinterpret_cast<bf16x4*>(row + 64 + 8 * q) = l;
+}
+
+}  // namespace
+
+template <int WM, int WN, int TM, int TN, int HMAX>
+__global__ void __launch_bounds__(WM * WN * 64)
+conv_brick_x3_kernel(BrickArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int NSL = (HMAX * 8 + NT - 1) / NT;      // halo float4 slices per thread per chunk
+  // next-chunk halo: slice s is loaded at step 3s and split + stored kHD steps later (a ring of
+  // 3 float4); vmcnt drains in issue order, so a load's real deadline is the next weight wait
+  // kPF steps on — kHD < kPF keeps the store inside that window
+  constexpr int kHD = 8;
+  static_assert(3 * (NSL - 1) + kHD < kSteps, "halo slices do not fit the chunk's steps");
+  static_assert(BN % 32 == 0 && BM % 32 == 0, "tile");
+  // weight prefetch distance in steps; divides kSteps so a ring slot maps to the same step
+  // residue in every chunk
+  constexpr int kPF = 9;
+  constexpr int kP = 18;                             // unrolled period: ring slots compile-time
+  static_assert(kSteps % kP == 0 && kP % kPF == 0 && kP % 9 == 0 && kHD < kPF, "step period");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* halo_buf = smem;                                                // [2][HMAX][kRow]
+  int* out_off = reinterpret_cast<int*>(smem + 2 * HMAX * kRow);       // [BM]
+  int* hoff = out_off + BM;                                            // [HMAX]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // tile → (instance, brick, n-block); XCD-aware order (n fastest, then bricks)
+  int L = blockIdx.x, tile = L;
+  if ((a.ntiles & 7) == 0) tile = (L & 7) * (a.ntiles >> 3) + (L >> 3);
+  const int nbk = tile % a.gn;
+  int rest = tile / a.gn;
+  const int bw_i = rest % a.nbw; rest /= a.nbw;
+  const int bh_i = rest % a.nbh; rest /= a.nbh;
+  const int bd_i = rest % a.nbd;
+  const int nb = rest / a.nbd;
+  const int od0 = bd_i * a.BD, oh0 = bh_i * a.BH, ow0 = bw_i * a.BW;
+  const int n0 = nbk * BN;
+  const int HP = a.HD * a.HH * a.HW;
+
+  for (int r = tid; r < BM; r += NT) {
+    int off = -1;
+    const int v = a.rowvox[r];
+    if (v >= 0) {
+      const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
+      const int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+    }
+    out_off[r] = off;
+  }
+  for (int pos = tid; pos < HP; pos += NT) {
+    const int hw = pos % a.HW, hh = (pos / a.HW) % a.HH, hd = pos / (a.HW * a.HH);
+    const int id = od0 - a.p + hd, ih = oh0 - a.p + hh, iw = ow0 - a.p + hw;
+    const bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+    hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C : -1;
+  }
+  // A: byte offset of each fragment row in a halo buffer (tap 0, this lane's 16-B half)
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int v = a.rowvox[wm0 + i * 32 + li];
+    if (v < 0) v = -v - 1;
+    const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
+    abase[i] = ((bd * a.HH + bh) * a.HW + bw) * kRow + lh * 16;
+  }
+  // B: this lane's 16-B fragment inside each (tap, chunk, half, hi|lo) block of the packed weights
+  const __bf16* wx = reinterpret_cast<const __bf16*>(a.wx3);
+  int boff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) boff[j] = (n0 + wn0 + j * 32 + li) * 16 + lh * 8;
+  const int nch_ = a.C / kBK;
+  const int64_t blk = (int64_t)a.ny * 16;       // one (hi|lo) block
+  const float* xb = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C;
+  const int nchunks = a.C / kBK;
+  __syncthreads();
+
+  // whole halo of chunk 0
+  {
+    float4 pv[NSL];                      // all loads in flight before the first store
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+      const int e = sl * NT + tid, pos = e >> 3;
+      const int o = pos < HP ? hoff[pos] : -1;
+      pv[sl] = *reinterpret_cast<const float4*>(xb + (o < 0 ? 0 : o) + 4 * (e & 7));
+      if (o < 0) pv[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+      const int e = sl * NT + tid, pos = e >> 3;
+      if (pos < HP) split4_store(halo_buf + pos * kRow, e & 7, pv[sl]);
+    }
+  }
+
+  // weight prefetch ring: slot s holds the two float4 of every n-tile for some step ≡ s (mod kPF)
+  bf16x8 rb[kPF][TN][2];
+  auto b_load = [&](int chunk, int u, bf16x8 (&dst)[TN][2]) __attribute__((always_inline)) {
+    const int t = u >> 1, kk = u & 1;
+    const int tap = a.flip ? kTaps - 1 - t : t;
+    const __bf16* src = wx + (((int64_t)tap * nch_ + chunk) * 2 + kk) * 2 * blk;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      dst[j][0] = *reinterpret_cast<const bf16x8*>(src + boff[j]);
+      dst[j][1] = *reinterpret_cast<const bf16x8*>(src + blk + boff[j]);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < kPF; ++u) b_load(0, u, rb[u]);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const char* H = halo_buf + (c & 1) * HMAX * kRow;
+    char* Hn = halo_buf + ((c + 1) & 1) * HMAX * kRow;
+    const bool stream = c + 1 < nchunks;
+    float4 rh[3];
+    bf16x8 af[2][2][TM];       // [step parity][hi|lo][fragment]
+    auto a_read = [&](int u, bf16x8 (&dst)[2][TM]) __attribute__((always_inline)) {
+      const int t = u >> 1, kk = u & 1;
+      const int tap_off = (((t / 9) * a.HH + (t / 3) % 3) * a.HW + t % 3) * kRow + kk * 32;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        dst[0][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off);
+        dst[1][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off + 64);
+      }
+    };
+    a_read(0, af[0]);
+    for (int u0 = 0; u0 < kSteps; u0 += kP) {
+#pragma unroll
+    for (int du = 0; du < kP; ++du) {
+      const int u = u0 + du;
+      // next chunk's halo: slice s = u/3 loaded into ring slot s mod 3 (u0/3 ≡ 0 mod 3) …
+      if (du % 3 == 0 && u / 3 < NSL) {
+        const int e = (u / 3) * NT + tid, hpos = e >> 3;
+        const int o = (stream && hpos < HP) ? hoff[hpos] : -1;
+        float4& r = rh[(du / 3) % 3];
+        r = *reinterpret_cast<const float4*>(xb + (o < 0 ? 0 : o) + (c + 1 < nchunks ? c + 1 : c) * kBK + 4 * (e & 7));
+        if (o < 0) r = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      // … and split + stored kHD steps later
+      if ((du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
+        const int e = ((u - kHD) / 3) * NT + tid, hpos = e >> 3;
+        if (stream && hpos < HP) split4_store(Hn + hpos * kRow, e & 7, rh[((du + kP - kHD) / 3) % 3]);
+      }
+      // B fragments of this step (loaded kPF steps ago), then refill the slot with step u + kPF
+      bf16x8 bh[TN], bl[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = rb[du % kPF][j][0];
+        bl[j] = rb[du % kPF][j][1];
+      }
+      {
+        const int un = u + kPF;
+        if (un < kSteps) b_load(c, un, rb[du % kPF]);
+        else b_load(c + 1 < nchunks ? c + 1 : c, un - kSteps, rb[du % kPF]);
+      }
+      // A fragments of the NEXT step from the halo (software pipelined: the LDS latency hides
+      // under this step's MFMAs; the chunk's first step is read after its barrier)
+      if (u + 1 < kSteps) a_read(u + 1, af[(du + 1) & 1]);
+      const bf16x8 (&ah)[TM] = af[du & 1][0];
+      const bf16x8 (&al)[TM] = af[du & 1][1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn0 + j * 32 + li;
+    const float bsum = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int off = out_off[row];
+        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int HMAX>
+static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
+  constexpr int BM = WM * TM * 32;
+  const size_t lds = (size_t)2 * HMAX * kRow + (size_t)(BM + HMAX) * sizeof(int);
+  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.ntiles), dim3(WM * WN * 64), lds, st, a);
+  return check_launch("conv_brick_x3");
+}
+
+// bm ∈ {64, 128}, bn ∈ {64, 128}: 4 waves (one per SIMD), wave tile (bm/2)×(bn/2) — the
+// 117 KB LDS halo allows one block per CU, and two-per-SIMD (8-wave) variants spill at kPF = 9
+size_t conv_brick_x3_ws_bytes(int C, int ny) { return (size_t)kTaps * C * ny * sizeof(float); }
+
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, hipStream_t st) {
+  const size_t need = conv_brick_x3_ws_bytes(a.C, a.ny);
+  if (!ws || ws_bytes < need) {
+    set_error("conv_brick_x3: workspace %zu < %zu", ws_bytes, need);
+    return kWorkspace;
+  }
+  const int64_t groups = (int64_t)kTaps * a.ny * (a.C / 8);
+  hipLaunchKernelGGL(brick_x3_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny, a.C,
+                     static_cast<__bf16*>(ws));
+  int rc = check_launch("brick_x3_pack");
+  if (rc) return rc;
+  a.wx3 = ws;
+  if (bm == 128 && bn == 128) return launch_brick_x3<2, 2, 2, 2, 400>(a, st);
+  if (bm == 128) return launch_brick_x3<2, 2, 2, 1, 400>(a, st);
+  if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300>(a, st);
+  return launch_brick_x3<2, 2, 1, 1, 300>(a, st);
+}
+
+}  // namespace mragan

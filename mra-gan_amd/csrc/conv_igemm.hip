@@ -245,7 +245,8 @@ size_t conv_igemm_ws_bytes(IgemmArgs a) {
   int64_t max_mc, total_m;
   igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return 0;
-  if (!g_brick_off && conv_brick_applicable(a)) return 0;
+  if (!g_brick_off && conv_brick_applicable(a))
+    return conv_brick_x3_active(a) ? conv_brick_x3_ws_bytes(a.cx, a.ny) : 0;
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_ws_bytes(a, max_mc, total_m);
   return 0;
 }

@@ -28,15 +28,20 @@ size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_
 struct BrickArgs {
   const float* x; int N, Di, Hi, Wi, C;
   const float* w;   // packed [27][ny][C]
+  const void* wx3;  // bf16x3 fragment-ordered copy of w (conv_brick_x3.hip), set by the launcher
   const float* bias;
   float* y; int Do, Ho, Wo, ny;
   int p, flip, act;
+  short rowvox[128];  // GEMM row → brick voxel (bd·BH + bh)·BW + bw; −v−1: padding row reading voxel v
   int BD, BH, BW;   // output brick
   int HD, HH, HW;   // its input halo
   int nbd, nbh, nbw, gn, ntiles;
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st);
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, hipStream_t st);
+size_t conv_brick_x3_ws_bytes(int C, int ny);
+bool conv_brick_x3_active(const IgemmArgs& a);
 
 struct ThinArgs {
   const float* x; int N, Di, Hi, Wi, cx;
