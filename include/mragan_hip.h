@@ -137,6 +137,9 @@ int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int accumul
 int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
                 int step, float grad_scale, void* stream);
 int mragan_fill(float* p, int64_t n, float value, void* stream);
+/* diagnostics: copy the per-block phase timestamps (s_memtime) the 1-channel bf16x3 convolution
+ * records when MRAGAN_STAMPS is set; n ≤ 40960 values, 5 per block. */
+int mragan_debug_stamps(unsigned long long* host, int n);
 
 #ifdef __cplusplus
 }

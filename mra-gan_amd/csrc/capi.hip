@@ -41,6 +41,8 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
+    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_x3_applicable(cin, cout, k, stride))
+      return conv_thin1_x3(a, ws, ws_bytes, st);
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
@@ -80,7 +82,9 @@ int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int 
 
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,
                                int Ho, int Wo, int transposed) {
-  if (thin_side(cin, cout)) return 0;
+  if (thin_side(cin, cout))
+    return (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_x3_applicable(cin, cout, k, stride)) ? thin1_x3_ws_bytes(cout)
+                                                                                                    : 0;
   IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, 0, 1,
               g_conv_precision == MRAGAN_PREC_BF16X3, nullptr, 0};
   return conv_igemm_ws_bytes(a);
@@ -190,6 +194,8 @@ int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   MRAGAN_CHECK_ARG(p && g && m && v && step >= 1, "adam: bad args");
   return adam(p, g, m, v, n, lr, beta1, beta2, eps, step, grad_scale, static_cast<hipStream_t>(stream));
 }
+
+int mragan_debug_stamps(unsigned long long* host, int n) { return thin1_debug_stamps(host, n); }
 
 int mragan_fill(float* p, int64_t n, float value, void* stream) {
   MRAGAN_CHECK_ARG(p, "fill: null");

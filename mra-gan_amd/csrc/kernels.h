@@ -51,6 +51,11 @@ struct ThinArgs {
   int k, s, p, trans, act;
 };
 int conv_thin(ThinArgs a, hipStream_t st);
+// bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)
+bool thin1_x3_applicable(int cx, int ny, int k, int s);
+size_t thin1_x3_ws_bytes(int ny);
+int conv_thin1_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
+int thin1_debug_stamps(unsigned long long* host, int n);
 
 struct WgradArgs {
   const float* D; int N, Dd, Hd, Wd, Cd;

@@ -53,6 +53,7 @@ SIGNATURES = {
     "mragan_channel_sum": (i32, [vp, i64, i32, vp, i32, vp, sz, vp]),
     "mragan_adam": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, f32, vp]),
     "mragan_fill": (i32, [vp, i64, f32, vp]),
+    "mragan_debug_stamps": (i32, [vp, i32]),
 }
 
 _lock = threading.Lock()

@@ -389,3 +389,25 @@ def test_channel_concat_split(ops, Ca, Cb):
     da, du = ops.channel_split(ndhwc(dr.float()).cuda(), Ca, ndhwc(a.detach().float()).cuda(), "relu", None, None)
     assert rel(ncdhw(da), da_ref) < 1e-7
     assert rel(ncdhw(du), dr[:, Ca:]) < 1e-7      # raw: the IN backward applies ReLU'
+
+
+@pytest.mark.parametrize("N,ngf,S,p", [(2, 32, 12, 0), (1, 32, 40, 0), (1, 32, 11, 3), (2, 32, 9, 3)])
+def test_thin1_bf16x3_stem_fwd_head_dgrad(x3, N, ngf, S, p):
+    """1 → ngf k7 s1 convolutions on the bf16x3 MFMA path (conv_thin1_x3.hip): the G stem forward
+    and the G head's data gradient (transposed form, flipped taps), incl. partial w/h/d tiles."""
+    ops = x3
+    g = torch.Generator().manual_seed(ngf + S + p)
+    x = torch.randn(N, 1, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(ngf, 1, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(ngf, generator=g, dtype=torch.float64)
+    y = F.conv3d(x, w, b, padding=p)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), ngf, 7, 1, p, y.shape[2:],
+                     bias=b.float().cuda(), act="lrelu")
+    assert rel(ncdhw(out), F.leaky_relu(y, 0.2)) < X3_TOL
+    xh = torch.randn(N, ngf, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    wh = torch.randn(1, ngf, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1
+    yh = F.conv3d(xh, wh, padding=p)
+    dy = torch.randn(yh.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(yh, xh, dy)
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wh, False, True), ngf, 7, 1, p, xh.shape[2:], transposed=True)
+    assert rel(ncdhw(dx), dx_ref) < X3_TOL
