@@ -91,7 +91,11 @@ size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout,
 }
 
 size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride) {
-  if (thin_wgrad_side(Cd, Cg)) return conv_thin_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k, stride);
+  if (thin_wgrad_side(Cd, Cg)) {
+    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+      return thin1_wgrad_x3_ws_bytes();
+    return conv_thin_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k, stride);
+  }
   return conv_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k);
 }
 
@@ -101,6 +105,8 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
   MRAGAN_CHECK_ARG(dense && gathered && dw && ws, "wgrad: null pointer");
   MRAGAN_CHECK_ARG(Cd > 0 && Cg > 0 && k >= 1 && stride >= 1 && pad >= 0, "wgrad: bad args");
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (thin_wgrad_side(Cd, Cg) && g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+    return conv_thin1_wgrad_x3(dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, pad, dw, accumulate, ws, ws_bytes, st);
   if (thin_wgrad_side(Cd, Cg)) {
     ThinWgradArgs a{};
     a.D = dense; a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd;

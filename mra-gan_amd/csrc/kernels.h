@@ -56,6 +56,11 @@ bool thin1_x3_applicable(int cx, int ny, int k, int s);
 size_t thin1_x3_ws_bytes(int ny);
 int conv_thin1_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
 int thin1_debug_stamps(unsigned long long* host, int n);
+// bf16x3 MFMA weight gradient of the 1-channel k7 s1 convolutions (conv_thin1_wgrad_x3.hip)
+bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s);
+size_t thin1_wgrad_x3_ws_bytes();
+int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
+                        int Cg, int p, float* out, int accumulate, void* ws, size_t ws_bytes, hipStream_t st);
 
 struct WgradArgs {
   const float* D; int N, Dd, Hd, Wd, Cd;

@@ -411,3 +411,29 @@ def test_thin1_bf16x3_stem_fwd_head_dgrad(x3, N, ngf, S, p):
     (dx_ref,) = torch.autograd.grad(yh, xh, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wh, False, True), ngf, 7, 1, p, xh.shape[2:], transposed=True)
     assert rel(ncdhw(dx), dx_ref) < X3_TOL
+
+
+@pytest.mark.parametrize("N,ngf,S,p", [(2, 32, 12, 0), (1, 32, 37, 0), (2, 32, 9, 3)])
+def test_thin1_bf16x3_wgrad(x3, N, ngf, S, p):
+    """Weight gradients of the 1-channel k7 convolutions on the bf16x3 MFMA path
+    (conv_thin1_wgrad_x3.hip): G stem Conv3d(1→ngf) and G head Conv3d(ngf→1), partial bricks."""
+    ops = x3
+    g = torch.Generator().manual_seed(7 * ngf + S + p)
+    x = torch.randn(N, 1, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = (torch.randn(ngf, 1, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv3d(x, w, padding=p)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw = torch.full((ngf, 1, 7, 7, 7), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 7, 1, p, dw, accumulate=False)
+    assert rel(dw, dw_ref) < X3_TOL
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 7, 1, p, dw, accumulate=True)
+    assert rel(dw, 2 * dw_ref) < X3_TOL
+    xh = torch.randn(N, ngf, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    wh = (torch.randn(1, ngf, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    yh = F.conv3d(xh, wh, padding=p)
+    dz = torch.randn(yh.shape, generator=g, dtype=torch.float64)
+    (dwh_ref,) = torch.autograd.grad(yh, wh, dz)
+    dwh = torch.empty(1, ngf, 7, 7, 7, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dz.float()).cuda(), ndhwc(xh.float()).cuda(), 7, 1, p, dwh, accumulate=False)
+    assert rel(dwh, dwh_ref) < X3_TOL
