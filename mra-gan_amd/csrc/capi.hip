@@ -43,6 +43,8 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
     if (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_x3_applicable(cin, cout, k, stride))
       return conv_thin1_x3(a, ws, ws_bytes, st);
+    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thinn_x3_applicable(cin, cout, k, stride))
+      return conv_thinn_x3(a, ws, ws_bytes, st);
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
@@ -82,9 +84,12 @@ int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int 
 
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,
                                int Ho, int Wo, int transposed) {
-  if (thin_side(cin, cout))
-    return (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_x3_applicable(cin, cout, k, stride)) ? thin1_x3_ws_bytes(cout)
-                                                                                                    : 0;
+  if (thin_side(cin, cout)) {
+    if (g_conv_precision != MRAGAN_PREC_BF16X3) return 0;
+    if (thin1_x3_applicable(cin, cout, k, stride)) return thin1_x3_ws_bytes(cout);
+    if (thinn_x3_applicable(cin, cout, k, stride)) return thinn_x3_ws_bytes();
+    return 0;
+  }
   IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, 0, 1,
               g_conv_precision == MRAGAN_PREC_BF16X3, nullptr, 0};
   return conv_igemm_ws_bytes(a);

@@ -1,0 +1,254 @@
+// bf16x3 MFMA convolution from 32 input channels to ONE output channel, k = 7, stride 1 (gfx950).
+//
+//   G head   Conv3d(ngf → 1, k7) + bias + Tanh on the RPad3 input     networks3D.py:211-213
+//   G stem   data gradient of Conv3d(1 → ngf, k7)                     networks3D.py:185-186
+//            (transposed form s = 1 = forward form, pad 6 − p, taps flipped)
+//
+//   z[o] = Σ_{kd,kh,kw,c} x[o − pe + (kd,kh,kw)][c] · W[kd,kh,kw][c]
+//
+// With one output channel the natural GEMM has N = 1.  Here the MFMA's 16 columns are
+// (j, kw) — two output depths od = 2q + j and the 8 (padded) w-taps — and its rows are input w
+// positions w', so one v_mfma_f32_16x16x32_bf16 produces the partial sums
+//
+//   P[w'][j, kw] = Σ_{kd',kh,c} x[2q + kd' − pe][oh + kh − pe][w' − pe][c] · W[kd' − j, kh, kw][c]
+//
+// over K = (input plane kd' = 0..7, kh, c); then z[2q + j][oh][ow] = Σ_kw P[ow + kw][j, kw]
+// (an LDS epilogue).  Useful fraction 7/8 (kd' vs kd) × 7/8 (kw) × 64/80 (w halo).
+//
+// Block = 2 output depths × 8 output rows (two per wave) × 64 output columns.  The input is
+// streamed in 16 units (plane kd' × 16-channel half): each unit's 14 × 80 positions × 16
+// channels are staged split into bf16 hi/lo (64-B swizzled LDS records), double-buffered with
+// one barrier per unit and register-prefetched two units ahead; the weights come pre-split in
+// fragment order from L2 (thinn_x3_pack).
+#include "kernels.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kK = 7;
+constexpr int kC = 32;                  // input channels
+constexpr int kOW = 64;                 // output columns per block
+constexpr int kMW = 80;                 // w' rows: 64 + 6 halo, 5 M-tiles of 16
+constexpr int kBH = 8;                  // output rows per block (two per wave)
+constexpr int kRH = kBH + kK - 1;       // staged rows per plane
+constexpr int kRec = 64;                // LDS bytes per position: 4 16-B chunks (hi 0-7, hi 8-15,
+                                        // lo 0-7, lo 8-15) rotated by (pos >> 2) & 3 so the 16
+                                        // consecutive positions of a fragment read hit 16 slots
+constexpr int kUnits = 16;              // 8 planes × 2 channel halves
+constexpr int kUnitBytes = kRH * kMW * kRec;
+constexpr int kNF4 = kRH * kMW * 4;     // float4 per unit (16 channels)
+constexpr int kF4PT = (kNF4 + 255) / 256;
+
+// weight fragment table: [kd' 8][half 2][step 4][hi|lo][lane 64][8 bf16]
+//   lane = 16g + n: column n = 8j + kw, k-group g → kh = 2·step + (g >> 1), channels
+//   16·half + 8(g & 1) … +7; zero where kd = kd' − j ∉ [0, 7), kh = 7 or kw = 7
+__global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, __bf16* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 8 * 2 * 4 * 64) return;
+  const int lane = i & 63, s = (i >> 6) & 3, half = (i >> 8) & 1, kdp = i >> 9;
+  const int n = lane & 15, g = lane >> 4;
+  const int j = n >> 3, kw = n & 7, kh = 2 * s + (g >> 1), kd = kdp - j;
+  const int c0 = 16 * half + 8 * (g & 1);
+  f32x8 v;
+  const bool ok = kd >= 0 && kd < kK && kh < kK && kw < kK;
+  const int t = ok ? (kd * kK + kh) * kK + kw : 0;
+  const int tt = flip ? kK * kK * kK - 1 - t : t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = ok ? wp[tt * kC + c0 + e] : 0.f;
+  const bf16x8 hi = __builtin_convertvector(v, bf16x8);
+  const bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+  const int64_t base = ((int64_t)((kdp * 2 + half) * 4 + s) * 2) * 64 * 8;
+  *reinterpret_cast<bf16x8*>(out + base + lane * 8) = hi;
+  *reinterpret_cast<bf16x8*>(out + base + 64 * 8 + lane * 8) = lo;
+}
+
+}  // namespace
+
+struct ThinnArgs {
+  const float* x; int N, Di, Hi, Wi;      // [N][Di][Hi][Wi][32]
+  const __bf16* wx;
+  const float* bias;
+  float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo]
+  int pe, act;
+  int nq, nr, nw;                         // depth pairs, row blocks, column blocks
+};
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+thinn_x3_kernel(ThinnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][kUnitBytes]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int blk = blockIdx.x;
+  const int cw = blk % a.nw; blk /= a.nw;
+  const int r = blk % a.nr; blk /= a.nr;
+  const int q = blk % a.nq;
+  const int nb = blk / a.nq;
+  const int od0 = 2 * q, oh0 = r * kBH, ow0 = cw * kOW;
+  const float* xb = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * kC;
+
+  // staging of one unit (plane kd', channel half) into registers / LDS
+  // per-thread element offsets inside an input plane (−1: outside the input), fixed per block
+  int poff[kF4PT];
+#pragma unroll
+  for (int l = 0; l < kF4PT; ++l) {
+    const int e = l * 256 + tid;
+    const int pos = e >> 2, cq = e & 3;
+    const int h = oh0 - a.pe + pos / kMW, w = ow0 - a.pe + pos % kMW;
+    const bool ok = e < kNF4 && (unsigned)h < (unsigned)a.Hi && (unsigned)w < (unsigned)a.Wi;
+    poff[l] = ok ? (h * a.Wi + w) * kC + 4 * cq : -1;
+  }
+  const int64_t plane = (int64_t)a.Hi * a.Wi * kC;
+  auto stage_load = [&](int u, float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
+    const int d = od0 + (u >> 1) - a.pe, half = u & 1;     // callers pass valid units only
+    const float* src = xb + d * plane + 16 * half;
+#pragma unroll
+    for (int l = 0; l < kF4PT; ++l) {
+      const float4 t = *reinterpret_cast<const float4*>(src + (poff[l] < 0 ? 0 : poff[l]));
+      sv[l] = poff[l] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : t;
+    }
+  };
+  // element l of this thread sits at position 64l + tid/4 (channels 4(tid&3)…): its chunk
+  // rotation ((c + pos/4) & 3) depends on tid only, so every store is base + 4096·l
+  const int cq = tid & 3;
+  const int st_hi = (tid >> 2) * kRec + 16 * (((cq >> 1) + (tid >> 4)) & 3) + 8 * (cq & 1);
+  const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1) + (tid >> 4)) & 3) + 8 * (cq & 1);
+  auto stage_store = [&](char* buf, const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int l = 0; l < kF4PT; ++l) {
+      if (l * 256 + tid < kNF4) {
+        const f32x4 f = {sv[l].x, sv[l].y, sv[l].z, sv[l].w};
+        const bf16x4 h = __builtin_convertvector(f, bf16x4);
+        const bf16x4 lo = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
+        *reinterpret_cast<bf16x4*>(buf + l * 64 * kRec + st_hi) = h;
+        *reinterpret_cast<bf16x4*>(buf + l * 64 * kRec + st_lo) = lo;
+      }
+    }
+  };
+
+  f32x4 acc[2][5];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[rr][i] = f32x4{};
+  const int n16 = lane & 15, g = lane >> 4;
+  const int a_hi = 16 * (((g & 1) + (n16 >> 2)) & 3), a_lo = 16 * ((2 + (g & 1) + (n16 >> 2)) & 3);
+  const __bf16* wx = a.wx;
+
+  // valid units (input plane inside the input) form a contiguous range [u0, u1)
+  int u0 = 0, u1 = kUnits;
+  while (u0 < kUnits && (od0 + (u0 >> 1) - a.pe) < 0) ++u0;
+  while (u1 > u0 && (od0 + ((u1 - 1) >> 1) - a.pe) >= a.Di) --u1;
+
+  auto compute = [&](int u, const char* buf) __attribute__((always_inline)) {
+    const int kdp = u >> 1, half = u & 1;
+    const __bf16* wt = wx + ((int64_t)(kdp * 2 + half) * 4) * 2 * 64 * 8;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 0) * 64 * 8 + lane * 8);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8);
+      int kh = 2 * s + (g >> 1);
+      kh = kh < kK ? kh : kK - 1;           // the padding kh = 7 has zero weights
+      // position (2wave + rr + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
+      // positions, so the chunk rotation is the lane's own (n16 / 4) — addresses fold to
+      // lane base + immediate
+      const char* rowp = buf + ((2 * wave + kh) * kMW + n16) * kRec;
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int mt = 0; mt < 5; ++mt) {
+          const int cofs = (rr * kMW + mt * 16) * kRec;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_hi);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo);
+          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[rr][mt], 0, 0, 0);
+          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[rr][mt], 0, 0, 0);
+          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[rr][mt], 0, 0, 0);
+        }
+    }
+  };
+
+  // pipeline: LDS buffer (u & 1) holds unit u; register set A/B holds the unit after it
+  float4 sA[kF4PT], sB[kF4PT];
+  if (u0 < u1) {
+    stage_load(u0, sA);
+    stage_store(smem + (u0 & 1) * kUnitBytes, sA);
+    if (u0 + 1 < u1) stage_load(u0 + 1, sA);
+  }
+  __syncthreads();
+  for (int u = u0; u < u1; u += 2) {
+    // unit u (registers: sA = u + 1); prefetch u + 2 into sB
+    if (u + 2 < u1) stage_load(u + 2, sB);
+    compute(u, smem + (u & 1) * kUnitBytes);
+    if (u + 1 < u1) stage_store(smem + ((u + 1) & 1) * kUnitBytes, sA);
+    __syncthreads();
+    if (u + 1 >= u1) break;
+    // unit u + 1 (registers: sB = u + 2); prefetch u + 3 into sA
+    if (u + 3 < u1) stage_load(u + 3, sA);
+    compute(u + 1, smem + ((u + 1) & 1) * kUnitBytes);
+    if (u + 2 < u1) stage_store(smem + (u & 1) * kUnitBytes, sB);
+    __syncthreads();
+  }
+
+  // epilogue: P[w'][n] (n = 8j + kw) of each of the wave's two rows through its LDS slot, then
+  // z[od0 + j][oh][ow] = Σ_kw P[ow − ow0 + kw][8j + kw]
+  float* P = reinterpret_cast<float*>(smem) + wave * kMW * 17;   // [80][16] padded to 17
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+    for (int mt = 0; mt < 5; ++mt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) P[(mt * 16 + g * 4 + e) * 17 + n16] = acc[rr][mt][e];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    const int oh = oh0 + 2 * wave + rr;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int o = k * 64 + lane;               // 128 outputs: j = o / 64, ow = o % 64
+      const int j = o >> 6, owl = o & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int kw = 0; kw < kK; ++kw) sum += P[(owl + kw) * 17 + 8 * j + kw];
+      const int od = od0 + j, ow = ow0 + owl;
+      if (od < a.Do && oh < a.Ho && ow < a.Wo)
+        a.y[(((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow] = act_fwd(sum + (a.bias ? a.bias[0] : 0.f), a.act);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+
+bool thinn_x3_applicable(int cx, int ny, int k, int s) { return cx == kC && ny == 1 && k == kK && s == 1; }
+
+size_t thinn_x3_ws_bytes() { return (size_t)8 * 2 * 4 * 2 * 64 * 8 * sizeof(__bf16); }
+
+int conv_thinn_x3(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!ws || ws_bytes < thinn_x3_ws_bytes()) {
+    set_error("thinn_x3: workspace %zu < %zu", ws_bytes, thinn_x3_ws_bytes());
+    return kWorkspace;
+  }
+  hipLaunchKernelGGL(thinn_x3_pack_kernel, dim3(16), dim3(256), 0, st, t.w, t.trans ? 1 : 0, static_cast<__bf16*>(ws));
+  int rc = check_launch("thinn_x3_pack");
+  if (rc) return rc;
+  ThinnArgs a{};
+  a.x = t.x; a.N = t.N; a.Di = t.Di; a.Hi = t.Hi; a.Wi = t.Wi;
+  a.wx = static_cast<const __bf16*>(ws);
+  a.bias = t.bias; a.y = t.y; a.Do = t.Do; a.Ho = t.Ho; a.Wo = t.Wo;
+  a.pe = t.trans ? kK - 1 - t.p : t.p;
+  a.act = t.act;
+  a.nq = ceil_div(t.Do, 2); a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
+  const int64_t blocks = (int64_t)a.N * a.nq * a.nr * a.nw;
+  if (blocks == 0) return kOk;
+  const size_t lds = (size_t)2 * kUnitBytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(thinn_x3_kernel, dim3((unsigned)blocks), dim3(256), lds, st, a);
+  return check_launch("thinn_x3");
+}
+
+}  // namespace mragan

@@ -56,6 +56,10 @@ bool thin1_x3_applicable(int cx, int ny, int k, int s);
 size_t thin1_x3_ws_bytes(int ny);
 int conv_thin1_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
 int thin1_debug_stamps(unsigned long long* host, int n);
+// bf16x3 MFMA path for 32 → 1-channel k7 s1 convolutions (conv_thinn_x3.hip)
+bool thinn_x3_applicable(int cx, int ny, int k, int s);
+size_t thinn_x3_ws_bytes();
+int conv_thinn_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
 // bf16x3 MFMA weight gradient of the 1-channel k7 s1 convolutions (conv_thin1_wgrad_x3.hip)
 bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s);
 size_t thin1_wgrad_x3_ws_bytes();

@@ -437,3 +437,25 @@ def test_thin1_bf16x3_wgrad(x3, N, ngf, S, p):
     dwh = torch.empty(1, ngf, 7, 7, 7, device="cuda")
     ops.conv3d_wgrad(ndhwc(dz.float()).cuda(), ndhwc(xh.float()).cuda(), 7, 1, p, dwh, accumulate=False)
     assert rel(dwh, dwh_ref) < X3_TOL
+
+
+@pytest.mark.parametrize("N,S,p", [(2, 12, 0), (1, 37, 0), (2, 9, 3), (1, 70, 0)])
+def test_thinn_bf16x3_head_fwd_stem_dgrad(x3, N, S, p):
+    """32 → 1 k7 s1 convolutions on the bf16x3 MFMA path (conv_thinn_x3.hip): the G head forward
+    (bias + tanh fused) and the G stem's data gradient (transposed form, flipped taps)."""
+    ops = x3
+    g = torch.Generator().manual_seed(3 * S + p + N)
+    x = torch.randn(N, 32, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(1, 32, 7, 7, 7, generator=g, dtype=torch.float64) * 0.05
+    b = torch.randn(1, generator=g, dtype=torch.float64)
+    y = torch.tanh(F.conv3d(x, w, b, padding=p))
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), 1, 7, 1, p, y.shape[2:],
+                     bias=b.float().cuda(), act="tanh")
+    assert rel(ncdhw(out), y) < X3_TOL
+    xs = torch.randn(N, 1, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    ws = torch.randn(32, 1, 7, 7, 7, generator=g, dtype=torch.float64) * 0.05
+    ys = F.conv3d(xs, ws, padding=p)
+    dy = torch.randn(ys.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(ys, xs, dy)
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, ws, False, True), 1, 7, 1, p, xs.shape[2:], transposed=True)
+    assert rel(ncdhw(dx), dx_ref) < X3_TOL
