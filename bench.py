@@ -10,7 +10,7 @@ gradients all-reduced inside the step.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 64] [--batch 2]
 
 Prints ONE JSON line on rank 0 (contract in the task description), with:
-  roofline     — the dominant kernel (res-block 3×3×3 conv, implicit-GEMM f32 MFMA): algorithmic
+  roofline     — the dominant kernel (res-block 3×3×3 conv, LDS-halo implicit GEMM): algorithmic
                  FLOP per launch ÷ its mean launch duration, timed with HIP events around every
                  such launch inside the timed region;
   cpu_baseline — the CPU oracle (oracle/cyclegan_oracle.py, the reference's algorithm restated
@@ -273,7 +273,8 @@ def main():
                  f"[{n_launch}x{s4}^3 in]")
         traffic = measured_traffic(f"unet_up1:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
     else:
-        kname = f"conv_brick_kernel (LDS-halo implicit GEMM, {prec}) res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd"
+        kname = (f"{'conv_brick_x3_kernel' if x3 else 'conv_brick_kernel'} (LDS-halo implicit GEMM, {prec}) "
+                 f"res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd")
         traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
