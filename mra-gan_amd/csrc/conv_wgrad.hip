@@ -299,16 +299,24 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   }
 }
 
-// out[dn][gn][t] (=|+=) Σ_z ws[z][t][dn][gn]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int Cd, int Cg, int T,
-                                    int splits, int accumulate) {
-  int64_t total = (int64_t)Cd * Cg * T;
+// out[dn][gn][t] (=|+=) Σ_z ws[z][t][dn][gn].  Thread per output with gn fastest, so every
+// slab read of a wave is 256 contiguous bytes; the single store per thread is the strided one.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int Cd,
+                                                           int Cg, int T, int splits, int accumulate) {
+  const int64_t total = (int64_t)Cd * Cg * T;
+  const int64_t plane = (int64_t)T * Cd * Cg;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int t = (int)(e % T); int64_t u = e / T;
-    int gn = (int)(u % Cg); int dn = (int)(u / Cg);
+    const int gn = (int)(e % Cg);
+    const int64_t u = e / Cg;
+    const int dn = (int)(u % Cd), t = (int)(u / Cd);
+    const float* src = ws + ((int64_t)t * Cd + dn) * Cg + gn;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[(((int64_t)z * T + t) * Cd + dn) * Cg + gn];
-    out[e] = accumulate ? out[e] + s : s;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4)
+      s += (src[z * plane] + src[(z + 1) * plane]) + (src[(z + 2) * plane] + src[(z + 3) * plane]);
+    for (; z < splits; ++z) s += src[z * plane];
+    float* dst = out + ((int64_t)dn * Cg + gn) * T + t;
+    *dst = accumulate ? *dst + s : s;
   }
 }
 
@@ -368,7 +376,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   if (rc) return rc;
   int64_t total = (int64_t)a.Cd * a.Cg * T;
   int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.ws, out, a.Cd, a.Cg, T, a.splits, accumulate);
   return check_launch("wgrad_reduce");
 }
