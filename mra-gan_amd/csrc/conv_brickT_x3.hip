@@ -1,0 +1,324 @@
+// bf16x3 transposed 3D convolution with stride 2 (k = 3 or 4) from an LDS-resident input halo
+// (gfx950).  Serves every stride-2 transposed form of the step:
+//
+//   G up-convs      ConvTranspose3d(k3 s2 p1 op1)                   networks3D.py:203-210
+//   G down-convs    data gradient of Conv3d(k3 s2 p1)               networks3D.py:191-197
+//   D layers 2, 3   data gradient of Conv3d(k4 s2 p1)               networks3D.py:395-405
+//   UNet            ConvTranspose3d(k4 s2 p1) and down-conv dgrads   networks3D.py:307-343
+//
+// y[o] = Σ_t x[(o + p − t)/2] · W[t]   over the taps with o + p − t even (per dimension).
+// The generic implicit GEMM (conv_igemm_x3) gathers every input row once per tap from L2 — for
+// these layers (K = 27·Cin/8 per output parity class, 32–64 output channels) that re-read is the
+// bound.  Here a block owns an output brick of 4 × 16 × 16 voxels; its input halo
+// 4 × 10 × 10 × (32-channel chunk) sits in LDS (bf16 hi/lo 144-B rows, next chunk prefetched in
+// registers), and wave w takes the 4 × 4 × 16 sub-brick at h = 4w…4w+3, which holds exactly one
+// 32-voxel M-tile of each of the 8 output parity classes — so every wave runs all 27 (k = 3) or 64
+// (k = 4) class taps and the waves stay balanced.  Within a class the input offset of a tap is a
+// wave-uniform constant, so an A fragment is one 16-B LDS read at lane base + immediate.
+// Weights come pre-split in fragment order from L2 (brickT_pack), used as the MFMA's A operand,
+// through buffer loads whose step offset is a scalar (no per-load address VGPRs), D steps ahead.
+// The next chunk's halo is read whole at the chunk's first step; out-of-volume positions get an
+// offset past the descriptor's range, so the hardware returns the zero padding.  The epilogue
+// transposes the accumulators through LDS into whole-voxel 16-B-per-lane non-temporal stores.
+// Measured at 4 × 32³ × 64 → 4 × 64³ × 32 (k3): 132 µs (conv_igemm_x3: 304 µs); the store
+// stream is the bound (the same kernel without stores: 60 µs).
+#include "kernels.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 32;                    // channels per chunk
+constexpr int kRow = 144;                  // LDS row: hi 64 B, lo 64 B, 16 B pad
+constexpr int kOD = 4, kOH = 16, kOW = 16; // output brick
+constexpr int kHD = 4, kHH = 10, kHW = 10; // input halo (k ≤ 4, p = 1)
+constexpr int kHP = kHD * kHH * kHW;       // 400 positions
+constexpr int kSL = (kHP * 8 + 255) / 256; // float4 per thread per chunk (13)
+
+// packed [T][ny][C] fp32 → [T][chunk][kk][hi|lo][ny][lh][8] bf16 (one thread per 8 channels)
+__global__ void brickT_pack_kernel(const float* __restrict__ wp, int T, int ny, int C, __bf16* __restrict__ out) {
+  const int nch = C / kBK;
+  const int64_t total = (int64_t)T * ny * (C / 8);
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(e % (C / 8));
+    const int64_t tn = e / (C / 8);
+    const int n = (int)(tn % ny), tap = (int)(tn / ny);
+    const float* src = wp + tn * C + g * 8;
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+    const f32x8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const bf16x8 hi = __builtin_convertvector(v, bf16x8);
+    const bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+    const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
+    const int64_t base = ((((int64_t)tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + (int64_t)n * 16 + lh * 8;
+    *reinterpret_cast<bf16x8*>(out + base) = hi;
+    *reinterpret_cast<bf16x8*>(out + base + (int64_t)ny * 16) = lo;
+  }
+}
+
+__device__ __forceinline__ int floordiv2(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+
+// Compile-time (class, tap) sequence for p = 1: class c = (cd, ch, cw) runs the taps t ≡ c + 1
+// (mod 2) per dimension; its input offset inside the halo is (3 + c − t)/2 per dimension (the
+// halo origin is o0/2 − 1 for k = 3 and 4).
+struct TStep { signed char c, od, oh, ow; short tap; };
+template <int K> struct TSteps {
+  static constexpr int N = K == 3 ? 27 : 64;
+  TStep s[N];
+  constexpr TSteps() : s{} {
+    int n = 0;
+    for (int c = 0; c < 8; ++c) {
+      const int cd = c >> 2, ch = (c >> 1) & 1, cw = c & 1;
+      for (int td = (cd + 1) & 1; td < K; td += 2)
+        for (int th = (ch + 1) & 1; th < K; th += 2)
+          for (int tw = (cw + 1) & 1; tw < K; tw += 2) {
+            s[n].c = (signed char)c;
+            s[n].od = (signed char)((3 + cd - td) / 2);
+            s[n].oh = (signed char)((3 + ch - th) / 2);
+            s[n].ow = (signed char)((3 + cw - tw) / 2);
+            s[n].tap = (short)((td * K + th) * K + tw);
+            ++n;
+          }
+    }
+  }
+};
+
+}  // namespace
+
+struct BrickTArgs {
+  const float* x; int N, Di, Hi, Wi, C;    // C = contraction channels (multiple of 32)
+  const __bf16* wx;                        // brickT_pack output
+  const float* bias;
+  float* y; int Do, Ho, Wo, ny;            // ny = 32
+  int k, p, act;
+  int nbd, nbh, nbw;
+};
+
+template <int K>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+brickT_x3_kernel(BrickTArgs a) {
+  constexpr TSteps<K> ts{};
+  constexpr int NS = 2 * TSteps<K>::N;          // (class tap, 16-channel half) steps per chunk
+  // weight prefetch distance in steps (divides NS: a ring slot is compile-time in every chunk)
+  constexpr int D = K == 3 ? 9 : 8;
+  // next-chunk halo: all slices are loaded (from HBM) at step 0 and split + stored at step kHD.
+  // vmcnt retires in issue order, so the first weight wait behind those loads (step D) absorbs
+  // their latency once per chunk; streaming them in slices instead exposes it once per slice.
+  constexpr int kHD = D + 1;
+  static_assert(NS % D == 0, "prefetch ring");
+  static_assert(kHD < NS, "halo store step");
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 × [kHP][kRow] + [kHP] offsets
+  int* hoff = reinterpret_cast<int*>(smem + 2 * kHP * kRow);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  int blk = blockIdx.x;
+  const int bw_i = blk % a.nbw; blk /= a.nbw;
+  const int bh_i = blk % a.nbh; blk /= a.nbh;
+  const int bd_i = blk % a.nbd;
+  const int nb = blk / a.nbd;
+  const int o0d = bd_i * kOD, o0h = bh_i * kOH, o0w = bw_i * kOW;
+  // halo origin: lowest input index any output of the brick reads (tap k−1)
+  const int i0d = floordiv2(o0d + a.p - (a.k - 1)), i0h = floordiv2(o0h + a.p - (a.k - 1)),
+            i0w = floordiv2(o0w + a.p - (a.k - 1));
+  // byte offsets into this instance's volume; out-of-volume positions get an offset past the
+  // descriptor's range, so the buffer load returns zeros (the transposed conv's implicit padding)
+  for (int pos = tid; pos < kHP; pos += 256) {
+    const int hw = pos % kHW, hh = (pos / kHW) % kHH, hd = pos / (kHW * kHH);
+    const int id = i0d + hd, ih = i0h + hh, iw = i0w + hw;
+    const bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+    hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C * 4 : (int)0x80000000;
+  }
+  const int vol_bytes = a.Di * a.Hi * a.Wi * a.C * 4;     // < 2^31 (brickT_x3_applicable)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C, 0, vol_bytes, 0x00020000);
+  const int nch = a.C / kBK;
+  const int blkw = a.ny * 32;                                        // one (hi|lo) block, bytes
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(a.wx), 0, K * K * K * nch * 4 * blkw, 0x00020000);
+  __syncthreads();
+
+  auto halo_off = [&](int s) __attribute__((always_inline)) {
+    const int e = s * 256 + tid, pos = e >> 3;
+    const int o = pos < kHP ? hoff[pos] : (int)0x80000000;
+    return o + 16 * (e & 7);
+  };
+  auto halo_store = [&](char* buf, int s, const float4& v) __attribute__((always_inline)) {
+    const int e = s * 256 + tid, pos = e >> 3, q = e & 7;
+    if (pos < kHP) {
+      const f32x4 f = {v.x, v.y, v.z, v.w};
+      const bf16x4 h = __builtin_convertvector(f, bf16x4);
+      const bf16x4 lo = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
+      *reinterpret_cast<bf16x4*>(buf + pos * kRow + 8 * q) = h;
+      *reinterpret_cast<bf16x4*>(buf + pos * kRow + 64 + 8 * q) = lo;
+    }
+  };
+  auto bload = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) __attribute__((always_inline)) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  };
+  auto xload = [&](int voff, int soff) __attribute__((always_inline)) { return bload(xr, voff, soff); };
+
+  // chunk 0's halo: all slices in flight before the first store
+  {
+    float4 pv[kSL];
+#pragma unroll
+    for (int s = 0; s < kSL; ++s) pv[s] = xload(halo_off(s), 0);
+#pragma unroll
+    for (int s = 0; s < kSL; ++s) halo_store(smem, s, pv[s]);
+  }
+
+  // lane li of a class tile = voxel (qd, qh, qw) = (li / 16, (li / 8) & 1, li & 7) of the class
+  // sub-grid; output o = o0 + 2q + c (+ 4·wave along h).  Input index of tap t: (o + p − t)/2 =
+  // i0 + [q + (o0 − 2·i0 + c + p − t)/2] → lane part q, the rest wave-uniform.
+  const int qd = li >> 4, qh = (li >> 3) & 1, qw = li & 7;
+  const int lane_row = ((qd * kHH) + qh + 2 * wave) * kHW + qw;     // halo position (tap part added)
+  const int wlane = li * 32 + lh * 16;                               // this lane's 16 B of a fragment
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = f32x16{};
+
+  // weights of step i: tap ts.s[i/2], half i&1 — one 16-B hi and lo fragment per lane; the step
+  // offset is wave-uniform (soffset), the lane part a constant voffset
+  auto b_load = [&](int chunk, int i, bf16x8 (&dst)[2]) __attribute__((always_inline)) {
+    const int so = (((ts.s[i >> 1].tap * nch + chunk) * 2 + (i & 1)) * 2) * blkw;
+    dst[0] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so));
+    dst[1] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so + blkw));
+  };
+  bf16x8 rb[D][2];
+#pragma unroll
+  for (int i = 0; i < D; ++i) b_load(0, i, rb[i]);
+  __syncthreads();
+
+  for (int chunk = 0; chunk < nch; ++chunk) {
+    const char* H = smem + (chunk & 1) * kHP * kRow + lh * 16 + lane_row * kRow;
+    char* Hn = smem + ((chunk + 1) & 1) * kHP * kRow;
+    const int cn = chunk + 1 < nch ? chunk + 1 : chunk;
+    auto a_read = [&](int i, bf16x8 (&dst)[2]) __attribute__((always_inline)) {
+      const TStep st = ts.s[i >> 1];
+      const char* arow = H + ((st.od * kHH + st.oh) * kHW + st.ow) * kRow + (i & 1) * 32;
+      dst[0] = *reinterpret_cast<const bf16x8*>(arow);
+      dst[1] = *reinterpret_cast<const bf16x8*>(arow + 64);
+    };
+    float4 pv[kSL];
+    bf16x8 af[2][2];
+    a_read(0, af[0]);
+#pragma clang loop unroll(full)
+    for (int i = 0; i < NS; ++i) {
+      // (unconditional: on the last chunk this re-reads chunk cn = chunk into the idle buffer —
+      // a branch here makes the compiler unswitch the loop and serialize the copy without it)
+      if (i == 0) {
+#pragma unroll
+        for (int sl = 0; sl < kSL; ++sl) pv[sl] = xload(halo_off(sl), cn * kBK * 4);
+      }
+      if (i == kHD) {
+#pragma unroll
+        for (int sl = 0; sl < kSL; ++sl) halo_store(Hn, sl, pv[sl]);
+      }
+      const int c = ts.s[i >> 1].c;
+      const bf16x8 bh = rb[i % D][0], bl = rb[i % D][1];
+      if (i + D < NS) b_load(chunk, i + D, rb[i % D]);
+      else b_load(cn, i + D - NS, rb[i % D]);
+      if (i + 1 < NS) a_read(i + 1, af[(i + 1) & 1]);
+      const bf16x8 ah = af[i & 1][0], al = af[i & 1][1];
+      // weights as the A operand (rows = output channels), voxels as B (cols)
+      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, ah, acc[c], 0, 0, 0);
+      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, al, acc[c], 0, 0, 0);
+      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, ah, acc[c], 0, 0, 0);
+      // pin each step's loads to their step: under register pressure the scheduler otherwise
+      // sinks the prefetches next to their uses (load → vmcnt(0) → MFMA, measured 8× slower)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue through LDS (the halo buffers are free after the last chunk's barrier): in the MFMA
+  // layout a store instruction writes 32 B into each of 32 voxel lines; transposed, each lane
+  // stores 16 B and 8 lanes a whole 128-B voxel, 64 lanes 8 w-consecutive voxels (1 KB).
+  // Two halves (output depth parity cd), 128 voxels × 144-B rows per wave each.
+  char* ew = smem + wave * (128 * kRow);
+  const int q = lane & 7;                                   // read-back: channel quad 4q … 4q+3
+  float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + 4 * q);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int c = half * 4; c < half * 4 + 4; ++c) {
+      const int v = (qd * 4 + 2 * qh + ((c >> 1) & 1)) * 16 + 2 * qw + (c & 1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(ew + v * kRow + (8 * g + 4 * lh) * 4) =
+            f32x4{acc[c][4 * g], acc[c][4 * g + 1], acc[c][4 * g + 2], acc[c][4 * g + 3]};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int v = j * 8 + (lane >> 3);
+      const int dq = v >> 6, hh = (v >> 4) & 3, ww = v & 15;
+      const int od = o0d + 2 * dq + half, oh = o0h + 4 * wave + hh, ow = o0w + ww;
+      const f32x4 t = *reinterpret_cast<const f32x4*>(ew + v * kRow + 16 * q);
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) {
+        const float4 r = make_float4(act_fwd(t[0] + bq.x, a.act), act_fwd(t[1] + bq.y, a.act),
+                                     act_fwd(t[2] + bq.z, a.act), act_fwd(t[3] + bq.w, a.act));
+        float4* dst = reinterpret_cast<float4*>(a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * a.ny + 4 * q);
+        // non-temporal: the 134 MB output stream otherwise evicts the weight fragments every
+        // block re-reads from L2 (measured 165 → 132 µs at 4 × 64³ × 32)
+        __builtin_nontemporal_store(f32x4{r.x, r.y, r.z, r.w}, reinterpret_cast<f32x4*>(dst));
+      }
+    }
+    if (half == 0) __syncthreads();
+  }
+}
+
+bool brickT_x3_applicable(const IgemmArgs& g) {
+  // ny = 32 only: at 64 output channels the 16 class accumulators take the whole AGPR file
+  // and the halo prefetch spills (those layers stay on conv_igemm_x3)
+  return g.x3 && g.trans && g.s == 2 && g.p == 1 && (g.k == 3 || g.k == 4) && g.cx % kBK == 0 && g.ny == 32 &&
+         (int64_t)g.Di * g.Hi * g.Wi * g.cx * 4 < ((int64_t)1 << 31);
+}
+
+// one static per kernel instantiation (the LDS opt-in is per function)
+template <int K>
+static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
+  const size_t lds = (size_t)2 * kHP * kRow + kHP * sizeof(int);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(brickT_x3_kernel<K>, dim3(blocks), dim3(256), lds, st, a);
+}
+
+size_t brickT_x3_ws_bytes(const IgemmArgs& g) { return (size_t)g.k * g.k * g.k * g.cx * g.ny * sizeof(float); }
+
+int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) {
+  const size_t need = brickT_x3_ws_bytes(g);
+  if (!g.ws || g.ws_bytes < need) {
+    set_error("brickT_x3: workspace %zu < %zu", g.ws_bytes, need);
+    return kWorkspace;
+  }
+  const int T = g.k * g.k * g.k;
+  const int64_t groups = (int64_t)T * g.ny * (g.cx / 8);
+  hipLaunchKernelGGL(brickT_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, g.w, T, g.ny, g.cx,
+                     reinterpret_cast<__bf16*>(g.ws));
+  int rc = check_launch("brickT_pack");
+  if (rc) return rc;
+  BrickTArgs a{};
+  a.x = g.x; a.N = g.N; a.Di = g.Di; a.Hi = g.Hi; a.Wi = g.Wi; a.C = g.cx;
+  a.wx = reinterpret_cast<const __bf16*>(g.ws);
+  a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
+  a.k = g.k; a.p = g.p; a.act = g.act;
+  a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, kOH); a.nbw = ceil_div(g.Wo, kOW);
+  const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
+  if (blocks == 0) return kOk;
+  if (g.k == 3) launch_brickT<3>(a, (unsigned)blocks, st);
+  else launch_brickT<4>(a, (unsigned)blocks, st);
+  return check_launch("brickT_x3");
+}
+
+}  // namespace mragan

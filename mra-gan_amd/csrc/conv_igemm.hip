@@ -247,6 +247,7 @@ size_t conv_igemm_ws_bytes(IgemmArgs a) {
   if (max_mc == 0 || a.ny == 0) return 0;
   if (!g_brick_off && conv_brick_applicable(a))
     return conv_brick_x3_active(a) ? conv_brick_x3_ws_bytes(a.cx, a.ny) : 0;
+  if (!g_brick_off && brickT_x3_applicable(a)) return brickT_x3_ws_bytes(a);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_ws_bytes(a, max_mc, total_m);
   return 0;
 }
@@ -258,6 +259,7 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return kOk;
   if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+  if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3(a, max_mc, total_m, st);
   if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);
   if (a.cx % 16 == 0) return dispatch_tile<16>(a, max_mc, total_m, st);

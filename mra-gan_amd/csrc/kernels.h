@@ -42,6 +42,10 @@ int conv_brick(const IgemmArgs& a, hipStream_t st);
 int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, hipStream_t st);
 size_t conv_brick_x3_ws_bytes(int C, int ny);
 bool conv_brick_x3_active(const IgemmArgs& a);
+// bf16x3 stride-2 transposed convolutions from an LDS halo (conv_brickT_x3.hip)
+bool brickT_x3_applicable(const IgemmArgs& a);
+size_t brickT_x3_ws_bytes(const IgemmArgs& a);
+int conv_brickT_x3(const IgemmArgs& a, hipStream_t st);
 
 struct ThinArgs {
   const float* x; int N, Di, Hi, Wi, cx;

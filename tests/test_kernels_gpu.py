@@ -459,3 +459,25 @@ def test_thinn_bf16x3_head_fwd_stem_dgrad(x3, N, S, p):
     (dx_ref,) = torch.autograd.grad(ys, xs, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, ws, False, True), 1, 7, 1, p, xs.shape[2:], transposed=True)
     assert rel(ncdhw(dx), dx_ref) < X3_TOL
+
+
+@pytest.mark.parametrize("N,cin,S,k,op", [(2, 64, 8, 3, 1), (1, 64, 13, 3, 1), (2, 128, 6, 4, 0), (1, 32, 9, 4, 0)])
+def test_brickT_bf16x3(x3, N, cin, S, k, op):
+    """Stride-2 transposed convolutions to 32 channels on the LDS-halo path (conv_brickT_x3.hip):
+    ConvTranspose3d k3 s2 p1 op1 / k4 s2 p1 forward and the equivalent Conv3d data gradients,
+    incl. partial output bricks."""
+    ops = x3
+    g = torch.Generator().manual_seed(cin + S + k)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(cin, 32, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv_transpose3d(x, w, stride=2, padding=1, output_padding=op)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, True, False), 32, k, 2, 1, y.shape[2:], transposed=True)
+    assert rel(ncdhw(out), y) < X3_TOL
+    # the same form as the data gradient of Conv3d(32 → cin, k, s2, p1)
+    xc = torch.randn(N, 32, 2 * S, 2 * S + 1, 2 * S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    wc = torch.randn(cin, 32, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    yc = F.conv3d(xc, wc, stride=2, padding=1)
+    dy = torch.randn(yc.shape, generator=g, dtype=torch.float64)
+    (dx_ref,) = torch.autograd.grad(yc, xc, dy)
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wc, False, True), 32, k, 2, 1, xc.shape[2:], transposed=True)
+    assert rel(ncdhw(dx), dx_ref) < X3_TOL

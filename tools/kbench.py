@@ -50,7 +50,14 @@ def main():
     gw_res = torch.empty(c4 * c4 * 27, device=dev)
     gw_head = torch.empty(343 * ngf, device=dev)
 
+    s2 = S // 2
+    x_up2 = rnd(N, s2, s2, s2, 2 * ngf)
+    w_up2 = rnd(27 * ngf * 2 * ngf) * 0.01
+    x_dn1 = rnd(N, S, S, S, ngf)
+    w_dn1 = rnd(27 * ngf * 2 * ngf) * 0.01
     table = {
+        "up2_fwd": lambda: ops.conv3d(x_up2, w_up2, ngf, 3, 2, 1, (S, S, S), transposed=True),
+        "down1_fwd": lambda: ops.conv3d(x_dn1, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2)),
         "head_fwd": lambda: ops.conv3d(x_head, w_head, 1, 7, 1, 0, (S, S, S), act="tanh"),
         "stem_dgrad": lambda: ops.conv3d(dh1, w_head, 1, 7, 1, 0, (S + 6,) * 3, transposed=True),
         "stem_fwd": lambda: ops.conv3d(x_stem, w_stem, ngf, 7, 1, 0, (S, S, S)),
