@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3"],
                     help="dense-conv contraction: exact f32 MFMA or split-bf16 (bf16x3) MFMA, fp32 accumulate")
     ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch the step's kernels from Python every step (default: replay the step as HIP graphs)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--same-device", action="store_true",
@@ -192,7 +194,7 @@ def main():
     sys_argv = sys.argv
     sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
                 "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
-                "--conv_precision", args.precision]
+                "--conv_precision", args.precision] + (["--no_cuda_graph"] if args.no_graph else [])
     opt = TrainOptions().gather_options()
     sys.argv = sys_argv
     opt.isTrain, opt.gpu_ids = True, 0
@@ -211,25 +213,27 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        model.set_input(inputs[i])
-        model.optimize_parameters()
-    barrier()
-
     # dominant kernel of the batched first G pass: resnet — residual-block conv 4ngf→4ngf k3
     # (forward form); unet — the level-1 upconv ConvTranspose3d(4ngf → ngf, k4 s2) (the largest
-    # conv of the net)
+    # conv of the net).  Its launches are bracketed by HIP events: recorded eagerly in --no-graph
+    # mode, recorded into the captured step graph otherwise (event nodes, re-recorded by every
+    # replay, so after the timed region they hold the last timed step's launches).
     unet = args.netG.startswith("unet")
     c4 = 4 * args.ngf
     s4 = args.size // 4
     n_launch = 2 * args.batch
-    ops.TIMER.reset()
     if unet:
-        ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == args.ngf and i["k"] == 4 and i["transposed"]
-                                     and i["N"] == n_launch)
+        match = lambda i: (i["cin"] == c4 and i["cout"] == args.ngf and i["k"] == 4 and i["transposed"]
+                           and i["N"] == n_launch)
     else:
-        ops.TIMER.match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
-                                     not i["transposed"] and i["N"] == n_launch)
+        match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
+                           not i["transposed"] and i["N"] == n_launch)
+    ops.TIMER.match = match
+    for i in range(args.warmup):
+        model.set_input(inputs[i])
+        model.optimize_parameters()
+    barrier()
+    ops.TIMER.reset()
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     barrier()
@@ -242,12 +246,27 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     ops.TIMER.match = None
+    graphed = getattr(model, "_graphs", None) is not None
     elapsed = start.elapsed_time(end) / 1e3
     elapsed = max(elapsed, wall)
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    timing = "HIP events around each launch inside the timed region"
+    if graphed:
+        # ROCm refuses timing events inside a captured graph (torch: "External events are
+        # disallowed in rocm"; hipEventRecordWithFlags(external) fails in capture), so the same
+        # launches are timed in two eager steps right after the timed region
+        ops.TIMER.reset()
+        ops.TIMER.match = match
+        model._use_graph = False
+        for i in range(2):
+            model.set_input(inputs[args.warmup + i])
+            model.optimize_parameters()
+        model._use_graph = True
+        ops.TIMER.match = None
+        timing = "HIP events around each launch, 2 eager steps right after the timed (graph-replayed) region"
     kern_ms = ops.TIMER.mean_ms()
     n_kern = len(ops.TIMER.events)
 
@@ -295,12 +314,13 @@ def main():
                                   else "BASELINE configs[1] shape") + "; fp32 tensors)",
                    "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "step_launch": "hip_graph" if graphed else "eager"},
         "roofline": {"bound": "mfma", "kernel": kname,
                      "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "launch_ms": round(kern_ms, 4) if kern_ms else None,
-                     "launches_timed": n_kern, "flop_per_launch": flops_launch},
+                     "launches_timed": n_kern, "flop_per_launch": flops_launch, "timing": timing},
         "step_tflop": round(step_tf, 4),
         "step_tflops_achieved": round(step_tf * args.steps / elapsed, 2),
     }

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 3
+#define MRAGAN_ABI_VERSION 4
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -136,6 +136,12 @@ int mragan_channel_sum(const float* x, int64_t M, int C, float* out, int accumul
  * the gradient is multiplied by grad_scale first (1/world_size after a SUM all-reduce).      */
 int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
                 int step, float grad_scale, void* stream);
+/* The same Adam step with its per-step scalars in device memory (CUDA-graph replay: the graph
+ * holds the pointer, the host refreshes the six floats before each replay).  mragan_adam_hyper
+ * (host only) writes {lr/bc1, beta1, beta2, eps, sqrt(bc2), grad_scale} for step `step` exactly
+ * as mragan_adam derives them, so both entry points produce identical parameters.            */
+int mragan_adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out6);
+int mragan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, void* stream);
 int mragan_fill(float* p, int64_t n, float value, void* stream);
 /* diagnostics: copy the per-block phase timestamps (s_memtime) the 1-channel bf16x3 convolution
  * records when MRAGAN_STAMPS is set; n ≤ 40960 values, 5 per block. */

@@ -206,6 +206,17 @@ int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
   return adam(p, g, m, v, n, lr, beta1, beta2, eps, step, grad_scale, static_cast<hipStream_t>(stream));
 }
 
+int mragan_adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out6) {
+  MRAGAN_CHECK_ARG(out6 && step >= 1, "adam_hyper: bad args");
+  adam_hyper(lr, beta1, beta2, eps, step, grad_scale, out6);
+  return kOk;
+}
+
+int mragan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, void* stream) {
+  MRAGAN_CHECK_ARG(p && g && m && v && hyper, "adam_dev: bad args");
+  return adam_dev(p, g, m, v, n, hyper, static_cast<hipStream_t>(stream));
+}
+
 int mragan_debug_stamps(unsigned long long* host, int n) { return thin1_debug_stamps(host, n); }
 
 int mragan_fill(float* p, int64_t n, float value, void* stream) {

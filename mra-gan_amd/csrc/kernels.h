@@ -125,6 +125,8 @@ int channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* ws,
 size_t channel_sum_ws_bytes(int64_t M, int C);
 int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
          float grad_scale, hipStream_t st);
+void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out);
+int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st);
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);
 int fill(float* p, int64_t n, float v, hipStream_t st);
 

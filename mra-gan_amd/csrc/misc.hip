@@ -238,6 +238,26 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// Graph-replayable variant: the per-step scalars come from device memory, hyper =
+// {step_size, beta1, beta2, eps, sqrt(bc2), grad_scale} (adam_hyper computes them exactly as
+// adam() does, so both paths produce identical bits)
+__global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, int64_t n, const float* __restrict__ hyper) {
+  const float step_size = hyper[0], beta1 = hyper[1], beta2 = hyper[2], eps = hyper[3], bc2_sqrt = hyper[4],
+              grad_scale = hyper[5];
+  const float w1 = 1.f - beta1;
+  GRID_STRIDE(i, n) {
+    const float gi = g[i] * grad_scale;
+    float mi = m[i];
+    mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
 // ---- weight packing: src[A][B][T] → dst[T][A][B] (transpose_ab=0) or dst[T][B][A] (=1) ----
 __global__ void pack_kernel(const float* __restrict__ src, int A, int B, int T, int tr, float* __restrict__ dst) {
   const int64_t total = (int64_t)A * B * T;
@@ -315,6 +335,20 @@ int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, floa
   hipLaunchKernelGGL(adam_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, step_size, beta1, beta2, eps,
                      (float)sqrt(bc2), grad_scale);
   return check_launch("adam");
+}
+void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out) {
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  out[0] = (float)((double)lr / bc1);
+  out[1] = beta1;
+  out[2] = beta2;
+  out[3] = eps;
+  out[4] = (float)sqrt(bc2);
+  out[5] = grad_scale;
+}
+int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st) {
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, hyper);
+  return check_launch("adam_dev");
 }
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st) {
   hipLaunchKernelGGL(pack_kernel, dim3(grid_cap((int64_t)A * B * T)), dim3(256), 0, st, src, A, B, T, tr, dst);

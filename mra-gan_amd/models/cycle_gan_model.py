@@ -60,12 +60,67 @@ class ImagePool():
         return out
 
 
+class DeviceImagePool:
+    """ImagePool.query as a device-side index plan, for the fused (and graph-replayed) step.
+
+    `plan()` makes exactly the reference's draws (`random.uniform`, then `random.randint` for a
+    swap; cycle_gan_model.py:20-35) on the host and resolves them into two index vectors;
+    `apply()` executes them on the device: the pool's slots live in one tensor
+    [slots | trash | this batch's fakes]; the returned batch is an index_select (a slot's old
+    image, or a fake), the stores an index_copy of the fakes into the slots that end up holding
+    them (the others go to the trash row).  Same images, same order as ImagePool."""
+
+    def __init__(self, pool_size):
+        self.pool_size = pool_size
+        self.num_imgs = 0
+        self.buf = None
+
+    def plan(self, b):
+        """Host draws for a batch of b fakes → (ret[b], store[b]) row indices into `buf`."""
+        P = self.pool_size
+        ret, holder = [], {}
+        for k in range(b):
+            if P == 0:
+                ret.append(P + 1 + k)
+            elif self.num_imgs < P:
+                holder[self.num_imgs] = k
+                self.num_imgs += 1
+                ret.append(P + 1 + k)
+            elif random.uniform(0, 1) > 0.5:
+                rid = random.randint(0, P - 1)
+                ret.append(P + 1 + holder[rid] if rid in holder else rid)
+                holder[rid] = k
+            else:
+                ret.append(P + 1 + k)
+        store = [P] * b
+        for slot, k in holder.items():
+            store[k] = slot
+        return ret, store
+
+    def apply(self, fakes, out, ret_idx, store_idx):
+        """fakes [b, ...] → out [b, ...]; ret_idx/store_idx: int64 index tensors from plan()."""
+        P, b = self.pool_size, fakes.shape[0]
+        shape = (P + 1 + b,) + tuple(fakes.shape[1:])
+        if self.buf is None or tuple(self.buf.shape) != shape or self.buf.device != fakes.device:
+            if self.buf is not None and self.num_imgs:
+                raise RuntimeError("DeviceImagePool: image shape changed with images in the pool")
+            self.buf = torch.zeros(shape, device=fakes.device, dtype=fakes.dtype)
+        self.buf[P + 1:].copy_(fakes)
+        torch.index_select(self.buf, 0, ret_idx, out=out)
+        self.buf.index_copy_(0, store_idx, fakes)
+
+
 def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
     return x.float().permute(0, 2, 3, 4, 1).contiguous()
 
 
 def _to_ncdhw(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 4, 1, 2, 3)
+
+
+def ops_mod():
+    from mragan_hip import ops
+    return ops
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -86,6 +141,30 @@ class FusedAdam(torch.optim.Optimizer):
         for n in self.nets:
             networks3D.ensure_flat(n)
             ops.fill(n._flat_grad, 0.0)
+
+    def advance(self):
+        """Host half of a step: bump the step count and return the kernel's six scalars."""
+        self.step_count += 1
+        g = self.param_groups[0]
+        beta1, beta2 = g['betas']
+        return ops_mod().adam_hyper(g['lr'], beta1, beta2, g['eps'], self.step_count, self.grad_scale)
+
+    def _state(self, n):
+        key = id(n)
+        if key not in self._m or self._m[key].numel() != n._flat_param.numel():
+            self._m[key] = torch.zeros_like(n._flat_param)
+            self._v[key] = torch.zeros_like(n._flat_param)
+        return self._m[key], self._v[key]
+
+    @torch.no_grad()
+    def step_dev(self, hyper):
+        """Device half: one fused Adam kernel per flat buffer with the scalars in `hyper`
+        (written by the host before the kernels run; graph-replayable)."""
+        for n in self.nets:
+            networks3D.ensure_flat(n)
+            m, v = self._state(n)
+            ops_mod().adam_dev(n._flat_param, n._flat_grad, m, v, hyper)
+            n.mark_params_dirty()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -145,8 +224,8 @@ class CycleGANModel(BaseModel):
                                               opt.init_type, opt.init_gain, self.gpu_ids)
             self.netD_B = networks3D.define_D(opt.input_nc, opt.ndf, opt.netD, opt.n_layers_D, opt.norm, use_sigmoid,
                                               opt.init_type, opt.init_gain, self.gpu_ids)
-            self.fake_A_pool = ImagePool(opt.pool_size)
-            self.fake_B_pool = ImagePool(opt.pool_size)
+            self.fake_A_pool = DeviceImagePool(opt.pool_size)
+            self.fake_B_pool = DeviceImagePool(opt.pool_size)
             self.use_lsgan = not opt.no_lsgan
             self.criterionGAN = networks3D.GANLoss(use_lsgan=self.use_lsgan).to(self.device)
             self.criterionCycle = torch.nn.L1Loss()
@@ -158,12 +237,27 @@ class CycleGANModel(BaseModel):
             for i, n in enumerate(self.loss_names):
                 setattr(self, 'loss_' + n, self._loss_buf[i])
         self._dist = None
+        self._use_graph = self.isTrain and not getattr(opt, 'no_cuda_graph', False) and self.device.type == 'cuda'
+        self._graphs = None          # (G-phase graph, D-phase graph) once captured
+        self._rs_tables = None       # running-stat update tables of the captured step
+        self._graph_key = None
+        self._eager_steps = 0
+        self._in = {}                # persistent input buffers (the graphs read them)
 
     # ------------------------------------------------------------------ inputs / visuals
     def set_input(self, input):
         AtoB = self.opt.which_direction == 'AtoB'
-        self.real_A = input[0 if AtoB else 1].to(self.device, non_blocking=True)
-        self.real_B = input[1 if AtoB else 0].to(self.device, non_blocking=True)
+        self.real_A = self._stage_input('A', input[0 if AtoB else 1])
+        self.real_B = self._stage_input('B', input[1 if AtoB else 0])
+
+    def _stage_input(self, key, x):
+        """Copy into a persistent device buffer (same values; a captured step reads it)."""
+        buf = self._in.get(key)
+        if buf is None or buf.shape != x.shape or buf.dtype != x.dtype:
+            buf = torch.empty(x.shape, dtype=x.dtype, device=self.device)
+            self._in[key] = buf
+        buf.copy_(x, non_blocking=True)
+        return buf
 
     def _publish(self, **ndhwc):
         for k, v in ndhwc.items():
@@ -249,15 +343,14 @@ class CycleGANModel(BaseModel):
         pGA.backward(self._cGA1, [dGA1])
         pGB.backward(self._cGB1, [dGB1])
 
-    def backward_D_basic(self, netD, real, fake, loss_slot):
+    def backward_D_basic(self, netD, real, pool, fakes, ret_idx, store_idx, loss_slot):
         """cycle_gan_model.py:138-149 with real and (pooled, detached) fake batched."""
         from mragan_hip import ops
         b = real.shape[0]
         plan = netD.plan
         x = torch.empty((2 * b,) + tuple(real.shape[1:]), device=real.device, dtype=torch.float32)
         x[:b].copy_(real)
-        for i, f in enumerate(fake):
-            x[b + i:b + i + 1].copy_(f)
+        pool.apply(fakes, x[b:], ret_idx, store_idx)
         ctx = plan.forward(x)
         dlog = torch.empty_like(ctx.out)
         ops.gan_loss(ctx.out[:b], 1.0, self.use_lsgan, 0.5, loss_slot, dlog[:b])
@@ -266,52 +359,132 @@ class CycleGANModel(BaseModel):
         return ctx
 
     def backward_D_A(self):
-        fake_B = self.fake_B_pool.query(self._fake_B)
-        self._cDA2 = self.backward_D_basic(self.netD_A, self._B, fake_B, self._loss_buf[0:1])
+        i = self._step_idx
+        self._cDA2 = self.backward_D_basic(self.netD_A, self._B, self.fake_B_pool, self._fake_B, i[0], i[1],
+                                           self._loss_buf[0:1])
 
     def backward_D_B(self):
-        fake_A = self.fake_A_pool.query(self._fake_A)
-        self._cDB2 = self.backward_D_basic(self.netD_B, self._A, fake_A, self._loss_buf[4:5])
+        i = self._step_idx
+        self._cDB2 = self.backward_D_basic(self.netD_B, self._A, self.fake_A_pool, self._fake_A, i[2], i[3],
+                                           self._loss_buf[4:5])
+
+    def _running_entries(self):
+        """Per network, the IN running-stat updates of this step in the reference's call order."""
+        b = self._b
+        return [self.netG_A.plan.running_entries([(self._cGA1, 0, b), (self._cGA2, 0, b), (self._cGA1, b, b)]),
+                self.netG_B.plan.running_entries([(self._cGB2, 0, b), (self._cGB1, 0, b), (self._cGB1, b, b)]),
+                self.netD_A.plan.running_entries([(self._cDA1, 0, b), (self._cDA2, 0, b), (self._cDA2, b, b)]),
+                self.netD_B.plan.running_entries([(self._cDB1, 0, b), (self._cDB2, 0, b), (self._cDB2, b, b)])]
 
     def _running_stats(self):
+        """Eager step: build the tables (pointers into this step's tensors) and launch."""
         from mragan_hip import engine
-        b = self._b
-        dev = self._A.device
-        keep = []
-        keep.append(engine.apply_running_updates(self.netG_A.plan.running_entries(
-            [(self._cGA1, 0, b), (self._cGA2, 0, b), (self._cGA1, b, b)]), dev))
-        keep.append(engine.apply_running_updates(self.netG_B.plan.running_entries(
-            [(self._cGB2, 0, b), (self._cGB1, 0, b), (self._cGB1, b, b)]), dev))
-        keep.append(engine.apply_running_updates(self.netD_A.plan.running_entries(
-            [(self._cDA1, 0, b), (self._cDA2, 0, b), (self._cDA2, b, b)]), dev))
-        keep.append(engine.apply_running_updates(self.netD_B.plan.running_entries(
-            [(self._cDB1, 0, b), (self._cDB2, 0, b), (self._cDB2, b, b)]), dev))
-        self._keep = keep
+        self._keep = [engine.apply_running_updates(e, self._A.device) for e in self._running_entries()]
 
-    def optimize_parameters(self):
-        """cycle_gan_model.py:227-240.  Single GPU: the reference's order.  Data parallel:
-        G all-reduce overlapped with the D phase (see mragan_hip/dist.py)."""
-        from mragan_hip.dist import GradSync, default_sync
-        if self._dist is None:
-            self._dist = default_sync() or False
+    def _running_stats_graphed(self):
+        """Replayed step: the captured tensors are replay-stable, so the tables are built once
+        per capture and the four small update kernels are launched after the D-phase replay."""
+        from mragan_hip import engine
+        if self._rs_tables is None:
+            self._rs_tables = [(engine.running_table(e, self._A.device), len(e)) for e in self._running_entries() if e]
+        for tab, n in self._rs_tables:
+            engine.launch_running_update(tab, n)
+
+    # ------------------------------------------------------------------ the step
+    def _prepare_step(self):
+        """Host half of a step: both pools' draws (reference order: fake_B_pool, then
+        fake_A_pool) and both Adam steps' scalars, shipped to device buffers that the kernels
+        (eager or replayed) read.  Returns nothing; the device buffers are persistent."""
+        b = self.real_A.shape[0]
+        retB, stB = self.fake_B_pool.plan(b)
+        retA, stA = self.fake_A_pool.plan(b)
+        hyp = self.optimizer_G.advance() + self.optimizer_D.advance()
+        idx = torch.tensor([retB, stB, retA, stA], dtype=torch.int64).pin_memory()
+        hyp = torch.tensor(hyp, dtype=torch.float32).pin_memory()
+        if getattr(self, '_step_idx', None) is None or self._step_idx.shape != idx.shape:
+            self._step_idx = torch.empty(idx.shape, dtype=torch.int64, device=self.device)
+            self._step_hyper = torch.empty(12, dtype=torch.float32, device=self.device)
+        self._step_idx.copy_(idx, non_blocking=True)
+        self._step_hyper.copy_(hyp, non_blocking=True)
+
+    def _phase_G(self):
         self.forward_train()
         self.set_requires_grad([self.netD_A, self.netD_B], False)
         self.optimizer_G.zero_grad()
         self.backward_G()
-        if not self._dist:
-            self.optimizer_G.step()
-        else:
-            sync_G = GradSync(self._dist.dist, self._dist.group)
-            sync_G.start([self.netG_A._flat_grad, self.netG_B._flat_grad])
+
+    def _phase_D(self):
         self.set_requires_grad([self.netD_A, self.netD_B], True)
         self.optimizer_D.zero_grad()
         self.backward_D_A()
         self.backward_D_B()
-        if self._dist:
+        if not torch.cuda.is_current_stream_capturing():
+            self._running_stats()
+
+    def _capture_key(self):
+        nets = (self.netG_A, self.netG_B, self.netD_A, self.netD_B)
+        return (tuple(self.real_A.shape), tuple(self.real_B.shape), self.real_A.data_ptr(), self.real_B.data_ptr(),
+                tuple(n._flat_param.data_ptr() for n in nets), tuple(n._flat_grad.data_ptr() for n in nets),
+                self._step_idx.data_ptr(), self._step_hyper.data_ptr(), bool(self._dist))
+
+    def _capture(self):
+        """Record the G phase and the D phase as two HIP graphs (one memory pool).  Capturing
+        launches nothing; the caller replays them for this step."""
+        for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+            n.mark_params_dirty()            # the graphs must contain the weight repacks
+        torch.cuda.synchronize()
+        gG, gD = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(gG, stream=side):
+            self._phase_G()
+        with torch.cuda.graph(gD, pool=gG.pool(), stream=side):
+            self._phase_D()
+        torch.cuda.current_stream().wait_stream(side)
+        self._rs_tables = None
+        self._graphs = (gG, gD)
+        self._graph_key = self._capture_key()
+
+    def optimize_parameters(self):
+        """cycle_gan_model.py:227-240.  Single GPU: G phase, G Adam, D phase, D Adam (the
+        reference's order up to the exact reordering below).  Data parallel: the G all-reduce
+        overlaps the D phase (mragan_hip/dist.py) and both Adam steps follow it — exact, since
+        the D phase reads only pre-update fakes and D weights.  From the second step on, both
+        phases are replayed HIP graphs (captured once; `--no_cuda_graph` to disable)."""
+        from mragan_hip.dist import GradSync, default_sync
+        if self._dist is None:
+            self._dist = default_sync() or False
+            scale = 1.0 / self._dist.world if self._dist else 1.0
+            self.optimizer_G.grad_scale = self.optimizer_D.grad_scale = scale
+        for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+            networks3D.ensure_flat(n)
+        self._prepare_step()
+        hG, hD = self._step_hyper[0:6], self._step_hyper[6:12]
+        graphed = False
+        if self._use_graph and self._eager_steps >= 1:
+            if self._graphs is None or self._graph_key != self._capture_key():
+                self._capture()
+            graphed = True
+        run_G = self._graphs[0].replay if graphed else self._phase_G
+        run_D = self._graphs[1].replay if graphed else self._phase_D
+        run_G()
+        if graphed:
+            run_D = lambda: (self._graphs[1].replay(), self._running_stats_graphed())
+        if not self._dist:
+            self.optimizer_G.step_dev(hG)
+            run_D()
+        else:
+            sync_G = GradSync(self._dist.dist, self._dist.group)
+            sync_G.start([self.netG_A._flat_grad, self.netG_B._flat_grad])
+            run_D()
             sync_D = GradSync(self._dist.dist, self._dist.group)
             sync_D.start([self.netD_A._flat_grad, self.netD_B._flat_grad])
-            self.optimizer_G.grad_scale = sync_G.finish()
-            self.optimizer_G.step()
-            self.optimizer_D.grad_scale = sync_D.finish()
-        self.optimizer_D.step()
-        self._running_stats()
+            sync_G.finish()
+            self.optimizer_G.step_dev(hG)
+            sync_D.finish()
+        self.optimizer_D.step_dev(hD)
+        if graphed:
+            for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+                n.mark_params_dirty()
+        else:
+            self._eager_steps += 1

@@ -305,6 +305,17 @@ def apply_running_updates(entries, device):
     """Launch the running-stat update for a list of entries from NetPlan.running_entries."""
     if not entries:
         return
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("running-statistics update inside a HIP graph capture: launch it outside the graph "
+                           "with a table from running_table()")
+    dev = running_table(entries, device)
+    launch_running_update(dev, len(entries))
+    return dev   # keep alive until the stream consumed it (caller holds the reference)
+
+
+def running_table(entries, device):
+    """Device copy of the update table for `entries` (pointers only: reusable for as long as
+    the tensors it points to live, e.g. across replays of a captured step)."""
     arr = (_Entry * len(entries))()
     for e, (norm, bias, C_, S, segs) in zip(arr, entries):
         if len(segs) > 8:
@@ -320,10 +331,12 @@ def apply_running_updates(entries, device):
             e.seg[j].rstd = rp
             e.seg[j].count = cnt
     host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-    dev = host.to(device, non_blocking=False)
-    call("mragan_instnorm_running_update", dev.data_ptr(), len(entries), C.c_float(IN_MOMENTUM),
+    return host.pin_memory().to(device, non_blocking=True)
+
+
+def launch_running_update(table, n):
+    call("mragan_instnorm_running_update", table.data_ptr(), n, C.c_float(IN_MOMENTUM),
          torch.cuda.current_stream().cuda_stream)
-    return dev   # keep alive until the stream consumed it (caller holds the reference)
 
 
 # --------------------------------------------------------------------------------------

@@ -36,11 +36,16 @@ class Workspace:
 
     def __init__(self):
         self._buf = {}
+        self._retired = []      # outgrown buffers stay allocated: a captured HIP graph may hold them
 
     def get(self, nbytes: int) -> torch.Tensor:
         dev = torch.cuda.current_device()
         b = self._buf.get(dev)
         if b is None or b.numel() < nbytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("workspace growth during HIP graph capture (run the step eagerly first)")
+            if b is not None:
+                self._retired.append(b)
             b = torch.empty(max(int(nbytes * 1.25), 1 << 20), dtype=torch.uint8, device=f"cuda:{dev}")
             self._buf[dev] = b
         return b
@@ -60,8 +65,9 @@ class KernelTimer:
     def begin(self, info):
         if self.match is None or not self.match(info):
             return None
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
+        if torch.cuda.is_current_stream_capturing():
+            return None         # ROCm cannot time event nodes of a graph: eager launches only
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         return (s, e)
 
@@ -278,6 +284,21 @@ def adam(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, lr:
          eps: float, step: int, grad_scale: float = 1.0):
     call("mragan_adam", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
          int(step), float(grad_scale), _stream())
+
+
+def adam_hyper(lr: float, beta1: float, beta2: float, eps: float, step: int, grad_scale: float = 1.0):
+    """Host: the six per-step Adam scalars mragan_adam_dev reads (see include/mragan_hip.h)."""
+    import ctypes as C
+    out = (C.c_float * 6)()
+    call("mragan_adam_hyper", float(lr), float(beta1), float(beta2), float(eps), int(step), float(grad_scale), out)
+    return list(out)
+
+
+def adam_dev(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hyper: torch.Tensor):
+    """Adam step whose scalars live in device memory (hyper: 6 fp32 values) — graph-replayable."""
+    if hyper.dtype != torch.float32 or hyper.numel() < 6 or not hyper.is_cuda:
+        raise ValueError("adam_dev: hyper must be a device float32 tensor of 6 values")
+    call("mragan_adam_dev", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(hyper), _stream())
 
 
 def fill(t: torch.Tensor, value: float):

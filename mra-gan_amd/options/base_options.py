@@ -47,6 +47,10 @@ BASE_FLAGS = [
     # engine-only flag (not in the reference): contraction precision of the dense MFMA convolutions
     ('--conv_precision', dict(type=str, default='f32', choices=['f32', 'bf16x3'],
                               help='f32: exact fp32 MFMA; bf16x3: split-bf16 MFMA with fp32 accumulation')),
+    # engine-only flag: run optimize_parameters() as captured HIP graphs after its first step
+    ('--no_cuda_graph', dict(action='store_true',
+                             help='launch every kernel of the training step from Python instead of replaying '
+                                  'the step captured as HIP graphs')),
 ]
 
 

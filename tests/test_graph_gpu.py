@@ -1,0 +1,66 @@
+"""The HIP-graph step (default from the 2nd optimize_parameters() on) against the eager step
+(--no_cuda_graph): identical kernels in identical order, so losses, parameters, running
+statistics and generated volumes must agree bit for bit over several steps — with a 2-image
+pool, so the steps exercise the pool's swaps, and with an lr scheduler changing lr between
+steps (the graph reads Adam's scalars from device memory)."""
+import random
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tmp_path, graph, steps, precision):
+    from models import create_model
+    from options.train_options import TrainOptions
+    argv = sys.argv
+    try:
+        sys.argv = ["train.py", "--checkpoints_dir", str(tmp_path), "--conv_precision", precision,
+                    "--netG", "resnet_6blocks", "--ngf", "8", "--ndf", "8", "--pool_size", "2",
+                    "--batch_size", "2", "--lr_policy", "step", "--lr_decay_iters", "1"]
+        if not graph:
+            sys.argv.append("--no_cuda_graph")
+        opt = TrainOptions().gather_options()
+    finally:
+        sys.argv = argv
+    opt.isTrain, opt.gpu_ids = True, 0
+    torch.manual_seed(3)
+    random.seed(3)
+    model = create_model(opt)
+    model.setup(opt)
+    g = torch.Generator().manual_seed(5)
+    losses = []
+    for step in range(steps):
+        A = torch.randn(2, 1, 24, 24, 24, generator=g)
+        B = torch.randn(2, 1, 24, 24, 24, generator=g)
+        model.set_input([A, B])
+        model.optimize_parameters()
+        losses.append(torch.stack([getattr(model, "loss_" + n).detach().clone() for n in model.loss_names]))
+        if step == 2:
+            model.update_learning_rate()
+    torch.cuda.synchronize()
+    state = {}
+    for n in ("G_A", "G_B", "D_A", "D_B"):
+        for k, v in getattr(model, "net" + n).state_dict().items():
+            state[f"{n}/{k}"] = v.detach().cpu().clone()
+    vis = {v: getattr(model, v).detach().cpu().clone() for v in ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A")}
+    return torch.stack(losses).cpu(), state, vis, model
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_graph_step_bit_identical_to_eager(tmp_path, precision):
+    from mragan_hip import ops
+    try:
+        le, se, ve, me = _run(tmp_path / "e", False, 6, precision)
+        lg, sg, vg, mg = _run(tmp_path / "g", True, 6, precision)
+    finally:
+        ops.set_conv_precision("f32")
+    assert me._graphs is None and mg._graphs is not None
+    assert mg.fake_B_pool.num_imgs == 2
+    assert torch.equal(le, lg), (le - lg).abs().max()
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+    for k in ve:
+        assert torch.equal(ve[k], vg[k]), k
