@@ -18,6 +18,20 @@ namespace mragan {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Logical (tile, tap, split) of this block.  Workgroups are dispatched round-robin over the 8
+// XCDs in flattened-id order; remapping id L → (L mod 8)·(B/8) + L/8 gives each XCD a contiguous
+// range of splits with all their taps, so its L2 holds 1/8 of the voxel range instead of
+// every XCD streaming all of it (the taps re-read the same dy/x rows).
+__device__ __forceinline__ void wgrad_block(int& bx, int& by, int& bz) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int B = gx * gy * gridDim.z;
+  int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
+  bx = L % gx;
+  by = (L / gx) % gy;
+  bz = L / (gx * gy);
+}
+
 
 template <int WM, int WN, int TM, int TN>
 __global__ void __launch_bounds__(256)
@@ -35,11 +49,13 @@ conv_wgrad_f32_kernel(WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
   const int ntn = (a.Cg + BN - 1) / BN;
-  const int dn0 = (blockIdx.x / ntn) * BM, gn0 = (blockIdx.x % ntn) * BN;
-  const int t = blockIdx.y;
+  int bx, by, bz;
+  wgrad_block(bx, by, bz);
+  const int dn0 = (bx / ntn) * BM, gn0 = (bx % ntn) * BN;
+  const int t = by;
   const int tw = t % a.k, th = (t / a.k) % a.k, td = t / (a.k * a.k);
   const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
-  const int64_t mb = (int64_t)blockIdx.z * a.chunk;
+  const int64_t mb = (int64_t)bz * a.chunk;
   const int64_t me = min(M, mb + a.chunk);
   const int nK = (int)((me - mb + BKm - 1) / BKm);
 
@@ -120,7 +136,7 @@ conv_wgrad_f32_kernel(WgradArgs a) {
   }
 
   const int T = a.k * a.k * a.k;
-  float* slab = a.ws + ((int64_t)blockIdx.z * T + t) * a.Cd * a.Cg;
+  float* slab = a.ws + ((int64_t)bz * T + t) * a.Cd * a.Cg;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     int col = gn0 + wn0 + j * 32 + li;
@@ -176,11 +192,13 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
   const int li = lane & 31, lh = lane >> 5;
   const int ntn = (a.Cg + BN - 1) / BN;
-  const int dn0 = (blockIdx.x / ntn) * BM, gn0 = (blockIdx.x % ntn) * BN;
-  const int t = blockIdx.y;
+  int bx, by, bz;
+  wgrad_block(bx, by, bz);
+  const int dn0 = (bx / ntn) * BM, gn0 = (bx % ntn) * BN;
+  const int t = by;
   const int tw = t % a.k, th = (t / a.k) % a.k, td = t / (a.k * a.k);
   const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
-  const int64_t mb = (int64_t)blockIdx.z * a.chunk;
+  const int64_t mb = (int64_t)bz * a.chunk;
   const int64_t me = min(M, mb + a.chunk);
   const int nK = (int)((me - mb + BKm - 1) / BKm);
 
@@ -191,26 +209,35 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   const bool cd_ok = do_d && cd < a.Cd, cg_ok = do_g && cg < a.Cg;
 
   float4 rd[4], rg[4];
-  auto load = [&](int ks) __attribute__((always_inline)) {
-    const int64_t m_base = mb + (int64_t)ks * BKm + 4 * vq;
-    // voxel coordinates of m_base, then +1 with carry for the next three
-    int64_t mm = m_base < M ? m_base : M - 1;
-    int mw = (int)(mm % a.Wd); int64_t u = mm / a.Wd;
-    int mh = (int)(u % a.Hd); u /= a.Hd;
-    int md = (int)(u % a.Dd); int nb = (int)(u / a.Dd);
+  // voxel coordinates of this thread's first voxel of the current K-step, advanced by BKm per
+  // step with carries (32-bit index math: conv_wgrad checks that every offset fits)
+  int cm = (int)min(mb + 4 * vq, M - 1);
+  int cw = cm % a.Wd, ch_ = (cm / a.Wd) % a.Hd, cdd = (cm / (a.Wd * a.Hd)) % a.Dd, cn = cm / (a.Wd * a.Hd * a.Dd);
+  int m_base = (int)mb + 4 * vq;
+  const int me32 = (int)me;
+  auto load = [&]() __attribute__((always_inline)) {
+    int mw = cw, mh = ch_, md = cdd, nb = cn;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int64_t m = m_base + s;
-      const bool m_ok = m < me;
-      const float4 dv = *reinterpret_cast<const float4*>(a.D + (m_ok ? m : mb) * a.Cd + (cd_ok ? cd : 0));
+      const int m = m_base + s;
+      const bool m_ok = m < me32;
+      const float4 dv = *reinterpret_cast<const float4*>(a.D + (m_ok ? m : (int)mb) * a.Cd + (cd_ok ? cd : 0));
       rd[s] = (m_ok && cd_ok) ? dv : make_float4(0.f, 0.f, 0.f, 0.f);
       const int gd = md * a.s - a.p + td, gh = mh * a.s - a.p + th, gw = mw * a.s - a.p + tw;
       const bool g_in = m_ok && cg_ok && (unsigned)gd < (unsigned)a.Dg && (unsigned)gh < (unsigned)a.Hg &&
                         (unsigned)gw < (unsigned)a.Wg;
-      const int64_t goff = g_in ? ((((int64_t)nb * a.Dg + gd) * a.Hg + gh) * a.Wg + gw) * a.Cg + cg : 0;
+      const int goff = g_in ? (((nb * a.Dg + gd) * a.Hg + gh) * a.Wg + gw) * a.Cg + cg : 0;
       const float4 gv = *reinterpret_cast<const float4*>(a.G + goff);
       rg[s] = g_in ? gv : make_float4(0.f, 0.f, 0.f, 0.f);
       if (++mw == a.Wd) { mw = 0; if (++mh == a.Hd) { mh = 0; if (++md == a.Dd) { md = 0; ++nb; } } }
+    }
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
+    m_base += BKm;
+    cw += BKm;
+    while (cw >= a.Wd) {
+      cw -= a.Wd;
+      if (++ch_ == a.Hd) { ch_ = 0; if (++cdd == a.Dd) { cdd = 0; ++cn; } }
     }
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
@@ -247,12 +274,13 @@ conv_wgrad_x3_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
-  load(0);
+  load();
   store(0);
   __syncthreads();
   for (int ks = 0; ks < nK; ++ks) {
     const int buf = ks & 1;
-    load(ks + 1 < nK ? ks + 1 : ks);          // unconditional (last step reloads itself, unused)
+    if (ks + 1 < nK) advance();
+    load();                                   // unconditional (last step reloads itself, unused)
     const char* A = smem + buf * STAGE;
     const char* B = A + BM * kWRow;
 #pragma unroll
@@ -284,7 +312,7 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   }
 
   const int T = a.k * a.k * a.k;
-  float* slab = a.ws + ((int64_t)blockIdx.z * T + t) * a.Cd * a.Cg;
+  float* slab = a.ws + ((int64_t)bz * T + t) * a.Cd * a.Cg;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     int col = gn0 + wn0 + j * 32 + li;
@@ -355,7 +383,20 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
     set_error("conv_wgrad: workspace %zu < %zu", ws_bytes, need);
     return kWorkspace;
   }
-  if (a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0) {
+  static const bool no_w3 = getenv("MRAGAN_NO_WGRAD3") != nullptr;   // A/B switch
+  if (!no_w3 && wgrad3_x3_applicable(a)) {
+    const int used = conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st);
+    int rc = check_launch("wgrad3_x3");
+    if (rc) return rc;
+    int64_t total = (int64_t)a.Cd * a.Cg * T;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.ws, out, a.Cd, a.Cg, T, used, accumulate);
+    return check_launch("wgrad_reduce");
+  }
+  const bool idx32 = M * a.Cd < ((int64_t)1 << 31) &&
+                     (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31);
+  if (a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0 && idx32) {
     auto grid_of = [&](int bm, int bn) { return dim3(ceil_div(a.Cd, bm) * ceil_div(a.Cg, bn), T, a.splits); };
     if (a.Cd >= 128 && a.Cg >= 128)
       hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 2>), grid_of(128, 128), dim3(256), 0, st, a);

@@ -1,0 +1,258 @@
+// bf16x3 weight gradient of a "valid" 3×3×3 stride-1 convolution whose input is the
+// materialised replication-padded volume (every ResnetBlock conv, networks3D.py:241-257; the
+// engine feeds them a padded input and runs the conv with p = 0):
+//
+//   dW[co][ci][kd][kh][kw] = Σ_{n,d,h,w} dY[n,d,h,w][co] · X[n, d+kd, h+kh, w+kw][ci]
+//
+// conv_wgrad_x3 runs one GEMM per tap, so every (dY, X) element is loaded, split to bf16 hi/lo
+// and staged 27 times — VALU-bound at ~17 % MFMA (rocprofv3 PMC).  Here a block owns one
+// (kd, kh) pair and all three kw taps of a 64(co) × 64(ci) tile: the contraction runs over
+// "row segments" (n, d, h, 16 w-voxels), 8 segments per stage, with the K index ordered
+// k = w·8 + r (r = segment of the stage).  Then the X rows a kw tap needs are the staged rows
+// shifted by kw·8 K-entries = 16 B, so one staged X tile (18 w-positions) serves all three taps
+// and one staged dY tile serves all three: staging cost and L2 traffic per FLOP drop 3×.
+//
+// LDS (one stage, 70 KB → two blocks per CU): dY as [co][w 16][r 8] bf16 (hi 256 B, lo 256 B,
+// 16 B pad: 528-B rows), X as [ci][w' 18][r 8] (592-B rows); both row strides keep the 16-lane
+// ds_read_b128 groups conflict-free.  The next stage's global loads are in registers during the
+// MFMAs.  Partial tiles go to split-K slabs ws[z][t][co][ci], reduced by wgrad_reduce_kernel.
+#include "kernels.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kTile = 64;                 // co and ci per block
+constexpr int kR = 8;                     // row segments per stage
+constexpr int kSegW = 16;                 // voxels per row segment
+constexpr int kDRow = 2 * kSegW * 16 + 16;          // 528 B
+constexpr int kGRow = 2 * (kSegW + 2) * 16 + 16;    // 592 B
+constexpr int kDHalf = kSegW * 16;                  // lo part offset in a dY row
+constexpr int kGHalf = (kSegW + 2) * 16;            // lo part offset in an X row
+constexpr int kLds = kTile * kDRow + kTile * kGRow; // 71 680 B
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 → packed bf16 hi and lo words (hi + lo = x to 2^-17 relative)
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);
+  const f32x2 f = __builtin_convertvector(h, f32x2);
+  const bf16x2 l = __builtin_convertvector((f32x2){a - f.x, b - f.y}, bf16x2);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half (pairwise scalar splits: an
+// 8-wide vector built from the register array makes LLVM read the array through memory)
+__device__ __forceinline__ void split8_store(char* p, int half, float v0, float v1, float v2, float v3, float v4,
+                                             float v5, float v6, float v7) {
+  uint4 hi, lo;
+  split2(v0, v1, hi.x, lo.x);
+  split2(v2, v3, hi.y, lo.y);
+  split2(v4, v5, hi.z, lo.z);
+  split2(v6, v7, hi.w, lo.w);
+  *reinterpret_cast<uint4*>(p) = hi;
+  *reinterpret_cast<uint4*>(p + half) = lo;
+}
+
+}  // namespace
+
+struct Wgrad3Args {
+  const float* dy; int N, D, H, W, Cd;    // dY [N][D][H][W][Cd]
+  const float* x; int Cg;                 // X  [N][D+2][H+2][W+2][Cg]
+  float* ws;                              // slabs [splits][27][Cd][Cg]
+  int nseg, seg_per_split;                // row segments in total / per split (multiple of kR)
+};
+
+__global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ds = smem;
+  char* Gs = smem + kTile * kDRow;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 32;
+
+  // logical block: (co tile, ci tile) fastest, then (kd, kh), then split; XCD-aware remap so an
+  // XCD's blocks share a contiguous range of splits (their dY / X rows stay in its L2)
+  const int nco = a.Cd / kTile, nci = a.Cg / kTile;
+  const int B = gridDim.x;
+  int L = blockIdx.x;
+  if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
+  const int tile = L % (nco * nci);
+  const int kk9 = (L / (nco * nci)) % 9;
+  const int z = L / (nco * nci * 9);
+  const int co0 = (tile / nci) * kTile, ci0 = (tile % nci) * kTile;
+  const int kd = kk9 / 3, kh = kk9 % 3;
+  const int seg_lo = z * a.seg_per_split;
+  if (seg_lo >= a.nseg) return;                    // grid padding (a multiple of 8 blocks)
+  const int seg_hi = min(a.nseg, seg_lo + a.seg_per_split);
+  const int nstage = (seg_hi - seg_lo + kR - 1) / kR;
+
+  const int Dg = a.D + 2, Hg = a.H + 2, Wg = a.W + 2;
+  const int nsw = a.W / kSegW;
+  // staging units (w position, channel quad cq), cq fastest: 16 lanes read one voxel's 256
+  // contiguous bytes (a w-fastest order, conflict-free for the LDS writes below, measured 35 %
+  // slower overall)
+  const int cq = tid & 15, uw = tid >> 4;          // dY: w = uw (0..15); X: w' = uw
+  const bool g2 = tid < 32;                        // X: w' = 16, 17
+  const int uw2 = 16 + (tid >> 4);
+
+  float4 rd[kR], rg[kR], rg2[kR];
+  // (n, d, h, w-segment) of the stage's first row segment, advanced with carries (the per-segment
+  // divisions cost ~600 scalar instructions per stage)
+  int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
+  auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
+    if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
+  };
+  auto load = [&](int st) __attribute__((always_inline)) {
+    int cw = sw, chh = sh, cdd = sd, cn = sn;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int seg = seg_lo + st * kR + r;
+      const bool ok = seg < seg_hi;
+      // past the split's end: re-read segment (cw, …) clamped to a valid row (masked to zero)
+      const int n = ok ? cn : 0, d = ok ? cdd : 0, h = ok ? chh : 0;
+      const int w0 = (ok ? cw : 0) * kSegW;
+      bump(cw, chh, cdd, cn);
+      const float4 dv = *reinterpret_cast<const float4*>(
+          a.dy + ((((n * a.D + d) * a.H + h) * a.W + w0 + uw) * a.Cd + co0 + 4 * cq));
+      const int gbase = ((n * Dg + d + kd) * Hg + h + kh) * Wg + w0;
+      const float4 gv = *reinterpret_cast<const float4*>(a.x + ((gbase + uw) * a.Cg + ci0 + 4 * cq));
+      // per-component selects (a float4 `ok ? v : zero` is lowered through scratch memory)
+      rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
+      rg[r] = make_float4(ok ? gv.x : 0.f, ok ? gv.y : 0.f, ok ? gv.z : 0.f, ok ? gv.w : 0.f);
+      // w' = 16, 17 (threads 0–31; the others re-read their own unit: keeps rg2 a plain register
+      // array, a conditionally written one goes to scratch)
+      const float4 g = *reinterpret_cast<const float4*>(a.x + ((gbase + (g2 ? uw2 : uw)) * a.Cg + ci0 + 4 * cq));
+      rg2[r] = make_float4(ok ? g.x : 0.f, ok ? g.y : 0.f, ok ? g.z : 0.f, ok ? g.w : 0.f);
+    }
+  };
+  // one unit: 8 segments × 4 channels → 4 rows × (16 B hi + 16 B lo) at w-slot `w`.  Write j
+  // of lane cq goes to channel (j + rot) & 3, rot = (cq >> 1) & 3: an 8-lane ds_write_b128 group
+  // (cq = 8g … 8g+7) then covers 8 distinct 16-B bank groups for both row strides (528 B and
+  // 592 B rows, banks mod 32 dwords); unrotated, rows 4 apart collide 4-way (PMC: 51 % of the
+  // LDS cycles were conflicts)
+  const int rot = (cq >> 1) & 3;
+  auto rotv = [&](const float4& v) __attribute__((always_inline)) {
+    const float4 t = (rot & 1) ? make_float4(v.y, v.z, v.w, v.x) : v;
+    return (rot & 2) ? make_float4(t.z, t.w, t.x, t.y) : t;
+  };
+  auto put = [&](char* base, int row_bytes, int half, int w, const float4 (&v)[kR]) __attribute__((always_inline)) {
+    float4 u[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) u[r] = rotv(v[r]);
+    char* p = base + (4 * cq) * row_bytes + w * 16;
+    split8_store(p + ((0 + rot) & 3) * row_bytes, half, u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x);
+    split8_store(p + ((1 + rot) & 3) * row_bytes, half, u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y);
+    split8_store(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
+    split8_store(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+    put(Ds, kDRow, kDHalf, uw, rd);
+    put(Gs, kGRow, kGHalf, uw, rg);
+    if (g2) put(Gs, kGRow, kGHalf, uw2, rg2);
+  };
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
+
+  if (nstage > 0) load(0);
+  for (int st = 0; st < nstage; ++st) {
+    store();
+    __syncthreads();
+    if (st + 1 < nstage) {                          // lands during this stage's MFMAs
+#pragma unroll
+      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
+      load(st + 1);
+    }
+    const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
+    const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+    // fragments of K-step ks: A hi/lo (dY) and B hi/lo for the three kw taps (X shifted by kw
+    // slots); software-pipelined one K-step ahead so the LDS latency hides under the MFMAs
+    bf16x8 fa[2][2], fb[2][3][2];
+    auto frag = [&](int ks, bf16x8 (&A)[2], bf16x8 (&Bf)[3][2]) __attribute__((always_inline)) {
+      A[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
+      A[1] = *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        Bf[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16);
+        Bf[kw][1] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16 + kGHalf);
+      }
+    };
+    frag(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < kSegW / 2; ++ks) {
+      const int c = ks & 1;
+      if (ks + 1 < kSegW / 2) frag(ks + 1, fa[c ^ 1], fb[c ^ 1]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][1], fb[c][kw][0], acc[kw], 0, 0, 0);
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][0], fb[c][kw][1], acc[kw], 0, 0, 0);
+        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][0], fb[c][kw][0], acc[kw], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+
+  // slab[z][t][co][ci]: lane li = ci column, register r = co row (r & 3) + 8 (r >> 2) + 4 lh
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    const int t = (kd * 3 + kh) * 3 + kw;
+    float* slab = a.ws + ((int64_t)z * 27 + t) * a.Cd * a.Cg;
+    const int col = ci0 + wn0 + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = co0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      slab[(int64_t)row * a.Cg + col] = acc[kw][r];
+    }
+  }
+}
+
+bool wgrad3_x3_applicable(const WgradArgs& a) {
+  return a.x3 && a.k == 3 && a.s == 1 && a.p == 0 && a.Wd % kSegW == 0 && a.Dg == a.Dd + 2 && a.Hg == a.Hd + 2 &&
+         a.Wg == a.Wd + 2 && a.Cd % kTile == 0 && a.Cg % kTile == 0 &&
+         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31) &&
+         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd < ((int64_t)1 << 31);
+}
+
+// splits: at most 2 blocks per CU in total (one round: a 513th block doubles the time),
+// ≥ 6 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
+int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
+  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
+  const int tiles = (a.Cd / kTile) * (a.Cg / kTile) * 9;
+  int s = 512 / tiles;
+  const int by_len = nseg / (6 * kR);
+  if (s > by_len) s = by_len;
+  if (s > max_splits) s = max_splits;
+  if (s < 1) s = 1;
+  return s;
+}
+
+int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
+  Wgrad3Args a{};
+  a.dy = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
+  a.x = g.G; a.Cg = g.Cg;
+  a.ws = g.ws;
+  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / kSegW);
+  int per = (a.nseg + splits - 1) / splits;
+  per = (per + kR - 1) / kR * kR;
+  a.seg_per_split = per;
+  const int nsplit = (a.nseg + per - 1) / per;
+  const int blocks = ((g.Cd / kTile) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(wgrad3_x3_kernel, dim3(blocks), dim3(256), kLds, st, a);
+  return nsplit;
+}
+
+}  // namespace mragan

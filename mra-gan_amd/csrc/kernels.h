@@ -80,6 +80,10 @@ struct WgradArgs {
   int x3;          // bf16x3 split MFMA (needs Cd, Cg multiples of 32)
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
+// bf16x3 weight gradient of valid k3 s1 convs on padded inputs, 3 kw taps per block (conv_wgrad3_x3.hip)
+bool wgrad3_x3_applicable(const WgradArgs& a);
+int wgrad3_x3_splits(const WgradArgs& a, int max_splits);
+int conv_wgrad3_x3(const WgradArgs& a, int splits, hipStream_t st);   // returns the splits used
 size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k);
 
 struct ThinWgradArgs {

@@ -481,3 +481,23 @@ def test_brickT_bf16x3(x3, N, cin, S, k, op):
     (dx_ref,) = torch.autograd.grad(yc, xc, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wc, False, True), 32, k, 2, 1, xc.shape[2:], transposed=True)
     assert rel(ncdhw(dx), dx_ref) < X3_TOL
+
+
+@pytest.mark.parametrize("N,cin,cout,D,H,W", [(4, 128, 128, 16, 16, 16), (2, 128, 128, 8, 9, 16), (1, 64, 192, 5, 3, 32),
+                                              (3, 64, 64, 7, 2, 16), (1, 192, 64, 2, 2, 48)])
+def test_wgrad3_bf16x3(x3, N, cin, cout, D, H, W):
+    """Multi-tap weight gradient (conv_wgrad3_x3.hip) of the ResnetBlock form: valid k3 s1 conv
+    on a (D+2, H+2, W+2) input, W a multiple of 16 — incl. partial last stages, several channel
+    tiles and several w-segments per row."""
+    ops = x3
+    g = torch.Generator().manual_seed(N + cin + D * H + W)
+    x = torch.randn(N, cin, D + 2, H + 2, W + 2, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv3d(x, w)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw = torch.full((cout, cin, 3, 3, 3), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 1, 0, dw, accumulate=False)
+    assert rel(dw, dw_ref) < X3_TOL
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 1, 0, dw, accumulate=True)
+    assert rel(dw, 2 * dw_ref) < X3_TOL
