@@ -227,7 +227,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
           }
           v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
-          *reinterpret_cast<float4*>(yv + co) = v;
+          // non-temporal: the 134 MB output stream (64³ × 32 ch × 4 instances) would otherwise
+          // evict the halo and weight lines the persistent blocks re-read from L2
+          typedef float f32x4nt __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(f32x4nt{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4nt*>(yv + co));
         }
     }
     stampit(b, 4);

@@ -404,6 +404,12 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
       hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 1>), grid_of(128, 64), dim3(256), 0, st, a);
     else if (a.Cg >= 128)
       hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 2>), grid_of(64, 128), dim3(256), 0, st, a);
+    // 32-channel side (G down1 / up2 at full resolution): a 64×32 tile on two waves instead of
+    // a half-empty 64×64 one
+    else if (a.Cg == 32 && a.Cd >= 64)
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 1, 1, 1>), grid_of(64, 32), dim3(128), 0, st, a);
+    else if (a.Cd == 32 && a.Cg >= 64)
+      hipLaunchKernelGGL((conv_wgrad_x3_kernel<1, 2, 1, 1>), grid_of(32, 64), dim3(128), 0, st, a);
     else
       hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 1>), grid_of(64, 64), dim3(256), 0, st, a);
   } else if (big) {

@@ -199,7 +199,8 @@ def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
     assert rel(ncdhw(dx), dx_ref) < X3_TOL
 
 
-@pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1)])
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1),
+                                                   (2, 64, 32, 10, 3, 2, 1), (3, 32, 64, 11, 3, 2, 1)])
 def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
     ops = x3
     g = torch.Generator().manual_seed(13 + N * 10 + cin + cout)
