@@ -195,15 +195,27 @@ thin1_wgrad_x3_kernel(Thin1WArgs a) {
 }
 
 // out[c][t] (=|+=) Σ_blocks slab[z][τ(t)][c]   (τ = tap mirror for the head form)
-__global__ void thin1_wgrad_reduce_kernel(const float* __restrict__ slab, int nz, int flip, float* __restrict__ out,
-                                          int accumulate) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= kC * kT) return;
-  const int c = e / kT, t = e % kT;
+// One block per tap: 8 groups of 32 lanes (lane = channel: 128 contiguous bytes per slab row),
+// group g sums slabs z ≡ g (mod 8) in increasing z, then the 8 partials are added in g order —
+// fixed order, deterministic.  (One thread per output summing all slabs serially ran 83 µs on
+// 43 blocks.)
+__global__ void __launch_bounds__(256) thin1_wgrad_reduce_kernel(const float* __restrict__ slab, int nz, int flip,
+                                                                 float* __restrict__ out, int accumulate) {
+  __shared__ float part[8][kC];
+  const int t = blockIdx.x, c = threadIdx.x % kC, g = threadIdx.x / kC;
   const int ts = flip ? kT - 1 - t : t;
   float s = 0.f;
-  for (int z = 0; z < nz; ++z) s += slab[((int64_t)z * kT + ts) * kC + c];
-  out[e] = accumulate ? out[e] + s : s;
+#pragma unroll 8
+  for (int z = g; z < nz; z += 8) s += slab[((int64_t)z * kT + ts) * kC + c];
+  part[g][c] = s;
+  __syncthreads();
+  if (g == 0) {
+    float r = part[0][c];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) r += part[k][c];
+    const int e = c * kT + t;
+    out[e] = accumulate ? out[e] + r : r;
+  }
 }
 
 static int thin1w_grid() {
@@ -257,8 +269,8 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
   hipLaunchKernelGGL(thin1_wgrad_x3_kernel, dim3(grid), dim3(256), lds, st, a);
   int rc = check_launch("thin1_wgrad_x3");
   if (rc) return rc;
-  hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(ceil_div(kC * kT, 256)), dim3(256), 0, st, a.slab, grid, a.flip,
-                     out, accumulate);
+  static_assert(kC * 8 == 256, "reduce block = 8 groups of kC lanes");
+  hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, a.flip, out, accumulate);
   return check_launch("thin1_wgrad_reduce");
 }
 

@@ -436,9 +436,11 @@ class CycleGANModel(BaseModel):
         gG, gD = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(gG, stream=side):
+        # thread_local: other threads (the process group's watchdog) may query the runtime
+        # while this thread captures
+        with torch.cuda.graph(gG, stream=side, capture_error_mode="thread_local"):
             self._phase_G()
-        with torch.cuda.graph(gD, pool=gG.pool(), stream=side):
+        with torch.cuda.graph(gD, pool=gG.pool(), stream=side, capture_error_mode="thread_local"):
             self._phase_D()
         torch.cuda.current_stream().wait_stream(side)
         self._rs_tables = None

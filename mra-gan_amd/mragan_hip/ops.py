@@ -68,6 +68,9 @@ class KernelTimer:
         if torch.cuda.is_current_stream_capturing():
             return None         # ROCm cannot time event nodes of a graph: eager launches only
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # keep the GPU busy until the launch below is queued: otherwise the interval also holds
+        # the host's submission latency (the GPU reaches the start event, then idles)
+        torch.cuda._sleep(100000)
         s.record()
         return (s, e)
 
