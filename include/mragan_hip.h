@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 4
+#define MRAGAN_ABI_VERSION 5
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -77,6 +77,11 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
 
 /* src[A][B][k³] (torch layout) → dst[k³][A][B] (transpose_ab = 0) or dst[k³][B][A] (= 1). */
 int mragan_pack_weight(const float* src, int A, int B, int T, int transpose_ab, float* dst, void* stream);
+/* n packs in one launch (a network's repack after each optimizer step, networks3D.py's conv
+ * weights): `table` is a DEVICE array of n entries {const float* src; float* dst; int A, B, T,
+ * transpose_ab;} (mragan_pack_entry_size() bytes each), max_elems ≥ every entry's A·B·T.      */
+size_t mragan_pack_entry_size(void);
+int mragan_pack_weights(const void* table, int n, int64_t max_elems, void* stream);
 
 /* ---- InstanceNorm3d(affine=False, track_running_stats=True), train mode --------------------
  * y (replication-padded by ypad) = act((x − μ_nc)·rstd_nc) (+ resid interior of an rpad-padded

@@ -123,6 +123,13 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
   return conv_wgrad(a, dw, accumulate, ws_bytes, st);
 }
 
+size_t mragan_pack_entry_size(void) { return sizeof(PackEntry); }
+
+int mragan_pack_weights(const void* table, int n, int64_t max_elems, void* stream) {
+  MRAGAN_CHECK_ARG(table && n >= 0 && n <= 65535 && max_elems >= 0, "pack_weights: bad args");
+  return pack_weights_batched(static_cast<const PackEntry*>(table), n, max_elems, static_cast<hipStream_t>(stream));
+}
+
 int mragan_pack_weight(const float* src, int A, int B, int T, int tr, float* dst, void* stream) {
   MRAGAN_CHECK_ARG(src && dst && A > 0 && B > 0 && T > 0, "pack_weight: bad args");
   return pack_weight(src, A, B, T, tr, dst, static_cast<hipStream_t>(stream));

@@ -132,6 +132,12 @@ int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, floa
 void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out);
 int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st);
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);
+struct PackEntry {          // layout shared with include/mragan_hip.h (mragan_pack_entry)
+  const float* src;
+  float* dst;
+  int A, B, T, tr;
+};
+int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st);
 int fill(float* p, int64_t n, float v, hipStream_t st);
 
 }  // namespace mragan

@@ -271,6 +271,19 @@ __global__ void pack_kernel(const float* __restrict__ src, int A, int B, int T, 
   }
 }
 
+// Many packs in one launch (a network's repack after an optimizer step): blockIdx.y = entry,
+// the x blocks stride over its elements.  Same element mapping as pack_kernel.
+__global__ void pack_batched_kernel(const PackEntry* __restrict__ tab) {
+  const PackEntry e = tab[blockIdx.y];
+  const int AB = e.A * e.B, total = AB * e.T;          // < 2^31 (checked by the caller)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int t = i / AB, r = i - t * AB;
+    int a, b;
+    if (!e.tr) { a = r / e.B; b = r - a * e.B; } else { b = r / e.A; a = r - b * e.A; }
+    e.dst[i] = e.src[(a * e.B + b) * e.T + t];
+  }
+}
+
 __global__ void fill_kernel(float* __restrict__ p, int64_t n, float v) {
   GRID_STRIDE(i, n) p[i] = v;
 }
@@ -349,6 +362,15 @@ void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float g
 int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st) {
   hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, hyper);
   return check_launch("adam_dev");
+}
+int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st) {
+  if (n <= 0) return kOk;
+  if (max_elems >= ((int64_t)1 << 31)) { set_error("pack_weights: entry too large"); return kBadArg; }
+  int gx = (int)((max_elems + 255) / 256);             // the largest entry in one pass
+  if (gx > 2048) gx = 2048;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(pack_batched_kernel, dim3(gx, n), dim3(256), 0, st, table);
+  return check_launch("pack_batched");
 }
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st) {
   hipLaunchKernelGGL(pack_kernel, dim3(grid_cap((int64_t)A * B * T)), dim3(256), 0, st, src, A, B, T, tr, dst);

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -37,6 +37,8 @@ SIGNATURES = {
     "mragan_conv3d_wgrad_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),
     "mragan_conv3d_wgrad": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
     "mragan_pack_weight": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "mragan_pack_entry_size": (sz, []),
+    "mragan_pack_weights": (i32, [vp, i32, i64, vp]),
     "mragan_instnorm_workspace": (sz, [i32, i32, i32, i32, i32]),
     "mragan_instnorm_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, vp, vp, vp, sz, vp]),
     "mragan_instnorm_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, sz, vp]),

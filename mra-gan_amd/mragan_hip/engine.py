@@ -47,18 +47,22 @@ class ConvLayer:
         self.wp_fwd: Optional[torch.Tensor] = None
         self.wp_bwd: Optional[torch.Tensor] = None
 
-    def repack(self):
+    def packs(self):
+        """The two packs of this layer as (src, A, B, T, transpose_ab, dst) (buffers allocated)."""
         w = self.m.weight.data
         T = self.k ** 3
         if self.wp_fwd is None or self.wp_fwd.device != w.device:
             self.wp_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             self.wp_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
         if not self.transposed:     # torch [Cout][Cin][t]
-            ops.pack_weight(w, self.cout, self.cin, T, False, self.wp_fwd)   # [t][Cout][Cin]
-            ops.pack_weight(w, self.cout, self.cin, T, True, self.wp_bwd)    # [t][Cin][Cout]
-        else:                       # torch [Cin][Cout][t]
-            ops.pack_weight(w, self.cin, self.cout, T, True, self.wp_fwd)    # [t][Cout][Cin]
-            ops.pack_weight(w, self.cin, self.cout, T, False, self.wp_bwd)   # [t][Cin][Cout]
+            return [(w, self.cout, self.cin, T, False, self.wp_fwd),     # [t][Cout][Cin]
+                    (w, self.cout, self.cin, T, True, self.wp_bwd)]      # [t][Cin][Cout]
+        return [(w, self.cin, self.cout, T, True, self.wp_fwd),          # torch [Cin][Cout][t] → [t][Cout][Cin]
+                (w, self.cin, self.cout, T, False, self.wp_bwd)]         # [t][Cin][Cout]
+
+    def repack(self):
+        for src, A, B, T, tr, dst in self.packs():
+            ops.pack_weight(src, A, B, T, tr, dst)
 
     def out_spatial(self, d, h, w):
         if self.transposed:
@@ -144,8 +148,10 @@ class NetPlan:
                 yield st.conv
 
     def repack(self):
-        for c in self.conv_layers():
-            c.repack()
+        """Every conv layer's two packs in one launch (after each optimizer step)."""
+        if not hasattr(self, "_pack_table"):
+            self._pack_table = ops.PackTable()
+        self._pack_table.run([p for c in self.conv_layers() for p in c.packs()])
         self.dirty = False
 
     def ensure_packed(self):
@@ -453,8 +459,10 @@ class UnetPlan:
             yield lv.up
 
     def repack(self):
-        for c in self.conv_layers():
-            c.repack()
+        """Every conv layer's two packs in one launch (after each optimizer step)."""
+        if not hasattr(self, "_pack_table"):
+            self._pack_table = ops.PackTable()
+        self._pack_table.run([p for c in self.conv_layers() for p in c.packs()])
         self.dirty = False
 
     def ensure_packed(self):

@@ -163,6 +163,42 @@ def pack_weight(src: torch.Tensor, A: int, B: int, T: int, transpose_ab: bool, o
     return out
 
 
+class PackTable:
+    """Device table of weight packs (src, dst, A, B, T, transpose) run by ONE launch
+    (mragan_pack_weights).  Built once from stable pointers; `run` falls back to one launch per
+    pack when the table is stale inside a graph capture (no host→device copy allowed there)."""
+
+    def __init__(self):
+        self.key = None
+        self.dev = None
+        self.n = 0
+        self.max_elems = 0
+
+    def run(self, packs):
+        """packs: list of (src, A, B, T, transpose_ab, dst) tensors / ints."""
+        import ctypes as C
+
+        class _E(C.Structure):
+            _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("A", C.c_int32), ("B", C.c_int32),
+                        ("T", C.c_int32), ("tr", C.c_int32)]
+        key = tuple((src.data_ptr(), dst.data_ptr(), A, B, T, int(tr)) for src, A, B, T, tr, dst in packs)
+        if key != self.key:
+            if torch.cuda.is_current_stream_capturing():
+                for src, A, B, T, tr, dst in packs:
+                    pack_weight(src, A, B, T, tr, dst)
+                return
+            if query("mragan_pack_entry_size") != C.sizeof(_E):
+                raise RuntimeError("mragan_pack_entry_size mismatch")
+            arr = (_E * len(packs))()
+            for e, (sp, dp, A, B, T, tr) in zip(arr, key):
+                e.src, e.dst, e.A, e.B, e.T, e.tr = sp, dp, A, B, T, tr
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self.dev = host.to(packs[0][0].device)
+            self.key, self.n = key, len(packs)
+            self.max_elems = max(A * B * T for _, _, A, B, T, _ in key)
+        call("mragan_pack_weights", _ptr(self.dev), self.n, self.max_elems, _stream())
+
+
 def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch.Tensor] = None, rpad: int = 0,
                  out: Optional[torch.Tensor] = None, mean: Optional[torch.Tensor] = None,
                  rstd: Optional[torch.Tensor] = None):

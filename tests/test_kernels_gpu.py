@@ -502,3 +502,22 @@ def test_wgrad3_bf16x3(x3, N, cin, cout, D, H, W):
     assert rel(dw, dw_ref) < X3_TOL
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 1, 0, dw, accumulate=True)
     assert rel(dw, 2 * dw_ref) < X3_TOL
+
+
+def test_pack_weights_batched_equals_single(ops):
+    """mragan_pack_weights (one launch for a network's packs) = mragan_pack_weight per pack."""
+    g = torch.Generator().manual_seed(21)
+    packs, ref = [], []
+    for (A, B, T, tr) in [(128, 128, 27, False), (32, 1, 343, True), (64, 32, 27, True), (1, 32, 64, False)]:
+        src = torch.randn(A * B * T, generator=g).cuda()
+        dst = torch.empty_like(src)
+        want = torch.empty_like(src)
+        ops.pack_weight(src, A, B, T, tr, want)
+        packs.append((src, A, B, T, tr, dst))
+        ref.append(want)
+    tab = ops.PackTable()
+    tab.run(packs)
+    tab.run(packs)          # cached table path
+    torch.cuda.synchronize()
+    for (_, _, _, _, _, dst), want in zip(packs, ref):
+        assert torch.equal(dst, want)
