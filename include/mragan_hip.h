@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 5
+#define MRAGAN_ABI_VERSION 6
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -59,6 +59,14 @@ int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, co
 int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
                              const float* bias, int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho,
                              int Wo, void* ws, size_t ws_bytes, void* stream);
+/* Either form (transposed = 0/1) with the weight also given pre-split: `wsplit` is the same packed
+ * weight written by mragan_pack_weights with tr = 2 + transpose_ab (bf16x3 brick fragment order).
+ * Used by the k3 s1 bf16x3 brick kernel instead of re-splitting `wpacked` on every call (the
+ * ResnetBlock convs, networks3D.py:241-257, and their data gradients); ignored by every other
+ * kernel.  The caller keeps `wsplit` in step with `wpacked` (same pack launch).  (ABI 6) */
+int mragan_conv3d_presplit(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                           const void* wsplit, const float* bias, int cout, int k, int stride, int pad, int act,
+                           float* y, int Do, int Ho, int Wo, int transposed, void* ws, size_t ws_bytes, void* stream);
 
 /* Workspace (bytes) the two calls above need for these shapes in the current precision mode:
  * split-K partial tiles of small-M / large-K dense convolutions (PatchGAN layers 2-4 and their
@@ -79,7 +87,10 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
 int mragan_pack_weight(const float* src, int A, int B, int T, int transpose_ab, float* dst, void* stream);
 /* n packs in one launch (a network's repack after each optimizer step, networks3D.py's conv
  * weights): `table` is a DEVICE array of n entries {const float* src; float* dst; int A, B, T,
- * transpose_ab;} (mragan_pack_entry_size() bytes each), max_elems ≥ every entry's A·B·T.      */
+ * transpose_ab;} (mragan_pack_entry_size() bytes each), max_elems ≥ every entry's A·B·T.
+ * transpose_ab = 2 | 3: the pack of (transpose_ab & 1) written as bf16 hi/lo split fragments
+ * for mragan_conv3d_presplit (T = 27 and the contraction side a multiple of 32; dst holds
+ * A·B·T·4 bytes).                                                                          */
 size_t mragan_pack_entry_size(void);
 int mragan_pack_weights(const void* table, int n, int64_t max_elems, void* stream);
 

@@ -33,7 +33,7 @@ static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0
 
 static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
                        int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* ws,
-                       size_t ws_bytes, void* stream) {
+                       size_t ws_bytes, void* stream, const void* wx3 = nullptr) {
   MRAGAN_CHECK_ARG(x && w && y, "conv: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv: bad input shape");
   MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv: bad output shape");
@@ -48,7 +48,7 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
-              g_conv_precision == MRAGAN_PREC_BF16X3, static_cast<float*>(ws), ws_bytes};
+              g_conv_precision == MRAGAN_PREC_BF16X3, static_cast<float*>(ws), ws_bytes, wx3};
   return conv_igemm(a, st);
 }
 
@@ -80,6 +80,14 @@ int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int 
                              int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* ws,
                              size_t ws_bytes, void* stream) {
   return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, 1, ws, ws_bytes, stream);
+}
+
+int mragan_conv3d_presplit(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit,
+                           const float* bias, int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho,
+                           int Wo, int transposed, void* ws, size_t ws_bytes, void* stream) {
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_presplit: transposed must be 0/1");
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, transposed, ws, ws_bytes,
+                     stream, wsplit);
 }
 
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,

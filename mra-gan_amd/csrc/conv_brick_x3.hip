@@ -209,6 +209,9 @@ conv_brick_x3_kernel(BrickArgs a) {
 #pragma unroll
     for (int du = 0; du < kP; ++du) {
       const int u = u0 + du;
+      // one scheduling region per step, loads first: left free, the scheduler sinks the next
+      // step's A reads next to their MFMAs and every step waits out a full LDS round trip
+      __builtin_amdgcn_sched_barrier(0);
       // next chunk's halo: slice s = u/3 loaded into ring slot s mod 3 (u0/3 ≡ 0 mod 3) …
       if (du % 3 == 0 && u / 3 < NSL) {
         const int e = (u / 3) * NT + tid, hpos = e >> 3;
@@ -237,6 +240,7 @@ conv_brick_x3_kernel(BrickArgs a) {
       // A fragments of the NEXT step from the halo (software pipelined: the LDS latency hides
       // under this step's MFMAs; the chunk's first step is read after its barrier)
       if (u + 1 < kSteps) a_read(u + 1, af[(du + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
       const bf16x8 (&ah)[TM] = af[du & 1][0];
       const bf16x8 (&al)[TM] = af[du & 1][1];
 #pragma unroll
@@ -286,18 +290,22 @@ static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
 // 117 KB LDS halo allows one block per CU, and two-per-SIMD (8-wave) variants spill at kPF = 9
 size_t conv_brick_x3_ws_bytes(int C, int ny) { return (size_t)kTaps * C * ny * sizeof(float); }
 
-int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, hipStream_t st) {
-  const size_t need = conv_brick_x3_ws_bytes(a.C, a.ny);
-  if (!ws || ws_bytes < need) {
-    set_error("conv_brick_x3: workspace %zu < %zu", ws_bytes, need);
-    return kWorkspace;
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
+  if (wsplit) {
+    a.wx3 = wsplit;                     // pre-split by mragan_pack_weights (tr 2/3) with the fp32 pack
+  } else {
+    const size_t need = conv_brick_x3_ws_bytes(a.C, a.ny);
+    if (!ws || ws_bytes < need) {
+      set_error("conv_brick_x3: workspace %zu < %zu", ws_bytes, need);
+      return kWorkspace;
+    }
+    const int64_t groups = (int64_t)kTaps * a.ny * (a.C / 8);
+    hipLaunchKernelGGL(brick_x3_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny, a.C,
+                       static_cast<__bf16*>(ws));
+    int rc = check_launch("brick_x3_pack");
+    if (rc) return rc;
+    a.wx3 = ws;
   }
-  const int64_t groups = (int64_t)kTaps * a.ny * (a.C / 8);
-  hipLaunchKernelGGL(brick_x3_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny, a.C,
-                     static_cast<__bf16*>(ws));
-  int rc = check_launch("brick_x3_pack");
-  if (rc) return rc;
-  a.wx3 = ws;
   if (bm == 128 && bn == 128) return launch_brick_x3<2, 2, 2, 2, 400>(a, st);
   if (bm == 128) return launch_brick_x3<2, 2, 2, 1, 400>(a, st);
   if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300>(a, st);

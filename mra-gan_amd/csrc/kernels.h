@@ -18,6 +18,7 @@ struct IgemmArgs {
   int x3;           // 1: bf16x3 split MFMA (conv_igemm_x3.hip), 0: exact f32 MFMA
   float* ws;        // split-K partial tiles (conv_igemm_ws_bytes)
   size_t ws_bytes;
+  const void* wx3;  // optional: w pre-split in bf16x3 brick fragment order (pack tr 2/3), or null
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
@@ -39,7 +40,7 @@ struct BrickArgs {
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st);
-int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, hipStream_t st);
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st);
 size_t conv_brick_x3_ws_bytes(int C, int ny);
 bool conv_brick_x3_active(const IgemmArgs& a);
 // bf16x3 stride-2 transposed convolutions from an LDS halo (conv_brickT_x3.hip)
@@ -135,7 +136,7 @@ int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipSt
 struct PackEntry {          // layout shared with include/mragan_hip.h (mragan_pack_entry)
   const float* src;
   float* dst;
-  int A, B, T, tr;
+  int A, B, T, tr;  // tr 0/1: fp32 [T][A][B] / [T][B][A]; 2/3: same, bf16x3 brick fragment order
 };
 int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st);
 int fill(float* p, int64_t n, float v, hipStream_t st);

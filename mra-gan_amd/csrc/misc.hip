@@ -273,8 +273,48 @@ __global__ void pack_kernel(const float* __restrict__ src, int A, int B, int T, 
 
 // Many packs in one launch (a network's repack after an optimizer step): blockIdx.y = entry,
 // the x blocks stride over its elements.  Same element mapping as pack_kernel.
+//
+// tr = 2 | 3 (transpose_ab = tr & 1): the same [T][ny][C] packed weight, but written straight in
+// the bf16x3 brick kernel's fragment order (conv_brick_x3.hip: [tap][chunk][16-ch half][hi|lo]
+// [n][8-ch group][8] bf16, hi = rne(w), lo = rne(w − hi)), so the k3 s1 convs of a step skip
+// their per-call split.  Requires T = 27, C % 32 == 0 (entries that do not fit are skipped).
+typedef float pk_f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 pk_bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ void pack_split_entry(const PackEntry& e) {
+  const int tr = e.tr & 1;
+  const int ny = tr ? e.B : e.A, C = tr ? e.A : e.B;
+  if (e.T != 27 || C % 32 != 0) return;
+  const int G = C / 8, nch = C / 32;
+  const int total = e.T * ny * G;
+  __bf16* out = reinterpret_cast<__bf16*>(e.dst);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i % G, tn = i / G;
+    const int n = tn % ny, tap = tn / ny;
+    pk_f32x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = g * 8 + j;
+      const int a = tr ? c : n, b = tr ? n : c;
+      v[j] = e.src[(a * e.B + b) * e.T + tap];
+    }
+    const pk_bf16x8 hi = __builtin_convertvector(v, pk_bf16x8);
+    const pk_bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, pk_f32x8), pk_bf16x8);
+    const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
+    const int base = (((tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + n * 16 + lh * 8;
+    *reinterpret_cast<pk_bf16x8*>(out + base) = hi;
+    *reinterpret_cast<pk_bf16x8*>(out + base + ny * 16) = lo;
+  }
+}
+
+__global__ void pack_split_kernel(PackEntry e) { pack_split_entry(e); }
+
 __global__ void pack_batched_kernel(const PackEntry* __restrict__ tab) {
   const PackEntry e = tab[blockIdx.y];
+  if (e.tr >= 2) {
+    pack_split_entry(e);
+    return;
+  }
   const int AB = e.A * e.B, total = AB * e.T;          // < 2^31 (checked by the caller)
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int t = i / AB, r = i - t * AB;
@@ -373,6 +413,13 @@ int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipSt
   return check_launch("pack_batched");
 }
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st) {
+  if (tr >= 2) {
+    const int C = (tr & 1) ? A : B;
+    MRAGAN_CHECK_ARG(T == 27 && C % 32 == 0, "pack_weight: split pack needs T = 27, contraction %% 32 (T=%d C=%d)", T, C);
+    const PackEntry e{src, dst, A, B, T, tr};
+    hipLaunchKernelGGL(pack_split_kernel, dim3(grid_cap((int64_t)A * B * T / 8)), dim3(256), 0, st, e);
+    return check_launch("pack_split");
+  }
   hipLaunchKernelGGL(pack_kernel, dim3(grid_cap((int64_t)A * B * T)), dim3(256), 0, st, src, A, B, T, tr, dst);
   return check_launch("pack_weight");
 }

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -33,6 +33,8 @@ SIGNATURES = {
                                 vp]),
     "mragan_conv3d_transposed": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32,
                                        vp, sz, vp]),
+    "mragan_conv3d_presplit": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32,
+                                     i32, i32, vp, sz, vp]),
     "mragan_conv3d_workspace": (sz, [i32] * 13),
     "mragan_conv3d_wgrad_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),
     "mragan_conv3d_wgrad": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, sz, vp]),

@@ -46,6 +46,13 @@ class ConvLayer:
         self.cout = module.out_channels
         self.wp_fwd: Optional[torch.Tensor] = None
         self.wp_bwd: Optional[torch.Tensor] = None
+        self.ws_fwd: Optional[torch.Tensor] = None      # bf16x3 pre-split copies (brick convs only)
+        self.ws_bwd: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def _splittable(k, s, ny, C):
+        # the bf16x3 brick kernel's shapes (conv_brick_applicable): k3 s1, C % 32, ny % 64
+        return k == 3 and s == 1 and C % 32 == 0 and ny % 64 == 0
 
     def packs(self):
         """The two packs of this layer as (src, A, B, T, transpose_ab, dst) (buffers allocated)."""
@@ -55,10 +62,22 @@ class ConvLayer:
             self.wp_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             self.wp_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
         if not self.transposed:     # torch [Cout][Cin][t]
-            return [(w, self.cout, self.cin, T, False, self.wp_fwd),     # [t][Cout][Cin]
-                    (w, self.cout, self.cin, T, True, self.wp_bwd)]      # [t][Cin][Cout]
-        return [(w, self.cin, self.cout, T, True, self.wp_fwd),          # torch [Cin][Cout][t] → [t][Cout][Cin]
-                (w, self.cin, self.cout, T, False, self.wp_bwd)]         # [t][Cin][Cout]
+            out = [(w, self.cout, self.cin, T, False, self.wp_fwd),      # [t][Cout][Cin]
+                   (w, self.cout, self.cin, T, True, self.wp_bwd)]       # [t][Cin][Cout]
+        else:
+            out = [(w, self.cin, self.cout, T, True, self.wp_fwd),       # torch [Cin][Cout][t] → [t][Cout][Cin]
+                   (w, self.cin, self.cout, T, False, self.wp_bwd)]      # [t][Cin][Cout]
+        # pre-split bf16x3 copies for the brick kernel, refreshed by the same pack launch
+        (_, A, B, _, tf, _), (_, _, _, _, tb, _) = out
+        if self._splittable(self.k, self.s, self.cout, self.cin):
+            if self.ws_fwd is None or self.ws_fwd.device != w.device:
+                self.ws_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+            out.append((w, A, B, T, 2 + int(tf), self.ws_fwd))
+        if self._splittable(self.k, self.s, self.cin, self.cout):
+            if self.ws_bwd is None or self.ws_bwd.device != w.device:
+                self.ws_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+            out.append((w, A, B, T, 2 + int(tb), self.ws_bwd))
+        return out
 
     def repack(self):
         for src, A, B, T, tr, dst in self.packs():
@@ -74,12 +93,12 @@ class ConvLayer:
     def forward(self, x, bias=None, act=None):
         N, D, H, W, _ = x.shape
         return ops.conv3d(x, self.wp_fwd, self.cout, self.k, self.s, self.p, self.out_spatial(D, H, W),
-                          bias=bias, act=act, transposed=self.transposed)
+                          bias=bias, act=act, transposed=self.transposed, wsplit=self.ws_fwd)
 
     def dgrad(self, dy, in_spatial):
         """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
         return ops.conv3d(dy, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial,
-                          transposed=not self.transposed)
+                          transposed=not self.transposed, wsplit=self.ws_bwd)
 
     def wgrad(self, x, dy, accumulate=True):
         g = self.m.weight.grad

@@ -119,8 +119,9 @@ def convT_out_size(n: int, k: int, s: int, p: int, op: int = 0) -> int:
 
 def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
            bias: Optional[torch.Tensor] = None, act=None, transposed: bool = False,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Forward-form (transposed=False) or transposed-form convolution; see include/mragan_hip.h."""
+           out: Optional[torch.Tensor] = None, wsplit: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Forward-form (transposed=False) or transposed-form convolution; see include/mragan_hip.h.
+    `wsplit`: the same packed weight pre-split by a tr 2/3 pack (mragan_conv3d_presplit)."""
     _check(x, "conv3d.x")
     N, Di, Hi, Wi, cin = x.shape
     Do, Ho, Wo = out_spatial
@@ -135,8 +136,14 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
                           in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo))) if TIMER.match else None
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
     ws = WS.get(nbytes) if nbytes else None
-    call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo,
-         _ptr(ws), nbytes, _stream())
+    if wsplit is not None:
+        if wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+            raise ValueError("conv3d: wsplit size does not match the packed weight")
+        call("mragan_conv3d_presplit", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), _ptr(bias), cout, k, s, p,
+             ACT[act], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _stream())
+    else:
+        call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo,
+             _ptr(ws), nbytes, _stream())
     TIMER.end(tm)
     return out
 

@@ -24,7 +24,7 @@ def header_functions():
 
 def test_header_declares_entry_points():
     fns = header_functions()
-    for f in ("mragan_conv3d_fwd", "mragan_conv3d_transposed", "mragan_conv3d_wgrad", "mragan_instnorm_fwd",
+    for f in ("mragan_conv3d_fwd", "mragan_conv3d_transposed", "mragan_conv3d_presplit", "mragan_conv3d_wgrad", "mragan_instnorm_fwd",
               "mragan_instnorm_bwd", "mragan_adam", "mragan_gan_loss", "mragan_l1_loss"):
         assert f in fns
 
@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
     assert set(header_functions()) == set(mragan_hip.exported_symbols())
-    assert lib.mragan_abi_version() == 5
+    assert lib.mragan_abi_version() == 6
 
 
 def test_library_built_for_gfx950():

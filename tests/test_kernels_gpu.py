@@ -521,3 +521,35 @@ def test_pack_weights_batched_equals_single(ops):
     torch.cuda.synchronize()
     for (_, _, _, _, _, dst), want in zip(packs, ref):
         assert torch.equal(dst, want)
+
+
+@pytest.mark.parametrize("N,cin,cout,S,transposed", [(2, 64, 128, 13, False), (1, 128, 128, 8, False),
+                                                     (2, 128, 64, 9, True), (1, 128, 128, 7, True)])
+def test_brick_presplit_equals_per_call_split(ops, N, cin, cout, S, transposed):
+    """mragan_conv3d_presplit with weights split by a tr 2/3 batched pack is bit-identical to the
+    brick kernel splitting the fp32 pack itself (both forms of a k3 s1 conv, bf16x3)."""
+    prev = ops.get_conv_precision()
+    ops.set_conv_precision("bf16x3")
+    try:
+        g = torch.Generator().manual_seed(5 + cin + S)
+        w = (torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.05).cuda()
+        x = torch.randn(N, S, S, S, cin, generator=g).cuda()
+        A, B, T = cout, cin, 27
+        # forward form uses [t][cout][cin] (tr 0); the transposed form of the same layer's dgrad
+        # uses [t][cin][cout] (tr 1) with ny = cin
+        tr = 1 if transposed else 0
+        ny = cin if transposed else cout
+        if transposed:
+            x = torch.randn(N, S, S, S, cout, generator=g).cuda()
+        wp = torch.empty(w.numel(), device="cuda")
+        wsp = torch.empty(w.numel(), device="cuda")
+        ops.PackTable().run([(w, A, B, T, tr, wp), (w, A, B, T, 2 + tr, wsp)])
+        single = torch.empty_like(wsp)
+        ops.pack_weight(w, A, B, T, 2 + tr, single)
+        want = ops.conv3d(x, wp, ny, 3, 1, 1, (S, S, S), transposed=transposed)
+        got = ops.conv3d(x, wp, ny, 3, 1, 1, (S, S, S), transposed=transposed, wsplit=wsp)
+        torch.cuda.synchronize()
+        assert torch.equal(single, wsp)
+        assert torch.equal(got, want)
+    finally:
+        ops.set_conv_precision(prev)
