@@ -200,8 +200,11 @@ def main():
     opt.isTrain, opt.gpu_ids = True, 0
     torch.manual_seed(0)
     random.seed(0)
-    model = create_model(opt)
-    model.setup(opt)
+    # the reference's network-init banner goes to stderr: stdout carries only the JSON line
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):
+        model = create_model(opt)
+        model.setup(opt)
 
     g = torch.Generator().manual_seed(1000 + rank)
     shape = (args.batch, 1, args.size, args.size, args.size)
