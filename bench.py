@@ -9,12 +9,19 @@ gradients all-reduced inside the step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 64] [--batch 2]
 
+With --gpus N > 1 and no torch.distributed environment, the script launches its own N ranks
+(torch.distributed.run, one process per GPU, 127.0.0.1 rendezvous) as a child process before
+touching the GPU and exits with its status.
+
 Prints ONE JSON line on rank 0 (contract in the task description), with:
-  roofline     — the dominant kernel (res-block 3×3×3 conv, LDS-halo implicit GEMM): algorithmic
-                 FLOP per launch ÷ its mean launch duration, timed with HIP events around every
-                 such launch inside the timed region;
-  cpu_baseline — the CPU oracle (oracle/cyclegan_oracle.py, the reference's algorithm restated
-                 in PyTorch-CPU) timed on this host for one step of the same workload.
+  roofline      — the dominant kernel BY TIME: every instrumented C-ABI call of two eager steps
+                  (right after the timed region) is bracketed by HIP events on its stream and
+                  grouped by launch class (op + shape); the class with the largest total time is
+                  reported with its algorithmic FLOP (or bytes) per launch ÷ its mean duration;
+  step_roofline — SURVEY §8(d)'s whole-step figure, (F/P_mfma + B_ew/BW_hbm) / T_step;
+  cpu_baseline  — the CPU oracle (oracle/cyclegan_oracle.py, the reference's algorithm restated
+                  in PyTorch-CPU) timed on this host, median of --cpu-steps steps of the same
+                  workload.
 """
 import argparse
 import json
@@ -32,6 +39,7 @@ import torch  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix/vector peak
 MFMA_BF16_PEAK_TFLOPS = 2516.6   # 16 × the f32 MFMA rate (dense bf16, no sparsity)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 
 def parse():
@@ -46,7 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3"],
                     help="dense-conv contraction: exact f32 MFMA or split-bf16 (bf16x3) MFMA, fp32 accumulate")
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: median of this many oracle steps")
+    ap.add_argument("--nc", type=int, default=1, help="image channels (input_nc = output_nc)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels from Python every step (default: replay the step as HIP graphs)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
@@ -116,15 +125,16 @@ def cpu_baseline(args):
     torch.set_num_threads(host_threads())
     threads = torch.get_num_threads()
     torch.manual_seed(0)
-    orc = CycleGANOracle(ngf=args.ngf, ndf=args.ngf, netG=args.netG, pool_rng=random.Random(0))
-    shape = (args.batch, 1, args.size, args.size, args.size)
+    orc = CycleGANOracle(input_nc=args.nc, output_nc=args.nc, ngf=args.ngf, ndf=args.ngf, netG=args.netG,
+                         pool_rng=random.Random(0))
+    shape = (args.batch, args.nc, args.size, args.size, args.size)
     times = []
     for i in range(args.cpu_steps):
         A, B = synthetic_pair(shape, 1000 + i)
         t0 = time.perf_counter()
         orc.optimize_parameters(A, B)
         times.append(time.perf_counter() - t0)
-    t = min(times)
+    t = sorted(times)[len(times) // 2]
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -134,15 +144,17 @@ def cpu_baseline(args):
     except OSError:
         pass
     return {"value": args.batch / t, "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} optimize_parameters() step(s) of the CPU oracle (PyTorch-CPU fp32) on "
-                      f"{args.batch}x1x{args.size}^3, best {t:.2f} s, {cpu_model}"}
+            "sample": f"median of {len(times)} optimize_parameters() steps of the CPU oracle (PyTorch-CPU fp32) on "
+                      f"{args.batch}x{args.nc}x{args.size}^3: {t:.2f} s (all: "
+                      + ", ".join(f"{x:.2f}" for x in times) + f" s), {threads} threads, {cpu_model}"}
 
 
-def cpu_baseline_child(args, timeout_s=240):
+def cpu_baseline_child(args, timeout_s=300):
     """Run cpu_baseline() in a child process (the GPU process only waits), bounded in time."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--size", str(args.size),
-           "--batch", str(args.batch), "--ngf", str(args.ngf), "--netG", args.netG, "--cpu-steps", str(args.cpu_steps)]
+           "--batch", str(args.batch), "--ngf", str(args.ngf), "--netG", args.netG, "--cpu-steps", str(args.cpu_steps),
+           "--nc", str(args.nc)]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
         for line in r.stdout.splitlines():
@@ -155,16 +167,43 @@ def cpu_baseline_child(args, timeout_s=240):
                 "sample": f"CPU oracle step exceeded {timeout_s} s on this host; not reported"}
 
 
-def measured_traffic(key):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (profiles/traffic.json, written by tools/pmc_traffic.py: (2·FETCH_SIZE + WRITE_SIZE)·1 KiB,
-    the gfx950 correction); None when no pass was recorded for this configuration."""
+def measured_traffic(kernels, cls):
+    """HBM bytes per launch of the dominant launch class from the committed PMC passes
+    (profiles/traffic.json, written by tools/pmc_traffic.py: (2·FETCH_SIZE + WRITE_SIZE), the
+    gfx950 FETCH_SIZE correction), keyed by "<kernel names>|<launch class>"; None when no pass was
+    recorded for this configuration."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as fh:
-            return json.load(fh)[key]["hbm_bytes_per_launch"]
+            rec = json.load(fh)[f"{kernels}|{cls}"]
+        return rec["hbm_bytes_per_launch"], rec.get("source")
     except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def launch_ranks(args):
+    """--gpus N without a torch.distributed environment: run this script as N ranks under
+    torch.distributed.run (a child process; this process never touches the GPU) and return its
+    exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def ew_bytes_per_patch(S, netG, elem_bytes=4):
+    """SURVEY §8(d) secondary HBM term: the InstanceNorm/activation/pad/residual traffic of one
+    patch's step, ≈ 8 passes × 118·S³ elements per G fwd+bwd × 6 G passes = 5664·S³ elements
+    (resnet generators; None for the UNet)."""
+    if netG.startswith("unet"):
         return None
+    return 5664.0 * S ** 3 * elem_bytes
 
 
 def main():
@@ -172,9 +211,13 @@ def main():
     if args.cpu_baseline_only:
         print(json.dumps(cpu_baseline(args)), flush=True)
         return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -193,6 +236,7 @@ def main():
 
     sys_argv = sys.argv
     sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
+                "--input_nc", str(args.nc), "--output_nc", str(args.nc),
                 "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
                 "--conv_precision", args.precision] + (["--no_cuda_graph"] if args.no_graph else [])
     opt = TrainOptions().gather_options()
@@ -207,7 +251,7 @@ def main():
         model.setup(opt)
 
     g = torch.Generator().manual_seed(1000 + rank)
-    shape = (args.batch, 1, args.size, args.size, args.size)
+    shape = (args.batch, args.nc, args.size, args.size, args.size)
     n_in = args.warmup + args.steps
     inputs = [(torch.randn(shape, generator=g).cuda(), torch.randn(shape, generator=g).cuda()) for _ in range(n_in)]
 
@@ -216,62 +260,44 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # dominant kernel of the batched first G pass: resnet — residual-block conv 4ngf→4ngf k3
-    # (forward form); unet — the level-1 upconv ConvTranspose3d(4ngf → ngf, k4 s2) (the largest
-    # conv of the net).  Its launches are bracketed by HIP events: recorded eagerly in --no-graph
-    # mode, recorded into the captured step graph otherwise (event nodes, re-recorded by every
-    # replay, so after the timed region they hold the last timed step's launches).
-    unet = args.netG.startswith("unet")
-    c4 = 4 * args.ngf
-    s4 = args.size // 4
-    n_launch = 2 * args.batch
-    if unet:
-        match = lambda i: (i["cin"] == c4 and i["cout"] == args.ngf and i["k"] == 4 and i["transposed"]
-                           and i["N"] == n_launch)
-    else:
-        match = lambda i: (i["cin"] == c4 and i["cout"] == c4 and i["k"] == 3 and i["s"] == 1 and
-                           not i["transposed"] and i["N"] == n_launch)
-    ops.TIMER.match = match
     for i in range(args.warmup):
         model.set_input(inputs[i])
         model.optimize_parameters()
     barrier()
-    ops.TIMER.reset()
-    start = torch.cuda.Event(enable_timing=True)
-    end = torch.cuda.Event(enable_timing=True)
+    # per-step events on the step's stream (no host sync inside the timed region): the median
+    # step time; the JSON's value is the whole region's throughput
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     barrier()
     t0 = time.perf_counter()
-    start.record()
+    marks[0].record()
     for i in range(args.steps):
         model.set_input(inputs[args.warmup + i])
         model.optimize_parameters()
-    end.record()
+        marks[i + 1].record()
     barrier()
     wall = time.perf_counter() - t0
-    ops.TIMER.match = None
     graphed = getattr(model, "_graphs", None) is not None
-    elapsed = start.elapsed_time(end) / 1e3
-    elapsed = max(elapsed, wall)
+    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2]
+    elapsed = max(marks[0].elapsed_time(marks[-1]) / 1e3, wall)
     if dist is not None:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed, median_ms], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    timing = "HIP events around each launch inside the timed region"
-    if graphed:
-        # ROCm refuses timing events inside a captured graph (torch: "External events are
-        # disallowed in rocm"; hipEventRecordWithFlags(external) fails in capture), so the same
-        # launches are timed in two eager steps right after the timed region
-        ops.TIMER.reset()
-        ops.TIMER.match = match
-        model._use_graph = False
-        for i in range(2):
-            model.set_input(inputs[args.warmup + i])
-            model.optimize_parameters()
-        model._use_graph = True
-        ops.TIMER.match = None
-        timing = "HIP events around each launch, 2 eager steps right after the timed (graph-replayed) region"
-    kern_ms = ops.TIMER.mean_ms()
-    n_kern = len(ops.TIMER.events)
+        elapsed, median_ms = float(t[0]), float(t[1])
+
+    # dominant kernel by time: two eager steps right after the timed region, every instrumented
+    # C-ABI call bracketed by HIP events (ROCm refuses timing events inside a captured graph)
+    ops.TIMER.reset()
+    ops.TIMER.match = lambda info: True
+    use_graph = model._use_graph
+    model._use_graph = False
+    for i in range(2):
+        model.set_input(inputs[args.warmup + i])
+        model.optimize_parameters()
+    model._use_graph = use_graph
+    ops.TIMER.match = None
+    classes = ops.TIMER.classes()
+    barrier()
 
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
@@ -279,25 +305,27 @@ def main():
 
     patches = world * args.batch * args.steps
     value = patches / elapsed
-    if unet:
-        flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * args.ngf * 64
-    else:
-        flops_launch = 2.0 * n_launch * s4 ** 3 * c4 * c4 * 27
-    achieved = flops_launch / (kern_ms / 1e3) / 1e12 if kern_ms else None
-    step_tf = step_flops(args.size, args.batch, args.ngf, args.netG) / 1e12
     x3 = args.precision == "bf16x3"
-    # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic (fp32) FLOPs is
-    # the bf16 dense peak / 3
-    peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
+    mfma_peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
     prec = "bf16x3 split MFMA" if x3 else "f32 MFMA"
-    if unet:
-        kname = (f"conv_igemm_kernel ({prec}, parity classes) level-1 upconv ConvTranspose3d {c4}->{args.ngf} k4 s2 "
-                 f"[{n_launch}x{s4}^3 in]")
-        traffic = measured_traffic(f"unet_up1:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
+    dom_cls, dom = next(iter(classes.items()))
+    per_step_ms = dom["total_ms"] / 2
+    if dom["flops"]:
+        achieved = dom["flops"] / (dom["mean_ms"] / 1e3) / 1e12
+        peak, unit, bound = mfma_peak, "TFLOP/s", "mfma"
     else:
-        kname = (f"{'conv_brick_x3_kernel' if x3 else 'conv_brick_kernel'} (LDS-halo implicit GEMM, {prec}) "
-                 f"res-block conv {c4}->{c4} k3 [{n_launch}x{s4}^3] fwd")
-        traffic = measured_traffic(f"res_fwd:S{args.size}:N{n_launch}:ngf{args.ngf}" + (":bf16x3" if x3 else ""))
+        achieved = dom["bytes"] / (dom["mean_ms"] / 1e3) / 1e9
+        peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
+    traffic, traffic_src = measured_traffic(dom["kernels"], dom_cls)
+    top = [dict(cls=c, kernels=v["kernels"], launches_per_step=v["n"] // 2, ms_per_step=round(v["total_ms"] / 2, 4),
+                mean_us=round(1e3 * v["mean_ms"], 2),
+                frac=round((v["flops"] / (v["mean_ms"] / 1e3) / 1e12) / mfma_peak if v["flops"] else
+                           (v["bytes"] / (v["mean_ms"] / 1e3) / 1e9) / HBM_PEAK_GBS, 4))
+           for c, v in list(classes.items())[:8]]
+    step_tf = step_flops(args.size, args.batch, args.ngf, args.netG, nc=args.nc) / 1e12
+    ew = ew_bytes_per_patch(args.size, args.netG)
+    t_step = elapsed / args.steps
+    ideal_s = step_tf / mfma_peak + (args.batch * ew / (HBM_PEAK_GBS * 1e9) if ew else 0.0)
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
         "value": round(value, 3),
@@ -305,27 +333,36 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "ms_per_step": round(1e3 * t_step, 3),
+        "ms_per_step_median": round(median_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if not x3 else "f32 (bf16x3 split products, f32 accumulate)",
         "data": "synthetic N(0,1) volumes, random init (seed 0)",
-        "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, 1ch->1ch, "
-                               f"{args.size}^3 patch, batch {args.batch}/GPU ("
+        "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, "
+                               f"{args.nc}ch->{args.nc}ch, {args.size}^3 patch, batch {args.batch}/GPU ("
                                + ("BASELINE configs[3] generator family" if args.netG.startswith("unet")
-                                  else "BASELINE configs[1] shape") + "; fp32 tensors)",
+                                  else "BASELINE configs[1] shape" if (args.size, args.nc) == (64, 1)
+                                  else "per-GPU unit of a BASELINE config") + "; fp32 tensors)",
                    "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}",
                    "step_launch": "hip_graph" if graphed else "eager"},
-        "roofline": {"bound": "mfma", "kernel": kname,
-                     "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": traffic, "launch_ms": round(kern_ms, 4) if kern_ms else None,
-                     "launches_timed": n_kern, "flop_per_launch": flops_launch, "timing": timing},
+        "roofline": {"bound": bound, "kernel": f"{dom['kernels']} ({prec}) — {dom_cls}",
+                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
+                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "launch_ms": round(dom["mean_ms"], 4), "launches_per_step": dom["n"] // 2,
+                     "ms_per_step": round(per_step_ms, 4),
+                     "flop_per_launch": dom["flops"], "bytes_per_launch": dom["bytes"],
+                     "timing": "HIP events around each C-ABI call, 2 eager steps right after the timed region"},
+        "top_kernels": top,
+        "step_roofline": {"achieved": round(ideal_s / t_step, 4), "ideal_ms": round(1e3 * ideal_s, 3),
+                          "formula": "(F/P_mfma + B_ew/BW_hbm) / T_step (SURVEY 8d)",
+                          "F_tflop": round(step_tf, 4), "P_mfma_tflops": round(mfma_peak, 1),
+                          "B_ew_gb": round(args.batch * ew / 1e9, 3) if ew else None, "BW_hbm_gbs": HBM_PEAK_GBS},
         "step_tflop": round(step_tf, 4),
-        "step_tflops_achieved": round(step_tf * args.steps / elapsed, 2),
+        "step_tflops_achieved": round(step_tf / t_step, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_child(args)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 6
+#define MRAGAN_ABI_VERSION 7
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -159,6 +159,24 @@ int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
 int mragan_adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out6);
 int mragan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, void* stream);
 int mragan_fill(float* p, int64_t n, float value, void* stream);
+/* ---- sliding-window inference (test.py:38-207 + TestModel, models/test_model.py) -------------
+ * The normalised volume vol[X][Y][Z] (fp32, resident) is cut into the reference's patches and the
+ * generator's predictions are overlap-averaged back, both on the device.  (ABI 7)
+ *   gather:  out[p][a][b][c] = (vol[s_p + (a,b,c)] − 127.5) / 127.5   (test.py:150; numpy rounding)
+ *            starts: DEVICE int32 array of n (x, y, z) corners (test.py:111-143 order);
+ *   combine: pred[p][px][py][pz] for every patch p of the full grid, p = (i·jnum + j)·knum + k with
+ *            inum = ⌈(X−px)/stride_inplane⌉ + 1 etc.; per voxel, label = Σ_p (pred·127.5 + 127.5)
+ *            accumulated in fp32 in patch order from 0, divided by the cover count, + 0.01
+ *            (test.py:160-173) — bit-identical to the host loop for the same predictions.     */
+int mragan_patch_gather(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz,
+                        float* out, void* stream);
+int mragan_patch_combine(const float* pred, int X, int Y, int Z, int px, int py, int pz, int stride_inplane,
+                         int stride_layer, float* label, void* stream);
+
+/* diagnostics: the kernel families launched by this thread since the last reset, ';'-joined
+ * (e.g. "conv_wgrad3_x3;wgrad_reduce"); reset = 1 clears the log after copying it.  (ABI 7) */
+const char* mragan_launch_log(int reset);
+
 /* diagnostics: copy the per-block phase timestamps (s_memtime) the 1-channel bf16x3 convolution
  * records when MRAGAN_STAMPS is set; n ≤ 40960 values, 5 per block. */
 int mragan_debug_stamps(unsigned long long* host, int n);

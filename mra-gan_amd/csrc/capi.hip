@@ -17,7 +17,19 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// launch log (diagnostics): the names passed to check_launch since the last reset, ';'-joined,
+// so a caller can name the kernels one C-ABI call launched (bench.py's roofline label)
+static thread_local char g_log[1024] = "";
+static thread_local size_t g_log_len = 0;
+
 int check_launch(const char* what) {
+  const size_t n = strlen(what);
+  if (g_log_len + n + 2 < sizeof(g_log)) {
+    if (g_log_len) g_log[g_log_len++] = ';';
+    memcpy(g_log + g_log_len, what, n);
+    g_log_len += n;
+    g_log[g_log_len] = 0;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("%s: launch failed: %s", what, hipGetErrorString(e));
@@ -237,6 +249,35 @@ int mragan_debug_stamps(unsigned long long* host, int n) { return thin1_debug_st
 int mragan_fill(float* p, int64_t n, float value, void* stream) {
   MRAGAN_CHECK_ARG(p, "fill: null");
   return fill(p, n, value, static_cast<hipStream_t>(stream));
+}
+
+int mragan_patch_gather(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz,
+                        float* out, void* stream) {
+  MRAGAN_CHECK_ARG(vol && starts && out && n >= 0, "patch_gather: bad args");
+  MRAGAN_CHECK_ARG(px > 0 && py > 0 && pz > 0 && px <= X && py <= Y && pz <= Z, "patch_gather: patch larger than volume");
+  return patch_gather(vol, X, Y, Z, starts, n, px, py, pz, out, static_cast<hipStream_t>(stream));
+}
+
+int mragan_patch_combine(const float* pred, int X, int Y, int Z, int px, int py, int pz, int stride_inplane,
+                         int stride_layer, float* label, void* stream) {
+  MRAGAN_CHECK_ARG(pred && label, "patch_combine: null pointer");
+  MRAGAN_CHECK_ARG(px > 0 && py > 0 && pz > 0 && px <= X && py <= Y && pz <= Z, "patch_combine: patch larger than volume");
+  MRAGAN_CHECK_ARG(stride_inplane > 0 && stride_layer > 0, "patch_combine: bad stride");
+  const int inum = (X - px + stride_inplane - 1) / stride_inplane + 1;
+  const int jnum = (Y - py + stride_inplane - 1) / stride_inplane + 1;
+  const int knum = (Z - pz + stride_layer - 1) / stride_layer + 1;
+  return patch_combine(pred, X, Y, Z, px, py, pz, inum, jnum, knum, stride_inplane, stride_layer, label,
+                       static_cast<hipStream_t>(stream));
+}
+
+const char* mragan_launch_log(int reset) {
+  static thread_local char copy[1024];
+  memcpy(copy, g_log, sizeof(copy));
+  if (reset) {
+    g_log_len = 0;
+    g_log[0] = 0;
+  }
+  return copy;
 }
 
 }  // extern "C"

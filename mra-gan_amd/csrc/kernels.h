@@ -141,4 +141,10 @@ struct PackEntry {          // layout shared with include/mragan_hip.h (mragan_p
 int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st);
 int fill(float* p, int64_t n, float v, hipStream_t st);
 
+// sliding-window inference (sliding.hip)
+int patch_gather(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz, float* out,
+                 hipStream_t st);
+int patch_combine(const float* pred, int X, int Y, int Z, int px, int py, int pz, int inum, int jnum, int knum, int s_in,
+                  int s_lay, float* label, hipStream_t st);
+
 }  // namespace mragan

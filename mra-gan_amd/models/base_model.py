@@ -83,9 +83,30 @@ class BaseModel:
                 out[name] = float(getattr(self, 'loss_' + name))
         return out
 
+    def sync_running_stats(self):
+        """Data-parallel runs: every rank updates the InstanceNorm running statistics from its
+        own patches only (weights stay identical through the gradient all-reduce).  Average them
+        over the ranks — the statistics of the global batch's calls — so every rank holds, and
+        saves, the same buffers.  No-op on a single process."""
+        try:
+            import torch.distributed as dist
+        except ImportError:
+            return
+        if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            return
+        world = dist.get_world_size()
+        for name in self.model_names:
+            if isinstance(name, str):
+                for k, buf in getattr(self, 'net' + name).named_buffers():
+                    if k.endswith('running_mean') or k.endswith('running_var'):
+                        dist.all_reduce(buf)
+                        buf.div_(world)
+
     def save_networks(self, which_epoch):
         """Writes '<epoch>_net_<name>.pth' = the net's state_dict on CPU (reference :89-112).
-        The net itself is not moved (its parameters live in flat device buffers)."""
+        The net itself is not moved (its parameters live in flat device buffers).  Data parallel:
+        the running statistics are averaged over the ranks first (every rank must call this)."""
+        self.sync_running_stats()
         os.makedirs(self.save_dir, exist_ok=True)
         for name in self.model_names:
             if isinstance(name, str):

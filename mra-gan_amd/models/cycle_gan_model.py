@@ -31,7 +31,7 @@ device = networks3D.device
 
 class ImagePool():
     """cycle_gan_model.py:8-35: history of generated images (Python `random`, like the
-    reference).  Images are kept as NDHWC device tensors."""
+    reference).  Returns the batch as one tensor (torch.cat of the chosen images)."""
 
     def __init__(self, pool_size):
         self.pool_size = pool_size
@@ -47,17 +47,17 @@ class ImagePool():
             image = image.detach().unsqueeze(0)
             if self.num_imgs < self.pool_size:
                 self.num_imgs += 1
-                self.images.append(image.clone())
+                self.images.append(image)
                 out.append(image)
             else:
                 if random.uniform(0, 1) > 0.5:
                     rid = random.randint(0, self.pool_size - 1)
-                    tmp = self.images[rid]
-                    self.images[rid] = image.clone()
+                    tmp = self.images[rid].clone()
+                    self.images[rid] = image
                     out.append(tmp)
                 else:
                     out.append(image)
-        return out
+        return torch.cat(out, 0)
 
 
 class DeviceImagePool:
@@ -65,10 +65,12 @@ class DeviceImagePool:
 
     `plan()` makes exactly the reference's draws (`random.uniform`, then `random.randint` for a
     swap; cycle_gan_model.py:20-35) on the host and resolves them into two index vectors;
-    `apply()` executes them on the device: the pool's slots live in one tensor
-    [slots | trash | this batch's fakes]; the returned batch is an index_select (a slot's old
-    image, or a fake), the stores an index_copy of the fakes into the slots that end up holding
-    them (the others go to the trash row).  Same images, same order as ImagePool."""
+    `apply()` executes them on the device.  The pool's rows live in one tensor
+    [P slots | trash | fakes of this batch (capacity ≥ b)]: the returned batch is an index_select
+    (a slot's old image, or a fake), the stores an index_copy of the fakes into the slots that end
+    up holding them (the others go to the trash row).  Same images, same order as ImagePool, for
+    any sequence of batch sizes (the last, smaller batch of an epoch included: train.py:52 has no
+    drop_last) — the slot rows never move when the fake region grows."""
 
     def __init__(self, pool_size):
         self.pool_size = pool_size
@@ -97,17 +99,43 @@ class DeviceImagePool:
             store[k] = slot
         return ret, store
 
+    def reserve(self, b, image_shape, device, dtype=torch.float32):
+        """Make room for a batch of b images of `image_shape`; stored images are kept.  Called on
+        the host before the step (a graph capture must not allocate or move the pool)."""
+        P = self.pool_size
+        image_shape = tuple(image_shape)
+        if self.buf is not None and (tuple(self.buf.shape[1:]) != image_shape or self.buf.device != device):
+            if self.num_imgs:
+                raise RuntimeError("DeviceImagePool: image shape changed with images in the pool")
+            self.buf = None
+        if self.buf is None or self.buf.shape[0] < P + 1 + b:
+            nb = torch.zeros((P + 1 + b,) + image_shape, device=device, dtype=dtype)
+            if self.buf is not None:
+                nb[:P + 1].copy_(self.buf[:P + 1])
+            self.buf = nb
+        return self.buf
+
     def apply(self, fakes, out, ret_idx, store_idx):
         """fakes [b, ...] → out [b, ...]; ret_idx/store_idx: int64 index tensors from plan()."""
         P, b = self.pool_size, fakes.shape[0]
-        shape = (P + 1 + b,) + tuple(fakes.shape[1:])
-        if self.buf is None or tuple(self.buf.shape) != shape or self.buf.device != fakes.device:
-            if self.buf is not None and self.num_imgs:
-                raise RuntimeError("DeviceImagePool: image shape changed with images in the pool")
-            self.buf = torch.zeros(shape, device=fakes.device, dtype=fakes.dtype)
-        self.buf[P + 1:].copy_(fakes)
-        torch.index_select(self.buf, 0, ret_idx, out=out)
-        self.buf.index_copy_(0, store_idx, fakes)
+        buf = self.reserve(b, fakes.shape[1:], fakes.device, fakes.dtype)[:P + 1 + b]
+        buf[P + 1:].copy_(fakes)
+        torch.index_select(buf, 0, ret_idx, out=out)
+        buf.index_copy_(0, store_idx, fakes)
+
+    def query(self, images):
+        """The reference's `ImagePool.query` (cycle_gan_model.py:15-35) on a device batch
+        [b, C, D, H, W]: returns the pooled batch as one tensor, same draws, same images."""
+        if self.pool_size == 0:
+            return images
+        b = images.shape[0]
+        ret, store = self.plan(b)
+        x = images.detach().float().permute(0, 2, 3, 4, 1).contiguous()
+        out = torch.empty_like(x)
+        dev = x.device
+        self.apply(x, out, torch.tensor(ret, dtype=torch.int64, device=dev),
+                   torch.tensor(store, dtype=torch.int64, device=dev))
+        return out.permute(0, 4, 1, 2, 3)
 
 
 def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
@@ -165,6 +193,8 @@ class FusedAdam(torch.optim.Optimizer):
             m, v = self._state(n)
             ops_mod().adam_dev(n._flat_param, n._flat_grad, m, v, hyper)
             n.mark_params_dirty()
+        # what torch's step wrapper records for an LR scheduler (it warns otherwise)
+        self._opt_called = True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -181,6 +211,7 @@ class FusedAdam(torch.optim.Optimizer):
             ops.adam(n._flat_param, n._flat_grad, self._m[key], self._v[key], g['lr'], beta1, beta2, g['eps'],
                      self.step_count, self.grad_scale)
             n.mark_params_dirty()
+        self._opt_called = True
 
 
 class CycleGANModel(BaseModel):
@@ -242,6 +273,7 @@ class CycleGANModel(BaseModel):
         self._rs_tables = None       # running-stat update tables of the captured step
         self._graph_key = None
         self._eager_steps = 0
+        self._eager_shapes = set()   # input shapes stepped eagerly (workspaces sized for them)
         self._in = {}                # persistent input buffers (the graphs read them)
 
     # ------------------------------------------------------------------ inputs / visuals
@@ -288,22 +320,30 @@ class CycleGANModel(BaseModel):
 
     # ------------------------------------------------------------------ training step
     def forward_train(self):
-        """The four cycle passes plus the two identity passes, batched (see module doc)."""
+        """The four cycle passes plus the two identity passes, batched (see module doc).  With
+        lambda_identity <= 0 the reference runs no identity pass (cycle_gan_model.py:174-194),
+        so each generator then runs its own input only."""
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
             networks3D.ensure_flat(n)
         A, B = _to_ndhwc(self.real_A), _to_ndhwc(self.real_B)
         b = A.shape[0]
         self._A, self._B, self._b = A, B, b
+        self._idt = self.opt.lambda_identity > 0
         pGA, pGB = self.netG_A.plan, self.netG_B.plan
-        self._cGA1 = pGA.forward(torch.cat([A, B], 0))       # [fake_B; idt_A]
-        self._cGB1 = pGB.forward(torch.cat([B, A], 0))       # [fake_A; idt_B]
-        fake_B, idt_A = self._cGA1.out[:b], self._cGA1.out[b:]
-        fake_A, idt_B = self._cGB1.out[:b], self._cGB1.out[b:]
+        if self._idt:
+            self._cGA1 = pGA.forward(torch.cat([A, B], 0))       # [fake_B; idt_A]
+            self._cGB1 = pGB.forward(torch.cat([B, A], 0))       # [fake_A; idt_B]
+        else:
+            self._cGA1 = pGA.forward(A)                          # fake_B
+            self._cGB1 = pGB.forward(B)                          # fake_A
+        fake_B = self._cGA1.out[:b]
+        fake_A = self._cGB1.out[:b]
         self._cGB2 = pGB.forward(fake_B)                     # rec_A
         self._cGA2 = pGA.forward(fake_A)                     # rec_B
         self._fake_B, self._fake_A = fake_B, fake_A
-        self._publish(fake_B=fake_B, idt_A=idt_A, fake_A=fake_A, idt_B=idt_B, rec_A=self._cGB2.out,
-                      rec_B=self._cGA2.out)
+        self._publish(fake_B=fake_B, fake_A=fake_A, rec_A=self._cGB2.out, rec_B=self._cGA2.out)
+        if self._idt:
+            self._publish(idt_A=self._cGA1.out[b:], idt_B=self._cGB1.out[b:])
 
     def backward_G(self):
         """cycle_gan_model.py:163-225: identity, GAN and cycle losses; backward through the 6
@@ -325,12 +365,10 @@ class CycleGANModel(BaseModel):
         d_recB = torch.empty_like(self._cGA2.out)
         ops.l1_loss(self._cGB2.out, A, lA, L[2:3], d_recA)                             # loss_cycle_A
         ops.l1_loss(self._cGA2.out, B, lB, L[6:7], d_recB)                             # loss_cycle_B
-        if li > 0:
+        if self._idt:
             ops.l1_loss(self._cGA1.out[b:], B, lB * li, L[3:4], dGA1[b:])              # loss_idt_A
             ops.l1_loss(self._cGB1.out[b:], A, lA * li, L[7:8], dGB1[b:])              # loss_idt_B
-        else:
-            ops.fill(dGA1[b:], 0.0)
-            ops.fill(dGB1[b:], 0.0)
+        else:                                                                          # reference: 0
             ops.fill(L[3:4], 0.0)
             ops.fill(L[7:8], 0.0)
         # frozen D: data gradients only, written into the fake halves
@@ -371,8 +409,10 @@ class CycleGANModel(BaseModel):
     def _running_entries(self):
         """Per network, the IN running-stat updates of this step in the reference's call order."""
         b = self._b
-        return [self.netG_A.plan.running_entries([(self._cGA1, 0, b), (self._cGA2, 0, b), (self._cGA1, b, b)]),
-                self.netG_B.plan.running_entries([(self._cGB2, 0, b), (self._cGB1, 0, b), (self._cGB1, b, b)]),
+        idA = [(self._cGA1, b, b)] if self._idt else []     # idt_A = G_A(real_B), backward_G
+        idB = [(self._cGB1, b, b)] if self._idt else []     # idt_B = G_B(real_A)
+        return [self.netG_A.plan.running_entries([(self._cGA1, 0, b), (self._cGA2, 0, b)] + idA),
+                self.netG_B.plan.running_entries([(self._cGB2, 0, b), (self._cGB1, 0, b)] + idB),
                 self.netD_A.plan.running_entries([(self._cDA1, 0, b), (self._cDA2, 0, b), (self._cDA2, b, b)]),
                 self.netD_B.plan.running_entries([(self._cDB1, 0, b), (self._cDB2, 0, b), (self._cDB2, b, b)])]
 
@@ -398,6 +438,9 @@ class CycleGANModel(BaseModel):
         b = self.real_A.shape[0]
         retB, stB = self.fake_B_pool.plan(b)
         retA, stA = self.fake_A_pool.plan(b)
+        sp = tuple(self.real_A.shape[2:])
+        self.fake_B_pool.reserve(b, sp + (self.opt.output_nc,), self.device)
+        self.fake_A_pool.reserve(b, sp + (self.opt.input_nc,), self.device)
         hyp = self.optimizer_G.advance() + self.optimizer_D.advance()
         idx = torch.tensor([retB, stB, retA, stA], dtype=torch.int64).pin_memory()
         hyp = torch.tensor(hyp, dtype=torch.float32).pin_memory()
@@ -424,6 +467,7 @@ class CycleGANModel(BaseModel):
     def _capture_key(self):
         nets = (self.netG_A, self.netG_B, self.netD_A, self.netD_B)
         return (tuple(self.real_A.shape), tuple(self.real_B.shape), self.real_A.data_ptr(), self.real_B.data_ptr(),
+                self.fake_A_pool.buf.data_ptr(), self.fake_B_pool.buf.data_ptr(),
                 tuple(n._flat_param.data_ptr() for n in nets), tuple(n._flat_grad.data_ptr() for n in nets),
                 self._step_idx.data_ptr(), self._step_hyper.data_ptr(), bool(self._dist))
 
@@ -463,7 +507,10 @@ class CycleGANModel(BaseModel):
         self._prepare_step()
         hG, hD = self._step_hyper[0:6], self._step_hyper[6:12]
         graphed = False
-        if self._use_graph and self._eager_steps >= 1:
+        shape_key = (tuple(self.real_A.shape), tuple(self.real_B.shape))
+        # a shape is captured only after one eager step at it: that step grows the workspaces
+        # (a capture must not allocate them)
+        if self._use_graph and shape_key in self._eager_shapes:
             if self._graphs is None or self._graph_key != self._capture_key():
                 self._capture()
             graphed = True
@@ -490,3 +537,4 @@ class CycleGANModel(BaseModel):
                 n.mark_params_dirty()
         else:
             self._eager_steps += 1
+            self._eager_shapes.add(shape_key)

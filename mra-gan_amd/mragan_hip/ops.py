@@ -55,29 +55,34 @@ WS = Workspace()
 
 
 class KernelTimer:
-    """Optional per-launch HIP-event timing of selected conv launches (used by bench.py to
-    measure the dominant kernel inside the timed region, on the stream it runs on)."""
+    """Optional per-launch HIP-event timing of selected C-ABI calls (bench.py measures the
+    dominant kernel with it, on the stream the kernels run on).  Each instrumented wrapper passes
+    an info dict with a launch-class key `cls`, its algorithmic `flops` (MFMA-bound calls) or
+    `bytes` (HBM-bound calls); the library's launch log names the kernels the call launched."""
 
     def __init__(self):
         self.match = None       # callable(info: dict) -> bool
-        self.events = []
+        self.events = []        # (info, start, end, kernel names)
 
     def begin(self, info):
         if self.match is None or not self.match(info):
             return None
         if torch.cuda.is_current_stream_capturing():
             return None         # ROCm cannot time event nodes of a graph: eager launches only
+        from ._lib import lib
+        lib().mragan_launch_log(1)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # keep the GPU busy until the launch below is queued: otherwise the interval also holds
         # the host's submission latency (the GPU reaches the start event, then idles)
         torch.cuda._sleep(100000)
         s.record()
-        return (s, e)
+        return (info, s, e)
 
-    def end(self, pair):
-        if pair is not None:
-            pair[1].record()
-            self.events.append(pair)
+    def end(self, tok):
+        if tok is not None:
+            tok[2].record()
+            from ._lib import lib
+            self.events.append((tok[0], tok[1], tok[2], lib().mragan_launch_log(1).decode()))
 
     def reset(self):
         self.events = []
@@ -86,7 +91,21 @@ class KernelTimer:
         if not self.events:
             return None
         torch.cuda.synchronize()
-        return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
+        return sum(s.elapsed_time(e) for _, s, e, _ in self.events) / len(self.events)
+
+    def classes(self):
+        """{cls: dict(n, total_ms, mean_ms, flops|bytes per launch, kernels)} over the recorded
+        launches, largest total time first."""
+        torch.cuda.synchronize()
+        out = {}
+        for info, s, e, names in self.events:
+            c = out.setdefault(info["cls"], dict(n=0, total_ms=0.0, flops=info.get("flops"), bytes=info.get("bytes"),
+                                                 kernels=names, info=info))
+            c["n"] += 1
+            c["total_ms"] += s.elapsed_time(e)
+        for c in out.values():
+            c["mean_ms"] = c["total_ms"] / c["n"]
+        return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_ms"]))
 
 
 TIMER = KernelTimer()
@@ -132,8 +151,13 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     elif tuple(out.shape) != (N, Do, Ho, Wo, cout):
         raise ValueError(f"conv3d: out shape {tuple(out.shape)} != {(N, Do, Ho, Wo, cout)}")
     name = "mragan_conv3d_transposed" if transposed else "mragan_conv3d_fwd"
-    tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
-                          in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo))) if TIMER.match else None
+    tm = None
+    if TIMER.match:
+        vox = Di * Hi * Wi if transposed else Do * Ho * Wo       # algorithmic: every tap of every voxel
+        tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
+                              in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo),
+                              cls=f"{'convT' if transposed else 'conv'} {cin}->{cout} k{k} s{s} [{N}x{Di}x{Hi}x{Wi}]",
+                              flops=2.0 * N * vox * cin * cout * k ** 3))
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
     ws = WS.get(nbytes) if nbytes else None
     if wsplit is not None:
@@ -160,8 +184,11 @@ def conv3d_wgrad(dense: torch.Tensor, gathered: torch.Tensor, k: int, s: int, p:
         raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
     nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
     ws = WS.get(nbytes)
+    tm = TIMER.begin(dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
+                          flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3)) if TIMER.match else None
     call("mragan_conv3d_wgrad", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered), Dg, Hg, Wg, Cg, k, s, p, _ptr(dw),
          int(accumulate), _ptr(ws), ws.numel(), _stream())
+    TIMER.end(tm)
     return dw
 
 
@@ -224,8 +251,12 @@ def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch
             raise ValueError("instnorm: residual shape mismatch")
     nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
     ws = WS.get(nbytes)
+    # essential HBM bytes: read x (+ the residual), write y (padded)
+    tm = TIMER.begin(dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad}",
+                          bytes=4.0 * (x.numel() * (2 if resid is not None else 1) + out.numel()))) if TIMER.match else None
     call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad, _ptr(mean),
          _ptr(rstd), _ptr(ws), ws.numel(), _stream())
+    TIMER.end(tm)
     return out, mean, rstd
 
 
@@ -239,8 +270,13 @@ def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: to
         out = torch.empty_like(x)
     nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
     ws = WS.get(nbytes)
+    # essential HBM bytes: read x, dy (padded) (+ dy_add), write dx
+    tm = TIMER.begin(dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad}",
+                          bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0))))\
+        if TIMER.match else None
     call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
          ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
+    TIMER.end(tm)
     return out
 
 
@@ -349,3 +385,32 @@ def adam_dev(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
 
 def fill(t: torch.Tensor, value: float):
     call("mragan_fill", _ptr(t), t.numel(), float(value), _stream())
+
+
+def patch_gather(vol: torch.Tensor, starts: torch.Tensor, patch, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """vol [X, Y, Z] fp32 (device), starts int32 [n, 3] (device) → [n, px, py, pz, 1] NDHWC patches
+    scaled (v − 127.5)/127.5 (test.py:150)."""
+    _check(vol, "patch_gather.vol", ndim=3)
+    if starts.dtype != torch.int32 or not starts.is_cuda or starts.dim() != 2 or starts.shape[1] != 3:
+        raise ValueError("patch_gather: starts must be a device int32 [n, 3] tensor")
+    n = starts.shape[0]
+    px, py, pz = patch
+    if out is None:
+        out = torch.empty((n, px, py, pz, 1), device=vol.device, dtype=torch.float32)
+    X, Y, Z = vol.shape
+    call("mragan_patch_gather", _ptr(vol), X, Y, Z, _ptr(starts.contiguous()), n, px, py, pz, _ptr(out), _stream())
+    return out
+
+
+def patch_combine(pred: torch.Tensor, shape, patch, stride_inplane: int, stride_layer: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """pred: [n_patches, px, py, pz] (any trailing singleton) fp32 for the full patch grid in
+    the reference's visit order → overlap-averaged label volume [X, Y, Z] (test.py:160-173)."""
+    _check(pred, "patch_combine.pred", ndim=0)
+    X, Y, Z = shape
+    px, py, pz = patch
+    if out is None:
+        out = torch.empty((X, Y, Z), device=pred.device, dtype=torch.float32)
+    call("mragan_patch_combine", _ptr(pred), X, Y, Z, px, py, pz, int(stride_inplane), int(stride_layer), _ptr(out),
+         _stream())
+    return out

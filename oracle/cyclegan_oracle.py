@@ -473,11 +473,15 @@ class CycleGANOracle:
         rec_A = self._net("G_B", fake_B, lp["G_B"])
         fake_A = self._net("G_B", real_B, lp["G_B"])
         rec_B = self._net("G_A", fake_A, lp["G_A"])
-        # backward_G (:163-225)
-        idt_A = self._net("G_A", real_B, lp["G_A"])
-        loss_idt_A = l1_loss(idt_A, real_B) * self.lambda_B * self.lambda_idt
-        idt_B = self._net("G_B", real_A, lp["G_B"])
-        loss_idt_B = l1_loss(idt_B, real_A) * self.lambda_A * self.lambda_idt
+        # backward_G (:163-225); lambda_identity <= 0: no identity pass, losses 0 (:191-193)
+        if self.lambda_idt > 0:
+            idt_A = self._net("G_A", real_B, lp["G_A"])
+            loss_idt_A = l1_loss(idt_A, real_B) * self.lambda_B * self.lambda_idt
+            idt_B = self._net("G_B", real_A, lp["G_B"])
+            loss_idt_B = l1_loss(idt_B, real_A) * self.lambda_A * self.lambda_idt
+        else:
+            idt_A = idt_B = None
+            loss_idt_A = loss_idt_B = torch.zeros((), dtype=self.dtype)
         loss_G_A = gan_loss(self._net("D_A", fake_B, dp["D_A"]), True, self.use_lsgan)
         loss_G_B = gan_loss(self._net("D_B", fake_A, dp["D_B"]), True, self.use_lsgan)
         loss_cycle_A = l1_loss(rec_A, real_A) * self.lambda_A
@@ -499,7 +503,8 @@ class CycleGANOracle:
         self.grads.update({k: {n: t.grad.detach().clone() for n, t in dp[k].items()} for k in ("D_A", "D_B")})
         self._adam(["D_A", "D_B"], dp, "D")
         self.fake_B, self.rec_A, self.fake_A, self.rec_B = (t.detach() for t in (fake_B, rec_A, fake_A, rec_B))
-        self.idt_A, self.idt_B = idt_A.detach(), idt_B.detach()
+        self.idt_A = idt_A.detach() if idt_A is not None else None
+        self.idt_B = idt_B.detach() if idt_B is not None else None
         vals = dict(D_A=loss_D_A, G_A=loss_G_A, cycle_A=loss_cycle_A, idt_A=loss_idt_A,
                     D_B=loss_D_B, G_B=loss_G_B, cycle_B=loss_cycle_B, idt_B=loss_idt_B)
         return OrderedDict((k, float(vals[k].detach())) for k in self.LOSS_NAMES)
@@ -511,3 +516,61 @@ def synthetic_pair(shape, seed: int):
     a = torch.randn(shape, generator=g)
     b = torch.randn(shape, generator=g)
     return a, b
+
+
+# ------------------------------------------------------------------------------------------
+# Sliding-window inference (reference test.py:38-207, the array part: lines 96-186)
+# ------------------------------------------------------------------------------------------
+
+def sliding_window_starts(shape, patch, stride_inplane, stride_layer):
+    """test.py:111-143: the patch start corners in the order the reference visits them
+    (i over x, then j over y, then k over z; the last patch of an axis is clamped to the end)."""
+    import math as _m
+    px, py, pz = patch
+    inum = int(_m.ceil((shape[0] - px) / float(stride_inplane))) + 1
+    jnum = int(_m.ceil((shape[1] - py) / float(stride_inplane))) + 1
+    knum = int(_m.ceil((shape[2] - pz) / float(stride_layer))) + 1
+    out = []
+    for i in range(inum):
+        for j in range(jnum):
+            for k in range(knum):
+                istart = i * stride_inplane
+                if istart + px > shape[0]:
+                    istart = shape[0] - px
+                jstart = j * stride_inplane
+                if jstart + py > shape[1]:
+                    jstart = shape[1] - py
+                kstart = k * stride_layer
+                if kstart + pz > shape[2]:
+                    kstart = shape[2] - pz
+                out.append((istart, jstart, kstart))
+    return out
+
+
+def sliding_window_inference(g_forward, image_np, patch, stride_inplane, stride_layer):
+    """test.py:96-186 on an already normalised (0-255, Normalization :639-651), resampled and
+    padded volume `image_np` [x, y, z] float32.  `g_forward(batch [1,1,px,py,pz] float32 tensor)`
+    returns fake_B.  Returns the label volume [x, y, z] float32 (before the final un-padding
+    crop of :180, which the caller applies with its pre-padding size)."""
+    import numpy as np
+    image_np = np.asarray(image_np, dtype=np.float32)
+    label_np = np.zeros(image_np.shape, dtype=np.float32)
+    padding = image_np.shape[2] % 2 != 0                                     # :101-108
+    if padding:
+        image_np = np.pad(image_np, ((0, 0), (0, 0), (0, 1)), 'edge')
+        label_np = np.pad(label_np, ((0, 0), (0, 0), (0, 1)), 'edge')
+    weight_np = np.zeros(label_np.shape)                                     # :113 (float64)
+    px, py, pz = patch
+    for (i0, j0, k0) in sliding_window_starts(image_np.shape, patch, stride_inplane, stride_layer):
+        batch = image_np[i0:i0 + px, j0:j0 + py, k0:k0 + pz][np.newaxis]     # prepare_batch, bs 1
+        batch = (batch - 127.5) / 127.5                                      # :150
+        x = torch.from_numpy(batch[np.newaxis, :, :, :])                     # [1, 1, px, py, pz]
+        pred = g_forward(x)
+        pred = pred.squeeze().detach().cpu().numpy().astype(np.float32)
+        pred = (pred * 127.5) + 127.5                                        # :161
+        label_np[i0:i0 + px, j0:j0 + py, k0:k0 + pz] += pred[:, :, :]
+        weight_np[i0:i0 + px, j0:j0 + py, k0:k0 + pz] += 1.0
+    label_np = (np.float32(label_np) / np.float32(weight_np) + 0.01)        # :173
+    if padding:
+        label_np = label_np[:, :, 0:(label_np.shape[2] - 1)]
+    return label_np

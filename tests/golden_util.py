@@ -13,7 +13,19 @@ CASE_KW = {
     "step_r6_s24_b2_nc2_lsgan": dict(input_nc=2, output_nc=2, ngf=8, ndf=8, n_blocks=6, use_lsgan=True),
     "step_r9_s32_b2_ngf16": dict(input_nc=1, output_nc=1, ngf=16, ndf=16, n_blocks=9, use_lsgan=False),
     "step_unet_s32_b2_ngf8": dict(input_nc=1, output_nc=1, ngf=8, ndf=8, netG="unet_custom", use_lsgan=False),
+    "step_r6_s24_b1_noidt": dict(input_nc=1, output_nc=1, ngf=8, ndf=8, n_blocks=6, use_lsgan=False, lambda_identity=0.0),
+    # BASELINE-size workloads (per-GPU units of configs[1]..[4]); their fixtures carry fp64 runs at
+    # perturbed inputs (fp64p4e-6 / fp64p4e-5), so the tests need no fp64 oracle run of their own
+    "step_r9_s64_b2": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
+    "step_unet_s64_b1_ngf32": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, netG="unet_custom", use_lsgan=False),
+    "step_r9_s96_b1_nc2": dict(input_nc=2, output_nc=2, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
+    "step_r9_s128_b1": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
 }
+
+
+def available_cases():
+    """Step cases whose fixture file is present (the BASELINE-size ones are generated separately)."""
+    return [c for c in CASE_KW if os.path.exists(os.path.join(GOLDEN, c + ".npz"))]
 
 
 def load(name):

@@ -12,14 +12,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(tmp_path, graph, steps, precision):
+def _run(tmp_path, graph, steps, precision, batches=None, extra=()):
     from models import create_model
     from options.train_options import TrainOptions
     argv = sys.argv
     try:
         sys.argv = ["train.py", "--checkpoints_dir", str(tmp_path), "--conv_precision", precision,
                     "--netG", "resnet_6blocks", "--ngf", "8", "--ndf", "8", "--pool_size", "2",
-                    "--batch_size", "2", "--lr_policy", "step", "--lr_decay_iters", "1"]
+                    "--batch_size", "2", "--lr_policy", "step", "--lr_decay_iters", "1"] + list(extra)
         if not graph:
             sys.argv.append("--no_cuda_graph")
         opt = TrainOptions().gather_options()
@@ -33,8 +33,9 @@ def _run(tmp_path, graph, steps, precision):
     g = torch.Generator().manual_seed(5)
     losses = []
     for step in range(steps):
-        A = torch.randn(2, 1, 24, 24, 24, generator=g)
-        B = torch.randn(2, 1, 24, 24, 24, generator=g)
+        b = batches[step] if batches else 2
+        A = torch.randn(b, 1, 24, 24, 24, generator=g)
+        B = torch.randn(b, 1, 24, 24, 24, generator=g)
         model.set_input([A, B])
         model.optimize_parameters()
         losses.append(torch.stack([getattr(model, "loss_" + n).detach().clone() for n in model.loss_names]))
@@ -45,7 +46,8 @@ def _run(tmp_path, graph, steps, precision):
     for n in ("G_A", "G_B", "D_A", "D_B"):
         for k, v in getattr(model, "net" + n).state_dict().items():
             state[f"{n}/{k}"] = v.detach().cpu().clone()
-    vis = {v: getattr(model, v).detach().cpu().clone() for v in ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A")}
+    vis = {v: getattr(model, v).detach().cpu().clone() for v in ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A")
+           if hasattr(model, v)}
     return torch.stack(losses).cpu(), state, vis, model
 
 
@@ -60,6 +62,24 @@ def test_graph_step_bit_identical_to_eager(tmp_path, precision):
     assert me._graphs is None and mg._graphs is not None
     assert mg.fake_B_pool.num_imgs == 2
     assert torch.equal(le, lg), (le - lg).abs().max()
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+    for k in ve:
+        assert torch.equal(ve[k], vg[k]), k
+
+
+def test_graph_step_changing_batch_and_no_identity(tmp_path):
+    """An epoch's smaller last batch (train.py:52, no drop_last) between full ones, with
+    --lambda_identity 0 (no identity passes): the graphed step re-captures per batch shape, the
+    pool keeps its images across the change, and everything stays bit-identical to eager."""
+    batches = [2, 2, 1, 2, 2, 1, 2]
+    extra = ["--lambda_identity", "0"]
+    le, se, ve, me = _run(tmp_path / "e", False, len(batches), "f32", batches, extra)
+    lg, sg, vg, mg = _run(tmp_path / "g", True, len(batches), "f32", batches, extra)
+    assert mg._graphs is not None and not hasattr(mg, "idt_A")
+    assert mg.fake_B_pool.num_imgs == 2
+    assert torch.equal(le, lg), (le - lg).abs().max()
+    assert float(le[:, 3].abs().max()) == 0.0 and float(le[:, 7].abs().max()) == 0.0   # loss_idt_*
     for k in se:
         assert torch.equal(se[k], sg[k]), k
     for k in ve:

@@ -12,10 +12,12 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import CASE_KW, inputs, is_pre_in_bias, load, rel_err, sampled
+from golden_util import CASE_KW, available_cases, inputs, is_pre_in_bias, load, rel_err, sampled
 from oracle.cyclegan_oracle import CycleGANOracle
 
-CASES = list(CASE_KW)
+# the CPU oracle replays the small fixtures (the BASELINE-size ones compare the HIP engine with
+# the reference directly, tests/test_step_gpu.py; an fp64 CPU step at 128³ takes minutes)
+CASES = [c for c in available_cases() if load(c)[1]["S"] <= 32]
 
 
 def _build(name, dtype):
@@ -52,6 +54,9 @@ def test_step_fp64_matches_reference(name):
         assert rel_err(got, want) < 1e-9, (step, got, want)
         if step == 0:
             for vis in ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A", "idt_B"):
+                if f"fp64/step0/{vis}/idx" not in z.files:
+                    assert getattr(orc, vis) is None      # lambda_identity = 0: no identity pass
+                    continue
                 g, w = sampled(z, f"fp64/step0/{vis}", getattr(orc, vis))
                 assert rel_err(g, w) < 1e-9, vis
             for net in ("G_A", "G_B", "D_A", "D_B"):

@@ -27,3 +27,46 @@ def test_device_pool_matches_reference(pool_size, b, queries):
         assert torch.equal(out, want), f"query {q}"
         for k in range(min(pool_size, dev.num_imgs)):
             assert torch.equal(dev.buf[k], ref.images[k][0]), f"slot {k} after query {q}"
+
+
+@pytest.mark.parametrize("pool_size", [0, 1, 3, 5])
+def test_device_pool_changing_batch_size(pool_size):
+    """The last DataLoader batch of an epoch is smaller (train.py:52 has no drop_last): the pool
+    must keep its images across batch-size changes, in both directions."""
+    from models.cycle_gan_model import DeviceImagePool
+    g = torch.Generator().manual_seed(8)
+    ref = ImagePool(pool_size, random.Random(12))
+    random.seed(12)
+    dev = DeviceImagePool(pool_size)
+    for q, b in enumerate([2, 2, 1, 3, 2, 1, 1, 4, 2, 3, 1, 2] * 3):
+        fakes = torch.randn(b, 3, 2, 2, 1, generator=g)
+        want = ref.query(fakes.clone())
+        ret, store = dev.plan(b)
+        out = torch.empty_like(fakes)
+        dev.apply(fakes, out, torch.tensor(ret), torch.tensor(store))
+        assert torch.equal(out, want), f"query {q} (b={b})"
+        for k in range(min(pool_size, dev.num_imgs)):
+            assert torch.equal(dev.buf[k], ref.images[k][0]), f"slot {k} after query {q}"
+
+
+def test_query_returns_tensor_like_reference():
+    """ImagePool.query / DeviceImagePool.query return ONE tensor (reference torch.cat, :34)."""
+    from models.cycle_gan_model import DeviceImagePool
+    from models.cycle_gan_model import ImagePool as EngineImagePool
+    g = torch.Generator().manual_seed(9)
+    ref = ImagePool(2, random.Random(13))
+    random.seed(13)
+    eng = EngineImagePool(2)
+    for q in range(12):
+        x = torch.randn(2, 1, 3, 4, 5, generator=g)
+        want = ref.query(x.clone())
+        got = eng.query(x.clone())
+        assert isinstance(got, torch.Tensor) and torch.equal(got, want), q
+    random.seed(14)
+    ref = ImagePool(2, random.Random(14))
+    dev = DeviceImagePool(2)
+    for q in range(12):
+        x = torch.randn(2, 1, 3, 4, 5, generator=g)
+        want = ref.query(x.clone())
+        got = dev.query(x.clone())
+        assert isinstance(got, torch.Tensor) and got.shape == want.shape and torch.equal(got, want), q

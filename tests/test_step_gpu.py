@@ -7,7 +7,8 @@ Gates (calibrated on the reference's own fp32-vs-fp64 error):
   * step-1 gradients: ‖g − g64‖ ≤ max(1e-3‖g64‖, 2‖g_ref32 − g64‖) on the sampled elements;
     pre-InstanceNorm conv biases: exactly 0 (their true gradient is identically zero);
   * InstanceNorm running statistics after step 1: rel ≤ 1e-4;
-  * later steps: losses within 1e-2 rel (fp32 noise amplified by Adam, as for the reference).
+  * later steps: losses within max(1e-3, k × the reference's own fp32-vs-fp64 divergence at that
+    step) — fp32 noise amplified by Adam, as for the reference (k = 4 exact f32, 10 bf16x3).
 """
 import random
 import sys
@@ -16,11 +17,11 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import CASE_KW, inputs, is_pre_in_bias, load, rel_err, sampled
+from golden_util import CASE_KW, available_cases, inputs, is_pre_in_bias, load, rel_err, sampled
 
 pytestmark = pytest.mark.gpu
 
-CASES = list(CASE_KW)
+CASES = available_cases()
 
 
 def build_model(meta, ckdir, precision="f32"):
@@ -67,7 +68,7 @@ def stepped(request, tmp_path_factory):
         if step == 0:
             snap = dict(
                 vis={v: getattr(model, v).detach().cpu().clone() for v in
-                     ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A", "idt_B")},
+                     ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A", "idt_B") if f"fp64/step0/{v}/idx" in z.files},
                 grads={n: {k: p.grad.detach().cpu().clone() for k, p in getattr(model, "net" + n).named_parameters()}
                        for n in ("G_A", "G_B", "D_A", "D_B")},
                 params={n: {k: p.detach().cpu().clone() for k, p in getattr(model, "net" + n).named_parameters()}
@@ -95,6 +96,8 @@ def test_init_bit_exact(stepped):
 # forward-value gates: exact-f32 MFMA 1e-4 (measured 1e-6…2e-5); bf16x3 split MFMA (≤ 3·2⁻¹⁸ per
 # product) the north star's 1e-3 (measured ≤ 1.5e-4)
 VALUE_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
+# later-step losses: multiple of the reference's own fp32-vs-fp64 divergence at that step
+LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0}
 
 
 def test_losses(stepped):
@@ -103,8 +106,14 @@ def test_losses(stepped):
     want = z["fp64/step0/losses"]
     assert rel_err(got, want) < VALUE_TOL[meta["precision"]], (got, want)
     for step in range(1, meta["steps"]):
+        # after an Adam step the reference's own fp32 run has left its fp64 run (elements with a
+        # round-off-sized gradient step by ±lr either way): gate on that measured divergence
         w = z[f"fp64/step{step}/losses"]
-        assert rel_err(history[step], w) < 1e-2, (step, history[step], w)
+        ref32 = rel_err(z[f"fp32/step{step}/losses"], w)
+        env = max(1e-3, LATER_STEP_FACTOR[meta["precision"]] * ref32)
+        err = rel_err(history[step], w)
+        print(f"{name} step {step}: loss rel err {err:.2e} (reference fp32 {ref32:.2e}, gate {env:.2e})")
+        assert err < env, (step, history[step], w)
 
 
 def test_generated_volumes(stepped):
@@ -127,8 +136,13 @@ def conditioning(stepped):
     makes the step's gradients 1e-3…1e-2-conditioned (tools/diag_d.py traces it)."""
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
-    A, B = inputs(meta, 0)
     eps = PERTURB[meta["precision"]]
+    pre = f"fp64p{eps:g}"
+    if any(k.startswith(pre + "/") for k in z.files):
+        # BASELINE-size cases: the fixture holds the perturbed fp64 run (same protocol, one
+        # realization, generator seed 77) — returned as sampled vectors keyed like the grads
+        return [{"sampled": pre}]
+    A, B = inputs(meta, 0)
     out = []
     for r in range(2):
         g = torch.Generator().manual_seed(77 + r)
@@ -156,7 +170,8 @@ def test_gradients(stepped, conditioning):
             key64 = f"fp64/step0/grad/{net}/{k}"
             g, w64 = sampled(z, key64, gr)
             w32 = z[f"fp32/step0/grad/{net}/{k}/val"]
-            wp = [sampled(z, key64, c[net][k])[0] for c in conditioning]
+            wp = [z[f"{c['sampled']}/step0/grad/{net}/{k}/val"] if "sampled" in c else sampled(z, key64, c[net][k])[0]
+                  for c in conditioning]
             env = max(1e-3, 2 * rel_err(w32, w64), *[2 * rel_err(x, w64) for x in wp])
             r = rel_err(g, w64)
             if r > env:

@@ -33,11 +33,68 @@ CASES = {
                              ["fp32", "fp64"], 3, 2),
     # UnetGenerator (BASELINE configs[3] generator family; unet_custom = 5 downsamplings)
     "step_unet_s32_b2_ngf8": (["--netG", "unet_custom", "--ngf", "8", "--ndf", "8"], 32, 2, 1, ["fp32", "fp64"], 2, 3),
+    # BASELINE-size workloads (the per-GPU unit of each config), default widths ngf = ndf = 32.
+    # "fp64pE" = an fp64 run at inputs perturbed by a relative E (N(0,1) noise, generator seed 77):
+    # how far the exact gradient moves when the forward pass moves by that much (test gate)
+    "step_r9_s64_b2": (["--netG", "resnet_9blocks"], 64, 2, 1, ["fp32", "fp64", "fp64p4e-6", "fp64p4e-5"], 2, 4),
+    "step_unet_s64_b1_ngf32": (["--netG", "unet_custom"], 64, 1, 1, ["fp32", "fp64", "fp64p4e-6", "fp64p4e-5"], 2, 5),
+    "step_r9_s96_b1_nc2": (["--netG", "resnet_9blocks", "--input_nc", "2", "--output_nc", "2"], 96, 1, 2,
+                           ["fp32", "fp64", "fp64p4e-6", "fp64p4e-5"], 1, 6),
+    "step_r9_s128_b1": (["--netG", "resnet_9blocks"], 128, 1, 1, ["fp32", "fp64", "fp64p4e-6", "fp64p4e-5"], 1, 7),
+    # lambda_identity = 0: no identity passes (reference cycle_gan_model.py:174-194 else branch);
+    # the running statistics then see only the four cycle passes
+    "step_r6_s24_b1_noidt": (["--netG", "resnet_6blocks", "--ngf", "8", "--ndf", "8", "--lambda_identity", "0"],
+                             24, 1, 1, ["fp32", "fp64"], 2, 9),
+}
+# reference-written checkpoint (base_model.py:89-112) of a tiny model after one step, plus the
+# losses of the step the reference takes right after it (ckpt_* cases, see run_checkpoint)
+CKPT_CASES = {
+    "ckpt_r6_ngf4": (["--netG", "resnet_6blocks", "--ngf", "4", "--ndf", "4"], 24, 1, 1, 8),
 }
 N_SAMPLES = 256
+DTYPE_PREFIXES = ("fp32", "fp64", "fp64p4e-6", "fp64p4e-5")
+
+
+COL_LIMIT = 2 << 30      # bytes of one im2col buffer of an fp64 CPU convolution
+
+
+def _chunked_conv3d(orig):
+    """fp64 Conv3d on the CPU is ATen's slow_conv3d, whose im2col buffer is (Cin·k³) × (output
+    voxels) elements: 78 GB for the 32→2 head conv at 96³, 184 GB at 128³.  For such calls the
+    output depth is cut into slabs (zero padding applied once up front, each slab convolved
+    'valid' on its input rows, results concatenated): every output element is the same sum over
+    the same products, only the GEMM's blocking changes.  fp32 calls (mkldnn) are untouched."""
+    import torch.nn.functional as F
+
+    def conv3d(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
+        def t3(v):
+            return tuple(v) if isinstance(v, (tuple, list)) else (v, v, v)
+        st, pd, dl = t3(stride), t3(padding), t3(dilation)
+        if isinstance(padding, str) or input.dtype != torch.float64 or groups != 1 or dl != (1, 1, 1):
+            return orig(input, weight, bias, stride, padding, dilation, groups)
+        k = weight.shape[2:]
+        x = F.pad(input, (pd[2], pd[2], pd[1], pd[1], pd[0], pd[0])) if any(pd) else input
+        Do = (x.shape[2] - k[0]) // st[0] + 1
+        Ho = (x.shape[3] - k[1]) // st[1] + 1
+        Wo = (x.shape[4] - k[2]) // st[2] + 1
+        per_row = weight.shape[1] * k[0] * k[1] * k[2] * Ho * Wo * 8
+        rows = max(1, COL_LIMIT // per_row)
+        if rows >= Do:
+            return orig(input, weight, bias, stride, padding, dilation, groups)
+        outs = []
+        for o0 in range(0, Do, rows):
+            o1 = min(Do, o0 + rows)
+            xs = x[:, :, o0 * st[0]:(o1 - 1) * st[0] + k[0]]
+            outs.append(orig(xs, weight, bias, st, 0, 1, 1))
+        return torch.cat(outs, 2)
+    return conv3d
 
 
 def import_reference():
+    import torch.nn.functional as F
+    if not getattr(F.conv3d, "_chunked", False):
+        F.conv3d = _chunked_conv3d(F.conv3d)
+        F.conv3d._chunked = True
     sys.modules["monai"] = types.ModuleType("monai")
     sys.path.insert(0, REF)
     from options.train_options import TrainOptions   # noqa: E402
@@ -54,7 +111,7 @@ def sample(t: torch.Tensor, key: str, out: dict, n=N_SAMPLES):
     flat = t.detach().reshape(-1).double()
     # the sample positions depend on the tensor's name only (not on the fp32/fp64 prefix), so
     # the fp32 and fp64 runs are sampled at identical indices and can be compared directly
-    name = key.split("/", 1)[1] if key.startswith(("fp32/", "fp64/")) else key
+    name = key.split("/", 1)[1] if key.split("/", 1)[0] in DTYPE_PREFIXES else key
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     idx = np.sort(rng.choice(flat.numel(), size=min(n, flat.numel()), replace=False))
     out[key + "/idx"] = idx.astype(np.int64)
@@ -64,11 +121,18 @@ def sample(t: torch.Tensor, key: str, out: dict, n=N_SAMPLES):
     out[key + "/sqsum"] = np.array((flat * flat).sum().item())
 
 
+def perturb(x, eps, g):
+    return x * (1 + eps * torch.randn(x.shape, generator=g, dtype=torch.float64))
+
+
 def run_case(name, argv, S, B, nc, dtypes, steps, seed):
     TrainOptions, create_model = import_reference()
+    import gc
     import random
     out = {}
     for dt in dtypes:
+        eps = float(dt[len("fp64p"):]) if dt.startswith("fp64p") else 0.0
+        gc.collect()
         sys.argv = ["train.py", "--checkpoints_dir", "/tmp/gen_fixtures_ck"] + argv
         opt = TrainOptions().gather_options()
         opt.isTrain = True
@@ -77,7 +141,7 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
         random.seed(seed)
         model = create_model(opt)
         model.setup(opt)
-        if dt == "fp64":
+        if dt.startswith("fp64"):
             for n in ("G_A", "G_B", "D_A", "D_B"):
                 getattr(model, "net" + n).double()
             model.criterionGAN.double()
@@ -88,16 +152,26 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
                     if v.is_floating_point() and k.endswith("weight"):
                         sample(v, f"init/{n}/{k}", out, n=32)
         shape = (B, nc, S, S, S)
-        for step in range(steps):
+        for step in range(steps if not eps else 1):
             A, Bt = synthetic_pair(shape, 1000 + seed + step)
-            if dt == "fp64":
+            if dt.startswith("fp64"):
                 A, Bt = A.double(), Bt.double()
+            if eps:
+                g = torch.Generator().manual_seed(77)
+                A, Bt = perturb(A, eps, g), perturb(Bt, eps, g)
             model.set_input([A, Bt])
             model.optimize_parameters()
             losses = model.get_current_losses()
             out[f"{pre}/step{step}/losses"] = np.array([losses[k] for k in model.loss_names], dtype=np.float64)
+            if eps:
+                for n in ("G_A", "G_B", "D_A", "D_B"):
+                    for k, p in getattr(model, "net" + n).named_parameters():
+                        sample(p.grad, f"{pre}/step0/grad/{n}/{k}", out, n=64)
+                continue
             if step == 0:
                 for vis in ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A", "idt_B"):
+                    if not hasattr(model, vis):      # lambda_identity = 0: no identity passes
+                        continue
                     sample(getattr(model, vis), f"{pre}/step0/{vis}", out)
                 for n in ("G_A", "G_B", "D_A", "D_B"):
                     net = getattr(model, "net" + n)
@@ -110,6 +184,7 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
                         if "running" in k:
                             sample(b, f"{pre}/step0/buf/{n}/{k}", out, n=16)
         out[f"{pre}/loss_names"] = np.array(model.loss_names)
+        del model
     meta = dict(argv=" ".join(argv), S=S, B=B, nc=nc, steps=steps, seed=seed, torch=torch.__version__)
     out["meta"] = np.array(repr(meta))
     path = os.path.join(OUT, name + ".npz")
@@ -117,11 +192,51 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def run_checkpoint(name, argv, S, B, nc, seed):
+    """One reference step, save_networks('1') into tests/golden/<name>/, then record the losses of
+    the next step (inputs seed 1000+seed+1) and the saved state_dicts' key / shape / dtype table."""
+    import json
+    import random
+    TrainOptions, create_model = import_reference()
+    ck = os.path.abspath(OUT)
+    sys.argv = ["train.py", "--checkpoints_dir", ck, "--name", name] + argv
+    opt = TrainOptions().gather_options()
+    opt.isTrain = True
+    opt.gpu_ids = 0
+    torch.manual_seed(seed)
+    random.seed(seed)
+    model = create_model(opt)
+    model.setup(opt)
+    os.makedirs(os.path.join(ck, name), exist_ok=True)
+    shape = (B, nc, S, S, S)
+    model.set_input(list(synthetic_pair(shape, 1000 + seed)))
+    model.optimize_parameters()
+    model.save_networks("1")
+    table = {}
+    for n in ("G_A", "G_B", "D_A", "D_B"):
+        sd = torch.load(os.path.join(ck, name, "1_net_%s.pth" % n), map_location="cpu", weights_only=True)
+        table[n] = [[k, list(v.shape), str(v.dtype)] for k, v in sd.items()]
+    model.set_input(list(synthetic_pair(shape, 1000 + seed + 1)))
+    model.optimize_parameters()
+    losses = model.get_current_losses()
+    meta = dict(argv=" ".join(argv), S=S, B=B, nc=nc, seed=seed, torch=torch.__version__,
+                next_losses=[losses[k] for k in model.loss_names], loss_names=list(model.loss_names), keys=table)
+    with open(os.path.join(ck, name, "meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+    opt_txt = os.path.join(ck, name, "train_opt.txt")
+    if os.path.exists(opt_txt):
+        os.remove(opt_txt)
+    print("wrote", os.path.join(ck, name))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(os.cpu_count())
-    which = sys.argv[1:] or list(CASES)
+    which = sys.argv[1:] or list(CASES) + list(CKPT_CASES)
     for name in which:
+        if name in CKPT_CASES:
+            run_checkpoint(name, *CKPT_CASES[name])
+            continue
         argv, S, B, nc, dtypes, steps, seed = CASES[name]
         run_case(name, argv, S, B, nc, dtypes, steps, seed)
 
