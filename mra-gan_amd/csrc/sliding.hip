@@ -23,6 +23,7 @@ namespace {
 
 __global__ void patch_gather_kernel(const float* __restrict__ vol, int Y, int Z, const int* __restrict__ starts, int n,
                                     int px, int py, int pz, float* __restrict__ out) {
+#pragma clang fp contract(off)
   const int64_t per = (int64_t)px * py * pz;
   const int64_t total = per * n;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -33,7 +34,8 @@ __global__ void patch_gather_kernel(const float* __restrict__ vol, int Y, int Z,
     const int a = (int)(r / ((int64_t)pz * py));
     const int x = starts[3 * p] + a, y = starts[3 * p + 1] + b, z = starts[3 * p + 2] + c;
     const float v = vol[((int64_t)x * Y + y) * Z + z];
-    out[e] = __fdiv_rn(__fsub_rn(v, 127.5f), 127.5f);
+    const float d = v - 127.5f;
+    out[e] = d / 127.5f;
   }
 }
 
@@ -60,6 +62,10 @@ __device__ __forceinline__ int axis_start(int i, int stride, int N, int P) {
 
 __global__ void patch_combine_kernel(const float* __restrict__ pred, int X, int Y, int Z, int px, int py, int pz,
                                      int inum, int jnum, int knum, int s_in, int s_lay, float* __restrict__ label) {
+  // numpy rounds every operation: no mul+add → fma contraction here (hipcc contracts by default;
+  // the pragma covers only operators written in this scope — HIP's __fmul_rn / __fadd_rn are
+  // header functions whose operators stay contractible after inlining)
+#pragma clang fp contract(off)
   const int64_t total = (int64_t)X * Y * Z;
   const int64_t per = (int64_t)px * py * pz;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -80,12 +86,14 @@ __global__ void patch_combine_kernel(const float* __restrict__ pred, int X, int 
           const int c = z - axis_start(k, s_lay, Z, pz);
           const int64_t p = ((int64_t)i * jnum + j) * knum + k;
           const float v = pred[p * per + ((int64_t)a * py + b) * pz + c];
-          acc = __fadd_rn(acc, __fadd_rn(__fmul_rn(v, 127.5f), 127.5f));
+          const float sv = v * 127.5f;
+          acc = acc + (sv + 127.5f);
           cnt += 1.f;
         }
       }
     }
-    label[e] = __fadd_rn(__fdiv_rn(acc, cnt), 0.01f);
+    const float q = acc / cnt;          // IEEE division (hipcc's default for fp32 '/')
+    label[e] = q + 0.01f;
   }
 }
 

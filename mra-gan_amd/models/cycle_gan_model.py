@@ -439,8 +439,8 @@ class CycleGANModel(BaseModel):
         retB, stB = self.fake_B_pool.plan(b)
         retA, stA = self.fake_A_pool.plan(b)
         sp = tuple(self.real_A.shape[2:])
-        self.fake_B_pool.reserve(b, sp + (self.opt.output_nc,), self.device)
-        self.fake_A_pool.reserve(b, sp + (self.opt.input_nc,), self.device)
+        self.fake_B_pool.reserve(b, sp + (self.opt.output_nc,), self.real_A.device)
+        self.fake_A_pool.reserve(b, sp + (self.opt.input_nc,), self.real_A.device)
         hyp = self.optimizer_G.advance() + self.optimizer_D.advance()
         idx = torch.tensor([retB, stB, retA, stA], dtype=torch.int64).pin_memory()
         hyp = torch.tensor(hyp, dtype=torch.float32).pin_memory()
