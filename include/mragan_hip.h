@@ -34,16 +34,28 @@ enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2
 int mragan_abi_version(void);
 const char* mragan_last_error(void);
 
-/* Contraction precision of the dense (MFMA) convolutions, process-wide.  The reference computes
- * in fp32 (ATen conv); both modes take and return fp32 tensors.
- *   MRAGAN_PREC_F32    exact fp32 products (v_mfma_f32_32x32x2_f32), 157 TF peak;
+/* Contraction precision of the MFMA convolutions, process-wide.  The reference computes in fp32
+ * (ATen conv); every mode takes and returns fp32 tensors (activations, weights and gradients stay
+ * fp32 in HBM; only the MFMA operands are rounded).
+ *   MRAGAN_PREC_F32    exact fp32 products (v_mfma_f32_32x32x2_f32 / VALU), 157 TF peak;
  *   MRAGAN_PREC_BF16X3 each operand split into bf16 hi + lo, a·b ≈ lo·hi + hi·lo + hi·hi with fp32
  *                      accumulation (3 × v_mfma_f32_32x32x16_bf16), ≤ 3·2⁻¹⁸ relative error per
- *                      product, up to 5.3× the exact rate.
- * Thin (VALU) convolutions and weight gradients are exact fp32 in both modes.              */
-enum mragan_precision { MRAGAN_PREC_F32 = 0, MRAGAN_PREC_BF16X3 = 1 };
+ *                      product, up to 5.3× the exact rate;
+ *   MRAGAN_PREC_BF16   operands rounded to bf16, one v_mfma_f32_32x32x16_bf16 per product, fp32
+ *                      accumulation (BASELINE configs[1]/[2] "bf16"), 2.5 PF peak;     (ABI 7)
+ *   MRAGAN_PREC_F16    operands rounded to fp16, one v_mfma_f32_32x32x16_f16 per product, fp32
+ *                      accumulation (configs[4] "fp16"); use with a loss scale.          (ABI 7)
+ * The non-MFMA thin convolutions (D first/last layers) and their weight gradients stay exact
+ * fp32 in every mode.                                                                         */
+enum mragan_precision { MRAGAN_PREC_F32 = 0, MRAGAN_PREC_BF16X3 = 1, MRAGAN_PREC_BF16 = 2, MRAGAN_PREC_F16 = 3 };
 int mragan_set_conv_precision(int mode);
 int mragan_get_conv_precision(void);
+/* Loss scale (static, process-wide; default 1): mragan_l1_loss / mragan_gan_loss multiply the
+ * gradients they write (not the loss values) by it, so every gradient of the backward — and the
+ * weight gradients in the flat buffers — carry the factor; the optimizer divides it out through
+ * its grad_scale.  The fp16 mode uses it to keep gradients in fp16's normal range.  (ABI 7)    */
+int mragan_set_loss_scale(float scale);
+float mragan_get_loss_scale(void);
 
 /* ---- convolution --------------------------------------------------------------------------
  * Forward form:     y[n,o,:] = act(bias + Σ_{j<k³} x[n, o*stride − pad + j, :] · Wp[j])  (zero fill)

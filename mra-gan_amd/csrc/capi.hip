@@ -38,8 +38,10 @@ int check_launch(const char* what) {
   return kOk;
 }
 
-// contraction precision of the dense (MFMA) convolutions: kPrecF32 or kPrecBf16x3
+// contraction precision of the MFMA convolutions (prec.h): f32, bf16x3, bf16 or fp16
 static int g_conv_precision = MRAGAN_PREC_F32;
+// loss scale applied to the gradients the loss kernels emit (fp16 mode; 1 otherwise)
+static float g_loss_scale = 1.0f;
 
 static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0; }
 
@@ -53,14 +55,14 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
-    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_x3_applicable(cin, cout, k, stride))
-      return conv_thin1_x3(a, ws, ws_bytes, st);
-    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thinn_x3_applicable(cin, cout, k, stride))
-      return conv_thinn_x3(a, ws, ws_bytes, st);
+    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride))
+      return conv_thin1_x3(a, g_conv_precision, ws, ws_bytes, st);
+    if (g_conv_precision != MRAGAN_PREC_F32 && thinn_x3_applicable(cin, cout, k, stride))
+      return conv_thinn_x3(a, g_conv_precision, ws, ws_bytes, st);
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
-              g_conv_precision == MRAGAN_PREC_BF16X3, static_cast<float*>(ws), ws_bytes, wx3};
+              g_conv_precision, static_cast<float*>(ws), ws_bytes, wx3};
   return conv_igemm(a, st);
 }
 
@@ -76,11 +78,18 @@ int mragan_abi_version(void) { return MRAGAN_ABI_VERSION; }
 const char* mragan_last_error(void) { return g_err; }
 
 int mragan_set_conv_precision(int mode) {
-  MRAGAN_CHECK_ARG(mode == MRAGAN_PREC_F32 || mode == MRAGAN_PREC_BF16X3, "set_conv_precision: unknown mode %d", mode);
+  MRAGAN_CHECK_ARG(mode >= MRAGAN_PREC_F32 && mode <= MRAGAN_PREC_F16, "set_conv_precision: unknown mode %d", mode);
   g_conv_precision = mode;
   return kOk;
 }
 int mragan_get_conv_precision(void) { return g_conv_precision; }
+
+int mragan_set_loss_scale(float s) {
+  MRAGAN_CHECK_ARG(s > 0.f && s < 1e30f, "set_loss_scale: bad scale");
+  g_loss_scale = s;
+  return kOk;
+}
+float mragan_get_loss_scale(void) { return g_loss_scale; }
 
 int mragan_conv3d_fwd(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
                       int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, void* ws, size_t ws_bytes,
@@ -105,19 +114,19 @@ int mragan_conv3d_presplit(const float* x, int N, int Di, int Hi, int Wi, int ci
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,
                                int Ho, int Wo, int transposed) {
   if (thin_side(cin, cout)) {
-    if (g_conv_precision != MRAGAN_PREC_BF16X3) return 0;
+    if (g_conv_precision == MRAGAN_PREC_F32) return 0;
     if (thin1_x3_applicable(cin, cout, k, stride)) return thin1_x3_ws_bytes(cout);
     if (thinn_x3_applicable(cin, cout, k, stride)) return thinn_x3_ws_bytes();
     return 0;
   }
   IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, 0, 1,
-              g_conv_precision == MRAGAN_PREC_BF16X3, nullptr, 0};
+              g_conv_precision, nullptr, 0};
   return conv_igemm_ws_bytes(a);
 }
 
 size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride) {
   if (thin_wgrad_side(Cd, Cg)) {
-    if (g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
       return thin1_wgrad_x3_ws_bytes();
     return conv_thin_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k, stride);
   }
@@ -130,8 +139,9 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
   MRAGAN_CHECK_ARG(dense && gathered && dw && ws, "wgrad: null pointer");
   MRAGAN_CHECK_ARG(Cd > 0 && Cg > 0 && k >= 1 && stride >= 1 && pad >= 0, "wgrad: bad args");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (thin_wgrad_side(Cd, Cg) && g_conv_precision == MRAGAN_PREC_BF16X3 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
-    return conv_thin1_wgrad_x3(dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, pad, dw, accumulate, ws, ws_bytes, st);
+  if (thin_wgrad_side(Cd, Cg) && g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+    return conv_thin1_wgrad_x3(dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, pad, dw, accumulate, g_conv_precision,
+                               ws, ws_bytes, st);
   if (thin_wgrad_side(Cd, Cg)) {
     ThinWgradArgs a{};
     a.D = dense; a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd;
@@ -139,7 +149,7 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
     return conv_thin_wgrad(a, dw, accumulate, static_cast<float*>(ws), ws_bytes, st);
   }
   WgradArgs a{dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0,
-              g_conv_precision == MRAGAN_PREC_BF16X3};
+              g_conv_precision};
   return conv_wgrad(a, dw, accumulate, ws_bytes, st);
 }
 
@@ -211,13 +221,14 @@ int mragan_channel_split(const float* g, int Ca, int Cb, int64_t M, const float*
 int mragan_l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad,
                    int grad_acc, void* ws, void* stream) {
   MRAGAN_CHECK_ARG(a && b && loss && ws && n > 0, "l1_loss: bad args");
-  return l1_loss(a, b, n, scale, loss, loss_acc, grad, grad_acc, static_cast<float*>(ws), static_cast<hipStream_t>(stream));
+  return l1_loss(a, b, n, scale, g_loss_scale, loss, loss_acc, grad, grad_acc, static_cast<float*>(ws),
+                 static_cast<hipStream_t>(stream));
 }
 
 int mragan_gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc,
                     float* dlogit, void* ws, void* stream) {
   MRAGAN_CHECK_ARG(p && loss && ws && n > 0, "gan_loss: bad args");
-  return gan_loss(p, n, target, lsgan, scale, loss, loss_acc, dlogit, static_cast<float*>(ws),
+  return gan_loss(p, n, target, lsgan, scale, g_loss_scale, loss, loss_acc, dlogit, static_cast<float*>(ws),
                   static_cast<hipStream_t>(stream));
 }
 

@@ -361,7 +361,10 @@ static void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short
 }
 
 static const bool g_staged_x3 = getenv("MRAGAN_BRICK_STAGED") != nullptr;   // A/B switch
-bool conv_brick_x3_active(const IgemmArgs& a) { return a.x3 && !g_staged_x3 && conv_brick_applicable(a); }
+// the staged variant exists for bf16x3 only (MFMA split modes 2/3 always run conv_brick_x3.hip)
+bool conv_brick_x3_active(const IgemmArgs& a) {
+  return a.x3 && !(g_staged_x3 && a.x3 == 1) && conv_brick_applicable(a);
+}
 
 bool conv_brick_applicable(const IgemmArgs& a) {
   return a.k == 3 && a.s == 1 && a.cx % kBrickBK == 0 && a.ny % 64 == 0 && a.Di > 0;
@@ -384,7 +387,7 @@ int conv_brick(const IgemmArgs& g, hipStream_t st) {
   a.ntiles = (int)c.blocks;
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, c.bm, a.rowvox);
-  if (conv_brick_x3_active(g)) return conv_brick_x3_launch(a, c.bm, c.bn, g.ws, g.ws_bytes, g.wx3, st);
+  if (conv_brick_x3_active(g)) return conv_brick_x3_launch(a, c.bm, c.bn, g.ws, g.ws_bytes, g.wx3, g.x3, st);
   // 8 waves (two per SIMD) for the 128-row bricks: one wave's LDS reads and staging overlap the
   // other's MFMAs
   if (c.bm == 128 && c.bn == 128)

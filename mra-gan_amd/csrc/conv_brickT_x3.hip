@@ -23,6 +23,7 @@
 // Measured at 4 × 32³ × 64 → 4 × 64³ × 32 (k3): 132 µs (conv_igemm_x3: 304 µs); the store
 // stream is the bound (the same kernel without stores: 60 µs).
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -42,6 +43,7 @@ constexpr int kHP = kHD * kHH * kHW;       // 400 positions
 constexpr int kSL = (kHP * 8 + 255) / 256; // float4 per thread per chunk (13)
 
 // packed [T][ny][C] fp32 → [T][chunk][kk][hi|lo][ny][lh][8] bf16 (one thread per 8 channels)
+template <int PM>
 __global__ void brickT_pack_kernel(const float* __restrict__ wp, int T, int ny, int C, __bf16* __restrict__ out) {
   const int nch = C / kBK;
   const int64_t total = (int64_t)T * ny * (C / 8);
@@ -51,13 +53,12 @@ __global__ void brickT_pack_kernel(const float* __restrict__ wp, int T, int ny, 
     const int n = (int)(tn % ny), tap = (int)(tn / ny);
     const float* src = wp + tn * C + g * 8;
     const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-    const f32x8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const bf16x8 hi = __builtin_convertvector(v, bf16x8);
-    const bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+    bf16x8 hi, lo;
+    prec::split8<PM>(a, b, hi, lo);
     const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
     const int64_t base = ((((int64_t)tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + (int64_t)n * 16 + lh * 8;
     *reinterpret_cast<bf16x8*>(out + base) = hi;
-    *reinterpret_cast<bf16x8*>(out + base + (int64_t)ny * 16) = lo;
+    if constexpr (prec::has_lo<PM>()) *reinterpret_cast<bf16x8*>(out + base + (int64_t)ny * 16) = lo;
   }
 }
 
@@ -99,7 +100,7 @@ struct BrickTArgs {
   int nbd, nbh, nbw;
 };
 
-template <int K>
+template <int K, int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 brickT_x3_kernel(BrickTArgs a) {
   constexpr TSteps<K> ts{};
@@ -150,11 +151,10 @@ brickT_x3_kernel(BrickTArgs a) {
   auto halo_store = [&](char* buf, int s, const float4& v) __attribute__((always_inline)) {
     const int e = s * 256 + tid, pos = e >> 3, q = e & 7;
     if (pos < kHP) {
-      const f32x4 f = {v.x, v.y, v.z, v.w};
-      const bf16x4 h = __builtin_convertvector(f, bf16x4);
-      const bf16x4 lo = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
-      *reinterpret_cast<bf16x4*>(buf + pos * kRow + 8 * q) = h;
-      *reinterpret_cast<bf16x4*>(buf + pos * kRow + 64 + 8 * q) = lo;
+      uint2 h, lo;
+      prec::split4<PM>(v, h, lo);
+      *reinterpret_cast<uint2*>(buf + pos * kRow + 8 * q) = h;
+      if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + pos * kRow + 64 + 8 * q) = lo;
     }
   };
   auto bload = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) __attribute__((always_inline)) {
@@ -187,7 +187,8 @@ brickT_x3_kernel(BrickTArgs a) {
   auto b_load = [&](int chunk, int i, bf16x8 (&dst)[2]) __attribute__((always_inline)) {
     const int so = (((ts.s[i >> 1].tap * nch + chunk) * 2 + (i & 1)) * 2) * blkw;
     dst[0] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so));
-    dst[1] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so + blkw));
+    if constexpr (prec::has_lo<PM>()) dst[1] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so + blkw));
+    else dst[1] = dst[0];
   };
   bf16x8 rb[D][2];
 #pragma unroll
@@ -202,7 +203,8 @@ brickT_x3_kernel(BrickTArgs a) {
       const TStep st = ts.s[i >> 1];
       const char* arow = H + ((st.od * kHH + st.oh) * kHW + st.ow) * kRow + (i & 1) * 32;
       dst[0] = *reinterpret_cast<const bf16x8*>(arow);
-      dst[1] = *reinterpret_cast<const bf16x8*>(arow + 64);
+      if constexpr (prec::has_lo<PM>()) dst[1] = *reinterpret_cast<const bf16x8*>(arow + 64);
+      else dst[1] = dst[0];
     };
     float4 pv[kSL];
     bf16x8 af[2][2];
@@ -226,9 +228,7 @@ brickT_x3_kernel(BrickTArgs a) {
       if (i + 1 < NS) a_read(i + 1, af[(i + 1) & 1]);
       const bf16x8 ah = af[i & 1][0], al = af[i & 1][1];
       // weights as the A operand (rows = output channels), voxels as B (cols)
-      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, ah, acc[c], 0, 0, 0);
-      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, al, acc[c], 0, 0, 0);
-      acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, ah, acc[c], 0, 0, 0);
+      acc[c] = prec::mma<PM>(bh, bl, ah, al, acc[c]);
       // pin each step's loads to their step: under register pressure the scheduler otherwise
       // sinks the prefetches next to their uses (load → vmcnt(0) → MFMA, measured 8× slower)
       __builtin_amdgcn_sched_barrier(0);
@@ -282,21 +282,22 @@ bool brickT_x3_applicable(const IgemmArgs& g) {
 }
 
 // one static per kernel instantiation (the LDS opt-in is per function)
-template <int K>
+template <int K, int PM>
 static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
   const size_t lds = (size_t)2 * kHP * kRow + kHP * sizeof(int);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(brickT_x3_kernel<K>, dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((brickT_x3_kernel<K, PM>), dim3(blocks), dim3(256), lds, st, a);
 }
 
 size_t brickT_x3_ws_bytes(const IgemmArgs& g) { return (size_t)g.k * g.k * g.k * g.cx * g.ny * sizeof(float); }
 
-int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) {
+template <int PM>
+static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   const size_t need = brickT_x3_ws_bytes(g);
   if (!g.ws || g.ws_bytes < need) {
     set_error("brickT_x3: workspace %zu < %zu", g.ws_bytes, need);
@@ -304,8 +305,8 @@ int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) {
   }
   const int T = g.k * g.k * g.k;
   const int64_t groups = (int64_t)T * g.ny * (g.cx / 8);
-  hipLaunchKernelGGL(brickT_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, g.w, T, g.ny, g.cx,
-                     reinterpret_cast<__bf16*>(g.ws));
+  hipLaunchKernelGGL(brickT_pack_kernel<PM>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, g.w, T, g.ny,
+                     g.cx, reinterpret_cast<__bf16*>(g.ws));
   int rc = check_launch("brickT_pack");
   if (rc) return rc;
   BrickTArgs a{};
@@ -316,9 +317,11 @@ int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) {
   a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, kOH); a.nbw = ceil_div(g.Wo, kOW);
   const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
   if (blocks == 0) return kOk;
-  if (g.k == 3) launch_brickT<3>(a, (unsigned)blocks, st);
-  else launch_brickT<4>(a, (unsigned)blocks, st);
+  if (g.k == 3) launch_brickT<3, PM>(a, (unsigned)blocks, st);
+  else launch_brickT<4, PM>(a, (unsigned)blocks, st);
   return check_launch("brickT_x3");
 }
+
+int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) { MRAGAN_PREC_DISPATCH(g.x3, return conv_brickT_pm<PM>(g, st)) }
 
 }  // namespace mragan

@@ -19,8 +19,12 @@
 //
 // Products: a·b ≈ a_hi·b_hi + a_hi·b_lo + a_lo·b_hi (three v_mfma_f32_32x32x16_bf16, fp32
 // accumulate; see conv_igemm_x3.hip for the error bound).
+//
+// Precision modes (prec.h): bf16x3 as above; bf16 / fp16 run one MFMA per block product and
+// neither store nor load the lo planes (halo rows keep their layout, the lo half stays unused).
 #include "conv_geo.h"
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -37,14 +41,9 @@ constexpr int kRow = 144;               // LDS row bytes: hi 64 B, lo 64 B, 16 B
 constexpr int kTaps = 27;
 constexpr int kSteps = 2 * kTaps;       // (tap, 16-channel half) steps per chunk
 
-__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
-  const f32x8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  hi = __builtin_convertvector(v, bf16x8);
-  lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
-}
-
 // packed weights [27][ny][C] fp32 → fragment order (see the file comment); one thread per 8
 // channels of one (tap, n)
+template <int PM>
 __global__ void brick_x3_pack_kernel(const float* __restrict__ wp, int ny, int C, __bf16* __restrict__ out) {
   const int nch = C / kBK;
   const int64_t total = (int64_t)kTaps * ny * (C / 8);
@@ -55,7 +54,7 @@ __global__ void brick_x3_pack_kernel(const float* __restrict__ wp, int ny, int C
     const float* src = wp + tn * C + g * 8;
     const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
     bf16x8 hi, lo;
-    split8(a, b, hi, lo);
+    prec::split8<PM>(a, b, hi, lo);
     const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
     const int64_t base = ((((int64_t)tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + (int64_t)n * 16 + lh * 8;
     *reinterpret_cast<bf16x8*>(out + base) = hi;
@@ -63,17 +62,17 @@ __global__ void brick_x3_pack_kernel(const float* __restrict__ wp, int ny, int C
   }
 }
 
+template <int PM>
 __device__ __forceinline__ void split4_store(char* row, int q, const float4& v) {
-  const f32x4 f = {v.x, v.y, v.z, v.w};
-  const bf16x4 h = __builtin_convertvector(f, bf16x4);
-  const bf16x4 l = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
-  *reinterpret_cast<bf16x4*>(row + 8 * q) = h;
-  *reinterpret_cast<bf16x4*>(row + 64 + 8 * q) = l;
+  uint2 h, l;
+  prec::split4<PM>(v, h, l);
+  *reinterpret_cast<uint2*>(row + 8 * q) = h;
+  if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(row + 64 + 8 * q) = l;
 }
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int HMAX>
+template <int WM, int WN, int TM, int TN, int HMAX, int PM>
 __global__ void __launch_bounds__(WM * WN * 64)
 conv_brick_x3_kernel(BrickArgs a) {
   constexpr int NT = WM * WN * 64;
@@ -163,7 +162,7 @@ conv_brick_x3_kernel(BrickArgs a) {
 #pragma unroll
     for (int sl = 0; sl < NSL; ++sl) {
       const int e = sl * NT + tid, pos = e >> 3;
-      if (pos < HP) split4_store(halo_buf + pos * kRow, e & 7, pv[sl]);
+      if (pos < HP) split4_store<PM>(halo_buf + pos * kRow, e & 7, pv[sl]);
     }
   }
 
@@ -176,7 +175,7 @@ conv_brick_x3_kernel(BrickArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       dst[j][0] = *reinterpret_cast<const bf16x8*>(src + boff[j]);
-      dst[j][1] = *reinterpret_cast<const bf16x8*>(src + blk + boff[j]);
+      if constexpr (prec::has_lo<PM>()) dst[j][1] = *reinterpret_cast<const bf16x8*>(src + blk + boff[j]);
     }
   };
 #pragma unroll
@@ -201,7 +200,7 @@ conv_brick_x3_kernel(BrickArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         dst[0][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off);
-        dst[1][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off + 64);
+        if constexpr (prec::has_lo<PM>()) dst[1][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off + 64);
       }
     };
     a_read(0, af[0]);
@@ -223,14 +222,14 @@ conv_brick_x3_kernel(BrickArgs a) {
       // … and split + stored kHD steps later
       if ((du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
         const int e = ((u - kHD) / 3) * NT + tid, hpos = e >> 3;
-        if (stream && hpos < HP) split4_store(Hn + hpos * kRow, e & 7, rh[((du + kP - kHD) / 3) % 3]);
+        if (stream && hpos < HP) split4_store<PM>(Hn + hpos * kRow, e & 7, rh[((du + kP - kHD) / 3) % 3]);
       }
       // B fragments of this step (loaded kPF steps ago), then refill the slot with step u + kPF
       bf16x8 bh[TN], bl[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[j] = rb[du % kPF][j][0];
-        bl[j] = rb[du % kPF][j][1];
+        bl[j] = prec::has_lo<PM>() ? rb[du % kPF][j][1] : bh[j];
       }
       {
         const int un = u + kPF;
@@ -247,9 +246,7 @@ conv_brick_x3_kernel(BrickArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = prec::mma<PM>(ah[i], prec::has_lo<PM>() ? al[i] : ah[i], bh[j], bl[j], acc[i][j]);
         }
     }
     }
@@ -272,11 +269,11 @@ conv_brick_x3_kernel(BrickArgs a) {
   }
 }
 
-template <int WM, int WN, int TM, int TN, int HMAX>
+template <int WM, int WN, int TM, int TN, int HMAX, int PM>
 static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
   constexpr int BM = WM * TM * 32;
   const size_t lds = (size_t)2 * HMAX * kRow + (size_t)(BM + HMAX) * sizeof(int);
-  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX>;
+  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -290,7 +287,8 @@ static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
 // 117 KB LDS halo allows one block per CU, and two-per-SIMD (8-wave) variants spill at kPF = 9
 size_t conv_brick_x3_ws_bytes(int C, int ny) { return (size_t)kTaps * C * ny * sizeof(float); }
 
-int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
+template <int PM>
+static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
   if (wsplit) {
     a.wx3 = wsplit;                     // pre-split by mragan_pack_weights (tr 2/3) with the fp32 pack
   } else {
@@ -300,16 +298,21 @@ int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes,
       return kWorkspace;
     }
     const int64_t groups = (int64_t)kTaps * a.ny * (a.C / 8);
-    hipLaunchKernelGGL(brick_x3_pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny, a.C,
-                       static_cast<__bf16*>(ws));
+    hipLaunchKernelGGL(brick_x3_pack_kernel<PM>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny,
+                       a.C, static_cast<__bf16*>(ws));
     int rc = check_launch("brick_x3_pack");
     if (rc) return rc;
     a.wx3 = ws;
   }
-  if (bm == 128 && bn == 128) return launch_brick_x3<2, 2, 2, 2, 400>(a, st);
-  if (bm == 128) return launch_brick_x3<2, 2, 2, 1, 400>(a, st);
-  if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300>(a, st);
-  return launch_brick_x3<2, 2, 1, 1, 300>(a, st);
+  if (bm == 128 && bn == 128) return launch_brick_x3<2, 2, 2, 2, 400, PM>(a, st);
+  if (bm == 128) return launch_brick_x3<2, 2, 2, 1, 400, PM>(a, st);
+  if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300, PM>(a, st);
+  return launch_brick_x3<2, 2, 1, 1, 300, PM>(a, st);
+}
+
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, int mode,
+                         hipStream_t st) {
+  MRAGAN_PREC_DISPATCH(mode, return brick_x3_launch_pm<PM>(a, bm, bn, ws, ws_bytes, wsplit, st))
 }
 
 }  // namespace mragan

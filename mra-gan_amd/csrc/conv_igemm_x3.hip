@@ -19,8 +19,12 @@
 // lane l for k-slice kk: row l&31, k = 16kk + 8(l>>5) … +7 — one ds_read_b128 per plane.
 // Grid: 1-D, XCD-aware — consecutive tiles (the n-blocks sharing an A row-block, then the
 // neighbouring row-blocks sharing input halo) are placed on the same XCD's L2.
+//
+// Precision modes (prec.h): the same kernel is instantiated for bf16x3 (three MFMAs, hi + lo
+// planes), bf16 and fp16 (one MFMA per block product, hi planes only).
 #include "conv_geo.h"
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -29,21 +33,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// split 4 floats into bf16 hi / lo quads (packed as 2 dwords each)
-__device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
-  bf16x2 h0 = __builtin_convertvector((f32x2){v.x, v.y}, bf16x2);
-  bf16x2 h1 = __builtin_convertvector((f32x2){v.z, v.w}, bf16x2);
-  f32x2 f0 = __builtin_convertvector(h0, f32x2);
-  f32x2 f1 = __builtin_convertvector(h1, f32x2);
-  bf16x2 l0 = __builtin_convertvector((f32x2){v.x - f0.x, v.y - f0.y}, bf16x2);
-  bf16x2 l1 = __builtin_convertvector((f32x2){v.z - f1.x, v.w - f1.y}, bf16x2);
-  hi.x = __builtin_bit_cast(uint32_t, h0);
-  hi.y = __builtin_bit_cast(uint32_t, h1);
-  lo.x = __builtin_bit_cast(uint32_t, l0);
-  lo.y = __builtin_bit_cast(uint32_t, l1);
-}
-
-template <int WM, int WN, int TM, int TN, int BK>
+template <int WM, int WN, int TM, int TN, int BK, int PM>
 __global__ void __launch_bounds__(256)
 conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   constexpr int BM = WM * TM * 32;
@@ -164,9 +154,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       int r = tid / LPR + i * ROWS_PER_PASS;
       if (r < BM) {
         uint2 hi, lo;
-        split4(ra[i], hi, lo);
+        prec::split4<PM>(ra[i], hi, lo);
         *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
-        *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
+        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
       }
     }
 #pragma unroll
@@ -174,9 +164,10 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       int r = tid / LPR + i * ROWS_PER_PASS;
       if (r < BN) {
         uint2 hi, lo;
-        split4(rb[i], hi, lo);
+        prec::split4<PM>(rb[i], hi, lo);
         *reinterpret_cast<uint2*>(st + 2 * PLANE_A + r * LDK + 4 * q) = hi;
-        *reinterpret_cast<uint2*>(st + 2 * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
+        if constexpr (prec::has_lo<PM>())
+          *reinterpret_cast<uint2*>(st + 2 * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
       }
     }
   };
@@ -209,21 +200,21 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       for (int i = 0; i < TM; ++i) {
         int o = (wm0 + i * 32 + li) * LDK + kk * 16 + 8 * lh;
         ah[i] = *reinterpret_cast<const bf16x8*>(Ah + o);
-        al[i] = *reinterpret_cast<const bf16x8*>(Al + o);
+        if constexpr (prec::has_lo<PM>()) al[i] = *reinterpret_cast<const bf16x8*>(Al + o);
+        else al[i] = ah[i];
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         int o = (wn0 + j * 32 + li) * LDK + kk * 16 + 8 * lh;
         bh[j] = *reinterpret_cast<const bf16x8*>(Bh + o);
-        bl[j] = *reinterpret_cast<const bf16x8*>(Bl + o);
+        if constexpr (prec::has_lo<PM>()) bl[j] = *reinterpret_cast<const bf16x8*>(Bl + o);
+        else bl[j] = bh[j];
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = prec::mma<PM>(ah[i], al[i], bh[j], bl[j], acc[i][j]);
         }
     }
     if (ks + 1 < nK) store_tiles(buf ^ 1);
@@ -317,9 +308,11 @@ static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
   int ntiles = gm * gn * a.nclass;
-  hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK>), dim3(ntiles * splits), dim3(256), 0, st, a, gm, gn,
-                     ntiles, splits);
-  return check_launch("conv_igemm_x3");
+  MRAGAN_PREC_DISPATCH(a.x3, {
+    hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM>), dim3(ntiles * splits), dim3(256), 0, st, a, gm,
+                       gn, ntiles, splits);
+    return check_launch("conv_igemm_x3");
+  })
 }
 
 template <int BK>

@@ -19,9 +19,12 @@ namespace mragan {
 constexpr int TK_OD = 4, TK_OH = 8, TK_OW = 8;   // 256 voxels per block
 constexpr int TK_NB = 32;
 
-template <int CX>
+// NB: output channels per block (32, or 8 / 4 when ny is that small: the [T][NB][CX] weight
+// slice of a k7 layer then still fits LDS — 343·32·4·4 B alone would not, at cx = 4)
+template <int CX, int NB>
 __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w, int RD, int RH,
                                                      int RW) {
+  constexpr int TK_NB = NB;
   extern __shared__ __attribute__((aligned(16))) float xs[];   // [RD][RH][RW][CX]
   const int tid = threadIdx.x;
   int tile = blockIdx.x;
@@ -293,16 +296,22 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     int RD, RH, RW;
     if (!a.trans) { RD = (TK_OD - 1) * a.s + a.k; RH = (TK_OH - 1) * a.s + a.k; RW = (TK_OW - 1) * a.s + a.k; }
     else { RD = TK_OD + a.k - 1; RH = TK_OH + a.k - 1; RW = TK_OW + a.k - 1; }
-    size_t lds = ((((size_t)RD * RH * RW * a.cx + 3) & ~(size_t)3) + (size_t)a.k * a.k * a.k * TK_NB * a.cx) *
+    const int nb = a.ny <= 4 ? 4 : a.ny <= 8 ? 8 : TK_NB;
+    size_t lds = ((((size_t)RD * RH * RW * a.cx + 3) & ~(size_t)3) + (size_t)a.k * a.k * a.k * nb * a.cx) *
                  sizeof(float);
     MRAGAN_CHECK_ARG(lds <= 160 * 1024, "thin_k: LDS %zu too large", lds);
-    dim3 grid(a.N * td * th * tw, ceil_div(a.ny, TK_NB));
-    switch (a.cx) {
-      case 1: hipLaunchKernelGGL(thin_k_kernel<1>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
-      case 2: hipLaunchKernelGGL(thin_k_kernel<2>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
-      case 3: hipLaunchKernelGGL(thin_k_kernel<3>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
-      default: hipLaunchKernelGGL(thin_k_kernel<4>, grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break;
-    }
+    dim3 grid(a.N * td * th * tw, ceil_div(a.ny, nb));
+#define MRAGAN_THIN_K(NBV)                                                                                      \
+  switch (a.cx) {                                                                                              \
+    case 1: hipLaunchKernelGGL((thin_k_kernel<1, NBV>), grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break; \
+    case 2: hipLaunchKernelGGL((thin_k_kernel<2, NBV>), grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break; \
+    case 3: hipLaunchKernelGGL((thin_k_kernel<3, NBV>), grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break; \
+    default: hipLaunchKernelGGL((thin_k_kernel<4, NBV>), grid, dim3(256), lds, st, a, td, th, tw, RD, RH, RW); break; \
+  }
+    if (nb == 4) { MRAGAN_THIN_K(4) }
+    else if (nb == 8) { MRAGAN_THIN_K(8) }
+    else { MRAGAN_THIN_K(TK_NB) }
+#undef MRAGAN_THIN_K
     return check_launch("thin_k");
   }
   const int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;

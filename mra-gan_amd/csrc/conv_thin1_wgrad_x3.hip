@@ -16,6 +16,7 @@
 // tap tiles × 32 channels in accumulators across bricks; each block writes one partial
 // [343][32] slab, and a second kernel sums the slabs in fixed order (deterministic).
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -53,6 +54,7 @@ __device__ __forceinline__ int tap_of_row(int m) {
   return (kw < kK && g < kK * kK) ? g * kK + kw : -1;
 }
 
+template <int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 thin1_wgrad_x3_kernel(Thin1WArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -135,12 +137,11 @@ thin1_wgrad_x3_kernel(Thin1WArgs a) {
         const float c1[4] = {pv[l][1].x, pv[l][1].y, pv[l][1].z, pv[l][1].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 f = {c0[q], c1[q]};
-          const bf16x2 h = __builtin_convertvector(f, bf16x2);
-          const bf16x2 lo = __builtin_convertvector(f - __builtin_convertvector(h, f32x2), bf16x2);
+          uint32_t h, lo;
+          prec::split2<PM>(c0[q], c1[q], h, lo);
           const int idx = (4 * cq + q) * kPS + vox;
-          *reinterpret_cast<bf16x2*>(pth + idx) = h;
-          *reinterpret_cast<bf16x2*>(ptl + idx) = lo;
+          *reinterpret_cast<uint32_t*>(pth + idx) = h;
+          if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint32_t*>(ptl + idx) = lo;
         }
       }
     }
@@ -155,9 +156,10 @@ thin1_wgrad_x3_kernel(Thin1WArgs a) {
 #pragma unroll
       for (int dw = 0; dw < 4; ++dw) {
         const f32x8 v = {rr[dw], rr[dw + 1], rr[dw + 2], rr[dw + 3], rr[dw + 4], rr[dw + 5], rr[dw + 6], rr[dw + 7]};
-        const bf16x8 hi = __builtin_convertvector(v, bf16x8);
+        bf16x8 hi, lo;
+        prec::split8v<PM>(v, hi, lo);
         x8h[row * kBW + w0 + dw] = hi;
-        x8l[row * kBW + w0 + dw] = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+        if constexpr (prec::has_lo<PM>()) x8l[row * kBW + w0 + dw] = lo;
       }
     }
     __syncthreads();
@@ -167,15 +169,14 @@ thin1_wgrad_x3_kernel(Thin1WArgs a) {
       const int bh = ks >> 1, w8 = 16 * (ks & 1) + 8 * lh;
       const int pidx = li * kPS + bh * kBW + w8;
       const bf16x8 bhv = *reinterpret_cast<const bf16x8*>(pth + pidx);
-      const bf16x8 blv = *reinterpret_cast<const bf16x8*>(ptl + pidx);
+      const bf16x8 blv = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(ptl + pidx) : bhv;
       const int xo = bh * kBW + w8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i < ntile) {
-          const bf16x8 ah = x8h[aoff[i] + xo], al = x8l[aoff[i] + xo];
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhv, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blv, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhv, acc[i], 0, 0, 0);
+          const bf16x8 ah = x8h[aoff[i] + xo];
+          const bf16x8 al = prec::has_lo<PM>() ? x8l[aoff[i] + xo] : ah;
+          acc[i] = prec::mma<PM>(ah, al, bhv, blv, acc[i]);
         }
       }
     }
@@ -236,7 +237,7 @@ size_t thin1_wgrad_x3_ws_bytes() { return (size_t)thin1w_grid() * kT * kC * size
 
 // Same argument convention as conv_wgrad: dW[dn][gn][t] = Σ_m D[m][dn] · G[m − p + t][gn]
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
-                        int Cg, int p, float* out, int accumulate, void* ws, size_t ws_bytes, hipStream_t st) {
+                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
   Thin1WArgs a{};
   if (Cg == 1) {          // stem: P = D (32 ch), Q = G
     a.P = D; a.Dp = Dd; a.Hp = Hd; a.Wp = Wd;
@@ -260,14 +261,18 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
   a.slab = static_cast<float*>(ws);
   const size_t lds = (size_t)kRD * kRH * kRW * sizeof(float) + (size_t)2 * kRD * kRH * kBW * 16 +
                      (size_t)2 * kC * kPS * sizeof(__bf16);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1_wgrad_x3_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(thin1_wgrad_x3_kernel, dim3(grid), dim3(256), lds, st, a);
-  int rc = check_launch("thin1_wgrad_x3");
+  int rc = kOk;
+  MRAGAN_PREC_DISPATCH(mode, {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1_wgrad_x3_kernel<PM>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(thin1_wgrad_x3_kernel<PM>, dim3(grid), dim3(256), lds, st, a);
+    rc = check_launch("thin1_wgrad_x3");
+    break;
+  })
   if (rc) return rc;
   static_assert(kC * 8 == 256, "reduce block = 8 groups of kC lanes");
   hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, a.flip, out, accumulate);

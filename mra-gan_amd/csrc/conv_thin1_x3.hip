@@ -16,6 +16,7 @@
 // into X8 once, and the MFMA loop then runs barrier-free; the weights come pre-split and
 // fragment-ordered from L2 (thin1_x3_pack), prefetched 5 K-steps ahead.
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -34,6 +35,7 @@ constexpr int kRW = 40;                // raw halo row (39 used), float4-aligned
 constexpr int kPFS = 5;                // weight prefetch distance (K-steps), divides kKS
 
 // wp: packed [343][ny] (cin = 1) → out[(g·2 + hl)·ny + co][8] bf16, e = kw (e = 7 and g = 49: 0)
+template <int PM>
 __global__ void thin1_x3_pack_kernel(const float* __restrict__ wp, int ny, int flip, __bf16* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= kGroups * ny) return;
@@ -48,8 +50,8 @@ __global__ void thin1_x3_pack_kernel(const float* __restrict__ wp, int ny, int f
     }
     v[e] = w;
   }
-  const bf16x8 hi = __builtin_convertvector(v, bf16x8);
-  const bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+  bf16x8 hi, lo;
+  prec::split8v<PM>(v, hi, lo);
   *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 0) * ny + co) * 8) = hi;
   *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 1) * ny + co) * 8) = lo;
 }
@@ -70,7 +72,7 @@ struct Thin1Args {
   int nbd, nbh, nbw;
 };
 
-template <int BD, int TN>
+template <int BD, int TN, int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1_x3_kernel(Thin1Args a) {
   constexpr int RD = BD + kK - 1;
   constexpr int NRAW = RD * kRH * kRW;                 // raw halo floats
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     for (int j = 0; j < TN; ++j) {
       const int co = j * 32 + li;
       dst[j][0] = *reinterpret_cast<const bf16x8*>(wx + ((int64_t)(g * 2 + 0) * a.ny + co) * 8);
-      dst[j][1] = *reinterpret_cast<const bf16x8*>(wx + ((int64_t)(g * 2 + 1) * a.ny + co) * 8);
+      if constexpr (prec::has_lo<PM>()) dst[j][1] = *reinterpret_cast<const bf16x8*>(wx + ((int64_t)(g * 2 + 1) * a.ny + co) * 8);
     }
   };
   // MFMA row m of a tile ↔ voxel w = 4(m mod 8) + m/8 of its 32-voxel row; X8 stores voxel w at
@@ -160,10 +162,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
       for (int dw = 0; dw < 4; ++dw) {
         const f32x8 v = {r[dw], r[dw + 1], r[dw + 2], r[dw + 3], r[dw + 4], r[dw + 5], r[dw + 6], r[dw + 7]};
-        const bf16x8 hi = __builtin_convertvector(v, bf16x8);
+        bf16x8 hi, lo;
+        prec::split8v<PM>(v, hi, lo);
         const int pos = row * kBW + 8 * dw + (w0 >> 2);
         x8h[pos] = hi;
-        x8l[pos] = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+        if constexpr (prec::has_lo<PM>()) x8l[pos] = lo;
       }
     }
     __syncthreads();
@@ -183,7 +186,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         bh[j] = rb[ks % kPFS][j][0];
-        bl[j] = rb[ks % kPFS][j][1];
+        bl[j] = prec::has_lo<PM>() ? rb[ks % kPFS][j][1] : bh[j];
       }
       if (ks + kPFS < kKS) b_load(ks + kPFS, rb[ks % kPFS]);
       // this lane's k-group 2ks + lh → (kd, kh); the zero group 49 reads group 48's rows
@@ -191,14 +194,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const int off = lh ? ((g1 / kK) * kRH + g1 % kK) * kBW : ((g0 / kK) * kRH + g0 % kK) * kBW;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const bf16x8 ah = x8h[abase[i] + off], al = x8l[abase[i] + off];
+        const bf16x8 ah = x8h[abase[i] + off];
+        const bf16x8 al = prec::has_lo<PM>() ? x8l[abase[i] + off] : ah;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           // weights as the A operand (rows = channels), voxels as B (cols): each lane ends up
           // holding 4 consecutive channels of one voxel per register quad → 16-B stores
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], al, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], ah, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], ah, acc[i][j], 0, 0, 0);
+          acc[i][j] = prec::mma<PM>(bh[j], bl[j], ah, al, acc[i][j]);
         }
       }
       // one K-step per scheduling region: left free, the scheduler hoists the unrolled loop's
@@ -251,11 +253,11 @@ bool thin1_x3_applicable(int cx, int ny, int k, int s) { return cx == 1 && k == 
 
 size_t thin1_x3_ws_bytes(int ny) { return (size_t)kGroups * 2 * ny * 8 * sizeof(__bf16); }
 
-template <int BD, int TN>
+template <int BD, int TN, int PM>
 static int launch_thin1(const Thin1Args& a, hipStream_t st) {
   constexpr int RD = BD + kK - 1;
   const size_t lds = (size_t)RD * kRH * kRW * sizeof(float) + (size_t)2 * RD * kRH * kBW * 16;
-  auto kern = thin1_x3_kernel<BD, TN>;
+  auto kern = thin1_x3_kernel<BD, TN, PM>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -274,14 +276,15 @@ static int launch_thin1(const Thin1Args& a, hipStream_t st) {
   return check_launch("thin1_x3");
 }
 
-int conv_thin1_x3(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
+template <int PM>
+static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
   const size_t need = thin1_x3_ws_bytes(t.ny);
   if (!ws || ws_bytes < need) {
     set_error("thin1_x3: workspace %zu < %zu", ws_bytes, need);
     return kWorkspace;
   }
   const int flip = t.trans ? 1 : 0;
-  hipLaunchKernelGGL(thin1_x3_pack_kernel, dim3(ceil_div(kGroups * t.ny, 256)), dim3(256), 0, st, t.w, t.ny, flip,
+  hipLaunchKernelGGL(thin1_x3_pack_kernel<PM>, dim3(ceil_div(kGroups * t.ny, 256)), dim3(256), 0, st, t.w, t.ny, flip,
                      static_cast<__bf16*>(ws));
   int rc = check_launch("thin1_x3_pack");
   if (rc) return rc;
@@ -297,7 +300,11 @@ int conv_thin1_x3(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) 
   constexpr int BD = 2;
   a.nbd = ceil_div(t.Do, BD); a.nbh = ceil_div(t.Ho, 8); a.nbw = ceil_div(t.Wo, kBW);
   if ((int64_t)a.N * a.nbd * a.nbh * a.nbw == 0) return kOk;
-  return launch_thin1<BD, 1>(a, st);
+  return launch_thin1<BD, 1, PM>(a, st);
+}
+
+int conv_thin1_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
+  MRAGAN_PREC_DISPATCH(mode, return conv_thin1_pm<PM>(t, ws, ws_bytes, st))
 }
 
 }  // namespace mragan

@@ -21,6 +21,7 @@
 // one barrier per unit and register-prefetched two units ahead; the weights come pre-split in
 // fragment order from L2 (thinn_x3_pack).
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -48,6 +49,7 @@ constexpr int kF4PT = (kNF4 + 255) / 256;
 // weight fragment table: [kd' 8][half 2][step 4][hi|lo][lane 64][8 bf16]
 //   lane = 16g + n: column n = 8j + kw, k-group g → kh = 2·step + (g >> 1), channels
 //   16·half + 8(g & 1) … +7; zero where kd = kd' − j ∉ [0, 7), kh = 7 or kw = 7
+template <int PM>
 __global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, __bf16* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 8 * 2 * 4 * 64) return;
@@ -61,8 +63,8 @@ __global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, __b
   const int tt = flip ? kK * kK * kK - 1 - t : t;
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = ok ? wp[tt * kC + c0 + e] : 0.f;
-  const bf16x8 hi = __builtin_convertvector(v, bf16x8);
-  const bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), bf16x8);
+  bf16x8 hi, lo;
+  prec::split8v<PM>(v, hi, lo);
   const int64_t base = ((int64_t)((kdp * 2 + half) * 4 + s) * 2) * 64 * 8;
   *reinterpret_cast<bf16x8*>(out + base + lane * 8) = hi;
   *reinterpret_cast<bf16x8*>(out + base + 64 * 8 + lane * 8) = lo;
@@ -79,6 +81,7 @@ struct ThinnArgs {
   int nq, nr, nw;                         // depth pairs, row blocks, column blocks
 };
 
+template <int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 thinn_x3_kernel(ThinnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][kUnitBytes]
@@ -121,11 +124,10 @@ thinn_x3_kernel(ThinnArgs a) {
 #pragma unroll
     for (int l = 0; l < kF4PT; ++l) {
       if (l * 256 + tid < kNF4) {
-        const f32x4 f = {sv[l].x, sv[l].y, sv[l].z, sv[l].w};
-        const bf16x4 h = __builtin_convertvector(f, bf16x4);
-        const bf16x4 lo = __builtin_convertvector(f - __builtin_convertvector(h, f32x4), bf16x4);
-        *reinterpret_cast<bf16x4*>(buf + l * 64 * kRec + st_hi) = h;
-        *reinterpret_cast<bf16x4*>(buf + l * 64 * kRec + st_lo) = lo;
+        uint2 h, lo;
+        prec::split4<PM>(sv[l], h, lo);
+        *reinterpret_cast<uint2*>(buf + l * 64 * kRec + st_hi) = h;
+        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + l * 64 * kRec + st_lo) = lo;
       }
     }
   };
@@ -150,7 +152,7 @@ thinn_x3_kernel(ThinnArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const bf16x8 bh = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 0) * 64 * 8 + lane * 8);
-      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8);
+      const bf16x8 bl = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8) : bh;
       int kh = 2 * s + (g >> 1);
       kh = kh < kK ? kh : kK - 1;           // the padding kh = 7 has zero weights
       // position (2wave + rr + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
@@ -163,10 +165,8 @@ thinn_x3_kernel(ThinnArgs a) {
         for (int mt = 0; mt < 5; ++mt) {
           const int cofs = (rr * kMW + mt * 16) * kRec;
           const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_hi);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo);
-          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[rr][mt], 0, 0, 0);
-          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[rr][mt], 0, 0, 0);
-          acc[rr][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[rr][mt], 0, 0, 0);
+          const bf16x8 al = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo) : ah;
+          acc[rr][mt] = prec::mma16<PM>(ah, al, bh, bl, acc[rr][mt]);
         }
     }
   };
@@ -223,12 +223,14 @@ bool thinn_x3_applicable(int cx, int ny, int k, int s) { return cx == kC && ny =
 
 size_t thinn_x3_ws_bytes() { return (size_t)8 * 2 * 4 * 2 * 64 * 8 * sizeof(__bf16); }
 
-int conv_thinn_x3(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
+template <int PM>
+static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
   if (!ws || ws_bytes < thinn_x3_ws_bytes()) {
     set_error("thinn_x3: workspace %zu < %zu", ws_bytes, thinn_x3_ws_bytes());
     return kWorkspace;
   }
-  hipLaunchKernelGGL(thinn_x3_pack_kernel, dim3(16), dim3(256), 0, st, t.w, t.trans ? 1 : 0, static_cast<__bf16*>(ws));
+  hipLaunchKernelGGL(thinn_x3_pack_kernel<PM>, dim3(16), dim3(256), 0, st, t.w, t.trans ? 1 : 0,
+                     static_cast<__bf16*>(ws));
   int rc = check_launch("thinn_x3_pack");
   if (rc) return rc;
   ThinnArgs a{};
@@ -243,12 +245,16 @@ int conv_thinn_x3(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) 
   const size_t lds = (size_t)2 * kUnitBytes;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel<PM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(thinn_x3_kernel, dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)blocks), dim3(256), lds, st, a);
   return check_launch("thinn_x3");
+}
+
+int conv_thinn_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
+  MRAGAN_PREC_DISPATCH(mode, return conv_thinn_pm<PM>(t, ws, ws_bytes, st))
 }
 
 }  // namespace mragan

@@ -13,6 +13,7 @@
 // float atomics).  LDS tiles are [m][ch] rows straight from NDHWC memory; the MFMA fragments
 // are read with ds_read_b32 (lane = channel → consecutive banks, conflict-free).
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -166,19 +167,17 @@ typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 typedef float f32x4w __attribute__((ext_vector_type(4)));
 constexpr int kWRow = 144;
 
-// hi/lo of 4 voxel values of one channel → two 8-byte quads
-__device__ __forceinline__ void wsplit4(float a, float b, float c, float d, uint2& hi, uint2& lo) {
-  bf16x2w h0 = __builtin_convertvector((f32x2w){a, b}, bf16x2w);
-  bf16x2w h1 = __builtin_convertvector((f32x2w){c, d}, bf16x2w);
-  f32x2w f0 = __builtin_convertvector(h0, f32x2w);
-  f32x2w f1 = __builtin_convertvector(h1, f32x2w);
-  bf16x2w l0 = __builtin_convertvector((f32x2w){a - f0.x, b - f0.y}, bf16x2w);
-  bf16x2w l1 = __builtin_convertvector((f32x2w){c - f1.x, d - f1.y}, bf16x2w);
-  hi.x = __builtin_bit_cast(uint32_t, h0); hi.y = __builtin_bit_cast(uint32_t, h1);
-  lo.x = __builtin_bit_cast(uint32_t, l0); lo.y = __builtin_bit_cast(uint32_t, l1);
+// hi/lo of 4 voxel values of one channel → two 8-byte quads, stored at row (hi) and row + 64 (lo)
+template <int PM>
+__device__ __forceinline__ void wsplit4_store(char* row, float a, float b, float c, float d) {
+  uint2 hi, lo;
+  prec::split2<PM>(a, b, hi.x, lo.x);
+  prec::split2<PM>(c, d, hi.y, lo.y);
+  *reinterpret_cast<uint2*>(row) = hi;
+  if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(row + 64) = lo;
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int PM>
 __global__ void __launch_bounds__(256)
 conv_wgrad_x3_kernel(WgradArgs a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -243,28 +242,19 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   auto store = [&](int buf) __attribute__((always_inline)) {
     char* A = smem + buf * STAGE;
     char* B = A + BM * kWRow;
-    uint2 hi, lo;
     if (do_d) {
       const int r = 4 * cq;
-      wsplit4(rd[0].x, rd[1].x, rd[2].x, rd[3].x, hi, lo);
-      *reinterpret_cast<uint2*>(A + (r + 0) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 0) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rd[0].y, rd[1].y, rd[2].y, rd[3].y, hi, lo);
-      *reinterpret_cast<uint2*>(A + (r + 1) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 1) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rd[0].z, rd[1].z, rd[2].z, rd[3].z, hi, lo);
-      *reinterpret_cast<uint2*>(A + (r + 2) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 2) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rd[0].w, rd[1].w, rd[2].w, rd[3].w, hi, lo);
-      *reinterpret_cast<uint2*>(A + (r + 3) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(A + (r + 3) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4_store<PM>(A + (r + 0) * kWRow + 8 * vq, rd[0].x, rd[1].x, rd[2].x, rd[3].x);
+      wsplit4_store<PM>(A + (r + 1) * kWRow + 8 * vq, rd[0].y, rd[1].y, rd[2].y, rd[3].y);
+      wsplit4_store<PM>(A + (r + 2) * kWRow + 8 * vq, rd[0].z, rd[1].z, rd[2].z, rd[3].z);
+      wsplit4_store<PM>(A + (r + 3) * kWRow + 8 * vq, rd[0].w, rd[1].w, rd[2].w, rd[3].w);
     }
     if (do_g) {
       const int r = 4 * cq;
-      wsplit4(rg[0].x, rg[1].x, rg[2].x, rg[3].x, hi, lo);
-      *reinterpret_cast<uint2*>(B + (r + 0) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 0) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rg[0].y, rg[1].y, rg[2].y, rg[3].y, hi, lo);
-      *reinterpret_cast<uint2*>(B + (r + 1) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 1) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rg[0].z, rg[1].z, rg[2].z, rg[3].z, hi, lo);
-      *reinterpret_cast<uint2*>(B + (r + 2) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 2) * kWRow + 64 + 8 * vq) = lo;
-      wsplit4(rg[0].w, rg[1].w, rg[2].w, rg[3].w, hi, lo);
-      *reinterpret_cast<uint2*>(B + (r + 3) * kWRow + 8 * vq) = hi; *reinterpret_cast<uint2*>(B + (r + 3) * kWRow + 64 + 8 * vq) = lo;
+      wsplit4_store<PM>(B + (r + 0) * kWRow + 8 * vq, rg[0].x, rg[1].x, rg[2].x, rg[3].x);
+      wsplit4_store<PM>(B + (r + 1) * kWRow + 8 * vq, rg[0].y, rg[1].y, rg[2].y, rg[3].y);
+      wsplit4_store<PM>(B + (r + 2) * kWRow + 8 * vq, rg[0].z, rg[1].z, rg[2].z, rg[3].z);
+      wsplit4_store<PM>(B + (r + 3) * kWRow + 8 * vq, rg[0].w, rg[1].w, rg[2].w, rg[3].w);
     }
   };
 
@@ -290,21 +280,19 @@ conv_wgrad_x3_kernel(WgradArgs a) {
       for (int i = 0; i < TM; ++i) {
         const char* row = A + (wm0 + i * 32 + li) * kWRow + kk * 32 + lh * 16;
         ah[i] = *reinterpret_cast<const bf16x8w*>(row);
-        al[i] = *reinterpret_cast<const bf16x8w*>(row + 64);
+        al[i] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8w*>(row + 64) : ah[i];
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const char* row = B + (wn0 + j * 32 + li) * kWRow + kk * 32 + lh * 16;
         bh[j] = *reinterpret_cast<const bf16x8w*>(row);
-        bl[j] = *reinterpret_cast<const bf16x8w*>(row + 64);
+        bl[j] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8w*>(row + 64) : bh[j];
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = prec::mma<PM>(ah[i], al[i], bh[j], bl[j], acc[i][j]);
         }
     }
     if (ks + 1 < nK) store(buf ^ 1);
@@ -398,20 +386,23 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
                      (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31);
   if (a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0 && idx32) {
     auto grid_of = [&](int bm, int bn) { return dim3(ceil_div(a.Cd, bm) * ceil_div(a.Cg, bn), T, a.splits); };
-    if (a.Cd >= 128 && a.Cg >= 128)
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 2>), grid_of(128, 128), dim3(256), 0, st, a);
-    else if (a.Cd >= 128)
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 1>), grid_of(128, 64), dim3(256), 0, st, a);
-    else if (a.Cg >= 128)
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 2>), grid_of(64, 128), dim3(256), 0, st, a);
-    // 32-channel side (G down1 / up2 at full resolution): a 64×32 tile on two waves instead of
-    // a half-empty 64×64 one
-    else if (a.Cg == 32 && a.Cd >= 64)
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 1, 1, 1>), grid_of(64, 32), dim3(128), 0, st, a);
-    else if (a.Cd == 32 && a.Cg >= 64)
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<1, 2, 1, 1>), grid_of(32, 64), dim3(128), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 1>), grid_of(64, 64), dim3(256), 0, st, a);
+    MRAGAN_PREC_DISPATCH(a.x3, {
+      if (a.Cd >= 128 && a.Cg >= 128)
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 2, PM>), grid_of(128, 128), dim3(256), 0, st, a);
+      else if (a.Cd >= 128)
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 2, 1, PM>), grid_of(128, 64), dim3(256), 0, st, a);
+      else if (a.Cg >= 128)
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 2, PM>), grid_of(64, 128), dim3(256), 0, st, a);
+      // 32-channel side (G down1 / up2 at full resolution): a 64×32 tile on two waves instead of
+      // a half-empty 64×64 one
+      else if (a.Cg == 32 && a.Cd >= 64)
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 1, 1, 1, PM>), grid_of(64, 32), dim3(128), 0, st, a);
+      else if (a.Cd == 32 && a.Cg >= 64)
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<1, 2, 1, 1, PM>), grid_of(32, 64), dim3(128), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_wgrad_x3_kernel<2, 2, 1, 1, PM>), grid_of(64, 64), dim3(256), 0, st, a);
+      break;
+    })
   } else if (big) {
     dim3 grid(ceil_div(a.Cd, 128) * ceil_div(a.Cg, 128), T, a.splits);
     hipLaunchKernelGGL((conv_wgrad_f32_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);

@@ -17,6 +17,7 @@
 // ds_read_b128 groups conflict-free.  The next stage's global loads are in registers during the
 // MFMAs.  Partial tiles go to split-K slabs ws[z][t][co][ci], reduced by wgrad_reduce_kernel.
 #include "kernels.h"
+#include "prec.h"
 
 namespace mragan {
 
@@ -37,26 +38,18 @@ constexpr int kLds = kTile * kDRow + kTile * kGRow; // 71 680 B
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-// two fp32 → packed bf16 hi and lo words (hi + lo = x to 2^-17 relative)
-__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
-  const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);
-  const f32x2 f = __builtin_convertvector(h, f32x2);
-  const bf16x2 l = __builtin_convertvector((f32x2){a - f.x, b - f.y}, bf16x2);
-  hi = __builtin_bit_cast(uint32_t, h);
-  lo = __builtin_bit_cast(uint32_t, l);
-}
-
 // one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half (pairwise scalar splits: an
 // 8-wide vector built from the register array makes LLVM read the array through memory)
+template <int PM>
 __device__ __forceinline__ void split8_store(char* p, int half, float v0, float v1, float v2, float v3, float v4,
                                              float v5, float v6, float v7) {
   uint4 hi, lo;
-  split2(v0, v1, hi.x, lo.x);
-  split2(v2, v3, hi.y, lo.y);
-  split2(v4, v5, hi.z, lo.z);
-  split2(v6, v7, hi.w, lo.w);
+  prec::split2<PM>(v0, v1, hi.x, lo.x);
+  prec::split2<PM>(v2, v3, hi.y, lo.y);
+  prec::split2<PM>(v4, v5, hi.z, lo.z);
+  prec::split2<PM>(v6, v7, hi.w, lo.w);
   *reinterpret_cast<uint4*>(p) = hi;
-  *reinterpret_cast<uint4*>(p + half) = lo;
+  if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint4*>(p + half) = lo;
 }
 
 }  // namespace
@@ -68,6 +61,7 @@ struct Wgrad3Args {
   int nseg, seg_per_split;                // row segments in total / per split (multiple of kR)
 };
 
+template <int PM>
 __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ds = smem;
@@ -146,10 +140,10 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
 #pragma unroll
     for (int r = 0; r < kR; ++r) u[r] = rotv(v[r]);
     char* p = base + (4 * cq) * row_bytes + w * 16;
-    split8_store(p + ((0 + rot) & 3) * row_bytes, half, u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x);
-    split8_store(p + ((1 + rot) & 3) * row_bytes, half, u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y);
-    split8_store(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
-    split8_store(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
+    split8_store<PM>(p + ((0 + rot) & 3) * row_bytes, half, u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x);
+    split8_store<PM>(p + ((1 + rot) & 3) * row_bytes, half, u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y);
+    split8_store<PM>(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
+    split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
   };
   auto store = [&]() __attribute__((always_inline)) {
     put(Ds, kDRow, kDHalf, uw, rd);
@@ -177,11 +171,11 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
     bf16x8 fa[2][2], fb[2][3][2];
     auto frag = [&](int ks, bf16x8 (&A)[2], bf16x8 (&Bf)[3][2]) __attribute__((always_inline)) {
       A[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
-      A[1] = *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf);
+      A[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : A[0];
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         Bf[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16);
-        Bf[kw][1] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16 + kGHalf);
+        Bf[kw][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16 + kGHalf) : Bf[kw][0];
       }
     };
     frag(0, fa[0], fb[0]);
@@ -191,9 +185,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
       if (ks + 1 < kSegW / 2) frag(ks + 1, fa[c ^ 1], fb[c ^ 1]);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][1], fb[c][kw][0], acc[kw], 0, 0, 0);
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][0], fb[c][kw][1], acc[kw], 0, 0, 0);
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[c][0], fb[c][kw][0], acc[kw], 0, 0, 0);
+        acc[kw] = prec::mma<PM>(fa[c][0], fa[c][1], fb[c][kw][0], fb[c][kw][1], acc[kw]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -245,14 +237,16 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   a.seg_per_split = per;
   const int nsplit = (a.nseg + per - 1) / per;
   const int blocks = ((g.Cd / kTile) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kLds);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(wgrad3_x3_kernel, dim3(blocks), dim3(256), kLds, st, a);
-  return nsplit;
+  MRAGAN_PREC_DISPATCH(g.x3, {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<PM>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(wgrad3_x3_kernel<PM>, dim3(blocks), dim3(256), kLds, st, a);
+    return nsplit;
+  })
 }
 
 }  // namespace mragan

@@ -15,7 +15,7 @@ struct IgemmArgs {
   int trans;
   int act;
   int nclass;       // set by conv_igemm: 1 (forward or s==1) or s³
-  int x3;           // 1: bf16x3 split MFMA (conv_igemm_x3.hip), 0: exact f32 MFMA
+  int x3;           // precision mode (prec.h): 0 exact f32 MFMA; 1 bf16x3, 2 bf16, 3 fp16 (the *_x3 kernels)
   float* ws;        // split-K partial tiles (conv_igemm_ws_bytes)
   size_t ws_bytes;
   const void* wx3;  // optional: w pre-split in bf16x3 brick fragment order (pack tr 2/3), or null
@@ -40,7 +40,8 @@ struct BrickArgs {
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st);
-int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st);
+int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, int mode,
+                         hipStream_t st);
 size_t conv_brick_x3_ws_bytes(int C, int ny);
 bool conv_brick_x3_active(const IgemmArgs& a);
 // bf16x3 stride-2 transposed convolutions from an LDS halo (conv_brickT_x3.hip)
@@ -59,17 +60,17 @@ int conv_thin(ThinArgs a, hipStream_t st);
 // bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)
 bool thin1_x3_applicable(int cx, int ny, int k, int s);
 size_t thin1_x3_ws_bytes(int ny);
-int conv_thin1_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
+int conv_thin1_x3(const ThinArgs& a, int mode, void* ws, size_t ws_bytes, hipStream_t st);
 int thin1_debug_stamps(unsigned long long* host, int n);
 // bf16x3 MFMA path for 32 → 1-channel k7 s1 convolutions (conv_thinn_x3.hip)
 bool thinn_x3_applicable(int cx, int ny, int k, int s);
 size_t thinn_x3_ws_bytes();
-int conv_thinn_x3(const ThinArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
+int conv_thinn_x3(const ThinArgs& a, int mode, void* ws, size_t ws_bytes, hipStream_t st);
 // bf16x3 MFMA weight gradient of the 1-channel k7 s1 convolutions (conv_thin1_wgrad_x3.hip)
 bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s);
 size_t thin1_wgrad_x3_ws_bytes();
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
-                        int Cg, int p, float* out, int accumulate, void* ws, size_t ws_bytes, hipStream_t st);
+                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st);
 
 struct WgradArgs {
   const float* D; int N, Dd, Hd, Wd, Cd;
@@ -78,7 +79,7 @@ struct WgradArgs {
   float* ws;       // [splits][k³][Cd][Cg]
   int64_t chunk;   // set by conv_wgrad
   int splits;
-  int x3;          // bf16x3 split MFMA (needs Cd, Cg multiples of 32)
+  int x3;          // precision mode (prec.h): 0 f32; 1 bf16x3 / 2 bf16 / 3 fp16 MFMA (Cd, Cg multiples of 32)
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
 // bf16x3 weight gradient of valid k3 s1 convs on padded inputs, 3 kw taps per block (conv_wgrad3_x3.hip)
@@ -122,10 +123,10 @@ int channel_concat(const float* a, int Ca, int act_a, const float* b, int Cb, in
 int channel_split(const float* g, int Ca, int Cb, int64_t M, const float* ya, int act_a, float* da, const float* yb,
                   int act_b, float* db, hipStream_t st);
 int act_bwd(const float* y, const float* g0, const float* g1, const float* g2, int64_t n, int act, float* dx, hipStream_t st);
-int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad, int grad_acc,
-            float* ws, hipStream_t st);
-int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc, float* dlogit,
-             float* ws, hipStream_t st);
+int l1_loss(const float* a, const float* b, int64_t n, float scale, float gscale, float* loss, int loss_acc, float* grad,
+            int grad_acc, float* ws, hipStream_t st);
+int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float gscale, float* loss, int loss_acc,
+             float* dlogit, float* ws, hipStream_t st);
 int channel_sum(const float* x, int64_t M, int C, float* out, int acc, void* ws, size_t ws_bytes, hipStream_t st);
 size_t channel_sum_ws_bytes(int64_t M, int C);
 int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,

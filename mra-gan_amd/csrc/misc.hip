@@ -148,11 +148,14 @@ __device__ __forceinline__ double block_sum(double v) {
   return t;
 }
 
-// ---- L1 loss: loss += scale·mean|a−b| ; grad (=|+=) scale·sign(a−b)/n ---------------------
+// ---- L1 loss: loss += scale·mean|a−b| ; grad (=|+=) gscale·scale·sign(a−b)/n -------------
+// (gscale: the library's loss scale, mragan_set_loss_scale; 1 unless the fp16 mode scales the
+// backward — the loss value itself is never scaled)
 __global__ void __launch_bounds__(256) l1_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
-                                                 float scale, float* loss_partial, float* __restrict__ grad, int acc) {
+                                                 float scale, float gscale, float* loss_partial, float* __restrict__ grad,
+                                                 int acc) {
   double s = 0;
-  const float gs = scale / (float)n;
+  const float gs = scale * gscale / (float)n;
   GRID_STRIDE(i, n) {
     const float d = a[i] - b[i];
     s += fabsf(d);
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(256) l1_kernel(const float* __restrict__ a, co
 //   backward is applied by the discriminator's last stage)
 // MSE (--no_lsgan given → LSGAN): loss = mean((x−t)²); dp = scale/n · 2(x−t)
 __global__ void __launch_bounds__(256) gan_kernel(const float* __restrict__ p, int64_t n, float t, int lsgan, float scale,
-                                                  float* loss_partial, float* __restrict__ dlogit) {
+                                                  float gscale, float* loss_partial, float* __restrict__ dlogit) {
   double s = 0;
   GRID_STRIDE(i, n) {
     const float v = p[i];
@@ -185,7 +188,7 @@ __global__ void __launch_bounds__(256) gan_kernel(const float* __restrict__ p, i
       s += -(t * lp + (1.f - t) * l1p);
       g = (v - t) / fmaxf((1.f - v) * v, 1e-12f);
     }
-    if (dlogit) dlogit[i] = g * (scale / (float)n);
+    if (dlogit) dlogit[i] = g * (scale * gscale / (float)n);
   }
   const double tt = block_sum(s);
   if (threadIdx.x == 0) loss_partial[blockIdx.x] = (float)(tt * (double)scale / (double)n);
@@ -278,8 +281,10 @@ __global__ void pack_kernel(const float* __restrict__ src, int A, int B, int T, 
 // the bf16x3 brick kernel's fragment order (conv_brick_x3.hip: [tap][chunk][16-ch half][hi|lo]
 // [n][8-ch group][8] bf16, hi = rne(w), lo = rne(w − hi)), so the k3 s1 convs of a step skip
 // their per-call split.  Requires T = 27, C % 32 == 0 (entries that do not fit are skipped).
+// tr = 4 | 5: the same with fp16 hi / lo (the kPrecF16 mode, prec.h).
 typedef float pk_f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 pk_bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 pk_f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ void pack_split_entry(const PackEntry& e) {
   const int tr = e.tr & 1;
@@ -298,8 +303,15 @@ __device__ void pack_split_entry(const PackEntry& e) {
       const int a = tr ? c : n, b = tr ? n : c;
       v[j] = e.src[(a * e.B + b) * e.T + tap];
     }
-    const pk_bf16x8 hi = __builtin_convertvector(v, pk_bf16x8);
-    const pk_bf16x8 lo = __builtin_convertvector(v - __builtin_convertvector(hi, pk_f32x8), pk_bf16x8);
+    pk_bf16x8 hi, lo;
+    if (e.tr >= 4) {          // fp16 fragments (kPrecF16), bit patterns in the same 16-bit slots
+      const pk_f16x8 h = __builtin_convertvector(v, pk_f16x8);
+      hi = __builtin_bit_cast(pk_bf16x8, h);
+      lo = __builtin_bit_cast(pk_bf16x8, __builtin_convertvector(v - __builtin_convertvector(h, pk_f32x8), pk_f16x8));
+    } else {
+      hi = __builtin_convertvector(v, pk_bf16x8);
+      lo = __builtin_convertvector(v - __builtin_convertvector(hi, pk_f32x8), pk_bf16x8);
+    }
     const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
     const int base = (((tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + n * 16 + lh * 8;
     *reinterpret_cast<pk_bf16x8*>(out + base) = hi;
@@ -343,19 +355,19 @@ int act_bwd(const float* y, const float* g0, const float* g1, const float* g2, i
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, st, y, g0, g1, g2, n, act, dx);
   return check_launch("act_bwd");
 }
-int l1_loss(const float* a, const float* b, int64_t n, float scale, float* loss, int loss_acc, float* grad, int grad_acc,
-            float* ws, hipStream_t st) {
+int l1_loss(const float* a, const float* b, int64_t n, float scale, float gscale, float* loss, int loss_acc, float* grad,
+            int grad_acc, float* ws, hipStream_t st) {
   const int nb = grid_cap(n, 1024);
-  hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(256), 0, st, a, b, n, scale, ws, grad, grad_acc);
+  hipLaunchKernelGGL(l1_kernel, dim3(nb), dim3(256), 0, st, a, b, n, scale, gscale, ws, grad, grad_acc);
   int rc = check_launch("l1_loss");
   if (rc) return rc;
   hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, ws, nb, loss, loss_acc);
   return check_launch("l1_loss_sum");
 }
-int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float* loss, int loss_acc, float* dlogit,
-             float* ws, hipStream_t st) {
+int gan_loss(const float* p, int64_t n, float target, int lsgan, float scale, float gscale, float* loss, int loss_acc,
+             float* dlogit, float* ws, hipStream_t st) {
   const int nb = grid_cap(n, 1024);
-  hipLaunchKernelGGL(gan_kernel, dim3(nb), dim3(256), 0, st, p, n, target, lsgan, scale, ws, dlogit);
+  hipLaunchKernelGGL(gan_kernel, dim3(nb), dim3(256), 0, st, p, n, target, lsgan, scale, gscale, ws, dlogit);
   int rc = check_launch("gan_loss");
   if (rc) return rc;
   hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, ws, nb, loss, loss_acc);

@@ -235,7 +235,12 @@ class CycleGANModel(BaseModel):
     def initialize(self, opt):
         BaseModel.initialize(self, opt)
         from mragan_hip import ops
-        ops.set_conv_precision(getattr(opt, 'conv_precision', 'f32'))
+        self.precision = getattr(opt, 'conv_precision', 'f32')
+        ops.set_conv_precision(self.precision)
+        # fp16 operands: gradients are computed scaled (static loss scale) and unscaled by Adam;
+        # p.grad then holds loss_scale × the gradient (like torch.amp before unscale_)
+        self.loss_scale = float(getattr(opt, 'loss_scale', 1024.0)) if self.precision == 'fp16' else 1.0
+        ops.set_loss_scale(self.loss_scale)
         self.loss_names = ['D_A', 'G_A', 'cycle_A', 'idt_A', 'D_B', 'G_B', 'cycle_B', 'idt_B']
         visual_names_A = ['real_A', 'fake_B', 'rec_A']
         visual_names_B = ['real_B', 'fake_A', 'rec_B']
@@ -500,8 +505,11 @@ class CycleGANModel(BaseModel):
         from mragan_hip.dist import GradSync, default_sync
         if self._dist is None:
             self._dist = default_sync() or False
-            scale = 1.0 / self._dist.world if self._dist else 1.0
-            self.optimizer_G.grad_scale = self.optimizer_D.grad_scale = scale
+            scale = 1.0 / (self._dist.world if self._dist else 1)
+            self.optimizer_G.grad_scale = self.optimizer_D.grad_scale = scale / self.loss_scale
+        from mragan_hip import ops
+        ops.set_conv_precision(self.precision)      # process-wide: another model may have changed it
+        ops.set_loss_scale(self.loss_scale)
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
             networks3D.ensure_flat(n)
         self._prepare_step()

@@ -29,6 +29,8 @@ SIGNATURES = {
     "mragan_last_error": (C.c_char_p, []),
     "mragan_set_conv_precision": (i32, [i32]),
     "mragan_get_conv_precision": (i32, []),
+    "mragan_set_loss_scale": (i32, [f32]),
+    "mragan_get_loss_scale": (f32, []),
     "mragan_conv3d_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp, sz,
                                 vp]),
     "mragan_conv3d_transposed": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32,

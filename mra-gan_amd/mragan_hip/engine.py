@@ -67,16 +67,18 @@ class ConvLayer:
         else:
             out = [(w, self.cin, self.cout, T, True, self.wp_fwd),       # torch [Cin][Cout][t] → [t][Cout][Cin]
                    (w, self.cin, self.cout, T, False, self.wp_bwd)]      # [t][Cin][Cout]
-        # pre-split bf16x3 copies for the brick kernel, refreshed by the same pack launch
+        # pre-split 16-bit fragment copies for the brick kernel, refreshed by the same pack launch
+        # (tr 2|3: bf16 hi/lo — the bf16x3 and bf16 modes; tr 4|5: fp16 — the fp16 mode)
         (_, A, B, _, tf, _), (_, _, _, _, tb, _) = out
+        base = 4 if ops.get_conv_precision() == "fp16" else 2
         if self._splittable(self.k, self.s, self.cout, self.cin):
             if self.ws_fwd is None or self.ws_fwd.device != w.device:
                 self.ws_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
-            out.append((w, A, B, T, 2 + int(tf), self.ws_fwd))
+            out.append((w, A, B, T, base + int(tf), self.ws_fwd))
         if self._splittable(self.k, self.s, self.cin, self.cout):
             if self.ws_bwd is None or self.ws_bwd.device != w.device:
                 self.ws_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
-            out.append((w, A, B, T, 2 + int(tb), self.ws_bwd))
+            out.append((w, A, B, T, base + int(tb), self.ws_bwd))
         return out
 
     def repack(self):
@@ -170,11 +172,13 @@ class NetPlan:
         """Every conv layer's two packs in one launch (after each optimizer step)."""
         if not hasattr(self, "_pack_table"):
             self._pack_table = ops.PackTable()
+        self._packed_prec = ops.get_conv_precision()
         self._pack_table.run([p for c in self.conv_layers() for p in c.packs()])
         self.dirty = False
 
     def ensure_packed(self):
-        if self.dirty:
+        # the pre-split fragment copies depend on the precision mode (fp16 vs bf16 words)
+        if self.dirty or getattr(self, "_packed_prec", None) != ops.get_conv_precision():
             self.repack()
 
     def norms_in_order(self):
@@ -481,11 +485,12 @@ class UnetPlan:
         """Every conv layer's two packs in one launch (after each optimizer step)."""
         if not hasattr(self, "_pack_table"):
             self._pack_table = ops.PackTable()
+        self._packed_prec = ops.get_conv_precision()
         self._pack_table.run([p for c in self.conv_layers() for p in c.packs()])
         self.dirty = False
 
     def ensure_packed(self):
-        if self.dirty:
+        if self.dirty or getattr(self, "_packed_prec", None) != ops.get_conv_precision():
             self.repack()
 
     def _norms(self):

@@ -111,12 +111,13 @@ class KernelTimer:
 TIMER = KernelTimer()
 
 
-PRECISION = {"f32": 0, "bf16x3": 1}
+PRECISION = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
 
 
 def set_conv_precision(mode: str) -> None:
-    """Contraction precision of the dense MFMA convolutions ('f32' exact, 'bf16x3' split);
-    see include/mragan_hip.h.  Process-wide."""
+    """Contraction precision of the MFMA convolutions: 'f32' exact, 'bf16x3' split (fp32-grade),
+    'bf16' or 'fp16' (one MFMA per product, fp32 accumulation); see include/mragan_hip.h.
+    Process-wide."""
     if mode not in PRECISION:
         raise ValueError(f"conv precision must be one of {sorted(PRECISION)}, got {mode!r}")
     call("mragan_set_conv_precision", PRECISION[mode])
@@ -126,6 +127,17 @@ def get_conv_precision() -> str:
     from ._lib import lib
     code = lib().mragan_get_conv_precision()
     return {v: k for k, v in PRECISION.items()}[code]
+
+
+def set_loss_scale(scale: float) -> None:
+    """Static loss scale applied to the gradients the loss kernels emit (fp16 mode); the
+    optimizer's grad_scale must divide it out.  Process-wide."""
+    call("mragan_set_loss_scale", float(scale))
+
+
+def get_loss_scale() -> float:
+    from ._lib import lib
+    return float(lib().mragan_get_loss_scale())
 
 
 def conv_out_size(n: int, k: int, s: int, p: int) -> int:

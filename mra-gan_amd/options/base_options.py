@@ -45,8 +45,14 @@ BASE_FLAGS = [
     ('--verbose', dict(action='store_true', help='if specified, print more debugging information')),
     ('--suffix', dict(default='', type=str, help='customized suffix: opt.name = opt.name + suffix')),
     # engine-only flag (not in the reference): contraction precision of the dense MFMA convolutions
-    ('--conv_precision', dict(type=str, default='f32', choices=['f32', 'bf16x3'],
-                              help='f32: exact fp32 MFMA; bf16x3: split-bf16 MFMA with fp32 accumulation')),
+    ('--conv_precision', dict(type=str, default='f32', choices=['f32', 'bf16x3', 'bf16', 'fp16'],
+                              help='f32: exact fp32 MFMA; bf16x3: split-bf16 MFMA (fp32-grade); bf16 / fp16: one '
+                                   'MFMA per product on rounded operands; all with fp32 accumulation, fp32 '
+                                   'tensors and fp32 master weights / Adam')),
+    # engine-only flag: static loss scale of the fp16 mode (gradients stay in fp16's normal range)
+    ('--loss_scale', dict(type=float, default=1024.0,
+                          help='fp16 conv precision: gradients are computed scaled by this factor and '
+                               'unscaled inside the optimizer (ignored in the other precisions)')),
     # engine-only flag: run optimize_parameters() as captured HIP graphs after its first step
     ('--no_cuda_graph', dict(action='store_true',
                              help='launch every kernel of the training step from Python instead of replaying '

@@ -59,6 +59,7 @@ def main():
     model = build(f"/tmp/mragan_dp_{rank}", a.extra.split(), 1)
     model.setup(model.opt)
     losses = []
+    state1 = None
     for step in range(STEPS):
         A, B = batch_inputs(step)
         model.set_input([A[rank:rank + 1], B[rank:rank + 1]])
@@ -66,11 +67,14 @@ def main():
         mine = torch.tensor(list(model.get_current_losses().values()), dtype=torch.float64)
         dist.all_reduce(mine)
         losses.append(mine / world)
+        if step == 0:
+            model.sync_running_stats()     # averaging is linear: doing it now changes nothing later
+            state1 = snapshot(model)
     assert model._dist, "the data-parallel branch did not engage"
     model.sync_running_stats()
     torch.cuda.synchronize()
     if rank == 0:
-        torch.save(dict(losses=torch.stack(losses), state=snapshot(model),
+        torch.save(dict(losses=torch.stack(losses), state=snapshot(model), state1=state1,
                         graphed=model._graphs is not None), a.out)
     dist.barrier()
     dist.destroy_process_group()

@@ -5,10 +5,10 @@ stepping the same 2-patch batch.  The ranks run as tests/dp_worker.py under torc
 with a gloo group on the box's single MI355X (RCCL refuses two ranks on one device; the
 collective calls are the same torch.distributed ones).  Eager and HIP-graph-replayed steps.
 
-Gates: step-1 losses (mean over ranks) rel ≤ 1e-4; parameters after 4 steps: only elements
-whose gradient is round-off-sized step differently (< 2 % of elements differ by > 1e-6, none
-by more than 4 × 2.05 lr); running statistics averaged over the ranks = the single process's
-(linear recurrence) to 1e-3."""
+Gates: step-1 losses (mean over ranks) rel ≤ 1e-4; running statistics after step 1, averaged
+over the ranks = the single process's (a linear recurrence) to 1e-4; parameters after 4 steps:
+only elements whose gradient is round-off-sized step differently (< 2 % of elements differ by
+> 1e-6, none by more than 4 × 2.05 lr)."""
 import os
 import subprocess
 import sys
@@ -25,7 +25,7 @@ def _ranks(tmp_path, extra):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 2000),
-           os.path.join(HERE, "dp_worker.py"), "--out", str(out), "--extra", " ".join(extra)]
+           os.path.join(HERE, "dp_worker.py"), "--out", str(out), "--extra=" + " ".join(extra)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return torch.load(out, weights_only=True)
@@ -46,8 +46,16 @@ def test_dp_two_ranks_match_single_process(tmp_path, graph):
         model.set_input([A, B])
         model.optimize_parameters()
         losses.append(torch.tensor(list(model.get_current_losses().values()), dtype=torch.float64))
+        if step == 0:
+            single1 = W.snapshot(model)
     single = W.snapshot(model)
     losses = torch.stack(losses)
+    # running statistics after step 1 (weights still identical on both sides): averaged over
+    # the ranks = the single process's batch statistics (a linear recurrence), to fp32 noise
+    for k, v in single1.items():
+        if "running" in k:
+            r = float((dp["state1"][k] - v).norm() / v.norm())
+            assert r < 1e-4, (k, r)
     r0 = float((dp["losses"][0] - losses[0]).norm() / losses[0].norm())
     assert r0 < 1e-4, (dp["losses"][0], losses[0])
     lr = model.opt.lr
@@ -55,9 +63,8 @@ def test_dp_two_ranks_match_single_process(tmp_path, graph):
     for k, v in single.items():
         w = dp["state"][k]
         if "running" in k:
-            r = float((w - v).norm() / v.norm())
-            assert r < 1e-3, (k, r)
-        elif v.is_floating_point():
+            continue                      # after step 1 the weights differ by Adam's sign noise
+        if v.is_floating_point():
             d = (w - v).abs()
             assert float(d.max()) <= W.STEPS * 2.05 * lr, (k, float(d.max()))
             total += d.numel()

@@ -137,7 +137,7 @@ def conditioning(stepped):
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
     eps = PERTURB[meta["precision"]]
-    pre = f"fp64p{eps:g}"
+    pre = {4e-6: "fp64p4e-6", 4e-5: "fp64p4e-5"}[eps]
     if any(k.startswith(pre + "/") for k in z.files):
         # BASELINE-size cases: the fixture holds the perturbed fp64 run (same protocol, one
         # realization, generator seed 77) — returned as sampled vectors keyed like the grads
