@@ -52,8 +52,9 @@ def parse():
     ap.add_argument("--ngf", type=int, default=32)
     ap.add_argument("--netG", default="resnet_9blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3"],
-                    help="dense-conv contraction: exact f32 MFMA or split-bf16 (bf16x3) MFMA, fp32 accumulate")
+    ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3", "bf16", "fp16"],
+                    help="MFMA-conv contraction: exact f32, split-bf16 (bf16x3, fp32-grade), or bf16 / fp16 "
+                         "operands (one MFMA per product); fp32 accumulation, fp32 tensors and master weights")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: median of this many oracle steps")
     ap.add_argument("--nc", type=int, default=1, help="image channels (input_nc = output_nc)")
     ap.add_argument("--no-graph", action="store_true",
@@ -306,8 +307,11 @@ def main():
     patches = world * args.batch * args.steps
     value = patches / elapsed
     x3 = args.precision == "bf16x3"
-    mfma_peak = MFMA_BF16_PEAK_TFLOPS / 3 if x3 else MFMA_F32_PEAK_TFLOPS
-    prec = "bf16x3 split MFMA" if x3 else "f32 MFMA"
+    # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic FLOPs is the
+    # bf16 dense peak / 3; bf16 / fp16 run at the dense 16-bit MFMA peak
+    mfma_peak = {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x3": MFMA_BF16_PEAK_TFLOPS / 3}.get(args.precision,
+                                                                                       MFMA_BF16_PEAK_TFLOPS)
+    prec = {"bf16x3": "bf16x3 split MFMA", "f32": "f32 MFMA", "bf16": "bf16 MFMA", "fp16": "fp16 MFMA"}[args.precision]
     dom_cls, dom = next(iter(classes.items()))
     per_step_ms = dom["total_ms"] / 2
     if dom["flops"]:
@@ -338,7 +342,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if not x3 else "f32 (bf16x3 split products, f32 accumulate)",
+        "dtype": {"f32": "f32", "bf16x3": "f32", "bf16": "bf16", "fp16": "fp16"}[args.precision],
+        "dtype_detail": {"f32": "exact f32 products",
+                         "bf16x3": "f32-grade products as 3 split-bf16 MFMAs, f32 accumulate",
+                         "bf16": "bf16 conv operands, f32 accumulate; f32 tensors, InstanceNorm, losses, Adam",
+                         "fp16": "fp16 conv operands with a static loss scale, f32 accumulate; f32 tensors, "
+                                 "InstanceNorm, losses, Adam"}[args.precision],
         "data": "synthetic N(0,1) volumes, random init (seed 0)",
         "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, "
                                f"{args.nc}ch->{args.nc}ch, {args.size}^3 patch, batch {args.batch}/GPU ("

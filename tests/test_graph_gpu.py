@@ -51,7 +51,7 @@ def _run(tmp_path, graph, steps, precision, batches=None, extra=()):
     return torch.stack(losses).cpu(), state, vis, model
 
 
-@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("precision", ["f32", "bf16x3", "bf16", "fp16"])
 def test_graph_step_bit_identical_to_eager(tmp_path, precision):
     from mragan_hip import ops
     try:

@@ -42,8 +42,15 @@ def build_model(meta, ckdir, precision="f32"):
     return model
 
 
-# every case in both contraction precisions of the dense convolutions (include/mragan_hip.h)
-PARAMS = [(c, p) for p in ("f32", "bf16x3") for c in CASES]
+# every case in every contraction precision of the MFMA convolutions (include/mragan_hip.h)
+PRECISIONS = ("f32", "bf16x3", "bf16", "fp16")
+PARAMS = [(c, p) for p in PRECISIONS for c in CASES]
+# bf16 / fp16 round every MFMA operand once (one MFMA per product): their gates are the envelopes
+# measured against the reference's fp64 fixtures (tools/precision_envelope.py) with
+# ≈2× margin; a CPU restatement of the same operand rounding (fp64 oracle with bf16- / fp16-
+# rounded conv operands) reproduces the measured volume errors, so they are the arithmetic's,
+# not the kernels'.
+REDUCED = ("bf16", "fp16")
 
 
 @pytest.fixture(scope="module", params=PARAMS, ids=[f"{c}-{p}" for c, p in PARAMS])
@@ -66,10 +73,11 @@ def stepped(request, tmp_path_factory):
         model.optimize_parameters()
         history.append(np.array(list(model.get_current_losses().values())))
         if step == 0:
+            ls = model.loss_scale            # fp16: p.grad carries the static loss scale
             snap = dict(
                 vis={v: getattr(model, v).detach().cpu().clone() for v in
                      ("fake_B", "rec_A", "fake_A", "rec_B", "idt_A", "idt_B") if f"fp64/step0/{v}/idx" in z.files},
-                grads={n: {k: p.grad.detach().cpu().clone() for k, p in getattr(model, "net" + n).named_parameters()}
+                grads={n: {k: p.grad.detach().cpu().clone() / ls for k, p in getattr(model, "net" + n).named_parameters()}
                        for n in ("G_A", "G_B", "D_A", "D_B")},
                 params={n: {k: p.detach().cpu().clone() for k, p in getattr(model, "net" + n).named_parameters()}
                         for n in ("G_A", "G_B", "D_A", "D_B")},
@@ -96,21 +104,30 @@ def test_init_bit_exact(stepped):
 # forward-value gates: exact-f32 MFMA 1e-4 (measured 1e-6…2e-5); bf16x3 split MFMA (≤ 3·2⁻¹⁸ per
 # product) the north star's 1e-3 (measured ≤ 1.5e-4)
 VALUE_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
-# later-step losses: multiple of the reference's own fp32-vs-fp64 divergence at that step
-LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0}
+# reduced precisions: losses / generated volumes / running statistics (measured maxima over the
+# fixtures at 24³-64³: bf16 8.0e-4 / 8.8e-2 / 1.8e-2, fp16 1.4e-4 / 1.15e-2 / 5.2e-3)
+LOSS_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 2e-3, "fp16": 5e-4}
+VOL_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 0.15, "fp16": 2.5e-2}
+RS_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 4e-2, "fp16": 1.2e-2}
+# whole-network gradient rel-L2 of the reduced precisions (measured maxima 0.39 / 0.145)
+GRAD_TOL = {"bf16": 0.6, "fp16": 0.3}
+# later-step losses: multiple of the reference's own fp32-vs-fp64 divergence at that step, and at
+# least LATER_MIN (reduced precisions: measured maxima 3.0e-3 bf16, 1.3e-3 fp16)
+LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0, "bf16": 10.0, "fp16": 10.0}
+LATER_MIN = {"f32": 1e-3, "bf16x3": 1e-3, "bf16": 1e-2, "fp16": 4e-3}
 
 
 def test_losses(stepped):
     name, z, meta, _, history, _ = stepped
     got = history[0]
     want = z["fp64/step0/losses"]
-    assert rel_err(got, want) < VALUE_TOL[meta["precision"]], (got, want)
+    assert rel_err(got, want) < LOSS_TOL[meta["precision"]], (got, want)
     for step in range(1, meta["steps"]):
         # after an Adam step the reference's own fp32 run has left its fp64 run (elements with a
         # round-off-sized gradient step by ±lr either way): gate on that measured divergence
         w = z[f"fp64/step{step}/losses"]
         ref32 = rel_err(z[f"fp32/step{step}/losses"], w)
-        env = max(1e-3, LATER_STEP_FACTOR[meta["precision"]] * ref32)
+        env = max(LATER_MIN[meta["precision"]], LATER_STEP_FACTOR[meta["precision"]] * ref32)
         err = rel_err(history[step], w)
         print(f"{name} step {step}: loss rel err {err:.2e} (reference fp32 {ref32:.2e}, gate {env:.2e})")
         assert err < env, (step, history[step], w)
@@ -120,7 +137,7 @@ def test_generated_volumes(stepped):
     name, z, meta, _, _, snap = stepped
     for vis, t in snap["vis"].items():
         g, w = sampled(z, f"fp64/step0/{vis}", t)
-        assert rel_err(g, w) < VALUE_TOL[meta["precision"]], vis
+        assert rel_err(g, w) < VOL_TOL[meta["precision"]], vis
 
 
 # relative input perturbation ≈ the forward error of the generated volumes in each precision
@@ -136,6 +153,8 @@ def conditioning(stepped):
     makes the step's gradients 1e-3…1e-2-conditioned (tools/diag_d.py traces it)."""
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
+    if meta["precision"] in REDUCED:
+        return None                 # reduced precisions: whole-network envelope gate only
     eps = PERTURB[meta["precision"]]
     pre = {4e-6: "fp64p4e-6", 4e-5: "fp64p4e-5"}[eps]
     if any(k.startswith(pre + "/") for k in z.files):
@@ -160,6 +179,21 @@ def test_gradients(stepped, conditioning):
     (SURVEY §8c calibrated protocol, plus the measured conditioning of this step).  Pre-IN
     conv biases: exactly 0.  Whole network: the same rule on all sampled elements together."""
     name, z, meta, _, _, snap = stepped
+    if meta["precision"] in REDUCED:
+        ours, ref64 = [], []
+        for net, grads in snap["grads"].items():
+            for k, gr in grads.items():
+                if is_pre_in_bias(net, k):
+                    assert float(gr.abs().max()) == 0.0, (net, k)
+                    continue
+                g, w64 = sampled(z, f"fp64/step0/grad/{net}/{k}", gr)
+                scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
+                ours.append(g * scale)
+                ref64.append(w64 * scale)
+        whole = rel_err(np.concatenate(ours), np.concatenate(ref64))
+        print(f"{name} {meta['precision']}: whole-net grad rel err {whole:.2e}")
+        assert whole < GRAD_TOL[meta["precision"]], whole
+        return
     bad = []
     ours, ref32, ref64, pert = [], [], [], [[] for _ in conditioning]
     for net, grads in snap["grads"].items():
@@ -197,7 +231,7 @@ def test_running_stats(stepped):
     for net, bufs in snap["bufs"].items():
         for k, b in bufs.items():
             g, w = sampled(z, f"fp64/step0/buf/{net}/{k}", b)
-            assert rel_err(g, w) < VALUE_TOL[meta["precision"]], (net, k)
+            assert rel_err(g, w) < RS_TOL[meta["precision"]], (net, k)
 
 
 def test_params_after_adam(stepped):
@@ -215,4 +249,11 @@ def test_params_after_adam(stepped):
             assert d.max() <= 2.05 * lr, (net, k, d.max())
             total += d.size
             bad += int((d > 1e-6).sum())
-    assert bad / total < 0.02, (bad, total)
+    print(f"{name} {meta['precision']}: {bad}/{total} sampled weights stepped differently")
+    assert bad / total < ADAM_FLIP_TOL[meta["precision"]], (bad, total)
+
+
+# fraction of weights whose first Adam step (≈ ±lr) went the other way: f32-grade modes flip only
+# round-off-sized gradients (measured 0.2-0.3 %); the reduced modes flip every element whose
+# gradient their operand rounding moved across zero
+ADAM_FLIP_TOL = {"f32": 0.02, "bf16x3": 0.02, "bf16": 0.35, "fp16": 0.2}
