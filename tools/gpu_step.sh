@@ -4,11 +4,11 @@
 #   source tools/gpu_step.sh; step NAME SECONDS cmd...
 step() {
   local name=$1 secs=$2; shift 2
-  echo "[step] $name"
+  echo "[step] $name" >&2
   set +e
   timeout -k 10 "$secs" "$@"
   local rc=$?
   set -e
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[step] $name: rc $rc — stopping"; exit $rc; fi
-  echo "[step] $name: rc $rc"
+  echo "[step] $name: rc $rc" >&2
 }
