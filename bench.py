@@ -57,6 +57,9 @@ def parse():
                          "operands (one MFMA per product); fp32 accumulation, fp32 tensors and master weights")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: median of this many oracle steps")
     ap.add_argument("--nc", type=int, default=1, help="image channels (input_nc = output_nc)")
+    ap.add_argument("--alt-precisions", default="bf16",
+                    help="comma list of further precisions timed in the same run (same workload, same protocol) "
+                         "and reported under alt_precisions; '' for none")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels from Python every step (default: replay the step as HIP graphs)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
@@ -198,6 +201,51 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def build_model(args, precision):
+    from models import create_model
+    from options.train_options import TrainOptions
+    sys_argv = sys.argv
+    sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
+                "--input_nc", str(args.nc), "--output_nc", str(args.nc),
+                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
+                "--conv_precision", precision] + (["--no_cuda_graph"] if args.no_graph else [])
+    opt = TrainOptions().gather_options()
+    sys.argv = sys_argv
+    opt.isTrain, opt.gpu_ids = True, 0
+    torch.manual_seed(0)
+    random.seed(0)
+    # the reference's network-init banner goes to stderr: stdout carries only the JSON line
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):
+        model = create_model(opt)
+        model.setup(opt)
+    return model
+
+
+def time_alt_precision(args, precision, inputs, barrier, dist):
+    """The same workload and timing protocol in another contraction precision (a fresh model,
+    W warm-up steps, K timed steps between barriers, max over ranks)."""
+    model = build_model(args, precision)
+    for i in range(args.warmup):
+        model.set_input(inputs[i])
+        model.optimize_parameters()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        model.set_input(inputs[args.warmup + i])
+        model.optimize_parameters()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    del model
+    torch.cuda.empty_cache()
+    return {"ms_per_step": round(1e3 * elapsed / args.steps, 3), "dtype": precision,
+            "timing": "same protocol as the headline (barrier + synchronize around K steps, max over ranks)"}
+
+
 def ew_bytes_per_patch(S, netG, elem_bytes=4):
     """SURVEY §8(d) secondary HBM term: the InstanceNorm/activation/pad/residual traffic of one
     patch's step, ≈ 8 passes × 118·S³ elements per G fwd+bwd × 6 G passes = 5664·S³ elements
@@ -231,25 +279,8 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    from models import create_model
     from mragan_hip import ops
-    from options.train_options import TrainOptions
-
-    sys_argv = sys.argv
-    sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
-                "--input_nc", str(args.nc), "--output_nc", str(args.nc),
-                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
-                "--conv_precision", args.precision] + (["--no_cuda_graph"] if args.no_graph else [])
-    opt = TrainOptions().gather_options()
-    sys.argv = sys_argv
-    opt.isTrain, opt.gpu_ids = True, 0
-    torch.manual_seed(0)
-    random.seed(0)
-    # the reference's network-init banner goes to stderr: stdout carries only the JSON line
-    import contextlib
-    with contextlib.redirect_stdout(sys.stderr):
-        model = create_model(opt)
-        model.setup(opt)
+    model = build_model(args, args.precision)
 
     g = torch.Generator().manual_seed(1000 + rank)
     shape = (args.batch, args.nc, args.size, args.size, args.size)
@@ -285,6 +316,12 @@ def main():
         t = torch.tensor([elapsed, median_ms], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, median_ms = float(t[0]), float(t[1])
+
+    alt = {}
+    for prec_alt in [p for p in args.alt_precisions.split(",") if p and p != args.precision]:
+        alt[prec_alt] = time_alt_precision(args, prec_alt, inputs, barrier, dist)
+        ops.set_conv_precision(args.precision)
+        ops.set_loss_scale(model.loss_scale)
 
     # dominant kernel by time: two eager steps right after the timed region, every instrumented
     # C-ABI call bracketed by HIP events (ROCm refuses timing events inside a captured graph)
@@ -373,6 +410,9 @@ def main():
         "step_tflop": round(step_tf, 4),
         "step_tflops_achieved": round(step_tf / t_step, 2),
     }
+    if alt:
+        res["alt_precisions"] = {p: dict(v, value=round(world * args.batch / (v["ms_per_step"] / 1e3), 3))
+                                 for p, v in alt.items()}
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_child(args)
     print(json.dumps(res), flush=True)
