@@ -26,12 +26,9 @@ static int in_chunks(const InShape& s) {
   return (int)want;
 }
 
-static int in_fast_chunks(const InShape& s);
-
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
   InShape s{N, D, H, W, C};
-  const int ch = in_chunks(s) > in_fast_chunks(s) ? in_chunks(s) : in_fast_chunks(s);
-  return (size_t)N * ch * C * 2 * sizeof(double) + 16;
+  return (size_t)N * in_chunks(s) * C * 2 * sizeof(double) + 16;
 }
 
 // Σ over chunks of partials[n][chunk][C][2] in fixed order (deterministic).  Block = 4
@@ -274,235 +271,6 @@ __global__ void in_running_kernel(const RunningEntry* __restrict__ tab, float mo
   }
 }
 
-// ---- fast path (C/4 a power of two dividing 256): one launch for statistics + finalize -------
-// Each block reduces a contiguous span of voxels of one instance with a fixed channel quad per
-// thread (4 loads in flight per thread), writes its fp64 partials, and the LAST block of the
-// instance to finish (arrival ticket, the agent-scope release / acquire hand-off of
-// cdna_hip_programming.md §6 Guideline 16: plain stores → vmcnt(0) → barrier → lane-0 release
-// fence → vmcnt(0) → relaxed fetch_add; the last arriver: acquire fence → vmcnt(0) → barrier →
-// plain loads) folds every partial of the instance into mean / rstd (or the backward
-// coefficients) in the fixed chunk order: the separate finalize launch is gone and the result is
-// bit-identical to it.  The tickets live in a zero-initialised device array; the last arriver
-// resets its ticket, so the array is clean for the next launch (launches of this library that
-// use it are ordered on one stream; IN calls on two concurrent streams of one device would race).
-constexpr int kMaxTicketInst = 4096;
-__device__ unsigned int g_in_ticket[kMaxTicketInst];
-
-__device__ __forceinline__ bool in_arrive_last(unsigned int* ticket, int chunks, int* flag_lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == (unsigned int)(chunks - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag_lds = last;
-  }
-  __syncthreads();
-  return *flag_lds != 0;
-}
-
-// block reduction of the per-thread (Σa, Σb) of channel quad q = tid % CQ, written as partials
-__device__ __forceinline__ void in_block_partials(double (*red)[256 * 4], const double (&s0)[4], const double (&s1)[4],
-                                                  int CQ, double* __restrict__ out) {
-  const int tid = threadIdx.x, R = 256 / CQ;
-  for (int j = 0; j < 4; ++j) { red[0][tid * 4 + j] = s0[j]; red[1][tid * 4 + j] = s1[j]; }
-  __syncthreads();
-  if (tid < CQ) {
-    double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-    for (int rr = 0; rr < R; ++rr)
-      for (int j = 0; j < 4; ++j) { a[j] += red[0][(rr * CQ + tid) * 4 + j]; b[j] += red[1][(rr * CQ + tid) * 4 + j]; }
-    double* o = out + 8 * tid;
-    for (int j = 0; j < 4; ++j) { o[2 * j] = a[j]; o[2 * j + 1] = b[j]; }
-  }
-}
-
-__global__ void __launch_bounds__(256) in_stats_fast_kernel(const float* __restrict__ x, InShape s, int chunks,
-                                                            double* __restrict__ part, float* __restrict__ mean,
-                                                            float* __restrict__ rstd) {
-  __shared__ double red[2][256 * 4];
-  __shared__ int last_flag;
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  const int CQ = s.C / 4, tid = threadIdx.x;
-  const uint32_t total = (uint32_t)(s.S() * CQ);                  // float4 per instance (< 2^31)
-  const uint32_t per = ((total + chunks - 1) / chunks + 255) / 256 * 256;
-  const uint32_t j0 = chunk * per, j1 = min(total, j0 + per);
-  const float4* base = reinterpret_cast<const float4*>(x + (int64_t)n * s.S() * s.C);
-  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  uint32_t j = j0 + tid;
-  for (; j + 768 < j1; j += 1024) {
-    const float4 v0 = base[j], v1 = base[j + 256], v2 = base[j + 512], v3 = base[j + 768];
-    const float4 vv[4] = {v0, v1, v2, v3};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      s0[0] += vv[u].x; s0[1] += vv[u].y; s0[2] += vv[u].z; s0[3] += vv[u].w;
-      s1[0] += (double)vv[u].x * vv[u].x; s1[1] += (double)vv[u].y * vv[u].y;
-      s1[2] += (double)vv[u].z * vv[u].z; s1[3] += (double)vv[u].w * vv[u].w;
-    }
-  }
-  for (; j < j1; j += 256) {
-    const float4 v = base[j];
-    s0[0] += v.x; s0[1] += v.y; s0[2] += v.z; s0[3] += v.w;
-    s1[0] += (double)v.x * v.x; s1[1] += (double)v.y * v.y; s1[2] += (double)v.z * v.z; s1[3] += (double)v.w * v.w;
-  }
-  in_block_partials(red, s0, s1, CQ, part + ((int64_t)n * chunks + chunk) * s.C * 2);
-  if (!in_arrive_last(&g_in_ticket[n], chunks, &last_flag)) return;
-  for (int g = 0; g < (s.C + 3) / 4; ++g) {
-    in_finalize_group(part, s, chunks, n, g, 0, mean, rstd);
-    __syncthreads();
-  }
-}
-
-// y (padded by ypad) = act((x − μ)·rstd) (+ resid); the block sweeps a run of padded rows with
-// a fixed channel quad per thread
-__global__ void __launch_bounds__(256) in_apply_fast_kernel(const float* __restrict__ x, InShape s, int lgcq,
-                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                            int act, const float* __restrict__ resid, int rpad,
-                                                            float* __restrict__ y, int ypad, int rows_per_block) {
-  const int CQ = s.C / 4, tid = threadIdx.x, q = tid & (CQ - 1);
-  const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad;
-  const int rows = s.N * Dp * Hp;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  if (r0 >= r1) return;
-  const uint32_t span = (uint32_t)(r1 - r0) * Wp * CQ;
-  int n_cur = -1;
-  float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), rs = mu;
-  const int Dr = s.D + 2 * rpad, Hr = s.H + 2 * rpad, Wr = s.W + 2 * rpad;
-  for (uint32_t i = tid; i < span; i += 256) {
-    const uint32_t vv = i >> lgcq;                          // voxel index inside the block's rows
-    const int rl = (int)(vv / (uint32_t)Wp), w = (int)(vv - (uint32_t)rl * Wp);
-    const int r = r0 + rl;
-    const int h = r % Hp, t = r / Hp, d = t % Dp, n = t / Dp;
-    if (n != n_cur) {
-      n_cur = n;
-      mu = *reinterpret_cast<const float4*>(mean + n * s.C + 4 * q);
-      rs = *reinterpret_cast<const float4*>(rstd + n * s.C + 4 * q);
-    }
-    const int sd = min(max(d - ypad, 0), s.D - 1), sh = min(max(h - ypad, 0), s.H - 1), sw = min(max(w - ypad, 0), s.W - 1);
-    const int64_t src = (((int64_t)n * s.D + sd) * s.H + sh) * s.W + sw;
-    float4 v = *reinterpret_cast<const float4*>(x + src * s.C + 4 * q);
-    v = make_float4((v.x - mu.x) * rs.x, (v.y - mu.y) * rs.y, (v.z - mu.z) * rs.z, (v.w - mu.w) * rs.w);
-    v = f4_act(v, act);
-    if (resid) {
-      const float4 rr = *reinterpret_cast<const float4*>(
-          resid + ((((int64_t)n * Dr + sd + rpad) * Hr + sh + rpad) * Wr + sw + rpad) * s.C + 4 * q);
-      v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
-    }
-    const int64_t dst = (((int64_t)n * Dp + d) * Hp + h) * Wp + w;
-    *reinterpret_cast<float4*>(y + dst * s.C + 4 * q) = v;
-  }
-}
-
-// g and x̂ of voxel v of instance n (channel quad q), with the thread's μ / rstd in registers
-__device__ __forceinline__ void in_bwd_g_fast(const InBwdArgs& a, const InShape& s, int n, uint32_t v, int q,
-                                              const float4& mu, const float4& rs, float4& g, float4& xh) {
-  const uint32_t hw = (uint32_t)s.H * s.W;
-  const int d = (int)(v / hw);
-  const uint32_t rem = v - (uint32_t)d * hw;
-  const int h = (int)(rem / (uint32_t)s.W), w = (int)(rem - (uint32_t)h * s.W);
-  g = fold_read(a.dy, a.dypad, s, n, d, h, w, q);
-  const int64_t idx = ((int64_t)n * s.S() + v) * s.C + 4 * q;
-  if (a.dy_add) {
-    const float4 e = *reinterpret_cast<const float4*>(a.dy_add + idx);
-    g.x += e.x; g.y += e.y; g.z += e.z; g.w += e.w;
-  }
-  const float4 xv = *reinterpret_cast<const float4*>(a.x + idx);
-  xh = make_float4((xv.x - mu.x) * rs.x, (xv.y - mu.y) * rs.y, (xv.z - mu.z) * rs.z, (xv.w - mu.w) * rs.w);
-  g.x *= dact_from_xhat(xh.x, a.act); g.y *= dact_from_xhat(xh.y, a.act);
-  g.z *= dact_from_xhat(xh.z, a.act); g.w *= dact_from_xhat(xh.w, a.act);
-}
-
-__global__ void __launch_bounds__(256) in_bwd_stats_fast_kernel(InBwdArgs a, InShape s, int lgcq, int chunks,
-                                                                double* __restrict__ part, float* __restrict__ coef) {
-  __shared__ double red[2][256 * 4];
-  __shared__ int last_flag;
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  const int CQ = s.C / 4, tid = threadIdx.x, q = tid & (CQ - 1);
-  const uint32_t total = (uint32_t)(s.S() * CQ);
-  const uint32_t per = ((total + chunks - 1) / chunks + 255) / 256 * 256;
-  const uint32_t j0 = chunk * per, j1 = min(total, j0 + per);
-  const float4 mu = *reinterpret_cast<const float4*>(a.mean + n * s.C + 4 * q);
-  const float4 rs = *reinterpret_cast<const float4*>(a.rstd + n * s.C + 4 * q);
-  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  uint32_t j = j0 + tid;
-  for (; j + 256 < j1; j += 512) {
-    float4 g0, x0, g1, x1;
-    in_bwd_g_fast(a, s, n, j >> lgcq, q, mu, rs, g0, x0);
-    in_bwd_g_fast(a, s, n, (j + 256) >> lgcq, q, mu, rs, g1, x1);
-    s0[0] += g0.x; s0[1] += g0.y; s0[2] += g0.z; s0[3] += g0.w;
-    s1[0] += (double)g0.x * x0.x; s1[1] += (double)g0.y * x0.y; s1[2] += (double)g0.z * x0.z; s1[3] += (double)g0.w * x0.w;
-    s0[0] += g1.x; s0[1] += g1.y; s0[2] += g1.z; s0[3] += g1.w;
-    s1[0] += (double)g1.x * x1.x; s1[1] += (double)g1.y * x1.y; s1[2] += (double)g1.z * x1.z; s1[3] += (double)g1.w * x1.w;
-  }
-  for (; j < j1; j += 256) {
-    float4 g, xh;
-    in_bwd_g_fast(a, s, n, j >> lgcq, q, mu, rs, g, xh);
-    s0[0] += g.x; s0[1] += g.y; s0[2] += g.z; s0[3] += g.w;
-    s1[0] += (double)g.x * xh.x; s1[1] += (double)g.y * xh.y; s1[2] += (double)g.z * xh.z; s1[3] += (double)g.w * xh.w;
-  }
-  in_block_partials(red, s0, s1, CQ, part + ((int64_t)n * chunks + chunk) * s.C * 2);
-  if (!in_arrive_last(&g_in_ticket[n], chunks, &last_flag)) return;
-  for (int g = 0; g < (s.C + 3) / 4; ++g) {
-    in_finalize_group(part, s, chunks, n, g, 1, coef, nullptr);
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(256) in_bwd_apply_fast_kernel(InBwdArgs a, InShape s, int lgcq,
-                                                                const float* __restrict__ coef, int vox_per_block) {
-  const int CQ = s.C / 4, tid = threadIdx.x, q = tid & (CQ - 1);
-  const int64_t S = s.S();
-  const int64_t v0g = (int64_t)blockIdx.x * vox_per_block;      // global voxel (n·S + v)
-  const int64_t v1g = min((int64_t)s.N * S, v0g + vox_per_block);
-  if (v0g >= v1g) return;
-  const uint32_t span = (uint32_t)(v1g - v0g) * CQ;
-  int n_cur = -1;
-  float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), rs = mu;
-  float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f, c5 = 0.f, c6 = 0.f, c7 = 0.f;
-  for (uint32_t i = tid; i < span; i += 256) {
-    const int64_t vg = v0g + (i >> lgcq);
-    const int n = (int)(vg / S);
-    const uint32_t v = (uint32_t)(vg - (int64_t)n * S);
-    if (n != n_cur) {
-      n_cur = n;
-      mu = *reinterpret_cast<const float4*>(a.mean + n * s.C + 4 * q);
-      rs = *reinterpret_cast<const float4*>(a.rstd + n * s.C + 4 * q);
-      const float* cf = coef + 2 * ((int64_t)n * s.C + 4 * q);
-      c0 = cf[0]; c1 = cf[1]; c2 = cf[2]; c3 = cf[3]; c4 = cf[4]; c5 = cf[5]; c6 = cf[6]; c7 = cf[7];
-    }
-    float4 g, xh;
-    in_bwd_g_fast(a, s, n, v, q, mu, rs, g, xh);
-    float4 o;
-    o.x = rs.x * (g.x - c0 - xh.x * c1);
-    o.y = rs.y * (g.y - c2 - xh.y * c3);
-    o.z = rs.z * (g.z - c4 - xh.z * c5);
-    o.w = rs.w * (g.w - c6 - xh.w * c7);
-    *reinterpret_cast<float4*>(a.dx + (vg * s.C + 4 * q)) = o;
-  }
-}
-
-// fast path: C / 4 a power of two dividing 256, instances ≤ the ticket array, 32-bit indices
-static bool in_fast(const InShape& s) {
-  const int CQ = s.C / 4;
-  return CQ >= 1 && (CQ & (CQ - 1)) == 0 && 256 % CQ == 0 && s.N <= kMaxTicketInst &&
-         s.S() * CQ < ((int64_t)1 << 31) && (int64_t)s.N * s.S() < ((int64_t)1 << 31);
-}
-static int lg2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
-// statistics blocks per instance: ≈ 32 K elements each (≤ 128), so the last arriver folds at
-// most 128 × C partials
-static int in_fast_chunks(const InShape& s) {
-  int64_t c = s.S() * s.C / 32768;
-  if (c > 128) c = 128;
-  if (c < 1) c = 1;
-  return (int)c;
-}
-
 // ---- host entry points -------------------------------------------------------------------
 static int grid_for(int64_t work, int cap = 8192) {
   int64_t b = (work + 255) / 256;
@@ -519,23 +287,9 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
               s.H, s.W);
     return kBadArg;
   }
+  const int chunks = in_chunks(s);
   if (instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C) > ws_bytes) { set_error("instnorm: workspace too small"); return kWorkspace; }
   double* part = static_cast<double*>(ws);
-  if (in_fast(s)) {
-    const int fc = in_fast_chunks(s), lg = lg2(s.C / 4);
-    hipLaunchKernelGGL(in_stats_fast_kernel, dim3(fc, s.N), dim3(256), 0, st, x, s, fc, part, mean, rstd);
-    int rc = check_launch("in_stats_fast");
-    if (rc) return rc;
-    const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad;
-    const int64_t rows = (int64_t)s.N * Dp * Hp;
-    // ≈ 2 K float4 per block
-    int rpb = (int)(2048 / ((int64_t)Wp * (s.C / 4)));
-    if (rpb < 1) rpb = 1;
-    hipLaunchKernelGGL(in_apply_fast_kernel, dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, st, x, s, lg, mean,
-                       rstd, act, resid, rpad, y, ypad, rpb);
-    return check_launch("in_apply_fast");
-  }
-  const int chunks = in_chunks(s);
   hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, x, s, chunks, part);
   int rc = check_launch("in_stats");
   if (rc) return rc;
@@ -553,18 +307,6 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   if (need > ws_bytes) { set_error("instnorm_bwd: workspace too small"); return kWorkspace; }
   double* part = static_cast<double*>(ws);
   float* coef = reinterpret_cast<float*>(static_cast<char*>(ws) + instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C));
-  if (in_fast(s)) {
-    const int fc = in_fast_chunks(s), lg = lg2(s.C / 4);
-    hipLaunchKernelGGL(in_bwd_stats_fast_kernel, dim3(fc, s.N), dim3(256), 0, st, a, s, lg, fc, part, coef);
-    int rc = check_launch("in_bwd_stats_fast");
-    if (rc) return rc;
-    int vpb = 2048 / (s.C / 4);
-    if (vpb < 1) vpb = 1;
-    const int64_t vox = (int64_t)s.N * s.S();
-    hipLaunchKernelGGL(in_bwd_apply_fast_kernel, dim3((unsigned)((vox + vpb - 1) / vpb)), dim3(256), 0, st, a, s, lg, coef,
-                       vpb);
-    return check_launch("in_bwd_apply_fast");
-  }
   hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, a, s, chunks, part);
   int rc = check_launch("in_bwd_stats");
   if (rc) return rc;
