@@ -185,6 +185,12 @@ int mragan_patch_gather(const float* vol, int X, int Y, int Z, const int* starts
 int mragan_patch_combine(const float* pred, int X, int Y, int Z, int px, int py, int pz, int stride_inplane,
                          int stride_layer, float* label, void* stream);
 
+/* Training patch sampler (train.py:35-52, MONAI RandCropByPosNegLabeld crops, done on the device):
+ * out[p][a][b][c] = vol[s_p + (a,b,c)] for n corners s_p (DEVICE int32 [n][3]); every corner must
+ * keep the patch inside the volume (the sampler clamps the centers as MONAI does).  (ABI 7)      */
+int mragan_crop_patches(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz,
+                        float* out, void* stream);
+
 /* diagnostics: the kernel families launched by this thread since the last reset, ';'-joined
  * (e.g. "conv_wgrad3_x3;wgrad_reduce"); reset = 1 clears the log after copying it.  (ABI 7) */
 const char* mragan_launch_log(int reset);

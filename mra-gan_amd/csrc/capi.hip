@@ -291,4 +291,11 @@ const char* mragan_launch_log(int reset) {
   return copy;
 }
 
+int mragan_crop_patches(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz,
+                        float* out, void* stream) {
+  MRAGAN_CHECK_ARG(vol && starts && out && n >= 0, "crop_patches: bad args");
+  MRAGAN_CHECK_ARG(px > 0 && py > 0 && pz > 0 && px <= X && py <= Y && pz <= Z, "crop_patches: patch larger than volume");
+  return crop_patches(vol, X, Y, Z, starts, n, px, py, pz, out, static_cast<hipStream_t>(stream));
+}
+
 }  // extern "C"

@@ -145,6 +145,8 @@ int fill(float* p, int64_t n, float v, hipStream_t st);
 // sliding-window inference (sliding.hip)
 int patch_gather(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz, float* out,
                  hipStream_t st);
+int crop_patches(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz, float* out,
+                 hipStream_t st);
 int patch_combine(const float* pred, int X, int Y, int Z, int px, int py, int pz, int inum, int jnum, int knum, int s_in,
                   int s_lay, float* label, hipStream_t st);
 

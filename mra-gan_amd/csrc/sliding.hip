@@ -97,12 +97,36 @@ __global__ void patch_combine_kernel(const float* __restrict__ pred, int X, int 
   }
 }
 
+// plain crop of n patches (no scaling): the training patch sampler (train.py:42's
+// RandCropByPosNegLabeld crops, mragan_hip/patch_sampler.py)
+__global__ void crop_patches_kernel(const float* __restrict__ vol, int Y, int Z, const int* __restrict__ starts, int n,
+                                    int px, int py, int pz, float* __restrict__ out) {
+  const int64_t per = (int64_t)px * py * pz;
+  const int64_t total = per * n;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(e / per);
+    const int64_t r = e - p * per;
+    const int c = (int)(r % pz);
+    const int b = (int)((r / pz) % py);
+    const int a = (int)(r / ((int64_t)pz * py));
+    out[e] = vol[((int64_t)(starts[3 * p] + a) * Y + starts[3 * p + 1] + b) * Z + starts[3 * p + 2] + c];
+  }
+}
+
 int grid_for(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g < 65536 ? (g < 1 ? 1 : g) : 65536);
 }
 
 }  // namespace
+
+int crop_patches(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz, float* out,
+                 hipStream_t st) {
+  (void)X;
+  const int64_t total = (int64_t)n * px * py * pz;
+  hipLaunchKernelGGL(crop_patches_kernel, dim3(grid_for(total)), dim3(256), 0, st, vol, Y, Z, starts, n, px, py, pz, out);
+  return check_launch("crop_patches");
+}
 
 int patch_gather(const float* vol, int X, int Y, int Z, const int* starts, int n, int px, int py, int pz, float* out,
                  hipStream_t st) {

@@ -63,6 +63,7 @@ SIGNATURES = {
     "mragan_fill": (i32, [vp, i64, f32, vp]),
     "mragan_debug_stamps": (i32, [vp, i32]),
     "mragan_launch_log": (C.c_char_p, [i32]),
+    "mragan_crop_patches": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
     "mragan_patch_gather": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
     "mragan_patch_combine": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
 }

@@ -426,3 +426,18 @@ def patch_combine(pred: torch.Tensor, shape, patch, stride_inplane: int, stride_
     call("mragan_patch_combine", _ptr(pred), X, Y, Z, px, py, pz, int(stride_inplane), int(stride_layer), _ptr(out),
          _stream())
     return out
+
+
+def crop_patches(vol: torch.Tensor, starts: torch.Tensor, patch, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """vol [X, Y, Z] fp32 (device), starts int32 [n, 3] (device; patches inside the volume) →
+    [n, px, py, pz] crops (no scaling)."""
+    _check(vol, "crop_patches.vol", ndim=3)
+    if starts.dtype != torch.int32 or not starts.is_cuda or starts.dim() != 2 or starts.shape[1] != 3:
+        raise ValueError("crop_patches: starts must be a device int32 [n, 3] tensor")
+    n = starts.shape[0]
+    px, py, pz = patch
+    if out is None:
+        out = torch.empty((n, px, py, pz), device=vol.device, dtype=torch.float32)
+    X, Y, Z = vol.shape
+    call("mragan_crop_patches", _ptr(vol), X, Y, Z, _ptr(starts.contiguous()), n, px, py, pz, _ptr(out), _stream())
+    return out

@@ -574,3 +574,58 @@ def sliding_window_inference(g_forward, image_np, patch, stride_inplane, stride_
     if padding:
         label_np = label_np[:, :, 0:(label_np.shape[2] - 1)]
     return label_np
+
+
+# ------------------------------------------------------------------------------------------
+# Training patch sampling (reference train.py:35-52, MONAI transforms — third-party, unpinned and
+# absent here: restated from MONAI's published algorithm; "parity unpinned" beyond this restatement)
+# ------------------------------------------------------------------------------------------
+
+def monai_normalize_intensity(img):
+    """NormalizeIntensityd(keys=['image'], channel_wise=True): (x − mean) / std, np.std (ddof 0),
+    a zero std treated as 1."""
+    import numpy as np
+    x = np.asarray(img, dtype=np.float32)
+    mean = x.mean()
+    std = x.std()
+    if std == 0:
+        std = 1.0
+    return ((x - mean) / std).astype(np.float32)
+
+
+def monai_crop_foreground(img, label):
+    """CropForegroundd(keys=['image','label'], source_key='image'), select_fn x > 0, margin 0."""
+    import numpy as np
+    coords = np.argwhere(img > 0)
+    if coords.size == 0:
+        return img, label
+    lo = coords.min(0)
+    hi = coords.max(0) + 1
+    return img[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]], label[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]]
+
+
+def monai_pos_neg_crops(image, label, spatial_size, num_samples, rand_state, pos=20, neg=0):
+    """RandCropByPosNegLabeld(label_key='label', spatial_size, pos, neg, num_samples): the crops of
+    one volume, each (image_patch, label_patch), drawn from rand_state (np.random.RandomState)."""
+    import numpy as np
+    shape = label.shape
+    fg = [i for i, v in enumerate(label.reshape(-1)) if v != 0]
+    bg = [i for i, v in enumerate(label.reshape(-1)) if v == 0] if neg > 0 else []
+    ratio = pos / float(pos + neg)
+    if not fg and not bg:
+        raise ValueError("No sampling location available.")
+    if not fg or not bg:
+        ratio = 0 if not fg else 1
+    half = [s // 2 for s in spatial_size]
+    end = [int(np.uint16(shape[i] + 1 - spatial_size[i] / 2.0)) for i in range(3)]
+    end = [e + 1 if e == h else e for e, h in zip(end, half)]
+    out = []
+    for _ in range(num_samples):
+        use = fg if rand_state.rand() < ratio else bg
+        flat = use[rand_state.randint(len(use))]
+        c = [flat // (shape[1] * shape[2]), (flat // shape[2]) % shape[1], flat % shape[2]]
+        c = [min(max(c[i], half[i]), end[i] - 1) for i in range(3)]
+        s0 = [c[i] - half[i] for i in range(3)]
+        sl = tuple(slice(s0[i], s0[i] + spatial_size[i]) for i in range(3))
+        out.append((image[sl], label[sl]))
+    return out
