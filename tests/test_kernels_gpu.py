@@ -67,7 +67,7 @@ CONV_CASES = [
     # ngf = 4 generators (thin_k with a cut weight slice: cin ≤ 4, k7, few output channels)
     (1, 4, 1, 12, 7, 1, 0),
     (1, 4, 2, 11, 7, 1, 0),
-    (1, 3, 6, 10, 7, 1, 0),
+    (1, 4, 4, 10, 7, 1, 0),
     # large enough for the row-sweep thin_n kernel (fwd: ≥ 4096 output voxels; dgrad likewise)
     (1, 32, 1, 22, 7, 1, 0),
     (1, 16, 2, 21, 7, 1, 0),
