@@ -47,6 +47,27 @@ struct Vol {   // batch + spatial extents of an NDHWC tensor
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Range-checked loads through a buffer descriptor: a byte offset at or beyond `bytes` reads 0
+// (the hardware bounds check), so a halo load needs no select after it — a select on the
+// loaded value makes the compiler wait for each load before issuing the next one.
+// Build the descriptor from wave-uniform values only (cdna_hip_programming.md T8 / T20).
+constexpr uint32_t kOobOffset = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));
+}
+// (the clang builtin __builtin_amdgcn_raw_buffer_load_b128 of ROCm 7.2 emits a single
+// buffer_load_dword: the 16-byte form goes through the LLVM intrinsic directly)
+typedef float buf_f32x4 __attribute__((ext_vector_type(4)));
+__device__ buf_f32x4 llvm_raw_buffer_load_f32x4(__amdgpu_buffer_rsrc_t r, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ __forceinline__ float4 buf_load_f32x4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const buf_f32x4 v = llvm_raw_buffer_load_f32x4(r, (int)byte_off, 0, 0);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 }  // namespace mragan
 
 #define MRAGAN_CHECK_ARG(cond, ...)           \

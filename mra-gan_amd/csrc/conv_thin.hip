@@ -2,7 +2,7 @@
 //   * G stem   Conv3d(nc→ngf, k7) on the RPad3 input      (networks3D.py:185-189)  fwd: thin_k
 //   * G head   Conv3d(ngf→nc, k7) + Tanh                   (networks3D.py:211-213)  fwd: thin_n
 //   * D first  Conv3d(nc→ndf, k4 s2 p1) + LeakyReLU        (networks3D.py:389-390)  fwd: thin_k
-//   * D last   Conv3d(8ndf→1, k4 s1 p1) (+ Sigmoid)        (networks3D.py:417-420)  fwd: naive
+//   * D last   Conv3d(8ndf→1, k4 s1 p1) (+ Sigmoid)        (networks3D.py:417-420)  fwd: thin_dot
 // and their data / weight gradients.  On fp32 the VALU FMA rate equals the f32 MFMA rate
 // (157 TF both), and these GEMMs have N or K of 1-2, so they are written as VALU direct
 // convolutions with the input halo staged in LDS and the per-tap weights read as
@@ -278,6 +278,52 @@ __global__ void __launch_bounds__(256) thin_naive_kernel(ThinArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// thin_dot: ny ≤ 4 outputs from a wide contraction on a SMALL output grid (the D-last layer
+// at 64³: 8ndf = 512 channels × 64 taps into 6³ voxels per patch).  One block per output
+// voxel: the 256 threads sweep the block's (tap, channel-quad) elements with float4 loads of
+// the input row and the weight row (both contiguous in cx), then a fixed-order block
+// reduction (deterministic).  Forward form, any stride.  Replaces one-wave-per-voxel
+// scalar loads (thin_naive, ≈10× slower on this shape).
+// ---------------------------------------------------------------------------------------
+template <int NY>
+__global__ void __launch_bounds__(256) thin_dot_kernel(ThinArgs a) {
+  __shared__ float red[NY][4];
+  const int tid = threadIdx.x;
+  int64_t o = blockIdx.x;
+  const int ow = (int)(o % a.Wo); o /= a.Wo;
+  const int oh = (int)(o % a.Ho); o /= a.Ho;
+  const int od = (int)(o % a.Do); const int nb = (int)(o / a.Do);
+  const int k = a.k, T = k * k * k, c4n = a.cx >> 2;
+  float acc[NY];
+#pragma unroll
+  for (int n = 0; n < NY; ++n) acc[n] = 0.f;
+  for (int e = tid; e < T * c4n; e += 256) {
+    const int t = e / c4n, c = (e - t * c4n) * 4;
+    const int tw = t % k, th = (t / k) % k, td = t / (k * k);
+    const int id = od * a.s - a.p + td, ih = oh * a.s - a.p + th, iw = ow * a.s - a.p + tw;
+    if ((unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi || (unsigned)iw >= (unsigned)a.Wi) continue;
+    const float4 xv = *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c);
+#pragma unroll
+    for (int n = 0; n < NY; ++n) {
+      const float4 wv = *reinterpret_cast<const float4*>(a.w + ((int64_t)t * NY + n) * a.cx + c);
+      acc[n] = fmaf(xv.x, wv.x, fmaf(xv.y, wv.y, fmaf(xv.z, wv.z, fmaf(xv.w, wv.w, acc[n]))));
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NY; ++n) {
+    float s = acc[n];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((tid & 63) == 0) red[n][tid >> 6] = s;
+  }
+  __syncthreads();
+  if (tid < NY) {
+    const float s = ((red[tid][0] + red[tid][1]) + red[tid][2]) + red[tid][3];
+    a.y[(int64_t)blockIdx.x * NY + tid] = act_fwd(s + (a.bias ? a.bias[tid] : 0.f), a.act);
+  }
+}
+
 template <int NY>
 static void launch_thin_n(const ThinArgs& a, dim3 grid, size_t lds, hipStream_t st, int th, int tw) {
   switch (a.k) {
@@ -338,6 +384,16 @@ int conv_thin(ThinArgs a, hipStream_t st) {
       default: hipLaunchKernelGGL(thin_n_class_kernel<4>, grid, dim3(256), 0, st, a); break;
     }
     return check_launch("thin_n_class");
+  }
+  if (a.ny <= 4 && !a.trans && a.cx % 4 == 0 && a.cx >= 32) {
+    dim3 grid((unsigned)total);
+    switch (a.ny) {
+      case 1: hipLaunchKernelGGL(thin_dot_kernel<1>, grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(thin_dot_kernel<2>, grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(thin_dot_kernel<3>, grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(thin_dot_kernel<4>, grid, dim3(256), 0, st, a); break;
+    }
+    return check_launch("thin_dot");
   }
   hipLaunchKernelGGL(thin_naive_kernel, dim3(ceil_div(total, 4)), dim3(256), 0, st, a);
   return check_launch("thin_naive");

@@ -1,0 +1,547 @@
+// Depth-streaming MFMA kernels for the ONE-channel k = 7, stride-1 convolutions (gfx950):
+//
+//   G stem   Conv3d(1 → ngf, k7) on the RPad3 input             networks3D.py:185-189 (forward)
+//   G head   data gradient of Conv3d(ngf → 1, k7)                networks3D.py:211-212 (transposed
+//            form s = 1 = forward form with pad 6 − p and the taps flipped)
+//   both     weight gradients (dW[c][t] = Σ_v P[v][c] · Q[v + t − pe], P the 32-channel operand)
+//
+// The single-channel operand Q enters every product through an "X8" image: X8[d][h][w] =
+// Q[d][h][w..w+7], split into planar bf16 hi / lo 16-B entries, so that one MFMA k-group of 8
+// is one w-row of taps (kw padded to 8 with a zero tap) and every fragment is one aligned 16-B
+// LDS read.  A block owns a column of the output (forward) or of P's grid (weight gradient) —
+// 8 rows × 16 columns — and walks it along depth: the 7 X8 planes a depth step reads stay
+// resident in an 8-slot ring, and each step expands exactly ONE new plane (the one 7 steps
+// ahead) into the slot the previous step retired, while its MFMAs run.  One barrier per step.
+// (A 7-deep halo re-expanded per brick cost more than the MFMAs: thin1_x3 of round 1.)
+//
+//   forward  rows = 32 output channels (the weights, all 25 K-steps held in registers),
+//            cols = 32 voxels (2 rows × 16 columns per wave), K = 50 (kd, kh) groups × 8 kw;
+//            the weight rows are permuted so a lane's 16 accumulators are 16 consecutive
+//            channels of one voxel (64 contiguous bytes stored per lane);
+//   wgrad    rows = 13 tiles of 32 taps (7·7·8 with kw padded), cols = 32 channels, K = the
+//            step's 128 voxels split over the 4 waves (2 brick rows each), accumulators kept
+//            across the block's whole work list; P's brick is staged transposed ([c][voxel],
+//            double-buffered).  The 4 waves' partial sums are added in LDS in wave order and
+//            each block writes one [343][32] slab; a second kernel sums the slabs in fixed
+//            order (deterministic).
+//
+// Work items = (column, depth chunk of L steps); L is chosen on the host so that the items
+// divide evenly over the CUs (one 4-wave block per CU, grid ≤ CU count, items strided).
+#include "kernels.h"
+#include "prec.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kK = 7;
+constexpr int kT = kK * kK * kK;        // 343 taps
+constexpr int kC = 32;                  // channels of the wide side
+constexpr int kGroups = 50;             // 49 (kd, kh) rows + 1 zero group
+constexpr int kKS = kGroups / 2;        // forward K-steps (two groups each: lane halves)
+constexpr int kMT = 13;                 // wgrad tap tiles: 7·7·8 rows → 13 × 32
+constexpr int kBH = 8, kBW = 16;        // brick: rows × columns per depth step
+constexpr int kRH = kBH + kK - 1;       // X8 rows per plane
+constexpr int kRing = 8;                // X8 planes resident
+constexpr int kPlaneE = kRH * kBW;      // 224 X8 entries per plane (hi or lo)
+constexpr int kPS = kBH * kBW + 8;      // P^T channel-row stride (bf16): 272 B, 17 16-B slots
+constexpr int kMaxItemsStamped = 4096;
+
+// X8 entry of (row, pos) in a plane.  The weight-gradient reads (lanes = taps: 8 kw of one
+// (kd, kh) row per 8 lanes, consecutive kh on neighbouring lane octets) hit distinct banks when
+// odd rows swap their column halves; the forward reads (lanes = 16 columns of 2 rows) need the
+// identity.
+template <bool SW>
+__device__ __forceinline__ int x8_entry(int row, int pos) {
+  return row * kBW + (SW ? (pos ^ ((row & 1) << 3)) : pos);
+}
+
+// eight consecutive w of one Q row (zero outside Q) through the volume's range-checked
+// descriptor: out-of-range elements get an offset past the end and read 0
+__device__ __forceinline__ void load_row8(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0,
+                                          float (&v)[8]) {
+  const bool okdh = (unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H;
+  const uint32_t rowb = (uint32_t)(((int64_t)d * H + h) * W) * 4u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int w = w0 + j;
+    const bool ok = okdh && (unsigned)w < (unsigned)W;
+    v[j] = buf_load_f32(q, ok ? rowb + 4u * (uint32_t)w : kOobOffset);
+  }
+}
+
+// X8 entry e of a plane (rows of kBW entries) from its 8 raw values, split hi / lo
+template <int PM, bool SW>
+__device__ __forceinline__ void store_x8(bf16x8* ringH, bf16x8* ringL, int plane_e, int slot, int e,
+                                         const float (&v)[8]) {
+  const f32x8 f = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+  bf16x8 hi, lo;
+  prec::split8v<PM>(f, hi, lo);
+  const int idx = slot * plane_e + x8_entry<SW>(e / kBW, e % kBW);
+  ringH[idx] = hi;
+  if constexpr (prec::has_lo<PM>()) ringL[idx] = lo;
+}
+
+// the depth-chunk length: items = columns × ⌈D / L⌉ spread over ≤ ncu blocks; cost ≈ rounds ×
+// (steps + the 7 prologue plane expansions, ≈ 1.5 steps)
+void pick_chunk(int64_t columns, int D, int ncu, int& L, int& nch, int& grid) {
+  double best = 1e30;
+  L = D; nch = 1; grid = 1;
+  for (int l = 4; l <= 32; ++l) {
+    const int ll = l < D ? l : D;
+    const int n = ceil_div(D, ll);
+    const int64_t items = columns * n;
+    const int g = (int)(items < ncu ? items : ncu);
+    const int64_t rounds = (items + g - 1) / g;
+    const double cost = (double)rounds * (ll + 1.5);
+    if (cost < best - 1e-9) { best = cost; L = ll; nch = n; grid = g; }
+    if (ll == D) break;
+  }
+}
+
+int cu_count() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+// wp: packed [343][ny] (cin = 1) → out[(g·2 + hl)·ny + co][8] bf16, e = kw (e = 7 and g = 49: 0)
+template <int PM>
+__global__ void thin1_pack_kernel(const float* __restrict__ wp, int ny, int flip, __bf16* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kGroups * ny) return;
+  const int co = i % ny, g = i / ny;
+  f32x8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float w = 0.f;
+    if (g < kK * kK && e < kK) {
+      const int t = g * kK + e;
+      w = wp[(int64_t)(flip ? kT - 1 - t : t) * ny + co];
+    }
+    v[e] = w;
+  }
+  bf16x8 hi, lo;
+  prec::split8v<PM>(v, hi, lo);
+  *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 0) * ny + co) * 8) = hi;
+  *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 1) * ny + co) * 8) = lo;
+}
+
+}  // namespace
+
+// diagnostic stamps (MRAGAN_STAMPS=1): s_memtime at item start / after the prologue / item end
+__device__ unsigned long long g_thin1_stamps[kMaxItemsStamped * 3];
+
+struct Thin1RArgs {
+  int stamp;
+  const float* x; int N, Di, Hi, Wi;      // [N][Di][Hi][Wi]
+  const __bf16* wx;
+  const float* bias;
+  float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo][32]
+  int pe, act;
+  int nbh, nbw, L, nch, items;
+};
+
+// forward brick: 16 rows × 16 columns per depth step, 4 rows (2 tiles) per wave
+constexpr int kFH = 16;
+constexpr int kFRH = kFH + kK - 1;      // 22 X8 rows per plane
+constexpr int kFPlaneE = kFRH * kBW;    // 352 entries per plane (hi or lo)
+constexpr int kFLds = 2 * kRing * kFPlaneE * 16 + kGroups * 2 * kC * 16;   // ring + weights: 141 312 B
+
+template <int PM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_fwd_kernel(Thin1RArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);       // [kRing][kFPlaneE]
+  bf16x8* ringL = ringH + kRing * kFPlaneE;
+  bf16x8* wsm = ringL + kRing * kFPlaneE;                // [kGroups][hi|lo][kC]: the packed table
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+
+  for (int e = tid; e < kGroups * 2 * kC; e += 256) wsm[e] = reinterpret_cast<const bf16x8*>(a.wx)[e];
+  // A row li (weights) holds channel perm(li) = 16·((li>>2)&1) + 4·(li>>3) + (li&3), so
+  // accumulator 4q + e of lane (li, lh) is channel 16·lh + 4q + e: 64 contiguous bytes per lane
+  const int co = ((li >> 2) & 1) * 16 + (li >> 3) * 4 + (li & 3);
+  float bias[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) bias[q] = a.bias ? a.bias[16 * lh + q] : 0.f;
+  // this lane's voxels (B columns): brick rows 4·wave + 2i + li/16 (tile i), column li % 16
+  const int bh0 = 4 * wave + (li >> 4), bw = li & 15;
+
+  for (int item = blockIdx.x; item < a.items; item += gridDim.x) {
+    int r = item;
+    const int cw = r % a.nbw; r /= a.nbw;
+    const int chh = r % a.nbh; r /= a.nbh;
+    const int chunk = r % a.nch;
+    const int nb = r / a.nch;
+    const int od0 = chunk * a.L, oh0 = chh * kFH, ow0 = cw * kBW;
+    const int nsteps = min(a.L, a.Do - od0);
+    const int nplanes = nsteps + kK - 1;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi, (uint32_t)a.Di * a.Hi * a.Wi * 4u);
+    const int d0 = od0 - a.pe, h0 = oh0 - a.pe, w0 = ow0 - a.pe;
+    // this thread's X8 entries of a plane: tid and tid + 256 (< 352)
+    const bool e1 = tid + 256 < kFPlaneE;
+    const int er0 = tid / kBW, er1 = (tid + 256) / kBW, ep = tid % kBW;
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 0] = __builtin_amdgcn_s_memtime();
+
+    // prologue: planes 0..6 → slots 0..6
+#pragma unroll
+    for (int rp = 0; rp < kK; ++rp) {
+      float v0[8], v1[8];
+      load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er0, w0 + ep, v0);
+      if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er1, w0 + ep, v1);
+      store_x8<PM, false>(ringH, ringL, kFPlaneE, rp, tid, v0);
+      if (e1) store_x8<PM, false>(ringH, ringL, kFPlaneE, rp, tid + 256, v1);
+    }
+    __syncthreads();
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
+
+    for (int s = 0; s < nsteps; ++s) {
+      const bool more = s + kK < nplanes;
+      float n0[8], n1[8];
+      if (more) {
+        load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er0, w0 + ep, n0);
+        if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er1, w0 + ep, n1);
+      }
+      f32x16 acc[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) {
+        // this lane's group 2ks + lh → (kd, kh); the zero group 49 reads group 48's entries
+        const int g = 2 * ks + lh;
+        const int g0 = 2 * ks, g1 = 2 * ks + 1 < kK * kK ? 2 * ks + 1 : kK * kK - 1;
+        const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
+        const bf16x8 ah = wsm[(g * 2 + 0) * kC + co];
+        const bf16x8 al = prec::has_lo<PM>() ? wsm[(g * 2 + 1) * kC + co] : ah;
+        const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<false>(bh0 + kh, bw);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 xh = ringH[base + 2 * i * kBW];
+          const bf16x8 xl = prec::has_lo<PM>() ? ringL[base + 2 * i * kBW] : xh;
+          acc[i] = prec::mma<PM>(ah, al, xh, xl, acc[i]);
+        }
+      }
+      if (more) {
+        store_x8<PM, false>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0);
+        if (e1) store_x8<PM, false>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid + 256, n1);
+      }
+
+      const int od = od0 + s, ow = ow0 + bw;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int oh = oh0 + bh0 + 2 * i;
+        if (oh < a.Ho && ow < a.Wo) {
+          float* yv = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * kC + 16 * lh;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 v = make_float4(acc[i][4 * q] + bias[4 * q], acc[i][4 * q + 1] + bias[4 * q + 1],
+                                   acc[i][4 * q + 2] + bias[4 * q + 2], acc[i][4 * q + 3] + bias[4 * q + 3]);
+            if (a.act != kActNone)
+              v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
+            *reinterpret_cast<float4*>(yv + 4 * q) = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 2] = __builtin_amdgcn_s_memtime();
+  }
+}
+
+int thin1_debug_stamps(unsigned long long* host, int n) {
+  if (n > kMaxItemsStamped * 3) n = kMaxItemsStamped * 3;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_thin1_stamps), (size_t)n * 8) == hipSuccess ? kOk : kLaunch;
+}
+
+bool thin1_x3_applicable(int cx, int ny, int k, int s) { return cx == 1 && k == kK && s == 1 && ny == kC; }
+
+size_t thin1_x3_ws_bytes(int ny) { return (size_t)kGroups * 2 * ny * 8 * sizeof(__bf16); }
+
+template <int PM>
+static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
+  const size_t need = thin1_x3_ws_bytes(t.ny);
+  if (!ws || ws_bytes < need) {
+    set_error("thin1_x3: workspace %zu < %zu", ws_bytes, need);
+    return kWorkspace;
+  }
+  hipLaunchKernelGGL(thin1_pack_kernel<PM>, dim3(ceil_div(kGroups * t.ny, 256)), dim3(256), 0, st, t.w, t.ny,
+                     t.trans ? 1 : 0, static_cast<__bf16*>(ws));
+  int rc = check_launch("thin1_x3_pack");
+  if (rc) return rc;
+  Thin1RArgs a{};
+  static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
+  a.stamp = stamps;
+  a.x = t.x; a.N = t.N; a.Di = t.Di; a.Hi = t.Hi; a.Wi = t.Wi;
+  a.wx = static_cast<const __bf16*>(ws);
+  a.bias = t.bias; a.y = t.y; a.Do = t.Do; a.Ho = t.Ho; a.Wo = t.Wo;
+  a.pe = t.trans ? kK - 1 - t.p : t.p;       // transposed s = 1: forward form, flipped taps
+  a.act = t.act;
+  a.nbh = ceil_div(t.Ho, kFH); a.nbw = ceil_div(t.Wo, kBW);
+  const int64_t columns = (int64_t)t.N * a.nbh * a.nbw;
+  if (columns == 0 || t.Do == 0) return kOk;
+  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * 4 < (int64_t)kOobOffset, "thin1_x3: input volume too large");
+  int grid = 1;
+  pick_chunk(columns, t.Do, cu_count(), a.L, a.nch, grid);
+  a.items = (int)(columns * a.nch);
+  const size_t lds = kFLds;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(thin1r_fwd_kernel<PM>, dim3(grid), dim3(256), lds, st, a);
+  return check_launch("thin1_x3");
+}
+
+int conv_thin1_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
+  MRAGAN_PREC_DISPATCH(mode, return conv_thin1_pm<PM>(t, ws, ws_bytes, st))
+}
+
+// ---------------------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------------------
+struct Thin1RWArgs {
+  const float* P; int N, Dp, Hp, Wp;          // [N][Dp][Hp][Wp][32]
+  const float* Q; int Dq, Hq, Wq;             // [N][Dq][Hq][Wq]
+  int pe;
+  int nbh, nbw, L, nch, items;
+  float* slab;                                // [gridDim.x][343][32]
+};
+
+template <int PM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_wgrad_kernel(Thin1RWArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);                     // [kRing][kPlaneE]
+  bf16x8* ringL = ringH + kRing * kPlaneE;
+  __bf16* pt = reinterpret_cast<__bf16*>(ringL + kRing * kPlaneE);     // [2 buf][hi|lo][32][kPS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // A rows of the 13 tap tiles: tap m = 32t + li → (kd, kh, kw); padding rows read tap 0
+  int tkd[kMT], toff[kMT][2];
+#pragma unroll
+  for (int t = 0; t < kMT; ++t) {
+    const int m = 32 * t + li, kw = m & 7, g = m >> 3;
+    const bool ok = kw < kK && g < kK * kK;
+    const int kd = ok ? g / kK : 0, kh = ok ? g % kK : 0, kwv = ok ? kw : 0;
+    tkd[t] = kd;
+#pragma unroll
+    for (int kss = 0; kss < 2; ++kss) toff[t][kss] = x8_entry<true>(2 * wave + kss + kh, 8 * lh + kwv);
+  }
+  f32x16 acc[kMT];
+#pragma unroll
+  for (int t = 0; t < kMT; ++t) acc[t] = f32x16{};
+
+  // P staging units: u = tid + 256i → voxel pair vp = u & 63 (voxels 2vp, 2vp + 1 of the
+  // brick: row vp / 8, columns 2(vp % 8) …), channel quad cq = u >> 6
+  auto p_load1 = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, int i, float4& v0, float4& v1)
+                     __attribute__((always_inline)) {
+    const int u = tid + 256 * i, vp = u & 63, cq = u >> 6;
+    const int ph = vh0 + (vp >> 3), pw = vw0 + 2 * (vp & 7);
+    const bool okr = vd < a.Dp && ph < a.Hp;
+    const bool ok0 = okr && pw < a.Wp, ok1 = okr && pw + 1 < a.Wp;
+    const uint32_t b0 = (uint32_t)((((int64_t)vd * a.Hp + ph) * a.Wp + pw) * kC + 4 * cq) * 4u;
+    v0 = buf_load_f32x4(pr, ok0 ? b0 : kOobOffset);
+    v1 = buf_load_f32x4(pr, ok1 ? b0 + kC * 4u : kOobOffset);
+  };
+  auto p_store1 = [&](int buf, int i, const float4 v0, const float4 v1) __attribute__((always_inline)) {
+    __bf16* ph = pt + (size_t)buf * 2 * kC * kPS;
+    __bf16* pl = ph + kC * kPS;
+    const int u = tid + 256 * i, vp = u & 63, cq = u >> 6;
+    auto put = [&](int q, float x0, float x1) __attribute__((always_inline)) {
+      uint32_t h, l;
+      prec::split2<PM>(x0, x1, h, l);
+      const int idx = (4 * cq + q) * kPS + 2 * vp;
+      *reinterpret_cast<uint32_t*>(ph + idx) = h;
+      if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint32_t*>(pl + idx) = l;
+    };
+    put(0, v0.x, v1.x);
+    put(1, v0.y, v1.y);
+    put(2, v0.z, v1.z);
+    put(3, v0.w, v1.w);
+  };
+
+  for (int item = blockIdx.x; item < a.items; item += gridDim.x) {
+    int r = item;
+    const int cw = r % a.nbw; r /= a.nbw;
+    const int chh = r % a.nbh; r /= a.nbh;
+    const int chunk = r % a.nch;
+    const int nb = r / a.nch;
+    const int vd0 = chunk * a.L, vh0 = chh * kBH, vw0 = cw * kBW;
+    const int nsteps = min(a.L, a.Dp - vd0);
+    const int nplanes = nsteps + kK - 1;
+    const __amdgpu_buffer_rsrc_t qr = make_rsrc(a.Q + (int64_t)nb * a.Dq * a.Hq * a.Wq, (uint32_t)a.Dq * a.Hq * a.Wq * 4u);
+    const __amdgpu_buffer_rsrc_t pr =
+        make_rsrc(a.P + (int64_t)nb * a.Dp * a.Hp * a.Wp * kC, (uint32_t)a.Dp * a.Hp * a.Wp * kC * 4u);
+    const int d0 = vd0 - a.pe, h0 = vh0 - a.pe, w0 = vw0 - a.pe;
+    const int erow = tid / kBW, epos = tid % kBW;
+
+    // prologue: P of step 0 → buffer 0, Q planes 0..6 → slots 0..6
+    {
+      float4 p00, p01, p10, p11;
+      p_load1(pr, vd0, vh0, vw0, 0, p00, p01);
+      p_load1(pr, vd0, vh0, vw0, 1, p10, p11);
+      if (tid < kPlaneE) {
+        float v[7][8];
+#pragma unroll
+        for (int rp = 0; rp < kK; ++rp) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + rp, h0 + erow, w0 + epos, v[rp]);
+#pragma unroll
+        for (int rp = 0; rp < kK; ++rp) store_x8<PM, true>(ringH, ringL, kPlaneE, rp, tid, v[rp]);
+      }
+      p_store1(0, 0, p00, p01);
+      p_store1(0, 1, p10, p11);
+    }
+    __syncthreads();
+
+    for (int s = 0; s < nsteps; ++s) {
+      const bool more_q = s + kK < nplanes, more_p = s + 1 < nsteps;
+      float nv[8];
+      float4 p00 = {}, p01 = {}, p10 = {}, p11 = {};
+      if (more_q && tid < kPlaneE) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos, nv);
+      if (more_p) {
+        p_load1(pr, vd0 + s + 1, vh0, vw0, 0, p00, p01);
+        p_load1(pr, vd0 + s + 1, vh0, vw0, 1, p10, p11);
+      }
+
+      const __bf16* ph = pt + (size_t)(s & 1) * 2 * kC * kPS;
+      const __bf16* pl = ph + kC * kPS;
+      int sb[kMT];
+#pragma unroll
+      for (int t = 0; t < kMT; ++t) sb[t] = ((s + tkd[t]) & (kRing - 1)) * kPlaneE;
+#pragma unroll
+      for (int kss = 0; kss < 2; ++kss) {
+        // K-step: brick row 2·wave + kss, voxels 8·lh … +7 of its 16
+        const int pidx = li * kPS + (2 * wave + kss) * kBW + 8 * lh;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(ph + pidx);
+        const bf16x8 bl = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(pl + pidx) : bh;
+#pragma unroll
+        for (int t = 0; t < kMT; ++t) {
+          const int idx = sb[t] + toff[t][kss];
+          const bf16x8 ah = ringH[idx];
+          const bf16x8 al = prec::has_lo<PM>() ? ringL[idx] : ah;
+          acc[t] = prec::mma<PM>(ah, al, bh, bl, acc[t]);
+        }
+        // one K-step per scheduling region (left free, the scheduler hoists the next K-step's
+        // 13 fragment reads and the single-plane modes spill)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (more_q && tid < kPlaneE) store_x8<PM, true>(ringH, ringL, kPlaneE, (s + kK) & (kRing - 1), tid, nv);
+      if (more_p) {
+        p_store1((s + 1) & 1, 0, p00, p01);
+        p_store1((s + 1) & 1, 1, p10, p11);
+      }
+      __syncthreads();
+    }
+  }
+
+  // the 4 waves' partial sums, added in wave order in LDS ([416 rows][32] floats over the ring),
+  // then this block's slab rows (taps) × 32 channels
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < kMT; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = 32 * t + 8 * (q >> 2) + 4 * lh + (q & 3);
+          const int idx = m * kC + li;
+          red[idx] = w == 0 ? acc[t][q] : red[idx] + acc[t][q];
+        }
+    }
+    __syncthreads();
+  }
+  float* slab = a.slab + (int64_t)blockIdx.x * kT * kC;
+  for (int e = tid; e < kT * kC; e += 256) {
+    const int tp = e / kC, c = e % kC;
+    const int m = (tp / kK) * 8 + tp % kK;
+    slab[e] = red[m * kC + c];
+  }
+}
+
+// out[c][t] (=|+=) Σ_blocks slab[z][τ(t)][c]   (τ = tap mirror for the head form)
+// One block per tap: 8 groups of 32 lanes (lane = channel: 128 contiguous bytes per slab row),
+// group g sums slabs z ≡ g (mod 8) in increasing z, then the 8 partials are added in g order —
+// fixed order, deterministic.
+__global__ void __launch_bounds__(256) thin1_wgrad_reduce_kernel(const float* __restrict__ slab, int nz, int flip,
+                                                                 float* __restrict__ out, int accumulate) {
+  __shared__ float part[8][kC];
+  const int t = blockIdx.x, c = threadIdx.x % kC, g = threadIdx.x / kC;
+  const int ts = flip ? kT - 1 - t : t;
+  float s = 0.f;
+#pragma unroll 8
+  for (int z = g; z < nz; z += 8) s += slab[((int64_t)z * kT + ts) * kC + c];
+  part[g][c] = s;
+  __syncthreads();
+  if (g == 0) {
+    float r = part[0][c];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) r += part[k][c];
+    const int e = c * kT + t;
+    out[e] = accumulate ? out[e] + r : r;
+  }
+}
+
+bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s) {
+  return k == kK && s == 1 && ((Cd == kC && Cg == 1) || (Cd == 1 && Cg == kC));
+}
+
+size_t thin1_wgrad_x3_ws_bytes() { return (size_t)cu_count() * kT * kC * sizeof(float); }
+
+// Same argument convention as conv_wgrad: dW[dn][gn][t] = Σ_m D[m][dn] · G[m − p + t][gn]
+int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
+                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
+  Thin1RWArgs a{};
+  int flip;
+  if (Cg == 1) {          // stem: P = D (32 ch), Q = G
+    a.P = D; a.Dp = Dd; a.Hp = Hd; a.Wp = Wd;
+    a.Q = G; a.Dq = Dg; a.Hq = Hg; a.Wq = Wg;
+    a.pe = p; flip = 0;
+  } else {                // head: P = G (32 ch), Q = D, u = m − p + t
+    a.P = G; a.Dp = Dg; a.Hp = Hg; a.Wp = Wg;
+    a.Q = D; a.Dq = Dd; a.Hq = Hd; a.Wq = Wd;
+    a.pe = kK - 1 - p; flip = 1;
+  }
+  a.N = N;
+  MRAGAN_CHECK_ARG((int64_t)a.Dp * a.Hp * a.Wp * kC * 4 < (int64_t)kOobOffset && (int64_t)a.Dq * a.Hq * a.Wq * 4 < (int64_t)kOobOffset,
+                   "thin1_wgrad_x3: volume too large");
+  a.nbh = ceil_div(a.Hp, kBH); a.nbw = ceil_div(a.Wp, kBW);
+  const int64_t columns = (int64_t)N * a.nbh * a.nbw;
+  int grid = 1;
+  if (columns > 0 && a.Dp > 0) pick_chunk(columns, a.Dp, cu_count(), a.L, a.nch, grid);
+  else { a.L = 1; a.nch = 0; }
+  a.items = (int)(columns * a.nch);
+  const size_t need = (size_t)grid * kT * kC * sizeof(float);
+  if (!ws || ws_bytes < need) {
+    set_error("thin1_wgrad_x3: workspace %zu < %zu", ws_bytes, need);
+    return kWorkspace;
+  }
+  a.slab = static_cast<float*>(ws);
+  const size_t lds = (size_t)2 * kRing * kPlaneE * 16 + (size_t)2 * 2 * kC * kPS * sizeof(__bf16);
+  static_assert(kMT * 32 * kC * 4 <= 2 * kRing * kPlaneE * 16, "the wave reduction fits the ring");
+  int rc = kOk;
+  MRAGAN_PREC_DISPATCH(mode, {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_wgrad_kernel<PM>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(256), lds, st, a);
+    rc = check_launch("thin1_wgrad_x3");
+    break;
+  })
+  if (rc) return rc;
+  static_assert(kC * 8 == 256, "reduce block = 8 groups of kC lanes");
+  hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, flip, out, accumulate);
+  return check_launch("thin1_wgrad_reduce");
+}
+
+}  // namespace mragan

@@ -15,11 +15,14 @@
 // over K = (input plane kd' = 0..7, kh, c); then z[2q + j][oh][ow] = Σ_kw P[ow + kw][j, kw]
 // (an LDS epilogue).  Useful fraction 7/8 (kd' vs kd) × 7/8 (kw) × 64/80 (w halo).
 //
-// Block = 2 output depths × 8 output rows (two per wave) × 64 output columns.  The input is
+// Block = 2 output depths × 8 output rows (two per wave) × 74 output columns (the 80 w' rows
+// less the 6-column halo: one column block covers both 64- and 70-wide outputs).  The input is
 // streamed in 16 units (plane kd' × 16-channel half): each unit's 14 × 80 positions × 16
 // channels are staged split into bf16 hi/lo (64-B swizzled LDS records), double-buffered with
 // one barrier per unit and register-prefetched two units ahead; the weights come pre-split in
-// fragment order from L2 (thinn_x3_pack).
+// fragment order from L2 (thinn_x3_pack).  Blocks are dealt to the 8 XCDs in contiguous
+// ranges of the (column, row, depth pair) order, so the blocks resident on one XCD at a time
+// are neighbours in depth and re-read their shared input planes from that XCD's L2.
 #include "kernels.h"
 #include "prec.h"
 
@@ -34,13 +37,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kK = 7;
 constexpr int kC = 32;                  // input channels
-constexpr int kOW = 64;                 // output columns per block
+constexpr int kOW = 74;                 // output columns per block (kMW − 6)
 constexpr int kMW = 80;                 // w' rows: 64 + 6 halo, 5 M-tiles of 16
 constexpr int kBH = 8;                  // output rows per block (two per wave)
 constexpr int kRH = kBH + kK - 1;       // staged rows per plane
 constexpr int kRec = 64;                // LDS bytes per position: 4 16-B chunks (hi 0-7, hi 8-15,
-                                        // lo 0-7, lo 8-15) rotated by (pos >> 2) & 3 so the 16
-                                        // consecutive positions of a fragment read hit 16 slots
+                                        // lo 0-7, lo 8-15); chunk L sits at slot L ^ rot(pos)
 constexpr int kUnits = 16;              // 8 planes × 2 channel halves
 constexpr int kUnitBytes = kRH * kMW * kRec;
 constexpr int kNF4 = kRH * kMW * 4;     // float4 per unit (16 channels)
@@ -79,14 +81,22 @@ struct ThinnArgs {
   float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo]
   int pe, act;
   int nq, nr, nw;                         // depth pairs, row blocks, column blocks
+  int total, per;                         // blocks, blocks per XCD range
 };
+
+// slot rotation of a position's 16-B chunks: rot = 2·(bit 1 ⊕ bit 3 of pos).  With it the
+// ds_read_b128 lane groups of a fragment read ({0–3,12–15,20–27}, … : positions n16, chunk
+// g & 1) and the ds_write_b64 groups of the staging stores (16 lanes = 4 positions × 4
+// channel quads) both land on distinct banks.
+__device__ __forceinline__ int thinn_rot(int pos) { return (pos ^ (pos >> 2)) & 2; }
 
 template <int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 thinn_x3_kernel(ThinnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][kUnitBytes]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int blk = blockIdx.x;
+  int blk = (blockIdx.x & 7) * a.per + (blockIdx.x >> 3);   // XCD-contiguous logical block
+  if (blk >= a.total) return;
   const int cw = blk % a.nw; blk /= a.nw;
   const int r = blk % a.nr; blk /= a.nr;
   const int q = blk % a.nq;
@@ -116,10 +126,10 @@ thinn_x3_kernel(ThinnArgs a) {
     }
   };
   // element l of this thread sits at position 64l + tid/4 (channels 4(tid&3)…): its chunk
-  // rotation ((c + pos/4) & 3) depends on tid only, so every store is base + 4096·l
-  const int cq = tid & 3;
-  const int st_hi = (tid >> 2) * kRec + 16 * (((cq >> 1) + (tid >> 4)) & 3) + 8 * (cq & 1);
-  const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1) + (tid >> 4)) & 3) + 8 * (cq & 1);
+  // rotation depends on tid only, so every store is base + 4096·l
+  const int cq = tid & 3, srot = thinn_rot(tid >> 2);
+  const int st_hi = (tid >> 2) * kRec + 16 * ((cq >> 1) ^ srot) + 8 * (cq & 1);
+  const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1)) ^ srot) + 8 * (cq & 1);
   auto stage_store = [&](char* buf, const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < kF4PT; ++l) {
@@ -138,7 +148,7 @@ thinn_x3_kernel(ThinnArgs a) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) acc[rr][i] = f32x4{};
   const int n16 = lane & 15, g = lane >> 4;
-  const int a_hi = 16 * (((g & 1) + (n16 >> 2)) & 3), a_lo = 16 * ((2 + (g & 1) + (n16 >> 2)) & 3);
+  const int a_hi = 16 * ((g & 1) ^ thinn_rot(n16)), a_lo = 16 * ((2 + (g & 1)) ^ thinn_rot(n16));
   const __bf16* wx = a.wx;
 
   // valid units (input plane inside the input) form a contiguous range [u0, u1)
@@ -146,17 +156,26 @@ thinn_x3_kernel(ThinnArgs a) {
   while (u0 < kUnits && (od0 + (u0 >> 1) - a.pe) < 0) ++u0;
   while (u1 > u0 && (od0 + ((u1 - 1) >> 1) - a.pe) >= a.Di) --u1;
 
-  auto compute = [&](int u, const char* buf) __attribute__((always_inline)) {
+  // the unit's weight fragments [step][hi|lo], issued at the top of the unit's iteration BEFORE
+  // that iteration's staging loads: the memory counter retires in order, so weights fetched
+  // after a staging batch would make the MFMAs wait for the whole batch
+  auto w_load = [&](int u, bf16x8 (&w)[4][2]) __attribute__((always_inline)) {
     const int kdp = u >> 1, half = u & 1;
     const __bf16* wt = wx + ((int64_t)(kdp * 2 + half) * 4) * 2 * 64 * 8;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 0) * 64 * 8 + lane * 8);
-      const bf16x8 bl = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8) : bh;
+      w[s][0] = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 0) * 64 * 8 + lane * 8);
+      w[s][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8) : w[s][0];
+    }
+  };
+  auto compute = [&](const char* buf, const bf16x8 (&w)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 bh = w[s][0], bl = w[s][1];
       int kh = 2 * s + (g >> 1);
       kh = kh < kK ? kh : kK - 1;           // the padding kh = 7 has zero weights
       // position (2wave + rr + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
-      // positions, so the chunk rotation is the lane's own (n16 / 4) — addresses fold to
+      // positions, so the chunk rotation is the lane's own (of n16) — addresses fold to
       // lane base + immediate
       const char* rowp = buf + ((2 * wave + kh) * kMW + n16) * kRec;
 #pragma unroll
@@ -168,11 +187,13 @@ thinn_x3_kernel(ThinnArgs a) {
           const bf16x8 al = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo) : ah;
           acc[rr][mt] = prec::mma16<PM>(ah, al, bh, bl, acc[rr][mt]);
         }
+      __builtin_amdgcn_sched_barrier(0);    // one step per scheduling region (register budget)
     }
   };
 
   // pipeline: LDS buffer (u & 1) holds unit u; register set A/B holds the unit after it
   float4 sA[kF4PT], sB[kF4PT];
+  bf16x8 w[4][2];
   if (u0 < u1) {
     stage_load(u0, sA);
     stage_store(smem + (u0 & 1) * kUnitBytes, sA);
@@ -181,14 +202,16 @@ thinn_x3_kernel(ThinnArgs a) {
   __syncthreads();
   for (int u = u0; u < u1; u += 2) {
     // unit u (registers: sA = u + 1); prefetch u + 2 into sB
+    w_load(u, w);
     if (u + 2 < u1) stage_load(u + 2, sB);
-    compute(u, smem + (u & 1) * kUnitBytes);
+    compute(smem + (u & 1) * kUnitBytes, w);
     if (u + 1 < u1) stage_store(smem + ((u + 1) & 1) * kUnitBytes, sA);
     __syncthreads();
     if (u + 1 >= u1) break;
     // unit u + 1 (registers: sB = u + 2); prefetch u + 3 into sA
+    w_load(u + 1, w);
     if (u + 3 < u1) stage_load(u + 3, sA);
-    compute(u + 1, smem + ((u + 1) & 1) * kUnitBytes);
+    compute(smem + ((u + 1) & 1) * kUnitBytes, w);
     if (u + 2 < u1) stage_store(smem + (u & 1) * kUnitBytes, sB);
     __syncthreads();
   }
@@ -205,9 +228,10 @@ thinn_x3_kernel(ThinnArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);
     const int oh = oh0 + 2 * wave + rr;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int o = k * 64 + lane;               // 128 outputs: j = o / 64, ow = o % 64
-      const int j = o >> 6, owl = o & 63;
+    for (int k = 0; k < 3; ++k) {
+      const int o = k * 64 + lane;               // 148 outputs: j = o / 74, ow = o % 74
+      if (o >= 2 * kOW) break;
+      const int j = o / kOW, owl = o - j * kOW;
       float sum = 0.f;
 #pragma unroll
       for (int kw = 0; kw < kK; ++kw) sum += P[(owl + kw) * 17 + 8 * j + kw];
@@ -242,6 +266,8 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   a.nq = ceil_div(t.Do, 2); a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
   const int64_t blocks = (int64_t)a.N * a.nq * a.nr * a.nw;
   if (blocks == 0) return kOk;
+  a.total = (int)blocks;
+  a.per = (int)ceil_div(blocks, 8);
   const size_t lds = (size_t)2 * kUnitBytes;
   static bool attr_set = false;
   if (!attr_set) {
@@ -249,7 +275,7 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)(8 * a.per)), dim3(256), lds, st, a);
   return check_launch("thinn_x3");
 }
 

@@ -64,6 +64,8 @@ CONV_CASES = [
     (1, 2, 16, 12, 4, 2, 1),
     (2, 256, 1, 7, 4, 1, 1),
     (1, 64, 1, 6, 4, 1, 1),
+    (4, 512, 1, 7, 4, 1, 1),        # D last at 64³ (thin_dot)
+    (1, 64, 2, 6, 4, 1, 1),
     # ngf = 4 generators (thin_k with a cut weight slice: cin ≤ 4, k7, few output channels)
     (1, 4, 1, 12, 7, 1, 0),
     (1, 4, 2, 11, 7, 1, 0),

@@ -55,7 +55,10 @@ def main():
     w_up2 = rnd(27 * ngf * 2 * ngf) * 0.01
     x_dn1 = rnd(N, S, S, S, ngf)
     w_dn1 = rnd(27 * ngf * 2 * ngf) * 0.01
+    x_dl = rnd(N, S // 8 - 1, S // 8 - 1, S // 8 - 1, 512)   # PatchGAN last layer input (ndf 64)
+    w_dl = rnd(64 * 512) * 0.01
     table = {
+        "dlast_fwd": lambda: ops.conv3d(x_dl, w_dl, 1, 4, 1, 1, (S // 8 - 2,) * 3),
         "up2_fwd": lambda: ops.conv3d(x_up2, w_up2, ngf, 3, 2, 1, (S, S, S), transposed=True),
         "down1_fwd": lambda: ops.conv3d(x_dn1, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2)),
         "head_fwd": lambda: ops.conv3d(x_head, w_head, 1, 7, 1, 0, (S, S, S), act="tanh"),
