@@ -51,13 +51,14 @@ constexpr int kPlaneE = kRH * kBW;      // 224 X8 entries per plane (hi or lo)
 constexpr int kPS = kBH * kBW + 8;      // P^T channel-row stride (bf16): 272 B, 17 16-B slots
 constexpr int kMaxItemsStamped = 4096;
 
-// X8 entry of (row, pos) in a plane.  The weight-gradient reads (lanes = taps: 8 kw of one
-// (kd, kh) row per 8 lanes, consecutive kh on neighbouring lane octets) hit distinct banks when
-// odd rows swap their column halves; the forward reads (lanes = 16 columns of 2 rows) need the
-// identity.
-template <bool SW>
-__device__ __forceinline__ int x8_entry(int row, int pos) {
-  return row * kBW + (SW ? (pos ^ ((row & 1) << 3)) : pos);
+// X8 entry of (row, pos) in a plane slot.  The forward reads (lanes = 16 columns of 2 rows)
+// are conflict-free on the identity layout.  The weight-gradient reads (lanes = taps: 8 kw of
+// one (kd, kh) row per lane octet, consecutive (kd, kh) rows on neighbouring octets) need the
+// octets' column halves to alternate: odd (row + slot) swaps them — rows alternate within a
+// plane, and the slot term keeps the alternation across the kh = 6 → 0 plane change.
+template <int SW>
+__device__ __forceinline__ int x8_entry(int row, int pos, int slot) {
+  return row * kBW + (SW ? (pos ^ (((row + slot) & 1) << 3)) : pos);
 }
 
 // eight consecutive w of one Q row (zero outside Q) through the volume's range-checked
@@ -75,13 +76,28 @@ __device__ __forceinline__ void load_row8(__amdgpu_buffer_rsrc_t q, int D, int H
 }
 
 // X8 entry e of a plane (rows of kBW entries) from its 8 raw values, split hi / lo
-template <int PM, bool SW>
+__device__ __forceinline__ f32x8 load_row8v(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0) {
+  float v[8];
+  load_row8(q, D, H, W, d, h, w0, v);
+  return f32x8{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+}
+
+template <int PM, int SW>
+__device__ __forceinline__ void store_x8v(bf16x8* ringH, bf16x8* ringL, int plane_e, int slot, int e, const f32x8 f) {
+  bf16x8 hi, lo;
+  prec::split8v<PM>(f, hi, lo);
+  const int idx = slot * plane_e + x8_entry<SW>(e / kBW, e % kBW, slot);
+  ringH[idx] = hi;
+  if constexpr (prec::has_lo<PM>()) ringL[idx] = lo;
+}
+
+template <int PM, int SW>
 __device__ __forceinline__ void store_x8(bf16x8* ringH, bf16x8* ringL, int plane_e, int slot, int e,
                                          const float (&v)[8]) {
   const f32x8 f = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
   bf16x8 hi, lo;
   prec::split8v<PM>(f, hi, lo);
-  const int idx = slot * plane_e + x8_entry<SW>(e / kBW, e % kBW);
+  const int idx = slot * plane_e + x8_entry<SW>(e / kBW, e % kBW, slot);
   ringH[idx] = hi;
   if constexpr (prec::has_lo<PM>()) ringL[idx] = lo;
 }
@@ -197,8 +213,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       float v0[8], v1[8];
       load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er0, w0 + ep, v0);
       if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er1, w0 + ep, v1);
-      store_x8<PM, false>(ringH, ringL, kFPlaneE, rp, tid, v0);
-      if (e1) store_x8<PM, false>(ringH, ringL, kFPlaneE, rp, tid + 256, v1);
+      store_x8<PM, 0>(ringH, ringL, kFPlaneE, rp, tid, v0);
+      if (e1) store_x8<PM, 0>(ringH, ringL, kFPlaneE, rp, tid + 256, v1);
     }
     __syncthreads();
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
@@ -219,7 +235,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
         const bf16x8 ah = wsm[(g * 2 + 0) * kC + co];
         const bf16x8 al = prec::has_lo<PM>() ? wsm[(g * 2 + 1) * kC + co] : ah;
-        const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<false>(bh0 + kh, bw);
+        const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<0>(bh0 + kh, bw, 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const bf16x8 xh = ringH[base + 2 * i * kBW];
@@ -228,8 +244,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
       }
       if (more) {
-        store_x8<PM, false>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0);
-        if (e1) store_x8<PM, false>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid + 256, n1);
+        store_x8<PM, 0>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0);
+        if (e1) store_x8<PM, 0>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid + 256, n1);
       }
 
       const int od = od0 + s, ow = ow0 + bw;
@@ -308,6 +324,7 @@ int conv_thin1_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStr
 // weight gradient
 // ---------------------------------------------------------------------------------------
 struct Thin1RWArgs {
+  int stamp;
   const float* P; int N, Dp, Hp, Wp;          // [N][Dp][Hp][Wp][32]
   const float* Q; int Dq, Hq, Wq;             // [N][Dq][Hq][Wq]
   int pe;
@@ -315,35 +332,35 @@ struct Thin1RWArgs {
   float* slab;                                // [gridDim.x][343][32]
 };
 
+// 8 waves (2 per SIMD): tap-tile group tg = wave / 4 (tiles 0–6 | 7–12) × K quarter kq = wave % 4
+// (brick rows 2kq, 2kq + 1 of each step)
+constexpr int kWT0 = 7;                 // tiles of group 0 (group 1: kMT − 7 = 6)
+
 template <int PM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_wgrad_kernel(Thin1RWArgs a) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) thin1r_wgrad_kernel(Thin1RWArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);                     // [kRing][kPlaneE]
   bf16x8* ringL = ringH + kRing * kPlaneE;
   __bf16* pt = reinterpret_cast<__bf16*>(ringL + kRing * kPlaneE);     // [2 buf][hi|lo][32][kPS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
+  const int tg = wave >> 2, kq = wave & 3;
+  const int t0 = tg ? kWT0 : 0, nt = tg ? kMT - kWT0 : kWT0;
 
-  // A rows of the 13 tap tiles: tap m = 32t + li → (kd, kh, kw); padding rows read tap 0
-  int tkd[kMT], toff[kMT][2];
+  // A rows of the tap tiles: tap m = 32t + li → (kd, kh, kw); the padding rows (kw = 7, or
+  // groups past 48) read the neighbouring real entries (their sums are dropped), which keeps
+  // the bank pattern of a full octet.  The offset inside the slot is row·16 + (pos ^ 8·((row +
+  // kd + s) & 1)) with row = 2·kq + kss + kh, pos = 8·lh + kw.
+  const int kw_l = li & 7;
+  f32x16 acc[kWT0];
 #pragma unroll
-  for (int t = 0; t < kMT; ++t) {
-    const int m = 32 * t + li, kw = m & 7, g = m >> 3;
-    const bool ok = kw < kK && g < kK * kK;
-    const int kd = ok ? g / kK : 0, kh = ok ? g % kK : 0, kwv = ok ? kw : 0;
-    tkd[t] = kd;
-#pragma unroll
-    for (int kss = 0; kss < 2; ++kss) toff[t][kss] = x8_entry<true>(2 * wave + kss + kh, 8 * lh + kwv);
-  }
-  f32x16 acc[kMT];
-#pragma unroll
-  for (int t = 0; t < kMT; ++t) acc[t] = f32x16{};
+  for (int i = 0; i < kWT0; ++i) acc[i] = f32x16{};
 
-  // P staging units: u = tid + 256i → voxel pair vp = u & 63 (voxels 2vp, 2vp + 1 of the
-  // brick: row vp / 8, columns 2(vp % 8) …), channel quad cq = u >> 6
-  auto p_load1 = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, int i, float4& v0, float4& v1)
-                     __attribute__((always_inline)) {
-    const int u = tid + 256 * i, vp = u & 63, cq = u >> 6;
+  // P staging unit of this thread: voxel pair vp = tid & 63 (voxels 2vp, 2vp + 1 of the brick:
+  // row vp / 8, columns 2(vp % 8) …), channel quad cq = tid >> 6
+  const int vp = tid & 63, cq = tid >> 6;
+  auto p_load = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, float4& v0, float4& v1)
+                    __attribute__((always_inline)) {
     const int ph = vh0 + (vp >> 3), pw = vw0 + 2 * (vp & 7);
     const bool okr = vd < a.Dp && ph < a.Hp;
     const bool ok0 = okr && pw < a.Wp, ok1 = okr && pw + 1 < a.Wp;
@@ -351,10 +368,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     v0 = buf_load_f32x4(pr, ok0 ? b0 : kOobOffset);
     v1 = buf_load_f32x4(pr, ok1 ? b0 + kC * 4u : kOobOffset);
   };
-  auto p_store1 = [&](int buf, int i, const float4 v0, const float4 v1) __attribute__((always_inline)) {
+  auto p_store = [&](int buf, const float4 v0, const float4 v1) __attribute__((always_inline)) {
     __bf16* ph = pt + (size_t)buf * 2 * kC * kPS;
     __bf16* pl = ph + kC * kPS;
-    const int u = tid + 256 * i, vp = u & 63, cq = u >> 6;
     auto put = [&](int q, float x0, float x1) __attribute__((always_inline)) {
       uint32_t h, l;
       prec::split2<PM>(x0, x1, h, l);
@@ -381,85 +397,84 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     const __amdgpu_buffer_rsrc_t pr =
         make_rsrc(a.P + (int64_t)nb * a.Dp * a.Hp * a.Wp * kC, (uint32_t)a.Dp * a.Hp * a.Wp * kC * 4u);
     const int d0 = vd0 - a.pe, h0 = vh0 - a.pe, w0 = vw0 - a.pe;
-    const int erow = tid / kBW, epos = tid % kBW;
+    const int erow = tid / kBW, epos = tid % kBW;      // this thread's X8 entry (tid < 224)
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 0] = __builtin_amdgcn_s_memtime();
 
     // prologue: P of step 0 → buffer 0, Q planes 0..6 → slots 0..6
     {
-      float4 p00, p01, p10, p11;
-      p_load1(pr, vd0, vh0, vw0, 0, p00, p01);
-      p_load1(pr, vd0, vh0, vw0, 1, p10, p11);
+      float4 v0, v1;
+      p_load(pr, vd0, vh0, vw0, v0, v1);
       if (tid < kPlaneE) {
         float v[7][8];
 #pragma unroll
         for (int rp = 0; rp < kK; ++rp) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + rp, h0 + erow, w0 + epos, v[rp]);
 #pragma unroll
-        for (int rp = 0; rp < kK; ++rp) store_x8<PM, true>(ringH, ringL, kPlaneE, rp, tid, v[rp]);
+        for (int rp = 0; rp < kK; ++rp) store_x8<PM, 1>(ringH, ringL, kPlaneE, rp, tid, v[rp]);
       }
-      p_store1(0, 0, p00, p01);
-      p_store1(0, 1, p10, p11);
+      p_store(0, v0, v1);
     }
     __syncthreads();
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
 
     for (int s = 0; s < nsteps; ++s) {
-      const bool more_q = s + kK < nplanes, more_p = s + 1 < nsteps;
-      float nv[8];
-      float4 p00 = {}, p01 = {}, p10 = {}, p11 = {};
-      if (more_q && tid < kPlaneE) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos, nv);
-      if (more_p) {
-        p_load1(pr, vd0 + s + 1, vh0, vw0, 0, p00, p01);
-        p_load1(pr, vd0 + s + 1, vh0, vw0, 1, p10, p11);
-      }
+      // P(s + 1) and Q plane s + 7 → registers before the MFMAs, → the free buffer / slot after
+      const bool more_q = s + kK < nplanes && tid < kPlaneE, more_p = s + 1 < nsteps;
+      float4 v0 = {}, v1 = {};
+      f32x8 q = {};
+      if (more_q) q = load_row8v(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos);
+      if (more_p) p_load(pr, vd0 + s + 1, vh0, vw0, v0, v1);
 
       const __bf16* ph = pt + (size_t)(s & 1) * 2 * kC * kPS;
       const __bf16* pl = ph + kC * kPS;
-      int sb[kMT];
-#pragma unroll
-      for (int t = 0; t < kMT; ++t) sb[t] = ((s + tkd[t]) & (kRing - 1)) * kPlaneE;
 #pragma unroll
       for (int kss = 0; kss < 2; ++kss) {
-        // K-step: brick row 2·wave + kss, voxels 8·lh … +7 of its 16
-        const int pidx = li * kPS + (2 * wave + kss) * kBW + 8 * lh;
+        // K-step: brick row 2·kq + kss, voxels 8·lh … +7 of its 16
+        const int pidx = li * kPS + (2 * kq + kss) * kBW + 8 * lh;
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(ph + pidx);
         const bf16x8 bl = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(pl + pidx) : bh;
 #pragma unroll
-        for (int t = 0; t < kMT; ++t) {
-          const int idx = sb[t] + toff[t][kss];
-          const bf16x8 ah = ringH[idx];
-          const bf16x8 al = prec::has_lo<PM>() ? ringL[idx] : ah;
-          acc[t] = prec::mma<PM>(ah, al, bh, bl, acc[t]);
+        for (int i = 0; i < kWT0; ++i) {
+          if (i < nt) {
+            const int g = min(4 * (t0 + i) + (li >> 3), kK * kK - 1);
+            const int kd = g / kK, kh = g - kd * kK;
+            const int row = 2 * kq + kss + kh;
+            const int idx = ((s + kd) & (kRing - 1)) * kPlaneE + row * kBW +
+                            ((8 * lh + kw_l) ^ (((row + kd + s) & 1) << 3));
+            const bf16x8 ah = ringH[idx];
+            const bf16x8 al = prec::has_lo<PM>() ? ringL[idx] : ah;
+            acc[i] = prec::mma<PM>(ah, al, bh, bl, acc[i]);
+          }
         }
-        // one K-step per scheduling region (left free, the scheduler hoists the next K-step's
-        // 13 fragment reads and the single-plane modes spill)
-        __builtin_amdgcn_sched_barrier(0);
       }
-      if (more_q && tid < kPlaneE) store_x8<PM, true>(ringH, ringL, kPlaneE, (s + kK) & (kRing - 1), tid, nv);
-      if (more_p) {
-        p_store1((s + 1) & 1, 0, p00, p01);
-        p_store1((s + 1) & 1, 1, p10, p11);
-      }
+      if (more_q) store_x8v<PM, 1>(ringH, ringL, kPlaneE, (s + kK) & (kRing - 1), tid, q);
+      if (more_p) p_store((s + 1) & 1, v0, v1);
       __syncthreads();
     }
+    if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 2] = __builtin_amdgcn_s_memtime();
   }
 
-  // the 4 waves' partial sums, added in wave order in LDS ([416 rows][32] floats over the ring),
-  // then this block's slab rows (taps) × 32 channels
+  // the K quarters' partial sums, added in quarter order in LDS ([416 rows][32] floats over the
+  // ring; the two tile groups own disjoint rows), then this block's slab rows (taps) × 32 channels
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
+  for (int rq = 0; rq < 4; ++rq) {
+    if (kq == rq) {
 #pragma unroll
-      for (int t = 0; t < kMT; ++t)
+      for (int i = 0; i < kWT0; ++i) {
+        if (i < nt) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = 32 * t + 8 * (q >> 2) + 4 * lh + (q & 3);
-          const int idx = m * kC + li;
-          red[idx] = w == 0 ? acc[t][q] : red[idx] + acc[t][q];
+          for (int q = 0; q < 16; ++q) {
+            const int m = 32 * (t0 + i) + 8 * (q >> 2) + 4 * lh + (q & 3);
+            const int idx = m * kC + li;
+            red[idx] = rq == 0 ? acc[i][q] : red[idx] + acc[i][q];
+          }
         }
+      }
     }
     __syncthreads();
   }
   float* slab = a.slab + (int64_t)blockIdx.x * kT * kC;
-  for (int e = tid; e < kT * kC; e += 256) {
+  for (int e = tid; e < kT * kC; e += 512) {
     const int tp = e / kC, c = e % kC;
     const int m = (tp / kK) * 8 + tp % kK;
     slab[e] = red[m * kC + c];
@@ -499,6 +514,8 @@ size_t thin1_wgrad_x3_ws_bytes() { return (size_t)cu_count() * kT * kC * sizeof(
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
                         int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
   Thin1RWArgs a{};
+  static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
+  a.stamp = stamps;
   int flip;
   if (Cg == 1) {          // stem: P = D (32 ch), Q = G
     a.P = D; a.Dp = Dd; a.Hp = Hd; a.Wp = Wd;
@@ -534,7 +551,7 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(512), lds, st, a);
     rc = check_launch("thin1_wgrad_x3");
     break;
   })

@@ -18,10 +18,16 @@ from mragan_hip._lib import lib  # noqa: E402
 
 ops.set_conv_precision("bf16x3")
 S, N, ngf = 64, int(sys.argv[1]) if len(sys.argv) > 1 else 2, 32
+which = sys.argv[2] if len(sys.argv) > 2 else "fwd"
 x = torch.randn(N, S + 6, S + 6, S + 6, 1, device="cuda")
 w = torch.randn(343 * ngf, device="cuda") * 0.01
+dh = torch.randn(N, S, S, S, ngf, device="cuda")
+gw = torch.empty(343 * ngf, device="cuda")
 for _ in range(3):
-    ops.conv3d(x, w, ngf, 7, 1, 0, (S, S, S))
+    if which == "fwd":
+        ops.conv3d(x, w, ngf, 7, 1, 0, (S, S, S))
+    else:            # the stem weight gradient
+        ops.conv3d_wgrad(dh, x, 7, 1, 0, gw, False)
 torch.cuda.synchronize()
 nitems = 4096
 buf = (C.c_ulonglong * (nitems * 3))()
