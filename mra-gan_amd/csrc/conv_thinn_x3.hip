@@ -15,7 +15,7 @@
 // over K = (input plane kd' = 0..7, kh, c); then z[2q + j][oh][ow] = Σ_kw P[ow + kw][j, kw]
 // (an LDS epilogue).  Useful fraction 7/8 (kd' vs kd) × 7/8 (kw) × 64/80 (w halo).
 //
-// Block = 2 output depths × 8 output rows (two per wave) × 74 output columns (the 80 w' rows
+// Block = 2 output depths × 8 output rows (one per wave, 8 waves) × 74 output columns (the 80 w' rows
 // less the 6-column halo: one column block covers both 64- and 70-wide outputs).  The input is
 // streamed in 16 units (plane kd' × 16-channel half): each unit's 14 × 80 positions × 16
 // channels are staged split into bf16 hi/lo (64-B swizzled LDS records), double-buffered with
@@ -46,7 +46,8 @@ constexpr int kRec = 64;                // LDS bytes per position: 4 16-B chunks
 constexpr int kUnits = 16;              // 8 planes × 2 channel halves
 constexpr int kUnitBytes = kRH * kMW * kRec;
 constexpr int kNF4 = kRH * kMW * 4;     // float4 per unit (16 channels)
-constexpr int kF4PT = (kNF4 + 255) / 256;
+constexpr int kThreads = 512;            // 8 waves, one output row each (2 per SIMD)
+constexpr int kF4PT = (kNF4 + kThreads - 1) / kThreads;
 
 // weight fragment table: [kd' 8][half 2][step 4][hi|lo][lane 64][8 bf16]
 //   lane = 16g + n: column n = 8j + kw, k-group g → kh = 2·step + (g >> 1), channels
@@ -91,7 +92,7 @@ struct ThinnArgs {
 __device__ __forceinline__ int thinn_rot(int pos) { return (pos ^ (pos >> 2)) & 2; }
 
 template <int PM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 thinn_x3_kernel(ThinnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][kUnitBytes]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -102,51 +103,46 @@ thinn_x3_kernel(ThinnArgs a) {
   const int q = blk % a.nq;
   const int nb = blk / a.nq;
   const int od0 = 2 * q, oh0 = r * kBH, ow0 = cw * kOW;
-  const float* xb = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * kC;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * kC, (uint32_t)a.Di * a.Hi * a.Wi * kC * 4u);
 
   // staging of one unit (plane kd', channel half) into registers / LDS
   // per-thread element offsets inside an input plane (−1: outside the input), fixed per block
   int poff[kF4PT];
 #pragma unroll
   for (int l = 0; l < kF4PT; ++l) {
-    const int e = l * 256 + tid;
+    const int e = l * kThreads + tid;
     const int pos = e >> 2, cq = e & 3;
     const int h = oh0 - a.pe + pos / kMW, w = ow0 - a.pe + pos % kMW;
     const bool ok = e < kNF4 && (unsigned)h < (unsigned)a.Hi && (unsigned)w < (unsigned)a.Wi;
     poff[l] = ok ? (h * a.Wi + w) * kC + 4 * cq : -1;
   }
-  const int64_t plane = (int64_t)a.Hi * a.Wi * kC;
+  const uint32_t plane = (uint32_t)a.Hi * a.Wi * kC;
   auto stage_load = [&](int u, float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
     const int d = od0 + (u >> 1) - a.pe, half = u & 1;     // callers pass valid units only
-    const float* src = xb + d * plane + 16 * half;
+    const uint32_t base = (uint32_t)d * plane + 16u * half;
 #pragma unroll
-    for (int l = 0; l < kF4PT; ++l) {
-      const float4 t = *reinterpret_cast<const float4*>(src + (poff[l] < 0 ? 0 : poff[l]));
-      sv[l] = poff[l] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : t;
-    }
+    for (int l = 0; l < kF4PT; ++l) sv[l] = buf_load_f32x4(xr, poff[l] < 0 ? kOobOffset : (base + poff[l]) * 4u);
   };
-  // element l of this thread sits at position 64l + tid/4 (channels 4(tid&3)…): its chunk
-  // rotation depends on tid only, so every store is base + 4096·l
+  // element l of this thread sits at position 128l + tid/4 (channels 4(tid&3)…): its chunk
+  // rotation depends on tid only, so every store is base + 8192·l
   const int cq = tid & 3, srot = thinn_rot(tid >> 2);
   const int st_hi = (tid >> 2) * kRec + 16 * ((cq >> 1) ^ srot) + 8 * (cq & 1);
   const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1)) ^ srot) + 8 * (cq & 1);
   auto stage_store = [&](char* buf, const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < kF4PT; ++l) {
-      if (l * 256 + tid < kNF4) {
+      if (l * kThreads + tid < kNF4) {
         uint2 h, lo;
         prec::split4<PM>(sv[l], h, lo);
-        *reinterpret_cast<uint2*>(buf + l * 64 * kRec + st_hi) = h;
-        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + l * 64 * kRec + st_lo) = lo;
+        *reinterpret_cast<uint2*>(buf + l * (kThreads / 4) * kRec + st_hi) = h;
+        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + l * (kThreads / 4) * kRec + st_lo) = lo;
       }
     }
   };
 
-  f32x4 acc[2][5];
+  f32x4 acc[5];
 #pragma unroll
-  for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-    for (int i = 0; i < 5; ++i) acc[rr][i] = f32x4{};
+  for (int i = 0; i < 5; ++i) acc[i] = f32x4{};
   const int n16 = lane & 15, g = lane >> 4;
   const int a_hi = 16 * ((g & 1) ^ thinn_rot(n16)), a_lo = 16 * ((2 + (g & 1)) ^ thinn_rot(n16));
   const __bf16* wx = a.wx;
@@ -174,19 +170,17 @@ thinn_x3_kernel(ThinnArgs a) {
       const bf16x8 bh = w[s][0], bl = w[s][1];
       int kh = 2 * s + (g >> 1);
       kh = kh < kK ? kh : kK - 1;           // the padding kh = 7 has zero weights
-      // position (2wave + rr + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
+      // position (wave + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
       // positions, so the chunk rotation is the lane's own (of n16) — addresses fold to
       // lane base + immediate
-      const char* rowp = buf + ((2 * wave + kh) * kMW + n16) * kRec;
+      const char* rowp = buf + ((wave + kh) * kMW + n16) * kRec;
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int mt = 0; mt < 5; ++mt) {
-          const int cofs = (rr * kMW + mt * 16) * kRec;
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_hi);
-          const bf16x8 al = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo) : ah;
-          acc[rr][mt] = prec::mma16<PM>(ah, al, bh, bl, acc[rr][mt]);
-        }
+      for (int mt = 0; mt < 5; ++mt) {
+        const int cofs = (mt * 16) * kRec;
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_hi);
+        const bf16x8 al = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo) : ah;
+        acc[mt] = prec::mma16<PM>(ah, al, bh, bl, acc[mt]);
+      }
       __builtin_amdgcn_sched_barrier(0);    // one step per scheduling region (register budget)
     }
   };
@@ -216,17 +210,16 @@ thinn_x3_kernel(ThinnArgs a) {
     __syncthreads();
   }
 
-  // epilogue: P[w'][n] (n = 8j + kw) of each of the wave's two rows through its LDS slot, then
+  // epilogue: P[w'][n] (n = 8j + kw) of the wave's row through its LDS slot, then
   // z[od0 + j][oh][ow] = Σ_kw P[ow − ow0 + kw][8j + kw]
   float* P = reinterpret_cast<float*>(smem) + wave * kMW * 17;   // [80][16] padded to 17
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
+  {
 #pragma unroll
     for (int mt = 0; mt < 5; ++mt)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) P[(mt * 16 + g * 4 + e) * 17 + n16] = acc[rr][mt][e];
+      for (int e = 0; e < 4; ++e) P[(mt * 16 + g * 4 + e) * 17 + n16] = acc[mt][e];
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    const int oh = oh0 + 2 * wave + rr;
+    const int oh = oh0 + wave;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int o = k * 64 + lane;               // 148 outputs: j = o / 74, ow = o % 74
@@ -266,6 +259,7 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   a.nq = ceil_div(t.Do, 2); a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
   const int64_t blocks = (int64_t)a.N * a.nq * a.nr * a.nw;
   if (blocks == 0) return kOk;
+  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * kC * 4 < (int64_t)kOobOffset, "thinn_x3: input volume too large");
   a.total = (int)blocks;
   a.per = (int)ceil_div(blocks, 8);
   const size_t lds = (size_t)2 * kUnitBytes;
@@ -275,7 +269,7 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)(8 * a.per)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)(8 * a.per)), dim3(kThreads), lds, st, a);
   return check_launch("thinn_x3");
 }
 
