@@ -372,8 +372,10 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
     return kWorkspace;
   }
   static const bool no_w3 = getenv("MRAGAN_NO_WGRAD3") != nullptr;   // A/B switch
-  if (!no_w3 && wgrad3_x3_applicable(a)) {
-    const int used = conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st);
+  const bool w3 = !no_w3 && wgrad3_x3_applicable(a), w3s2 = !no_w3 && !w3 && wgrad3s2_x3_applicable(a);
+  if (w3 || w3s2) {
+    const int used = w3 ? conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st)
+                        : conv_wgrad3s2_x3(a, wgrad3s2_x3_splits(a, a.splits), st);
     int rc = check_launch("wgrad3_x3");
     if (rc) return rc;
     int64_t total = (int64_t)a.Cd * a.Cg * T;

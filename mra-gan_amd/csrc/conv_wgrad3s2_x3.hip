@@ -1,0 +1,289 @@
+// bf16x3 weight gradient of the stride-2 k3 p1 convolutions of the generator (gfx950):
+//
+//   G down convs   Conv3d(c → 2c, k3, s2, p1)                 networks3D.py:192-197
+//                  dW[co][ci][t] = Σ_m dY[m][co] · X[2m − 1 + t][ci]
+//   G up convs     ConvTranspose3d(2c → c, k3, s2, p1, op1)   networks3D.py:203-210
+//                  dW[ci][co][t] = Σ_i X[i][ci] · dY[2i − 1 + t][co]
+//
+// Both are  Out[dn][gn][t] = Σ_m D[m][dn] · G[2m − 1 + t][gn]  with D on the coarse grid and G
+// on the fine grid (2× per axis).  conv_wgrad_x3 runs one GEMM per tap and re-reads D and G for
+// each of the 27 taps (PMC: 4× the operands' bytes fetched from HBM, MFMA busy < 20 %).  Here, as
+// in conv_wgrad3_x3.hip, a block owns one (kd, kh) pair and all three kw taps, the contraction
+// runs over row segments (n, d, h, 16 coarse w) 8 per stage with K index k = w·8 + r, and one
+// staged G tile serves all three taps: along w the taps read the fine positions 2w − 1, 2w,
+// 2w + 1, so the G row is staged as its even phase E[j] = G[2(w0 + j)] (slots 0–15) and odd
+// phase O[j] = G[2(w0 + j) + 1], j = −1 … 15 (slots 16–32): tap kw = 1 reads E[w], kw = 0 reads
+// O[w − 1], kw = 2 reads O[w] — each a plain 16-B fragment read at a fixed slot offset.  The 33
+// staged fine positions of a segment are contiguous in memory (2w0 − 1 … 2w0 + 31).
+//
+// Tiles: 64 D-channels × TG G-channels.  TG = 64: 4 waves as 2 × 2 32×32 sub-tiles.  TG = 32
+// (the 32-channel side at full resolution): 4 waves as 2 sub-tiles × 2 K halves (even / odd
+// K-steps), the halves added in LDS before the slab store.  Split-K partial tiles go to slabs
+// ws[z][t][dn][gn], reduced in fixed order by wgrad_reduce_kernel (deterministic).
+#include "kernels.h"
+#include "prec.h"
+
+namespace mragan {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kTD = 64;                             // D channels per block
+constexpr int kR = 8;                               // row segments per stage
+constexpr int kSegW = 16;                           // coarse voxels per row segment
+constexpr int kGPos = 2 * kSegW + 1;                // 33 fine positions per segment
+constexpr int kDRow = 2 * kSegW * 16 + 16;          // 528 B: hi 16 slots, lo 16 slots, pad
+constexpr int kGRow = 2 * kGPos * 16 + 16;          // 1072 B: hi 33 slots, lo 33 slots, pad
+constexpr int kDHalf = kSegW * 16;
+constexpr int kGHalf = kGPos * 16;
+
+// fine position q (0 … 32) of a segment → its slot: odd positions (q even) are the O phase
+__device__ __forceinline__ int gslot(int q) { return (q & 1) ? (q - 1) >> 1 : 16 + (q >> 1); }
+
+// one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half
+template <int PM>
+__device__ __forceinline__ void split8_store(char* p, int half, float v0, float v1, float v2, float v3, float v4,
+                                             float v5, float v6, float v7) {
+  uint4 hi, lo;
+  prec::split2<PM>(v0, v1, hi.x, lo.x);
+  prec::split2<PM>(v2, v3, hi.y, lo.y);
+  prec::split2<PM>(v4, v5, hi.z, lo.z);
+  prec::split2<PM>(v6, v7, hi.w, lo.w);
+  *reinterpret_cast<uint4*>(p) = hi;
+  if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint4*>(p + half) = lo;
+}
+
+}  // namespace
+
+struct Wgrad3s2Args {
+  const float* d; int N, D, H, W, Cd;     // D [N][D][H][W][Cd] (coarse)
+  const float* g; int Cg;                 // G [N][2D][2H][2W][Cg] (fine)
+  float* ws;                              // slabs [splits][27][Cd][Cg]
+  int nseg, seg_per_split;
+};
+
+template <int TG, int PM>
+__global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ds = smem;
+  char* Gs = smem + kTD * kDRow;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  // TG = 64: wave → (dn half, gn half); TG = 32: wave → (dn half, K half)
+  const int wm0 = (wave >> 1) * 32;
+  const int wn0 = TG == 64 ? (wave & 1) * 32 : 0;
+  const int kpar = TG == 64 ? -1 : (wave & 1);
+
+  // logical block: (dn tile, gn tile) fastest, then (kd, kh), then split; XCD-aware remap
+  const int ndn = a.Cd / kTD, ngn = a.Cg / TG;
+  const int B = gridDim.x;
+  int L = blockIdx.x;
+  if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
+  const int tile = L % (ndn * ngn);
+  const int kk9 = (L / (ndn * ngn)) % 9;
+  const int z = L / (ndn * ngn * 9);
+  const int dn0 = (tile / ngn) * kTD, gn0 = (tile % ngn) * TG;
+  const int kd = kk9 / 3, kh = kk9 % 3;
+  const int seg_lo = z * a.seg_per_split;
+  if (seg_lo >= a.nseg) return;                    // grid padding (a multiple of 8 blocks)
+  const int seg_hi = min(a.nseg, seg_lo + a.seg_per_split);
+  const int nstage = (seg_hi - seg_lo + kR - 1) / kR;
+
+  const int Dg = 2 * a.D, Hg = 2 * a.H, Wg = 2 * a.W;
+  const int nsw = a.W / kSegW;
+  // staging units, channel quad fastest.  D: (w = tid >> 4, cq = tid & 15).
+  // G: TG / 4 channel quads × 33 positions: q = tid / (TG/4) (+ 256/(TG/4) for the second pass)
+  // and the last position(s) on the first threads (the others re-read their own unit).
+  constexpr int GQ = TG / 4;                       // channel quads of G
+  constexpr int GP = 256 / GQ;                     // positions per pass: 16 (TG 64) or 32 (TG 32)
+  constexpr int GPASS = kGPos / GP;                // full passes: 2 or 1
+  const int cq = tid & 15, uw = tid >> 4;
+  const int gcq = tid % GQ, gq = tid / GQ;
+  const int gqx = GPASS * GP + gq;                 // the remainder pass (q = 32 …)
+  const bool gx = gqx < kGPos;
+
+  float4 rd[kR], rg[2][kR], rgx[kR];
+  int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
+  auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
+    if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
+  };
+  auto load = [&](int st) __attribute__((always_inline)) {
+    int cw = sw, chh = sh, cdd = sd, cn = sn;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int seg = seg_lo + st * kR + r;
+      const bool ok = seg < seg_hi;
+      const int n = ok ? cn : 0, d = ok ? cdd : 0, h = ok ? chh : 0;
+      const int w0 = (ok ? cw : 0) * kSegW;
+      bump(cw, chh, cdd, cn);
+      const float4 dv = *reinterpret_cast<const float4*>(a.d + ((((n * a.D + d) * a.H + h) * a.W + w0 + uw) * a.Cd + dn0 + 4 * cq));
+      rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
+      const int gd = 2 * d - 1 + kd, gh = 2 * h - 1 + kh;
+      const bool rok = ok && (unsigned)gd < (unsigned)Dg && (unsigned)gh < (unsigned)Hg;
+      const int grow = ((n * Dg + (rok ? gd : 0)) * Hg + (rok ? gh : 0)) * Wg;
+      auto gload = [&](int q) __attribute__((always_inline)) {
+        const int p = 2 * w0 - 1 + q;
+        const bool pok = rok && (unsigned)p < (unsigned)Wg;
+        const float4 v = *reinterpret_cast<const float4*>(a.g + ((int64_t)(grow + (pok ? p : 0)) * a.Cg + gn0 + 4 * gcq));
+        return make_float4(pok ? v.x : 0.f, pok ? v.y : 0.f, pok ? v.z : 0.f, pok ? v.w : 0.f);
+      };
+#pragma unroll
+      for (int pass = 0; pass < GPASS; ++pass) rg[pass][r] = gload(pass * GP + gq);
+      rgx[r] = gload(gx ? gqx : gq);
+    }
+  };
+  // one unit: 8 segments × 4 channels → 4 rows × (16 B hi + 16 B lo) at `slot`; write j of a
+  // lane goes to channel (j + rot) & 3, rot = (c >> 1) & 3 (conflict-free 8-lane write groups for
+  // both row strides: 33 and 67 16-B units per row)
+  auto put = [&](char* base, int row_bytes, int half, int slot, int c, const float4 (&v)[kR]) __attribute__((always_inline)) {
+    const int rot = (c >> 1) & 3;
+    auto rotv = [&](const float4& x) __attribute__((always_inline)) {
+      const float4 t = (rot & 1) ? make_float4(x.y, x.z, x.w, x.x) : x;
+      return (rot & 2) ? make_float4(t.z, t.w, t.x, t.y) : t;
+    };
+    float4 u[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) u[r] = rotv(v[r]);
+    char* p = base + (4 * c) * row_bytes + slot * 16;
+    split8_store<PM>(p + ((0 + rot) & 3) * row_bytes, half, u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x);
+    split8_store<PM>(p + ((1 + rot) & 3) * row_bytes, half, u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y);
+    split8_store<PM>(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
+    split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+    put(Ds, kDRow, kDHalf, uw, cq, rd);
+#pragma unroll
+    for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot(pass * GP + gq), gcq, rg[pass]);
+    if (gx) put(Gs, kGRow, kGHalf, gslot(gqx), gcq, rgx);
+  };
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
+
+  if (nstage > 0) load(0);
+  for (int st = 0; st < nstage; ++st) {
+    store();
+    __syncthreads();
+    if (st + 1 < nstage) {                          // lands during this stage's MFMAs
+#pragma unroll
+      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
+      load(st + 1);
+    }
+    const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
+    const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+#pragma unroll
+    for (int ks = 0; ks < kSegW / 2; ++ks) {
+      if (TG == 32 && (ks & 1) != kpar) continue;   // K half of this wave
+      // K-step ks: coarse w = 2ks + lh (folded into arow / brow) × 8 segments
+      bf16x8 fa[2], fb[3][2];
+      fa[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
+      fa[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : fa[0];
+      // tap kw: kw = 1 → E[w] (slot w), kw = 0 → O[w − 1] (slot 16 + w), kw = 2 → O[w] (slot 17 + w)
+      constexpr int koff[3] = {16 * 16, 0, 17 * 16};
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        fb[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw]);
+        fb[kw][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw] + kGHalf) : fb[kw][0];
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) acc[kw] = prec::mma<PM>(fa[0], fa[1], fb[kw][0], fb[kw][1], acc[kw]);
+    }
+    __syncthreads();
+  }
+
+  // TG = 32: the odd-K waves' partial sums join the even-K waves' through LDS (fixed order)
+  if constexpr (TG == 32) {
+    float* red = reinterpret_cast<float*>(smem);    // [2 dn halves][3 taps][16][64 lanes]
+    if (kpar == 1) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(((wave >> 1) * 3 + kw) * 16 + r) * 64 + lane] = acc[kw][r];
+    }
+    __syncthreads();
+    if (kpar == 1) return;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[kw][r] += red[(((wave >> 1) * 3 + kw) * 16 + r) * 64 + lane];
+  }
+
+  // slab[z][t][dn][gn]: lane li = gn column, register r = dn row (r & 3) + 8 (r >> 2) + 4 lh
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    const int t = (kd * 3 + kh) * 3 + kw;
+    float* slab = a.ws + ((int64_t)z * 27 + t) * a.Cd * a.Cg;
+    const int col = gn0 + wn0 + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = dn0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      slab[(int64_t)row * a.Cg + col] = acc[kw][r];
+    }
+  }
+}
+
+bool wgrad3s2_x3_applicable(const WgradArgs& a) {
+  return a.x3 && a.k == 3 && a.s == 2 && a.p == 1 && a.Wd % kSegW == 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
+         a.Wg == 2 * a.Wd && a.Cd % kTD == 0 && (a.Cg % 64 == 0 || a.Cg == 32) &&
+         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31) &&
+         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd < ((int64_t)1 << 31);
+}
+
+static int s2_tg(const WgradArgs& a) { return a.Cg % 64 == 0 ? 64 : 32; }
+
+static size_t s2_lds(int tg) { return (size_t)kTD * kDRow + (size_t)tg * kGRow; }
+
+// splits: one round of resident blocks (1 per CU at TG 64, 2 at TG 32), ≥ 4 stages per block;
+// never more than the generic plan's (its workspace query sizes the slabs)
+int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
+  const int tg = s2_tg(a);
+  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
+  const int tiles = (a.Cd / kTD) * (a.Cg / tg) * 9;
+  int s = (tg == 64 ? 256 : 512) / tiles;
+  const int by_len = nseg / (4 * kR);
+  if (s > by_len) s = by_len;
+  if (s > max_splits) s = max_splits;
+  if (s < 1) s = 1;
+  return s;
+}
+
+int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
+  Wgrad3s2Args a{};
+  a.d = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
+  a.g = g.G; a.Cg = g.Cg;
+  a.ws = g.ws;
+  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / kSegW);
+  int per = (a.nseg + splits - 1) / splits;
+  per = (per + kR - 1) / kR * kR;
+  a.seg_per_split = per;
+  const int nsplit = (a.nseg + per - 1) / per;
+  const int tg = s2_tg(g);
+  const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
+  const size_t lds = s2_lds(tg);
+  static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
+  MRAGAN_PREC_DISPATCH(g.x3, {
+    if (tg == 64) {
+      static bool attr64 = false;
+      if (!attr64) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<64, PM>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr64 = true;
+      }
+      hipLaunchKernelGGL((wgrad3s2_x3_kernel<64, PM>), dim3(blocks), dim3(256), lds, st, a);
+    } else {
+      static bool attr32 = false;
+      if (!attr32) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<32, PM>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr32 = true;
+      }
+      hipLaunchKernelGGL((wgrad3s2_x3_kernel<32, PM>), dim3(blocks), dim3(256), lds, st, a);
+    }
+    return nsplit;
+  })
+}
+
+}  // namespace mragan

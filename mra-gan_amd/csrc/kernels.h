@@ -86,6 +86,10 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
 bool wgrad3_x3_applicable(const WgradArgs& a);
 int wgrad3_x3_splits(const WgradArgs& a, int max_splits);
 int conv_wgrad3_x3(const WgradArgs& a, int splits, hipStream_t st);   // returns the splits used
+// bf16x3 weight gradient of the k3 s2 p1 convs / transposed convs, 3 kw taps per block (conv_wgrad3s2_x3.hip)
+bool wgrad3s2_x3_applicable(const WgradArgs& a);
+int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits);
+int conv_wgrad3s2_x3(const WgradArgs& a, int splits, hipStream_t st);   // returns the splits used
 size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k);
 
 struct ThinWgradArgs {

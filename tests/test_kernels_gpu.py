@@ -231,6 +231,35 @@ def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
     assert rel(dw, 2 * dw_ref) < xtol()
 
 
+@pytest.mark.parametrize("N,cin,cout,dims", [(1, 32, 64, (8, 10, 32)), (2, 64, 128, (6, 4, 64)), (1, 32, 128, (4, 2, 32)),
+                                             (3, 64, 64, (2, 6, 32))])
+def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
+    """Weight gradients of the k3 s2 p1 down convs (networks3D.py:192-197) and of the transposed
+    up convs (op 1, networks3D.py:203-210) on the 3-kw-tap even/odd-phase kernel
+    (conv_wgrad3s2_x3.hip: even fine grid, coarse w a multiple of 16; 32- and 64-channel G tiles,
+    several split-K slabs and D tiles), vs fp64."""
+    ops = x3
+    g = torch.Generator().manual_seed(17 + N + cin + cout)
+    x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
+    w = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    y = F.conv3d(x, w, stride=2, padding=1)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw = torch.full((cout, cin, 3, 3, 3), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 2, 1, dw, accumulate=False)
+    assert rel(dw, dw_ref) < xtol()
+    # transposed: ConvTranspose3d(cout → cin) on the coarse grid of y, output padding 1
+    xt = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    wt = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    yt = F.conv_transpose3d(xt, wt, stride=2, padding=1, output_padding=1)
+    assert tuple(yt.shape[2:]) == tuple(dims)
+    dyt = torch.randn(yt.shape, generator=g, dtype=torch.float64)
+    (dwt_ref,) = torch.autograd.grad(yt, wt, dyt)
+    dwt = torch.zeros((cout, cin, 3, 3, 3), device="cuda")
+    ops.conv3d_wgrad(ndhwc(xt.float()).cuda(), ndhwc(dyt.float()).cuda(), 3, 2, 1, dwt, accumulate=False)
+    assert rel(dwt, dwt_ref) < xtol()
+
+
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
 def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
     ops = x3

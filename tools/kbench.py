@@ -57,7 +57,14 @@ def main():
     w_dn1 = rnd(27 * ngf * 2 * ngf) * 0.01
     x_dl = rnd(N, S // 8 - 1, S // 8 - 1, S // 8 - 1, 512)   # PatchGAN last layer input (ndf 64)
     w_dl = rnd(64 * 512) * 0.01
+    dy_dn1 = rnd(N, s2, s2, s2, 2 * ngf)
+    gw_dn1 = torch.empty(27 * ngf * 2 * ngf, device=dev)
+    x_dn2 = rnd(N, s2, s2, s2, 2 * ngf)
+    dy_dn2 = rnd(N, s4, s4, s4, c4)
+    gw_dn2 = torch.empty(27 * 2 * ngf * c4, device=dev)
     table = {
+        "down1_wgrad": lambda: ops.conv3d_wgrad(dy_dn1, x_dn1, 3, 2, 1, gw_dn1, False),
+        "down2_wgrad": lambda: ops.conv3d_wgrad(dy_dn2, x_dn2, 3, 2, 1, gw_dn2, False),
         "dlast_fwd": lambda: ops.conv3d(x_dl, w_dl, 1, 4, 1, 1, (S // 8 - 2,) * 3),
         "up2_fwd": lambda: ops.conv3d(x_up2, w_up2, ngf, 3, 2, 1, (S, S, S), transposed=True),
         "down1_fwd": lambda: ops.conv3d(x_dn1, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2)),
