@@ -145,7 +145,12 @@ conv_brick_x3_kernel(BrickArgs a) {
   for (int j = 0; j < TN; ++j) boff[j] = (n0 + wn0 + j * 32 + li) * 16 + lh * 8;
   const int nch_ = a.C / kBK;
   const int64_t blk = (int64_t)a.ny * 16;       // one (hi|lo) block
-  const float* xb = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C;
+  // halo loads through the instance's range-checked descriptor: an out-of-volume position gets
+  // an offset past the end and reads 0, with no select on the loaded value (a conditional
+  // overwrite made hipcc drain the memory counter — the 9-step weight prefetch included — at
+  // every halo load)
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C,
+                                              (uint32_t)a.Di * a.Hi * a.Wi * a.C * 4u);
   const int nchunks = a.C / kBK;
   __syncthreads();
 
@@ -156,8 +161,7 @@ conv_brick_x3_kernel(BrickArgs a) {
     for (int sl = 0; sl < NSL; ++sl) {
       const int e = sl * NT + tid, pos = e >> 3;
       const int o = pos < HP ? hoff[pos] : -1;
-      pv[sl] = *reinterpret_cast<const float4*>(xb + (o < 0 ? 0 : o) + 4 * (e & 7));
-      if (o < 0) pv[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pv[sl] = buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + 4 * (e & 7)) * 4u);
     }
 #pragma unroll
     for (int sl = 0; sl < NSL; ++sl) {
@@ -215,9 +219,8 @@ conv_brick_x3_kernel(BrickArgs a) {
       if (du % 3 == 0 && u / 3 < NSL) {
         const int e = (u / 3) * NT + tid, hpos = e >> 3;
         const int o = (stream && hpos < HP) ? hoff[hpos] : -1;
-        float4& r = rh[(du / 3) % 3];
-        r = *reinterpret_cast<const float4*>(xb + (o < 0 ? 0 : o) + (c + 1 < nchunks ? c + 1 : c) * kBK + 4 * (e & 7));
-        if (o < 0) r = make_float4(0.f, 0.f, 0.f, 0.f);
+        rh[(du / 3) % 3] = buf_load_f32x4(
+            xr, o < 0 ? kOobOffset : (uint32_t)(o + (c + 1 < nchunks ? c + 1 : c) * kBK + 4 * (e & 7)) * 4u);
       }
       // … and split + stored kHD steps later
       if ((du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
