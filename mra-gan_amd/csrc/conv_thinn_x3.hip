@@ -15,14 +15,17 @@
 // over K = (input plane kd' = 0..7, kh, c); then z[2q + j][oh][ow] = Σ_kw P[ow + kw][j, kw]
 // (an LDS epilogue).  Useful fraction 7/8 (kd' vs kd) × 7/8 (kw) × 64/80 (w halo).
 //
-// Block = 2 output depths × 8 output rows (one per wave, 8 waves) × 74 output columns (the 80 w' rows
-// less the 6-column halo: one column block covers both 64- and 70-wide outputs).  The input is
-// streamed in 16 units (plane kd' × 16-channel half): each unit's 14 × 80 positions × 16
-// channels are staged split into bf16 hi/lo (64-B swizzled LDS records), double-buffered with
-// one barrier per unit and register-prefetched two units ahead; the weights come pre-split in
-// fragment order from L2 (thinn_x3_pack).  Blocks are dealt to the 8 XCDs in contiguous
-// ranges of the (column, row, depth pair) order, so the blocks resident on one XCD at a time
-// are neighbours in depth and re-read their shared input planes from that XCD's L2.
+// Block = a depth segment of P output-depth pairs × 8 output rows (one per wave, 8 waves) × 74
+// output columns (the 80 w' rows less the 6-column halo: one column block covers both 64- and
+// 70-wide outputs).  The block streams its 2P + 6 input planes once, in units (plane × 16-channel
+// half): each unit's 14 × 80 positions × 16 channels are staged split into bf16 hi/lo (64-B
+// swizzled LDS records) and feed every output pair whose 8-plane window contains it — up to 4
+// at a time, their accumulators held in a 4-slot ring (slot = pair mod 4), so each staged plane
+// is used by 4 pairs instead of being re-staged for each (round 1: 16 units per pair, 4× the
+// input through L2).  A fragments are read once per (step, M-tile) and reused across the active
+// pairs; the weights come pre-split in fragment order from L1/L2 (thinn_x3_pack).  A pair's
+// sums leave through the wave's own LDS scratch (the kw reduction) as soon as its last plane is
+// in.  Blocks are dealt to the 8 XCDs in contiguous ranges of the (column, row, segment) order.
 #include "kernels.h"
 #include "prec.h"
 
@@ -39,11 +42,10 @@ constexpr int kK = 7;
 constexpr int kC = 32;                  // input channels
 constexpr int kOW = 74;                 // output columns per block (kMW − 6)
 constexpr int kMW = 80;                 // w' rows: 64 + 6 halo, 5 M-tiles of 16
-constexpr int kBH = 8;                  // output rows per block (two per wave)
+constexpr int kBH = 8;                  // output rows per block (one per wave)
 constexpr int kRH = kBH + kK - 1;       // staged rows per plane
 constexpr int kRec = 64;                // LDS bytes per position: 4 16-B chunks (hi 0-7, hi 8-15,
                                         // lo 0-7, lo 8-15); chunk L sits at slot L ^ rot(pos)
-constexpr int kUnits = 16;              // 8 planes × 2 channel halves
 constexpr int kUnitBytes = kRH * kMW * kRec;
 constexpr int kNF4 = kRH * kMW * 4;     // float4 per unit (16 channels)
 constexpr int kThreads = 512;            // 8 waves, one output row each (2 per SIMD)
@@ -81,7 +83,7 @@ struct ThinnArgs {
   const float* bias;
   float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo]
   int pe, act;
-  int nq, nr, nw;                         // depth pairs, row blocks, column blocks
+  int P, nseg, nr, nw;                    // pairs per segment, segments, row blocks, column blocks
   int total, per;                         // blocks, blocks per XCD range
 };
 
@@ -91,22 +93,28 @@ struct ThinnArgs {
 // channel quads) both land on distinct banks.
 __device__ __forceinline__ int thinn_rot(int pos) { return (pos ^ (pos >> 2)) & 2; }
 
+constexpr int kScratch = kMW * 17;      // floats of a wave's epilogue scratch ([80][16] padded)
+
 template <int PM>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 thinn_x3_kernel(ThinnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];   // [2][kUnitBytes]
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // [kUnitBytes] | [8][kScratch]
+  char* buf = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* Pw = reinterpret_cast<float*>(smem + kUnitBytes) + wave * kScratch;
   int blk = (blockIdx.x & 7) * a.per + (blockIdx.x >> 3);   // XCD-contiguous logical block
   if (blk >= a.total) return;
   const int cw = blk % a.nw; blk /= a.nw;
   const int r = blk % a.nr; blk /= a.nr;
-  const int q = blk % a.nq;
-  const int nb = blk / a.nq;
-  const int od0 = 2 * q, oh0 = r * kBH, ow0 = cw * kOW;
+  const int seg = blk % a.nseg;
+  const int nb = blk / a.nseg;
+  const int od0 = 2 * a.P * seg, oh0 = r * kBH, ow0 = cw * kOW;
+  const int npairs = min(a.P, (a.Do - od0 + 1) / 2);
+  const int nunits = 2 * (2 * npairs + kK - 1);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * kC, (uint32_t)a.Di * a.Hi * a.Wi * kC * 4u);
 
-  // staging of one unit (plane kd', channel half) into registers / LDS
-  // per-thread element offsets inside an input plane (−1: outside the input), fixed per block
+  // staging of one unit (plane, channel half) into registers / LDS; per-thread element offsets
+  // inside an input plane (−1: outside the input), fixed per block
   int poff[kF4PT];
 #pragma unroll
   for (int l = 0; l < kF4PT; ++l) {
@@ -118,17 +126,19 @@ thinn_x3_kernel(ThinnArgs a) {
   }
   const uint32_t plane = (uint32_t)a.Hi * a.Wi * kC;
   auto stage_load = [&](int u, float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
-    const int d = od0 + (u >> 1) - a.pe, half = u & 1;     // callers pass valid units only
-    const uint32_t base = (uint32_t)d * plane + 16u * half;
+    const int d = od0 + (u >> 1) - a.pe, half = u & 1;
+    const bool dok = (unsigned)d < (unsigned)a.Di;          // planes outside the input read 0
+    const uint32_t base = (uint32_t)(dok ? d : 0) * plane + 16u * half;
 #pragma unroll
-    for (int l = 0; l < kF4PT; ++l) sv[l] = buf_load_f32x4(xr, poff[l] < 0 ? kOobOffset : (base + poff[l]) * 4u);
+    for (int l = 0; l < kF4PT; ++l)
+      sv[l] = buf_load_f32x4(xr, (!dok || poff[l] < 0) ? kOobOffset : (base + poff[l]) * 4u);
   };
   // element l of this thread sits at position 128l + tid/4 (channels 4(tid&3)…): its chunk
   // rotation depends on tid only, so every store is base + 8192·l
   const int cq = tid & 3, srot = thinn_rot(tid >> 2);
   const int st_hi = (tid >> 2) * kRec + 16 * ((cq >> 1) ^ srot) + 8 * (cq & 1);
   const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1)) ^ srot) + 8 * (cq & 1);
-  auto stage_store = [&](char* buf, const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
+  auto stage_store = [&](const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < kF4PT; ++l) {
       if (l * kThreads + tid < kNF4) {
@@ -140,99 +150,96 @@ thinn_x3_kernel(ThinnArgs a) {
     }
   };
 
-  f32x4 acc[5];
+  f32x4 acc[4][5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) acc[i] = f32x4{};
+  for (int sl = 0; sl < 4; ++sl)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[sl][i] = f32x4{};
   const int n16 = lane & 15, g = lane >> 4;
   const int a_hi = 16 * ((g & 1) ^ thinn_rot(n16)), a_lo = 16 * ((2 + (g & 1)) ^ thinn_rot(n16));
   const __bf16* wx = a.wx;
+  const float bias = a.bias ? a.bias[0] : 0.f;
+  const int oh = oh0 + wave;
 
-  // valid units (input plane inside the input) form a contiguous range [u0, u1)
-  int u0 = 0, u1 = kUnits;
-  while (u0 < kUnits && (od0 + (u0 >> 1) - a.pe) < 0) ++u0;
-  while (u1 > u0 && (od0 + ((u1 - 1) >> 1) - a.pe) >= a.Di) --u1;
-
-  // the unit's weight fragments [step][hi|lo], issued at the top of the unit's iteration BEFORE
-  // that iteration's staging loads: the memory counter retires in order, so weights fetched
-  // after a staging batch would make the MFMAs wait for the whole batch
-  auto w_load = [&](int u, bf16x8 (&w)[4][2]) __attribute__((always_inline)) {
-    const int kdp = u >> 1, half = u & 1;
-    const __bf16* wt = wx + ((int64_t)(kdp * 2 + half) * 4) * 2 * 64 * 8;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      w[s][0] = *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 0) * 64 * 8 + lane * 8);
-      w[s][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + (s * 2 + 1) * 64 * 8 + lane * 8) : w[s][0];
-    }
-  };
-  auto compute = [&](const char* buf, const bf16x8 (&w)[4][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 bh = w[s][0], bl = w[s][1];
-      int kh = 2 * s + (g >> 1);
-      kh = kh < kK ? kh : kK - 1;           // the padding kh = 7 has zero weights
-      // position (wave + kh)·80 + 16mt + n16: the wave/step part is a multiple of 16
-      // positions, so the chunk rotation is the lane's own (of n16) — addresses fold to
-      // lane base + immediate
-      const char* rowp = buf + ((wave + kh) * kMW + n16) * kRec;
-#pragma unroll
-      for (int mt = 0; mt < 5; ++mt) {
-        const int cofs = (mt * 16) * kRec;
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(rowp + cofs + a_hi);
-        const bf16x8 al = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + cofs + a_lo) : ah;
-        acc[mt] = prec::mma16<PM>(ah, al, bh, bl, acc[mt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);    // one step per scheduling region (register budget)
-    }
-  };
-
-  // pipeline: LDS buffer (u & 1) holds unit u; register set A/B holds the unit after it
-  float4 sA[kF4PT], sB[kF4PT];
-  bf16x8 w[4][2];
-  if (u0 < u1) {
-    stage_load(u0, sA);
-    stage_store(smem + (u0 & 1) * kUnitBytes, sA);
-    if (u0 + 1 < u1) stage_load(u0 + 1, sA);
-  }
-  __syncthreads();
-  for (int u = u0; u < u1; u += 2) {
-    // unit u (registers: sA = u + 1); prefetch u + 2 into sB
-    w_load(u, w);
-    if (u + 2 < u1) stage_load(u + 2, sB);
-    compute(smem + (u & 1) * kUnitBytes, w);
-    if (u + 1 < u1) stage_store(smem + ((u + 1) & 1) * kUnitBytes, sA);
-    __syncthreads();
-    if (u + 1 >= u1) break;
-    // unit u + 1 (registers: sB = u + 2); prefetch u + 3 into sA
-    w_load(u + 1, w);
-    if (u + 3 < u1) stage_load(u + 3, sA);
-    compute(smem + ((u + 1) & 1) * kUnitBytes, w);
-    if (u + 2 < u1) stage_store(smem + (u & 1) * kUnitBytes, sB);
-    __syncthreads();
-  }
-
-  // epilogue: P[w'][n] (n = 8j + kw) of the wave's row through its LDS slot, then
-  // z[od0 + j][oh][ow] = Σ_kw P[ow − ow0 + kw][8j + kw]
-  float* P = reinterpret_cast<float*>(smem) + wave * kMW * 17;   // [80][16] padded to 17
-  {
+  // pair j's sums → z[od0 + 2j + jj][oh][ow] = Σ_kw P[ow − ow0 + kw][8jj + kw] through the wave's
+  // own scratch (no other wave touches it: no barrier)
+  auto epilogue = [&](int j, const f32x4 (&c)[5]) __attribute__((always_inline)) {
 #pragma unroll
     for (int mt = 0; mt < 5; ++mt)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) P[(mt * 16 + g * 4 + e) * 17 + n16] = acc[mt][e];
+      for (int e = 0; e < 4; ++e) Pw[(mt * 16 + g * 4 + e) * 17 + n16] = c[mt][e];
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    const int oh = oh0 + wave;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int o = k * 64 + lane;               // 148 outputs: j = o / 74, ow = o % 74
+      const int o = k * 64 + lane;               // 148 outputs: jj = o / 74, ow = o % 74
       if (o >= 2 * kOW) break;
-      const int j = o / kOW, owl = o - j * kOW;
+      const int jj = o / kOW, owl = o - jj * kOW;
       float sum = 0.f;
 #pragma unroll
-      for (int kw = 0; kw < kK; ++kw) sum += P[(owl + kw) * 17 + 8 * j + kw];
-      const int od = od0 + j, ow = ow0 + owl;
+      for (int kw = 0; kw < kK; ++kw) sum += Pw[(owl + kw) * 17 + 8 * jj + kw];
+      const int od = od0 + 2 * j + jj, ow = ow0 + owl;
       if (od < a.Do && oh < a.Ho && ow < a.Wo)
-        a.y[(((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow] = act_fwd(sum + (a.bias ? a.bias[0] : 0.f), a.act);
+        a.y[(((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow] = act_fwd(sum + bias, a.act);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
+  };
+
+  float4 sv[kF4PT];
+  stage_load(0, sv);
+  for (int u = 0; u < nunits; ++u) {
+    __syncthreads();                            // every wave is done with the previous unit
+    stage_store(sv);
+    __syncthreads();
+    if (u + 1 < nunits) stage_load(u + 1, sv);  // in flight during this unit's MFMAs
+    const int kk = u >> 1, half = u & 1;
+    // active pairs: 2j ≤ kk ≤ 2j + 7 → j ∈ [jlo, jhi], at most 4, slot = j mod 4
+    const int jlo = kk >= kK ? (kk - 6) >> 1 : 0;
+    const int jhi = min(npairs - 1, kk >> 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 bh[4], bl[4];
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int j = jlo + ((sl - jlo) & 3);
+        const int kdp = j <= jhi ? kk - 2 * j : 0;
+        const __bf16* wt = wx + ((int64_t)((kdp * 2 + half) * 4 + s) * 2) * 64 * 8 + lane * 8;
+        bh[sl] = *reinterpret_cast<const bf16x8*>(wt);
+        bl[sl] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + 64 * 8) : bh[sl];
+      }
+      int kh = 2 * s + (g >> 1);
+      kh = kh < kK ? kh : kK - 1;               // the padding kh = 7 has zero weights
+      const char* rowp = buf + ((wave + kh) * kMW + n16) * kRec;
+      bf16x8 ah[5], al[5];
+#pragma unroll
+      for (int mt = 0; mt < 5; ++mt) {
+        ah[mt] = *reinterpret_cast<const bf16x8*>(rowp + mt * 16 * kRec + a_hi);
+        al[mt] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(rowp + mt * 16 * kRec + a_lo) : ah[mt];
+      }
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int j = jlo + ((sl - jlo) & 3);
+        if (j > jhi) continue;                  // wave-uniform
+        if (s == 0 && half == 0 && kk == 2 * j) {
+#pragma unroll
+          for (int mt = 0; mt < 5; ++mt) acc[sl][mt] = f32x4{};   // the pair's first plane
+        }
+#pragma unroll
+        for (int mt = 0; mt < 5; ++mt) acc[sl][mt] = prec::mma16<PM>(ah[mt], al[mt], bh[sl], bl[sl], acc[sl][mt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);        // one step per scheduling region (register budget)
+    }
+    // the pair whose last plane this was (kk = 2j + 7, second half)
+    if (half == 1 && kk >= kK && ((kk - kK) & 1) == 0) {
+      const int j = (kk - kK) >> 1;
+      if (j < npairs) {
+        switch (j & 3) {
+          case 0: epilogue(j, acc[0]); break;
+          case 1: epilogue(j, acc[1]); break;
+          case 2: epilogue(j, acc[2]); break;
+          default: epilogue(j, acc[3]); break;
+        }
+      }
+    }
   }
 }
 
@@ -256,13 +263,31 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   a.bias = t.bias; a.y = t.y; a.Do = t.Do; a.Ho = t.Ho; a.Wo = t.Wo;
   a.pe = t.trans ? kK - 1 - t.p : t.p;
   a.act = t.act;
-  a.nq = ceil_div(t.Do, 2); a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
-  const int64_t blocks = (int64_t)a.N * a.nq * a.nr * a.nw;
-  if (blocks == 0) return kOk;
+  a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
+  // pairs per depth segment: rounds of resident blocks (one per CU) × the segment's units
+  // (2P + 6 planes)
+  const int nq = ceil_div(t.Do, 2);
+  const int64_t cols = (int64_t)a.N * a.nr * a.nw;
+  if (cols == 0 || nq == 0) return kOk;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  double best = 1e30;
+  for (int P = 1; P <= 8; ++P) {
+    const int nseg = ceil_div(nq, P);
+    const int64_t rounds = (cols * nseg + ncu - 1) / ncu;
+    const double cost = (double)rounds * (P + 3);
+    if (cost < best - 1e-9) { best = cost; a.P = P; a.nseg = nseg; }
+    if (P >= nq) break;
+  }
+  const int64_t blocks = cols * a.nseg;
   MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * kC * 4 < (int64_t)kOobOffset, "thinn_x3: input volume too large");
   a.total = (int)blocks;
   a.per = (int)ceil_div(blocks, 8);
-  const size_t lds = (size_t)2 * kUnitBytes;
+  const size_t lds = (size_t)kUnitBytes + (size_t)kBH * kScratch * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel<PM>),
