@@ -307,8 +307,10 @@ static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_b
     if (rc) return rc;
     a.wx3 = ws;
   }
-  if (bm == 128 && bn == 128) return launch_brick_x3<2, 2, 2, 2, 400, PM>(a, st);
-  if (bm == 128) return launch_brick_x3<2, 2, 2, 1, 400, PM>(a, st);
+  // 128-row bricks on 8 waves (two per SIMD): one wave's halo staging and LDS waits overlap the
+  // other's MFMAs (the LDS-resident halo allows only one block per CU)
+  if (bm == 128 && bn == 128) return launch_brick_x3<2, 4, 2, 1, 400, PM>(a, st);
+  if (bm == 128) return launch_brick_x3<4, 2, 1, 1, 400, PM>(a, st);
   if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300, PM>(a, st);
   return launch_brick_x3<2, 2, 1, 1, 300, PM>(a, st);
 }
