@@ -26,7 +26,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kTile = 64;                 // co and ci per block
+constexpr int kTile = 64;                 // co and ci per block (4-wave variant)
 constexpr int kR = 8;                     // row segments per stage
 constexpr int kSegW = 16;                 // voxels per row segment
 constexpr int kDRow = 2 * kSegW * 16 + 16;          // 528 B
@@ -34,6 +34,7 @@ constexpr int kGRow = 2 * (kSegW + 2) * 16 + 16;    // 592 B
 constexpr int kDHalf = kSegW * 16;                  // lo part offset in a dY row
 constexpr int kGHalf = (kSegW + 2) * 16;            // lo part offset in an X row
 constexpr int kLds = kTile * kDRow + kTile * kGRow; // 71 680 B
+constexpr int kLdsW = 128 * kDRow + 64 * kGRow;     // 105 472 B (8-wave 128 × 64 variant)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -61,25 +62,31 @@ struct Wgrad3Args {
   int nseg, seg_per_split;                // row segments in total / per split (multiple of kR)
 };
 
-template <int PM>
-__global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
+// TC × TI = 64 × 64: 4 waves (2 × 2 sub-tiles of 32 × 32), two blocks per CU.  128 × 64 (the
+// 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
+// the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
+// kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
+template <int TC, int TI, int PM>
+__global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
+  constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
+  constexpr int WC = TC / 32;             // waves along co
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ds = smem;
-  char* Gs = smem + kTile * kDRow;
+  char* Gs = smem + TC * kDRow;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  const int wm0 = (wave >> 1) * 32, wn0 = (wave & 1) * 32;
+  const int wm0 = (wave % WC) * 32, wn0 = (wave / WC) * 32;
 
   // logical block: (co tile, ci tile) fastest, then (kd, kh), then split; XCD-aware remap so an
   // XCD's blocks share a contiguous range of splits (their dY / X rows stay in its L2)
-  const int nco = a.Cd / kTile, nci = a.Cg / kTile;
+  const int nco = a.Cd / TC, nci = a.Cg / TI;
   const int B = gridDim.x;
   int L = blockIdx.x;
   if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
   const int tile = L % (nco * nci);
   const int kk9 = (L / (nco * nci)) % 9;
   const int z = L / (nco * nci * 9);
-  const int co0 = (tile / nci) * kTile, ci0 = (tile % nci) * kTile;
+  const int co0 = (tile / nci) * TC, ci0 = (tile % nci) * TI;
   const int kd = kk9 / 3, kh = kk9 % 3;
   const int seg_lo = z * a.seg_per_split;
   if (seg_lo >= a.nseg) return;                    // grid padding (a multiple of 8 blocks)
@@ -88,12 +95,19 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
 
   const int Dg = a.D + 2, Hg = a.H + 2, Wg = a.W + 2;
   const int nsw = a.W / kSegW;
-  // staging units (w position, channel quad cq), cq fastest: 16 lanes read one voxel's 256
+  // staging units (w position, channel quad), quad fastest: 16 lanes read one voxel's 256
   // contiguous bytes (a w-fastest order, conflict-free for the LDS writes below, measured 35 %
-  // slower overall)
-  const int cq = tid & 15, uw = tid >> 4;          // dY: w = uw (0..15); X: w' = uw
-  const bool g2 = tid < 32;                        // X: w' = 16, 17
-  const int uw2 = 16 + (tid >> 4);
+  // slower overall).  dY: TC/4 quads × 16 w = one unit per thread.  X: TI/4 quads × 18 w'.
+  constexpr int DQ = TC / 4, GQ = TI / 4;
+  static_assert(NT == 16 * DQ, "one dY unit per thread");
+  const int cq = tid % DQ, uw = tid / DQ;          // dY unit
+  const int gcq = tid % GQ, gw = tid / GQ;         // X unit: w' = gw
+  // TC == TI: threads own w' 0..15 and threads < 2·GQ also w' 16, 17 (rg2).  TC = 2·TI: threads
+  // < 16·GQ own w' 0..15, the next 2·GQ own w' 16, 17, the rest no X unit.
+  constexpr bool kSplitG = TC == TI;
+  const bool g1 = kSplitG || tid < 18 * GQ;        // has an X unit in rg
+  const bool g2 = kSplitG && tid < 2 * GQ;         // second X unit (w' 16, 17) in rg2
+  const int uw2 = 16 + tid / GQ;
 
   float4 rd[kR], rg[kR], rg2[kR];
   // (n, d, h, w-segment) of the stage's first row segment, advanced with carries (the per-segment
@@ -115,14 +129,16 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
       const float4 dv = *reinterpret_cast<const float4*>(
           a.dy + ((((n * a.D + d) * a.H + h) * a.W + w0 + uw) * a.Cd + co0 + 4 * cq));
       const int gbase = ((n * Dg + d + kd) * Hg + h + kh) * Wg + w0;
-      const float4 gv = *reinterpret_cast<const float4*>(a.x + ((gbase + uw) * a.Cg + ci0 + 4 * cq));
+      const float4 gv = *reinterpret_cast<const float4*>(a.x + ((gbase + (g1 ? gw : 0)) * a.Cg + ci0 + 4 * gcq));
       // per-component selects (a float4 `ok ? v : zero` is lowered through scratch memory)
       rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
       rg[r] = make_float4(ok ? gv.x : 0.f, ok ? gv.y : 0.f, ok ? gv.z : 0.f, ok ? gv.w : 0.f);
-      // w' = 16, 17 (threads 0–31; the others re-read their own unit: keeps rg2 a plain register
+      // w' = 16, 17 (threads < 2·GQ; the others re-read their own unit: keeps rg2 a plain register
       // array, a conditionally written one goes to scratch)
-      const float4 g = *reinterpret_cast<const float4*>(a.x + ((gbase + (g2 ? uw2 : uw)) * a.Cg + ci0 + 4 * cq));
-      rg2[r] = make_float4(ok ? g.x : 0.f, ok ? g.y : 0.f, ok ? g.z : 0.f, ok ? g.w : 0.f);
+      if constexpr (kSplitG) {
+        const float4 g = *reinterpret_cast<const float4*>(a.x + ((gbase + (g2 ? uw2 : gw)) * a.Cg + ci0 + 4 * gcq));
+        rg2[r] = make_float4(ok ? g.x : 0.f, ok ? g.y : 0.f, ok ? g.z : 0.f, ok ? g.w : 0.f);
+      }
     }
   };
   // one unit: 8 segments × 4 channels → 4 rows × (16 B hi + 16 B lo) at w-slot `w`.  Write j
@@ -130,25 +146,27 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
   // (cq = 8g … 8g+7) then covers 8 distinct 16-B bank groups for both row strides (528 B and
   // 592 B rows, banks mod 32 dwords); unrotated, rows 4 apart collide 4-way (PMC: 51 % of the
   // LDS cycles were conflicts)
-  const int rot = (cq >> 1) & 3;
-  auto rotv = [&](const float4& v) __attribute__((always_inline)) {
-    const float4 t = (rot & 1) ? make_float4(v.y, v.z, v.w, v.x) : v;
-    return (rot & 2) ? make_float4(t.z, t.w, t.x, t.y) : t;
-  };
-  auto put = [&](char* base, int row_bytes, int half, int w, const float4 (&v)[kR]) __attribute__((always_inline)) {
+  auto put = [&](char* base, int row_bytes, int half, int w, int q, const float4 (&v)[kR]) __attribute__((always_inline)) {
+    const int rot = (q >> 1) & 3;
+    auto rotv = [&](const float4& x) __attribute__((always_inline)) {
+      const float4 t = (rot & 1) ? make_float4(x.y, x.z, x.w, x.x) : x;
+      return (rot & 2) ? make_float4(t.z, t.w, t.x, t.y) : t;
+    };
     float4 u[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) u[r] = rotv(v[r]);
-    char* p = base + (4 * cq) * row_bytes + w * 16;
+    char* p = base + (4 * q) * row_bytes + w * 16;
     split8_store<PM>(p + ((0 + rot) & 3) * row_bytes, half, u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x);
     split8_store<PM>(p + ((1 + rot) & 3) * row_bytes, half, u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y);
     split8_store<PM>(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
     split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
   };
   auto store = [&]() __attribute__((always_inline)) {
-    put(Ds, kDRow, kDHalf, uw, rd);
-    put(Gs, kGRow, kGHalf, uw, rg);
-    if (g2) put(Gs, kGRow, kGHalf, uw2, rg2);
+    put(Ds, kDRow, kDHalf, uw, cq, rd);
+    if (g1) put(Gs, kGRow, kGHalf, gw, gcq, rg);
+    if constexpr (kSplitG) {
+      if (g2) put(Gs, kGRow, kGHalf, uw2, gcq, rg2);
+    }
   };
 
   f32x16 acc[3];
@@ -206,6 +224,8 @@ __global__ void __launch_bounds__(256, 2) wgrad3_x3_kernel(Wgrad3Args a) {
   }
 }
 
+static bool w3_wide(const WgradArgs& a) { return a.Cd % 128 == 0 && a.Cg % 64 == 0; }
+
 bool wgrad3_x3_applicable(const WgradArgs& a) {
   return a.x3 && a.k == 3 && a.s == 1 && a.p == 0 && a.Wd % kSegW == 0 && a.Dg == a.Dd + 2 && a.Hg == a.Hd + 2 &&
          a.Wg == a.Wd + 2 && a.Cd % kTile == 0 && a.Cg % kTile == 0 &&
@@ -217,8 +237,9 @@ bool wgrad3_x3_applicable(const WgradArgs& a) {
 // ≥ 6 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
 int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
-  const int tiles = (a.Cd / kTile) * (a.Cg / kTile) * 9;
-  int s = 512 / tiles;
+  const bool wide = w3_wide(a);
+  const int tiles = (a.Cd / (wide ? 128 : kTile)) * (a.Cg / kTile) * 9;
+  int s = (wide ? 256 : 512) / tiles;
   const int by_len = nseg / (6 * kR);
   if (s > by_len) s = by_len;
   if (s > max_splits) s = max_splits;
@@ -236,15 +257,26 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   per = (per + kR - 1) / kR * kR;
   a.seg_per_split = per;
   const int nsplit = (a.nseg + per - 1) / per;
-  const int blocks = ((g.Cd / kTile) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
+  const bool wide = w3_wide(g);
+  const int blocks = ((g.Cd / (wide ? 128 : kTile)) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
   MRAGAN_PREC_DISPATCH(g.x3, {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<PM>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-      attr_set = true;
+    if (wide) {
+      static bool attr_w = false;
+      if (!attr_w) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<128, 64, PM>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsW);
+        attr_w = true;
+      }
+      hipLaunchKernelGGL((wgrad3_x3_kernel<128, 64, PM>), dim3(blocks), dim3(512), kLdsW, st, a);
+    } else {
+      static bool attr_set = false;
+      if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<64, 64, PM>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+        attr_set = true;
+      }
+      hipLaunchKernelGGL((wgrad3_x3_kernel<64, 64, PM>), dim3(blocks), dim3(256), kLds, st, a);
     }
-    hipLaunchKernelGGL(wgrad3_x3_kernel<PM>, dim3(blocks), dim3(256), kLds, st, a);
     return nsplit;
   })
 }
