@@ -62,6 +62,8 @@ def parse():
                          "and reported under alt_precisions; '' for none")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels from Python every step (default: replay the step as HIP graphs)")
+    ap.add_argument("--single-stream", action="store_true",
+                    help="issue the step on one stream (default: G_A / G_B and D_A / D_B chains on two)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--same-device", action="store_true",
@@ -208,7 +210,8 @@ def build_model(args, precision):
     sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
                 "--input_nc", str(args.nc), "--output_nc", str(args.nc),
                 "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
-                "--conv_precision", precision] + (["--no_cuda_graph"] if args.no_graph else [])
+                "--conv_precision", precision] + (["--no_cuda_graph"] if args.no_graph else []) + \
+        (["--single_stream"] if args.single_stream else [])
     opt = TrainOptions().gather_options()
     sys.argv = sys_argv
     opt.isTrain, opt.gpu_ids = True, 0
@@ -327,12 +330,13 @@ def main():
     # C-ABI call bracketed by HIP events (ROCm refuses timing events inside a captured graph)
     ops.TIMER.reset()
     ops.TIMER.match = lambda info: True
-    use_graph = model._use_graph
-    model._use_graph = False
+    # (one stream: a kernel's interval must not include the other lane's concurrent kernels)
+    use_graph, lanes = model._use_graph, model.parallel_lanes
+    model._use_graph, model.parallel_lanes = False, False
     for i in range(2):
         model.set_input(inputs[args.warmup + i])
         model.optimize_parameters()
-    model._use_graph = use_graph
+    model._use_graph, model.parallel_lanes = use_graph, lanes
     ops.TIMER.match = None
     classes = ops.TIMER.classes()
     barrier()
@@ -394,7 +398,8 @@ def main():
                    "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}",
-                   "step_launch": "hip_graph" if graphed else "eager"},
+                   "step_launch": "hip_graph" if graphed else "eager",
+                   "streams": 1 if args.single_stream else 2},
         "roofline": {"bound": bound, "kernel": f"{dom['kernels']} ({prec}) — {dom_cls}",
                      "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
                      "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,

@@ -138,6 +138,52 @@ class DeviceImagePool:
         return out.permute(0, 4, 1, 2, 3)
 
 
+class _Lanes:
+    """Two in-order lanes for the step's independent chains: lane 0 is the current stream,
+    lane 1 an auxiliary stream forked from it (under capture: two branches of the HIP graph).
+    `on(i)` issues on lane i with lane i's workspace; `mark` / `wait` order one lane after a
+    point of the other; `join` ends the fork.  With `parallel=False` both lanes are the current
+    stream (the --single_stream order, also what bench.py times kernels under)."""
+
+    def __init__(self, aux, parallel=True):
+        from mragan_hip import ops
+        self._ops = ops
+        cur = torch.cuda.current_stream()
+        self.s = [cur, aux if parallel else cur]
+        self.parallel = parallel
+        if parallel:
+            aux.wait_stream(cur)
+
+    def on(self, i):
+        lanes = self
+
+        class _On:
+            def __enter__(self_):
+                self_.st = torch.cuda.stream(lanes.s[i])
+                self_.ln = lanes._ops.lane(i)
+                self_.st.__enter__()
+                self_.ln.__enter__()
+
+            def __exit__(self_, *exc):
+                self_.ln.__exit__(*exc)
+                self_.st.__exit__(*exc)
+                return False
+        return _On()
+
+    def mark(self, i):
+        ev = torch.cuda.Event()
+        ev.record(self.s[i])
+        return ev
+
+    def wait(self, i, ev):
+        if self.parallel:
+            self.s[i].wait_event(ev)
+
+    def join(self):
+        if self.parallel:
+            self.s[0].wait_stream(self.s[1])
+
+
 def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
     return x.float().permute(0, 2, 3, 4, 1).contiguous()
 
@@ -274,6 +320,8 @@ class CycleGANModel(BaseModel):
                 setattr(self, 'loss_' + n, self._loss_buf[i])
         self._dist = None
         self._use_graph = self.isTrain and not getattr(opt, 'no_cuda_graph', False) and self.device.type == 'cuda'
+        self.parallel_lanes = not getattr(opt, 'single_stream', False)
+        self._aux_stream = None
         self._graphs = None          # (G-phase graph, D-phase graph) once captured
         self._rs_tables = None       # running-stat update tables of the captured step
         self._graph_key = None
@@ -335,16 +383,19 @@ class CycleGANModel(BaseModel):
         self._A, self._B, self._b = A, B, b
         self._idt = self.opt.lambda_identity > 0
         pGA, pGB = self.netG_A.plan, self.netG_B.plan
-        if self._idt:
-            self._cGA1 = pGA.forward(torch.cat([A, B], 0))       # [fake_B; idt_A]
-            self._cGB1 = pGB.forward(torch.cat([B, A], 0))       # [fake_A; idt_B]
-        else:
-            self._cGA1 = pGA.forward(A)                          # fake_B
-            self._cGB1 = pGB.forward(B)                          # fake_A
-        fake_B = self._cGA1.out[:b]
-        fake_A = self._cGB1.out[:b]
-        self._cGB2 = pGB.forward(fake_B)                     # rec_A
-        self._cGA2 = pGA.forward(fake_A)                     # rec_B
+        # both lanes read both generators' packed weights: pack before the fork
+        for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+            n.plan.ensure_packed()
+        ln = self._lanes()
+        with ln.on(0):          # lane 0: G_A(real_A) → G_B(fake_B)
+            self._cGA1 = pGA.forward(torch.cat([A, B], 0) if self._idt else A)   # [fake_B; idt_A]
+            fake_B = self._cGA1.out[:b]
+            self._cGB2 = pGB.forward(fake_B)                     # rec_A
+        with ln.on(1):          # lane 1: G_B(real_B) → G_A(fake_A)
+            self._cGB1 = pGB.forward(torch.cat([B, A], 0) if self._idt else B)   # [fake_A; idt_B]
+            fake_A = self._cGB1.out[:b]
+            self._cGA2 = pGA.forward(fake_A)                     # rec_B
+        ln.join()
         self._fake_B, self._fake_A = fake_B, fake_A
         self._publish(fake_B=fake_B, fake_A=fake_A, rec_A=self._cGB2.out, rec_B=self._cGA2.out)
         if self._idt:
@@ -358,33 +409,52 @@ class CycleGANModel(BaseModel):
         lA, lB, li = self.opt.lambda_A, self.opt.lambda_B, self.opt.lambda_identity
         L = self._loss_buf
         pDA, pDB = self.netD_A.plan, self.netD_B.plan
-        self._cDA1 = pDA.forward(self._fake_B)
-        self._cDB1 = pDB.forward(self._fake_A)
-        dlogA = torch.empty_like(self._cDA1.out)
-        dlogB = torch.empty_like(self._cDB1.out)
-        ops.gan_loss(self._cDA1.out, 1.0, self.use_lsgan, 1.0, L[1:2], dlogA)          # loss_G_A
-        ops.gan_loss(self._cDB1.out, 1.0, self.use_lsgan, 1.0, L[5:6], dlogB)          # loss_G_B
+        pGA, pGB = self.netG_A.plan, self.netG_B.plan
+        # allocated before the fork: both lanes' tensors outlive it
         dGA1 = torch.empty_like(self._cGA1.out)     # d/d[fake_B; idt_A]
         dGB1 = torch.empty_like(self._cGB1.out)     # d/d[fake_A; idt_B]
         d_recA = torch.empty_like(self._cGB2.out)
         d_recB = torch.empty_like(self._cGA2.out)
-        ops.l1_loss(self._cGB2.out, A, lA, L[2:3], d_recA)                             # loss_cycle_A
-        ops.l1_loss(self._cGA2.out, B, lB, L[6:7], d_recB)                             # loss_cycle_B
-        if self._idt:
-            ops.l1_loss(self._cGA1.out[b:], B, lB * li, L[3:4], dGA1[b:])              # loss_idt_A
-            ops.l1_loss(self._cGB1.out[b:], A, lA * li, L[7:8], dGB1[b:])              # loss_idt_B
-        else:                                                                          # reference: 0
+        if not self._idt:                                                              # reference: 0
             ops.fill(L[3:4], 0.0)
             ops.fill(L[7:8], 0.0)
-        # frozen D: data gradients only, written into the fake halves
-        pDA.backward(self._cDA1, [dlogA], need_wgrad=False, need_input_grad=True, dx_out=dGA1[:b])
-        pDB.backward(self._cDB1, [dlogB], need_wgrad=False, need_input_grad=True, dx_out=dGB1[:b])
-        # cycle passes: weight gradients + data gradient into the fakes
-        pGA, pGB = self.netG_A.plan, self.netG_B.plan
-        pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b])
-        pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b])
-        pGA.backward(self._cGA1, [dGA1])
-        pGB.backward(self._cGB1, [dGB1])
+        ln = self._lanes()
+
+        def head(pD, fake, slot, rec, real_rec, lam, d_rec, cG1, dG1, real_idt, lam_idt, idt_slot, cyc_slot):
+            cD = pD.forward(fake)
+            dlog = torch.empty_like(cD.out)
+            ops.gan_loss(cD.out, 1.0, self.use_lsgan, 1.0, L[slot:slot + 1], dlog)
+            ops.l1_loss(rec, real_rec, lam, L[cyc_slot:cyc_slot + 1], d_rec)
+            if self._idt:
+                ops.l1_loss(cG1.out[b:], real_idt, lam_idt, L[idt_slot:idt_slot + 1], dG1[b:])
+            # frozen D: data gradient only, written into the fake half
+            pD.backward(cD, [dlog], need_wgrad=False, need_input_grad=True, dx_out=dG1[:b])
+            return cD
+
+        # lane 0: D_A(fake_B), loss_G_A, loss_cycle_A, loss_idt_A, then G_B's rec_A pass (G_B
+        # weight gradients + d fake_B); lane 1 the mirror image.  The first-pass backwards of
+        # G_A / G_B accumulate into the weight gradients the other lane's cycle pass wrote, so
+        # each waits for that pass.
+        with ln.on(0):
+            self._cDA1 = head(pDA, self._fake_B, 1, self._cGB2.out, A, lA, d_recA, self._cGA1, dGA1, B, lB * li, 3, 2)
+            pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b])
+            rec_done_0 = ln.mark(0)
+        with ln.on(1):
+            self._cDB1 = head(pDB, self._fake_A, 5, self._cGA2.out, B, lB, d_recB, self._cGB1, dGB1, A, lA * li, 7, 6)
+            pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b])
+            rec_done_1 = ln.mark(1)
+        with ln.on(0):
+            ln.wait(0, rec_done_1)
+            pGA.backward(self._cGA1, [dGA1])
+        with ln.on(1):
+            ln.wait(1, rec_done_0)
+            pGB.backward(self._cGB1, [dGB1])
+        ln.join()
+
+    def _lanes(self):
+        if self.parallel_lanes and self._aux_stream is None:
+            self._aux_stream = torch.cuda.Stream(device=self.device)
+        return _Lanes(self._aux_stream, self.parallel_lanes)
 
     def backward_D_basic(self, netD, real, pool, fakes, ret_idx, store_idx, loss_slot):
         """cycle_gan_model.py:138-149 with real and (pooled, detached) fake batched."""
@@ -464,8 +534,12 @@ class CycleGANModel(BaseModel):
     def _phase_D(self):
         self.set_requires_grad([self.netD_A, self.netD_B], True)
         self.optimizer_D.zero_grad()
-        self.backward_D_A()
-        self.backward_D_B()
+        ln = self._lanes()
+        with ln.on(0):
+            self.backward_D_A()
+        with ln.on(1):
+            self.backward_D_B()
+        ln.join()
         if not torch.cuda.is_current_stream_capturing():
             self._running_stats()
 

@@ -31,22 +31,43 @@ def _check(t: torch.Tensor, name: str, ndim: int = 5):
         raise ValueError(f"{name}: expected {ndim}-d NDHWC tensor, got shape {tuple(t.shape)}")
 
 
+_LANE = [0]
+
+
+class lane:
+    """`with ops.lane(i):` — calls inside use lane i's workspace.  Work issued concurrently on
+    two streams must use two lanes (the model's G_A / G_B chains); the lane index, not the
+    stream, keys the buffer, so an eager step and its graph capture use the same buffers."""
+
+    def __init__(self, i: int):
+        self.i = i
+
+    def __enter__(self):
+        self.prev = _LANE[0]
+        _LANE[0] = self.i
+        return self
+
+    def __exit__(self, *exc):
+        _LANE[0] = self.prev
+        return False
+
+
 class Workspace:
-    """Grow-only scratch buffer per device (sized by the first step; reused afterwards)."""
+    """Grow-only scratch buffer per (device, lane) (sized by the first step; reused afterwards)."""
 
     def __init__(self):
         self._buf = {}
         self._retired = []      # outgrown buffers stay allocated: a captured HIP graph may hold them
 
     def get(self, nbytes: int) -> torch.Tensor:
-        dev = torch.cuda.current_device()
+        dev = (torch.cuda.current_device(), _LANE[0])
         b = self._buf.get(dev)
         if b is None or b.numel() < nbytes:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("workspace growth during HIP graph capture (run the step eagerly first)")
             if b is not None:
                 self._retired.append(b)
-            b = torch.empty(max(int(nbytes * 1.25), 1 << 20), dtype=torch.uint8, device=f"cuda:{dev}")
+            b = torch.empty(max(int(nbytes * 1.25), 1 << 20), dtype=torch.uint8, device=f"cuda:{dev[0]}")
             self._buf[dev] = b
         return b
 

@@ -57,6 +57,11 @@ BASE_FLAGS = [
     ('--no_cuda_graph', dict(action='store_true',
                              help='launch every kernel of the training step from Python instead of replaying '
                                   'the step captured as HIP graphs')),
+    # engine-only flag: the G_A / G_B (and D_A / D_B) chains of a step are independent until their
+    # weight gradients meet; by default they run on two HIP streams (two branches of the graph)
+    ('--single_stream', dict(action='store_true',
+                             help='issue the whole training step on one HIP stream (no G_A / G_B, D_A / D_B '
+                                  'overlap)')),
 ]
 
 
