@@ -15,15 +15,23 @@ namespace mragan {
 constexpr float kInEps = 1e-5f;
 
 
-// voxel chunks per instance: ≈2048 blocks per launch, but ≥ 4 voxel rows per thread
+// row chunks per instance: ≈2048 blocks per launch, but ≥ 4 float4 loads per thread
 static int in_chunks(const InShape& s) {
-  const int CQ = s.C / 4;
-  const int R = CQ >= 256 ? 1 : 256 / CQ;
+  const int rows = s.D * s.H;
+  const int64_t rowq = (int64_t)s.W * (s.C / 4);
   int64_t want = (2048 + s.N - 1) / s.N;
-  int64_t cap = s.S() / (4 * R);
+  int64_t min_rows = (4 * 256 + rowq - 1) / rowq;            // rows per block for ≥ 4 loads/thread
+  int64_t cap = (rows + min_rows - 1) / min_rows;
   if (want > cap) want = cap;
+  if (want > rows) want = rows;
   if (want < 1) want = 1;
   return (int)want;
+}
+
+// all in-kernel offsets are 32-bit (element counts of every tensor < 2^31)
+static bool in_fits(const InShape& s, int pad) {
+  const int64_t e = (int64_t)s.N * (s.D + 2 * pad) * (s.H + 2 * pad) * (s.W + 2 * pad) * s.C;
+  return e < (int64_t(1) << 31);
 }
 
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
@@ -80,35 +88,47 @@ __device__ __forceinline__ float dact_from_xhat(float xh, int act) {
 }
 
 // ---- forward statistics: partials[n][chunk][C][2] (Σx, Σx²) --------------------------------
-__global__ void __launch_bounds__(256) in_stats_kernel(const float* __restrict__ x, InShape s, int chunks,
-                                                       double* __restrict__ part) {
+// Rows (d, h) of one instance per block; thread = (voxel slot wt, channel quad q), q fixed per
+// thread, the row's voxels dealt to the 256 / (C/4) slots: no per-element 64-bit index math.
+__device__ __forceinline__ void in_block_reduce(double (&s0)[4], double (&s1)[4], int CQ, double* __restrict__ out) {
   __shared__ double red[2][256 * 4];
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  const int CQ = s.C / 4, R = 256 / CQ;
   const int tid = threadIdx.x;
-  const int q = tid % CQ, r = tid / CQ;
-  const int64_t S = s.S();
-  const int64_t per = (S + chunks - 1) / chunks;
-  const int64_t v0 = chunk * per, v1 = min(S, v0 + per);
-  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  if (r < R) {
-    const float* base = x + (int64_t)n * S * s.C + 4 * q;
-    for (int64_t v = v0 + r; v < v1; v += R) {
-      float4 val = *reinterpret_cast<const float4*>(base + v * s.C);
-      s0[0] += val.x; s0[1] += val.y; s0[2] += val.z; s0[3] += val.w;
-      s1[0] += (double)val.x * val.x; s1[1] += (double)val.y * val.y;
-      s1[2] += (double)val.z * val.z; s1[3] += (double)val.w * val.w;
-    }
-  }
   for (int j = 0; j < 4; ++j) { red[0][tid * 4 + j] = s0[j]; red[1][tid * 4 + j] = s1[j]; }
   __syncthreads();
   if (tid < CQ) {
+    const int R = 256 / CQ;
     double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     for (int rr = 0; rr < R; ++rr)
       for (int j = 0; j < 4; ++j) { a[j] += red[0][(rr * CQ + tid) * 4 + j]; b[j] += red[1][(rr * CQ + tid) * 4 + j]; }
-    double* out = part + (((int64_t)n * chunks + chunk) * s.C + 4 * tid) * 2;
-    for (int j = 0; j < 4; ++j) { out[2 * j] = a[j]; out[2 * j + 1] = b[j]; }
+    for (int j = 0; j < 4; ++j) { out[8 * tid + 2 * j] = a[j]; out[8 * tid + 2 * j + 1] = b[j]; }
   }
+}
+
+__device__ __forceinline__ void in_rows(const InShape& s, int chunks, int chunk, int& r0, int& r1) {
+  const int rows = s.D * s.H, per = (rows + chunks - 1) / chunks;
+  r0 = chunk * per;
+  r1 = min(rows, r0 + per);
+}
+
+__global__ void __launch_bounds__(256) in_stats_kernel(const float* __restrict__ x, InShape s, int chunks,
+                                                       double* __restrict__ part) {
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  const int CQ = s.C / 4, tid = threadIdx.x, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
+  const int rowq = s.W * CQ;                       // float4s per row
+  int r0, r1;
+  in_rows(s, chunks, chunk, r0, r1);
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  const float4* base = reinterpret_cast<const float4*>(x) + (size_t)n * s.D * s.H * rowq + q;
+  for (int r = r0; r < r1; ++r) {
+    const float4* row = base + (size_t)r * rowq;
+    for (int w = wt; w < s.W; w += WS) {
+      const float4 v = row[w * CQ];
+      s0[0] += v.x; s0[1] += v.y; s0[2] += v.z; s0[3] += v.w;
+      s1[0] += (double)v.x * v.x; s1[1] += (double)v.y * v.y; s1[2] += (double)v.z * v.z; s1[3] += (double)v.w * v.w;
+    }
+  }
+  in_block_reduce(s0, s1, CQ, part + ((size_t)n * chunks + chunk) * s.C * 2);
 }
 
 // one block per instance (kernel boundary = coherence point for the partials of all XCDs; an
@@ -119,97 +139,118 @@ __global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restri
 }
 
 // ---- forward apply: y (padded by ypad) = act((x − μ)·rstd) + resid(interior of rpad-padded) --
+// One output row (n, dp, hp) of the padded y per block iteration; source row and the residual
+// row are fixed per row, each thread walks its float4s (q fixed per thread).
 __global__ void __launch_bounds__(256) in_apply_kernel(const float* __restrict__ x, InShape s, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, int act,
                                                        const float* __restrict__ resid, int rpad, float* __restrict__ y,
                                                        int ypad) {
-  const int CQ = s.C / 4;
+  const int CQ = s.C / 4, tid = threadIdx.x, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
   const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad;
-  const int64_t total = (int64_t)s.N * Dp * Hp * Wp * CQ;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % CQ); int64_t u = e / CQ;
-    const int w = (int)(u % Wp); u /= Wp;
-    const int h = (int)(u % Hp); u /= Hp;
-    const int d = (int)(u % Dp); const int n = (int)(u / Dp);
-    const int sd = min(max(d - ypad, 0), s.D - 1), sh = min(max(h - ypad, 0), s.H - 1), sw = min(max(w - ypad, 0), s.W - 1);
-    const int64_t src = (((int64_t)n * s.D + sd) * s.H + sh) * s.W + sw;
-    float4 v = *reinterpret_cast<const float4*>(x + src * s.C + 4 * q);
-    const float4 mu = *reinterpret_cast<const float4*>(mean + n * s.C + 4 * q);
-    const float4 rs = *reinterpret_cast<const float4*>(rstd + n * s.C + 4 * q);
-    v = make_float4((v.x - mu.x) * rs.x, (v.y - mu.y) * rs.y, (v.z - mu.z) * rs.z, (v.w - mu.w) * rs.w);
-    v = f4_act(v, act);
-    if (resid) {
-      const int Dr = s.D + 2 * rpad, Hr = s.H + 2 * rpad, Wr = s.W + 2 * rpad;
-      const float4 r = *reinterpret_cast<const float4*>(
-          resid + ((((int64_t)n * Dr + sd + rpad) * Hr + sh + rpad) * Wr + sw + rpad) * s.C + 4 * q);
-      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  const int Dr = s.D + 2 * rpad, Hr = s.H + 2 * rpad, Wr = s.W + 2 * rpad;
+  const int rows = s.N * Dp * Hp, rowq = Wp * CQ;
+  const float4* xv = reinterpret_cast<const float4*>(x);
+  const float4* rv = reinterpret_cast<const float4*>(resid);
+  float4* yv = reinterpret_cast<float4*>(y);
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int hp = row % Hp, t = row / Hp, dp = t % Dp, n = t / Dp;
+    const int sd = min(max(dp - ypad, 0), s.D - 1), sh = min(max(hp - ypad, 0), s.H - 1);
+    const float4 mu = reinterpret_cast<const float4*>(mean + n * s.C)[q];
+    const float4 rs = reinterpret_cast<const float4*>(rstd + n * s.C)[q];
+    const float4* xrow = xv + (size_t)((n * s.D + sd) * s.H + sh) * s.W * CQ;
+    const float4* rrow = resid ? rv + ((size_t)((n * Dr + sd + rpad) * Hr + sh + rpad) * Wr + rpad) * CQ : nullptr;
+    float4* yrow = yv + (size_t)row * rowq + q;
+    for (int wp = wt; wp < Wp; wp += WS) {
+      const int sw = min(max(wp - ypad, 0), s.W - 1);
+      float4 v = xrow[sw * CQ + q];
+      v = make_float4((v.x - mu.x) * rs.x, (v.y - mu.y) * rs.y, (v.z - mu.z) * rs.z, (v.w - mu.w) * rs.w);
+      v = f4_act(v, act);
+      if (resid) {
+        const float4 r = rrow[sw * CQ + q];
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      }
+      yrow[wp * CQ] = v;
     }
-    *reinterpret_cast<float4*>(y + u * 0 + e * 4) = v;   // e*4 == (((n*Dp+d)*Hp+h)*Wp+w)*C + 4q
   }
 }
 
 // ---- backward -----------------------------------------------------------------------------
-__device__ __forceinline__ float4 fold_read(const float* __restrict__ dy, int pad, const InShape& s, int n, int d, int h,
-                                            int w, int q) {
-  if (pad == 0) return *reinterpret_cast<const float4*>(dy + ((((int64_t)n * s.D + d) * s.H + h) * s.W + w) * s.C + 4 * q);
-  const int Dp = s.D + 2 * pad, Hp = s.H + 2 * pad, Wp = s.W + 2 * pad;
-  const int d0 = d == 0 ? 0 : d + pad, d1 = d == s.D - 1 ? s.D - 1 + 2 * pad : d + pad;
-  const int h0 = h == 0 ? 0 : h + pad, h1 = h == s.H - 1 ? s.H - 1 + 2 * pad : h + pad;
-  const int w0 = w == 0 ? 0 : w + pad, w1 = w == s.W - 1 ? s.W - 1 + 2 * pad : w + pad;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int a = d0; a <= d1; ++a)
-    for (int b = h0; b <= h1; ++b)
-      for (int c = w0; c <= w1; ++c) {
-        const float4 v = *reinterpret_cast<const float4*>(dy + ((((int64_t)n * Dp + a) * Hp + b) * Wp + c) * s.C + 4 * q);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-  return acc;
+// g = fold_pad(dy) (+ dy_add) · act'(x̂).  Per row (n, d, h) the padded rows folded into it are
+// fixed ([d0, d1] × [h0, h1], one each inside the volume); per voxel w the padded columns
+// [w0, w1].  32-bit offsets (the host checks the sizes).
+struct InRow {
+  const float4* dy;    // first padded row (d0, h0) of the fold, at column 0
+  int nd, nh;          // rows folded along d and h
+  int dstride, hstride;  // float4 strides between folded rows
+  const float4* x;     // x row
+  const float4* add;   // dy_add row or null
+  float4 mu, rs;
+};
+
+__device__ __forceinline__ InRow in_bwd_row(const InBwdArgs& a, const InShape& s, int n, int d, int h, int q) {
+  const int CQ = s.C / 4, p = a.dypad;
+  const int Hp = s.H + 2 * p, Wp = s.W + 2 * p, Dp = s.D + 2 * p;
+  const int d0 = d == 0 ? 0 : d + p, d1 = d == s.D - 1 ? s.D - 1 + 2 * p : d + p;
+  const int h0 = h == 0 ? 0 : h + p, h1 = h == s.H - 1 ? s.H - 1 + 2 * p : h + p;
+  InRow r;
+  r.dy = reinterpret_cast<const float4*>(a.dy) + ((size_t)(n * Dp + d0) * Hp + h0) * Wp * CQ + q;
+  r.nd = d1 - d0 + 1;
+  r.nh = h1 - h0 + 1;
+  r.hstride = Wp * CQ;
+  r.dstride = Hp * Wp * CQ;
+  const size_t xo = ((size_t)(n * s.D + d) * s.H + h) * s.W * CQ + q;
+  r.x = reinterpret_cast<const float4*>(a.x) + xo;
+  r.add = a.dy_add ? reinterpret_cast<const float4*>(a.dy_add) + xo : nullptr;
+  r.mu = reinterpret_cast<const float4*>(a.mean + n * s.C)[q];
+  r.rs = reinterpret_cast<const float4*>(a.rstd + n * s.C)[q];
+  return r;
 }
 
-
-__device__ __forceinline__ void in_bwd_g(const InBwdArgs& a, const InShape& s, int n, int64_t v, int q, float4& g,
-                                         float4& xh) {
-  const int w = (int)(v % s.W); const int64_t u = v / s.W;
-  const int h = (int)(u % s.H); const int d = (int)(u / s.H);
-  g = fold_read(a.dy, a.dypad, s, n, d, h, w, q);
-  const int64_t idx = ((int64_t)n * s.S() + v) * s.C + 4 * q;
-  if (a.dy_add) {
-    const float4 e = *reinterpret_cast<const float4*>(a.dy_add + idx);
+__device__ __forceinline__ void in_bwd_voxel(const InBwdArgs& a, const InShape& s, const InRow& r, int w, float4& g,
+                                             float4& xh) {
+  const int CQ = s.C / 4, p = a.dypad;
+  const int w0 = w == 0 ? 0 : w + p, w1 = w == s.W - 1 ? s.W - 1 + 2 * p : w + p;
+  g = r.dy[w0 * CQ];
+  if (p && (r.nd > 1 || r.nh > 1 || w1 > w0)) {      // border: sum the folded padded voxels
+    g = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < r.nd; ++i)
+      for (int j = 0; j < r.nh; ++j) {
+        const float4* rowp = r.dy + i * r.dstride + j * r.hstride;
+        for (int c = w0; c <= w1; ++c) {
+          const float4 v = rowp[c * CQ];
+          g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+        }
+      }
+  }
+  if (r.add) {
+    const float4 e = r.add[w * CQ];
     g.x += e.x; g.y += e.y; g.z += e.z; g.w += e.w;
   }
-  const float4 xv = *reinterpret_cast<const float4*>(a.x + idx);
-  const float4 mu = *reinterpret_cast<const float4*>(a.mean + n * s.C + 4 * q);
-  const float4 rs = *reinterpret_cast<const float4*>(a.rstd + n * s.C + 4 * q);
-  xh = make_float4((xv.x - mu.x) * rs.x, (xv.y - mu.y) * rs.y, (xv.z - mu.z) * rs.z, (xv.w - mu.w) * rs.w);
+  const float4 xv = r.x[w * CQ];
+  xh = make_float4((xv.x - r.mu.x) * r.rs.x, (xv.y - r.mu.y) * r.rs.y, (xv.z - r.mu.z) * r.rs.z,
+                   (xv.w - r.mu.w) * r.rs.w);
   g.x *= dact_from_xhat(xh.x, a.act); g.y *= dact_from_xhat(xh.y, a.act);
   g.z *= dact_from_xhat(xh.z, a.act); g.w *= dact_from_xhat(xh.w, a.act);
 }
 
 __global__ void __launch_bounds__(256) in_bwd_stats_kernel(InBwdArgs a, InShape s, int chunks, double* __restrict__ part) {
-  __shared__ double red[2][256 * 4];
   const int n = blockIdx.y, chunk = blockIdx.x;
-  const int CQ = s.C / 4, R = 256 / CQ;
-  const int tid = threadIdx.x, q = tid % CQ, r = tid / CQ;
-  const int64_t S = s.S(), per = (S + chunks - 1) / chunks;
-  const int64_t v0 = chunk * per, v1 = min(S, v0 + per);
+  const int CQ = s.C / 4, tid = threadIdx.x, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
+  int r0, r1;
+  in_rows(s, chunks, chunk, r0, r1);
   double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  if (r < R) {
-    for (int64_t v = v0 + r; v < v1; v += R) {
+  for (int r = r0; r < r1; ++r) {
+    const InRow row = in_bwd_row(a, s, n, r / s.H, r % s.H, q);
+    for (int w = wt; w < s.W; w += WS) {
       float4 g, xh;
-      in_bwd_g(a, s, n, v, q, g, xh);
+      in_bwd_voxel(a, s, row, w, g, xh);
       s0[0] += g.x; s0[1] += g.y; s0[2] += g.z; s0[3] += g.w;
       s1[0] += (double)g.x * xh.x; s1[1] += (double)g.y * xh.y; s1[2] += (double)g.z * xh.z; s1[3] += (double)g.w * xh.w;
     }
   }
-  for (int j = 0; j < 4; ++j) { red[0][tid * 4 + j] = s0[j]; red[1][tid * 4 + j] = s1[j]; }
-  __syncthreads();
-  if (tid < CQ) {
-    double a0[4] = {0, 0, 0, 0}, b0[4] = {0, 0, 0, 0};
-    for (int rr = 0; rr < R; ++rr)
-      for (int j = 0; j < 4; ++j) { a0[j] += red[0][(rr * CQ + tid) * 4 + j]; b0[j] += red[1][(rr * CQ + tid) * 4 + j]; }
-    double* out = part + (((int64_t)n * chunks + chunk) * s.C + 4 * tid) * 2;
-    for (int j = 0; j < 4; ++j) { out[2 * j] = a0[j]; out[2 * j + 1] = b0[j]; }
-  }
+  in_block_reduce(s0, s1, CQ, part + ((size_t)n * chunks + chunk) * s.C * 2);
 }
 
 __global__ void __launch_bounds__(256) in_bwd_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
@@ -218,22 +259,26 @@ __global__ void __launch_bounds__(256) in_bwd_finalize_kernel(const double* __re
 }
 
 __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape s, const float* __restrict__ coef) {
-  const int CQ = s.C / 4;
-  const int64_t S = s.S();
-  const int64_t total = (int64_t)s.N * S * CQ;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % CQ); const int64_t u = e / CQ;
-    const int64_t v = u % S; const int n = (int)(u / S);
-    float4 g, xh;
-    in_bwd_g(a, s, n, v, q, g, xh);
-    const float* cf = coef + 2 * ((int64_t)n * s.C + 4 * q);
-    const float4 rs = *reinterpret_cast<const float4*>(a.rstd + n * s.C + 4 * q);
-    float4 o;
-    o.x = rs.x * (g.x - cf[0] - xh.x * cf[1]);
-    o.y = rs.y * (g.y - cf[2] - xh.y * cf[3]);
-    o.z = rs.z * (g.z - cf[4] - xh.z * cf[5]);
-    o.w = rs.w * (g.w - cf[6] - xh.w * cf[7]);
-    *reinterpret_cast<float4*>(a.dx + e * 4) = o;
+  const int CQ = s.C / 4, tid = threadIdx.x, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
+  const int rows = s.N * s.D * s.H;
+  float4* dx = reinterpret_cast<float4*>(a.dx);
+  for (int rr = blockIdx.x; rr < rows; rr += gridDim.x) {
+    const int h = rr % s.H, t = rr / s.H, d = t % s.D, n = t / s.D;
+    const InRow row = in_bwd_row(a, s, n, d, h, q);
+    const float4 c0 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[0];   // (mg0, mgx0, mg1, mgx1)
+    const float4 c1 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[1];
+    float4* out = dx + (size_t)rr * s.W * CQ + q;
+    for (int w = wt; w < s.W; w += WS) {
+      float4 g, xh;
+      in_bwd_voxel(a, s, row, w, g, xh);
+      float4 o;
+      o.x = row.rs.x * (g.x - c0.x - xh.x * c0.y);
+      o.y = row.rs.y * (g.y - c0.z - xh.y * c0.w);
+      o.z = row.rs.z * (g.z - c1.x - xh.z * c1.y);
+      o.w = row.rs.w * (g.w - c1.z - xh.w * c1.w);
+      out[w * CQ] = o;
+    }
   }
 }
 
@@ -282,6 +327,7 @@ static int grid_for(int64_t work, int cap = 8192) {
 int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
                  float* rstd, void* ws, size_t ws_bytes, hipStream_t st) {
   MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm: C=%d must be a multiple of 4 (≤1024)", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, ypad > rpad ? ypad : rpad), "instnorm: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
   if (s.S() <= 1) {
     set_error("Expected more than 1 spatial element when training, got input size [%d, %d, %d, %d, %d]", s.N, s.C, s.D,
               s.H, s.W);
@@ -295,13 +341,15 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   if (rc) return rc;
   hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
   if ((rc = check_launch("in_finalize"))) return rc;
-  const int64_t total = (int64_t)s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad) * (s.W + 2 * ypad) * (s.C / 4);
-  hipLaunchKernelGGL(in_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad);
+  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
+  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
+                     rpad, y, ypad);
   return check_launch("in_apply");
 }
 
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st) {
   MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm_bwd: C=%d must be a multiple of 4", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, a.dypad), "instnorm_bwd: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
   const int chunks = in_chunks(s);
   const size_t need = instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C) + (size_t)s.N * s.C * 2 * sizeof(float);
   if (need > ws_bytes) { set_error("instnorm_bwd: workspace too small"); return kWorkspace; }
@@ -312,8 +360,8 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   if (rc) return rc;
   hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
   if ((rc = check_launch("in_bwd_finalize"))) return rc;
-  const int64_t total = (int64_t)s.N * s.S() * (s.C / 4);
-  hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, a, s, coef);
+  const int rows = s.N * s.D * s.H;
+  hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, a, s, coef);
   return check_launch("in_bwd_apply");
 }
 
