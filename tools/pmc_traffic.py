@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--key", required=True)
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--source", default=None, help="what was profiled (recorded in the entry)")
     a = ap.parse_args()
     fetch_kib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
     write_kib, nw = per_launch(a.write, "WRITE_SIZE", a.kernel)
@@ -62,6 +63,8 @@ def main():
         "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)",
         "launches": [nf, nw],
     }
+    if a.source:
+        entry["source"] = a.source
     if a.algorithmic_bytes:
         entry["algorithmic_bytes"] = a.algorithmic_bytes
         entry["ratio"] = entry["hbm_bytes_per_launch"] / a.algorithmic_bytes
