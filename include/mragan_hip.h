@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 7
+#define MRAGAN_ABI_VERSION 8
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -119,6 +119,13 @@ int mragan_instnorm_fwd(const float* x, int N, int D, int H, int W, int C, float
 int mragan_instnorm_bwd(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                         const float* dy, int dypad, const float* dy_add, int act, float* dx, void* ws, size_t ws_bytes,
                         void* stream);
+/* Same, and also writes g_out = fold(dy, dypad) + dy_add (before act') — the gradient w.r.t. a
+ * ResnetBlock's input, x + conv_block(x) (networks3D.py:262-263), which the block's skip path
+ * adds again one block earlier: the ReplicationPad3d backward and the skip-gradient add of the
+ * reference's autograd happen in this one pass (no separate mragan_rpad_fold).  ABI 8. */
+int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                          const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out, void* ws,
+                          size_t ws_bytes, void* stream);
 
 /* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
  * entry listing the per-instance statistics of the reference's sequential calls in call order. */

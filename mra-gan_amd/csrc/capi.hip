@@ -180,7 +180,16 @@ int mragan_instnorm_bwd(const float* x, const float* mean, const float* rstd, in
                         const float* dy, int dypad, const float* dy_add, int act, float* dx, void* ws, size_t ws_bytes,
                         void* stream) {
   MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx && ws, "instnorm_bwd: null pointer");
-  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, dx};
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, dx, nullptr};
+  return instnorm_bwd(a, InShape{N, D, H, W, C}, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                          const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out, void* ws,
+                          size_t ws_bytes, void* stream) {
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx && g_out && ws, "instnorm_bwd_g: null pointer");
+  MRAGAN_CHECK_ARG(g_out != dx && g_out != dy && g_out != dy_add, "instnorm_bwd_g: g_out aliases an operand");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, dx, g_out};
   return instnorm_bwd(a, InShape{N, D, H, W, C}, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 

@@ -245,6 +245,88 @@ __global__ void __launch_bounds__(256) thin_n_class_kernel(ThinArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// thin_n_class8: the same parity-class form for ceil(k/s) = 2 (k3/k4, s2: the D-first data
+// gradient) with 8 lanes per output voxel.  Lane j of a group reads channel quads j, j+8 of each
+// tap's input row, so 8 lanes read one voxel's 32-channel row as 128 contiguous bytes (the
+// one-thread-per-voxel form above made every load instruction touch 64 different lines: ~3 TF/s);
+// the class's ≤ 8 tap weights for those quads live in registers for the whole grid-stride walk;
+// the 8 partial dots are summed with three xor-shuffles in a fixed order.  Products accumulate
+// in fp64 (rounded once): the step's G gradients pass this through ~10 InstanceNorm backwards
+// whose mean-subtraction cancels, so the fp32 rounding order of this sum is visible in them.
+// ---------------------------------------------------------------------------------------
+template <int NY, int QPL>
+__global__ void __launch_bounds__(256) thin_n_class8_kernel(ThinArgs a) {
+  const int s = a.s, k = a.k;
+  const int cls = blockIdx.y;
+  const int cw = cls % s, ch = (cls / s) % s, cd = cls / (s * s);
+  const int Qd = (a.Do - cd + s - 1) / s, Qh = (a.Ho - ch + s - 1) / s, Qw = (a.Wo - cw + s - 1) / s;
+  const int M = a.N * Qd * Qh * Qw;                   // < 2^31 (host check)
+  const int t0d = (cd + a.p) % s, t0h = (ch + a.p) % s, t0w = (cw + a.p) % s;
+  const int j = threadIdx.x & 7;
+  const int CQ = a.cx / 4;
+  float4 wr[8][QPL][NY];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int td = t0d + s * (t >> 2), th = t0h + s * ((t >> 1) & 1), tw = t0w + s * (t & 1);
+    const bool tok = td < k && th < k && tw < k;
+    const float* wt = a.w + (int64_t)((min(td, k - 1) * k + min(th, k - 1)) * k + min(tw, k - 1)) * NY * a.cx;
+#pragma unroll
+    for (int u = 0; u < QPL; ++u) {
+      const int q = j + 8 * u;
+#pragma unroll
+      for (int n = 0; n < NY; ++n)
+        wr[t][u][n] = (tok && q < CQ) ? *reinterpret_cast<const float4*>(wt + n * a.cx + 4 * q)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const int HWi = a.Hi * a.Wi;
+  for (int m = blockIdx.x * 32 + (threadIdx.x >> 3); m < M; m += gridDim.x * 32) {
+    const int qw = m % Qw;
+    int u_ = m / Qw;
+    const int qh = u_ % Qh; u_ /= Qh;
+    const int qd = u_ % Qd;
+    const int nb = u_ / Qd;
+    const int od = qd * s + cd, oh = qh * s + ch, ow = qw * s + cw;
+    double acc[NY];
+#pragma unroll
+    for (int n = 0; n < NY; ++n) acc[n] = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int td = t0d + s * (t >> 2), th = t0h + s * ((t >> 1) & 1), tw = t0w + s * (t & 1);
+      const int id = (od + a.p - td) / s, ih = (oh + a.p - th) / s, iw = (ow + a.p - tw) / s;
+      if (td >= k || th >= k || tw >= k || (unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi ||
+          (unsigned)iw >= (unsigned)a.Wi)
+        continue;
+      const float* xr = a.x + ((int64_t)nb * a.Di * HWi + (id * a.Hi + ih) * a.Wi + iw) * a.cx;
+#pragma unroll
+      for (int u = 0; u < QPL; ++u) {
+        const int q = j + 8 * u;
+        if (q < CQ) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * q);
+#pragma unroll
+          for (int n = 0; n < NY; ++n) {
+            const float4 wv = wr[t][u][n];
+            acc[n] = fma((double)xv.x, (double)wv.x, fma((double)xv.y, (double)wv.y,
+                         fma((double)xv.z, (double)wv.z, fma((double)xv.w, (double)wv.w, acc[n]))));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NY; ++n) {
+      acc[n] += __shfl_xor(acc[n], 4, 8);
+      acc[n] += __shfl_xor(acc[n], 2, 8);
+      acc[n] += __shfl_xor(acc[n], 1, 8);
+    }
+    if (j == 0) {
+      float* dst = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * NY;
+#pragma unroll
+      for (int n = 0; n < NY; ++n) dst[n] = act_fwd((float)acc[n] + (a.bias ? a.bias[n] : 0.f), a.act);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // naive: one wave per output voxel (lanes split taps × channels), any stride / transposed
 // form.  Used for the tiny D-last convolution and the D-first data gradient.
 // ---------------------------------------------------------------------------------------
@@ -373,6 +455,25 @@ int conv_thin(ThinArgs a, hipStream_t st) {
       default: launch_thin_n<4>(a, grid, lds, st, th, tw); break;
     }
     return check_launch("thin_n");
+  }
+  // ≤ 32 contraction channels (one quad per lane, 8 taps × NY float4 of weights in registers):
+  // the D-first data gradient (ndf ≤ 32).  The UNet outermost upconv at 2·ngf = 64 stays on
+  // thin_n_class — it is a forward layer, and the f32 step-parity envelopes of the 64³ UNet
+  // fixture were measured with its summation order.
+  if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && a.cx <= 32 && ceil_div(a.k, a.s) == 2 &&
+      (int64_t)a.N * a.Do * a.Ho * a.Wo < ((int64_t)1 << 31) &&
+      (int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx < ((int64_t)1 << 31)) {
+    const int64_t maxq = (int64_t)a.N * ceil_div(a.Do, a.s) * ceil_div(a.Ho, a.s) * ceil_div(a.Wo, a.s);
+    int64_t gx = ceil_div(maxq, 32 * 4);             // ≈ 4 voxels per lane group: the weights load once per 4
+    if (gx > 4096) gx = 4096;
+    dim3 grid((unsigned)gx, a.s * a.s * a.s);
+    switch (a.ny) {
+      case 1: hipLaunchKernelGGL((thin_n_class8_kernel<1, 1>), grid, dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL((thin_n_class8_kernel<2, 1>), grid, dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL((thin_n_class8_kernel<3, 1>), grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL((thin_n_class8_kernel<4, 1>), grid, dim3(256), 0, st, a); break;
+    }
+    return check_launch("thin_n_class8");
   }
   if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0) {
     const int64_t maxq = (int64_t)a.N * ceil_div(a.Do, a.s) * ceil_div(a.Ho, a.s) * ceil_div(a.Wo, a.s);

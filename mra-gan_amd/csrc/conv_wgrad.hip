@@ -315,25 +315,46 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   }
 }
 
-// out[dn][gn][t] (=|+=) Σ_z ws[z][t][dn][gn].  Thread per output with gn fastest, so every
-// slab read of a wave is 256 contiguous bytes; the single store per thread is the strided one.
+// out[dn][gn][t] (=|+=) Σ_z ws[z][t][dn][gn].  Block = one dn × 64 gn × 4 t, one output per
+// thread: every thread's `splits` slab loads are in flight together (a block walking several
+// outputs per thread waits out the slab latency once per output), the slab reads run along gn
+// (64 contiguous floats per (z, t)), and the sums are transposed through LDS so each gn's run of
+// 4 taps is stored contiguously (a store per thread strided by T, plus 64-bit index math per
+// element, took 7.7 µs for a 128×128×27 gradient).  Summation order over z is fixed (groups of
+// four, pairwise): bit-reproducible.
+constexpr int kRedG = 64, kRedT = 4;
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int Cd,
                                                            int Cg, int T, int splits, int accumulate) {
-  const int64_t total = (int64_t)Cd * Cg * T;
-  const int64_t plane = (int64_t)T * Cd * Cg;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int gn = (int)(e % Cg);
-    const int64_t u = e / Cg;
-    const int dn = (int)(u % Cd), t = (int)(u / Cd);
-    const float* src = ws + ((int64_t)t * Cd + dn) * Cg + gn;
-    float s = 0.f;
+  __shared__ float tile[kRedG][kRedT + 1];
+  const int dn = blockIdx.x, g0 = blockIdx.y * kRedG, t0 = blockIdx.z * kRedT;
+  const int tid = threadIdx.x;
+  const int gl = tid % kRedG, tl = tid / kRedG;
+  const int plane = T * Cd * Cg;                      // < 2^31 (host check)
+  if (g0 + gl < Cg && t0 + tl < T) {
+    const float* src = ws + ((t0 + tl) * Cd + dn) * Cg + g0 + gl;
+    float v = 0.f;
     int z = 0;
     for (; z + 4 <= splits; z += 4)
-      s += (src[z * plane] + src[(z + 1) * plane]) + (src[(z + 2) * plane] + src[(z + 3) * plane]);
-    for (; z < splits; ++z) s += src[z * plane];
-    float* dst = out + ((int64_t)dn * Cg + gn) * T + t;
-    *dst = accumulate ? *dst + s : s;
+      v += (src[(int64_t)z * plane] + src[(int64_t)(z + 1) * plane]) +
+           (src[(int64_t)(z + 2) * plane] + src[(int64_t)(z + 3) * plane]);
+    for (; z < splits; ++z) v += src[(int64_t)z * plane];
+    tile[gl][tl] = v;
   }
+  __syncthreads();
+  const int g2 = tid / kRedT, t2 = tid % kRedT;
+  if (g0 + g2 < Cg && t0 + t2 < T) {
+    float* dst = out + ((int64_t)dn * Cg + g0 + g2) * T + t0 + t2;
+    const float v = tile[g2][t2];
+    *dst = accumulate ? *dst + v : v;
+  }
+}
+
+static int launch_wgrad_reduce(const float* ws, float* out, int Cd, int Cg, int T, int splits, int accumulate,
+                               hipStream_t st) {
+  MRAGAN_CHECK_ARG((int64_t)T * Cd * Cg < ((int64_t)1 << 31), "wgrad_reduce: %d x %d x %d too large", Cd, Cg, T);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(Cd, ceil_div(Cg, kRedG), ceil_div(T, kRedT)), dim3(256), 0, st, ws, out,
+                     Cd, Cg, T, splits, accumulate);
+  return check_launch("wgrad_reduce");
 }
 
 static int wgrad_plan(int Cd, int Cg, int T, int64_t M, int* splits, int64_t* chunk, bool* big) {
@@ -378,11 +399,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
                         : conv_wgrad3s2_x3(a, wgrad3s2_x3_splits(a, a.splits), st);
     int rc = check_launch("wgrad3_x3");
     if (rc) return rc;
-    int64_t total = (int64_t)a.Cd * a.Cg * T;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.ws, out, a.Cd, a.Cg, T, used, accumulate);
-    return check_launch("wgrad_reduce");
+    return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, used, accumulate, st);
   }
   const bool idx32 = M * a.Cd < ((int64_t)1 << 31) &&
                      (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31);
@@ -414,11 +431,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   }
   int rc = check_launch("conv_wgrad_f32");
   if (rc) return rc;
-  int64_t total = (int64_t)a.Cd * a.Cg * T;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.ws, out, a.Cd, a.Cg, T, a.splits, accumulate);
-  return check_launch("wgrad_reduce");
+  return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, a.splits, accumulate, st);
 }
 
 }  // namespace mragan

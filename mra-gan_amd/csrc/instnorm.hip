@@ -5,7 +5,9 @@
 //             output (the ReplicationPad3d that precedes the next conv, networks3D.py:185/211/
 //             233/249) — so neither the pad nor the activation costs a separate pass.
 //   backward: g = fold(dy_padded) (+ dy_add) (ReplicationPad3d backward), × act'(x̂),
-//             dx = rstd·(g − mean(g) − x̂·mean(g·x̂)).
+//             dx = rstd·(g − mean(g) − x̂·mean(g·x̂)); optionally also writes the folded g
+//             before act' (a ResnetBlock's input gradient, which its skip path needs again) —
+//             the separate rpad_fold pass then disappears.
 // Statistics are accumulated in fp64 from fp32 data (per-thread → block → chunk partials),
 // so the single-pass Σx / Σx² form keeps full fp32 accuracy.
 #include "kernels.h"
@@ -208,7 +210,7 @@ __device__ __forceinline__ InRow in_bwd_row(const InBwdArgs& a, const InShape& s
 }
 
 __device__ __forceinline__ void in_bwd_voxel(const InBwdArgs& a, const InShape& s, const InRow& r, int w, float4& g,
-                                             float4& xh) {
+                                             float4& xh, float4* graw = nullptr) {
   const int CQ = s.C / 4, p = a.dypad;
   const int w0 = w == 0 ? 0 : w + p, w1 = w == s.W - 1 ? s.W - 1 + 2 * p : w + p;
   g = r.dy[w0 * CQ];
@@ -227,6 +229,7 @@ __device__ __forceinline__ void in_bwd_voxel(const InBwdArgs& a, const InShape& 
     const float4 e = r.add[w * CQ];
     g.x += e.x; g.y += e.y; g.z += e.z; g.w += e.w;
   }
+  if (graw) *graw = g;
   const float4 xv = r.x[w * CQ];
   xh = make_float4((xv.x - r.mu.x) * r.rs.x, (xv.y - r.mu.y) * r.rs.y, (xv.z - r.mu.z) * r.rs.z,
                    (xv.w - r.mu.w) * r.rs.w);
@@ -269,9 +272,11 @@ __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape 
     const float4 c0 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[0];   // (mg0, mgx0, mg1, mgx1)
     const float4 c1 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[1];
     float4* out = dx + (size_t)rr * s.W * CQ + q;
+    float4* gout = a.g_out ? reinterpret_cast<float4*>(a.g_out) + (size_t)rr * s.W * CQ + q : nullptr;
     for (int w = wt; w < s.W; w += WS) {
-      float4 g, xh;
-      in_bwd_voxel(a, s, row, w, g, xh);
+      float4 g, xh, graw;
+      in_bwd_voxel(a, s, row, w, g, xh, &graw);
+      if (gout) gout[w * CQ] = graw;
       float4 o;
       o.x = row.rs.x * (g.x - c0.x - xh.x * c0.y);
       o.y = row.rs.y * (g.y - c0.z - xh.y * c0.w);

@@ -112,6 +112,7 @@ struct InBwdArgs {
   const float* x; const float* mean; const float* rstd;
   const float* dy; int dypad; const float* dy_add; int act;
   float* dx;
+  float* g_out;        // optional: g = fold(dy) + dy_add before act' (the ResnetBlock's input gradient)
 };
 int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
                  float* rstd, void* ws, size_t ws_bytes, hipStream_t st);

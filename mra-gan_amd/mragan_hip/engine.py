@@ -240,8 +240,14 @@ class NetPlan:
             st, sc = self.stages[i], ctx.stages[i]
             want_dgrad = i > 0 or need_input_grad
             if st.kind == "block":
-                G = g if (gpad == 0 and gadd is None) else ops.rpad_fold(g, gpad, add=gadd)
-                dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                if gpad == 0 and gadd is None:
+                    G = g
+                    dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                else:
+                    # the block-output gradient G = fold(g) + skip gradient is needed again below
+                    # (the skip path): the IN backward writes it in the same pass
+                    G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
+                    dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
                     st.conv2.wgrad(sc.z1, dh2)
                 dz1 = st.conv2.dgrad(dh2, sc.z1.shape[1:4])

@@ -294,7 +294,10 @@ def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch
 
 
 def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int = 0,
-                 dy_add: Optional[torch.Tensor] = None, act=None, out: Optional[torch.Tensor] = None):
+                 dy_add: Optional[torch.Tensor] = None, act=None, out: Optional[torch.Tensor] = None,
+                 g_out: Optional[torch.Tensor] = None):
+    """dx of InstanceNorm(+act) from dy (replication-padded by dypad: folded) + dy_add.  With
+    g_out, the folded gradient before act' is written there in the same pass (ABI 8)."""
     _check(x, "instnorm_bwd.x")
     N, D, H, W, C = x.shape
     if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
@@ -305,10 +308,18 @@ def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: to
     ws = WS.get(nbytes)
     # essential HBM bytes: read x, dy (padded) (+ dy_add), write dx
     tm = TIMER.begin(dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad}",
-                          bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0))))\
+                          bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                           + (x.numel() if g_out is not None else 0))))\
         if TIMER.match else None
-    call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
-         ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
+    if g_out is None:
+        call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
+             ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
+    else:
+        _check(g_out, "instnorm_bwd.g_out")
+        if tuple(g_out.shape) != tuple(x.shape):
+            raise ValueError("instnorm_bwd: g_out shape mismatch")
+        call("mragan_instnorm_bwd_g", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
+             ACT[act], _ptr(out), _ptr(g_out), _ptr(ws), ws.numel(), _stream())
     TIMER.end(tm)
     return out
 

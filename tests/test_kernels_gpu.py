@@ -142,6 +142,14 @@ CONVT_CASES = [
     (1, 128, 32, 4, 4, 2, 1, 0),
     (2, 16, 1, 8, 4, 2, 1, 0),
     (1, 16, 2, 6, 4, 2, 1, 0),
+    # thin_n_class8 (≤ 4 outputs, ≤ 32 contraction channels, ceil(k/s) = 2): the D-first
+    # data-gradient shape (32 → 1, k4 s2 p1), partial lane groups, k3 s2 with output padding, 4
+    # outputs; 64 / 40 channels take thin_n_class
+    (2, 32, 1, 9, 4, 2, 1, 0),
+    (1, 24, 3, 4, 3, 2, 1, 1),
+    (2, 8, 4, 5, 4, 2, 1, 0),
+    (1, 64, 2, 5, 4, 2, 1, 0),
+    (1, 40, 3, 4, 3, 2, 1, 1),
 ]
 
 
@@ -334,6 +342,24 @@ def test_instnorm_bwd(ops, N, C, S, act, dypad, with_add):
     dx = ops.instnorm_bwd(xg, mean, rstd, ndhwc(dyp.float()).cuda(), dypad,
                           ndhwc(add.float()).cuda() if with_add else None, act=act)
     assert rel(ncdhw(dx), dx_ref) < 5e-5
+
+
+@pytest.mark.parametrize("C,dypad,act", [(128, 1, None), (32, 3, "relu"), (8, 0, "lrelu")])
+def test_instnorm_bwd_g_out(ops, C, dypad, act):
+    """mragan_instnorm_bwd_g: dx as mragan_instnorm_bwd, and g_out = fold(dy) + dy_add (the
+    ResnetBlock input gradient that replaces a separate rpad_fold pass) equal to rpad_fold's."""
+    g = torch.Generator().manual_seed(C + dypad)
+    x = torch.randn(2, C, 5, 6, 7, generator=g, dtype=torch.float64)
+    xg = ndhwc(x.float()).cuda()
+    _, mean, rstd = ops.instnorm_fwd(xg, act=act)
+    dyp = ndhwc(torch.randn(2, C, 5 + 2 * dypad, 6 + 2 * dypad, 7 + 2 * dypad, generator=g).float()).cuda()
+    add = ndhwc(torch.randn(2, C, 5, 6, 7, generator=g).float()).cuda()
+    dx_ref = ops.instnorm_bwd(xg, mean, rstd, dyp, dypad, add, act=act)
+    G = torch.full_like(xg, float("nan"))
+    dx = ops.instnorm_bwd(xg, mean, rstd, dyp, dypad, add, act=act, g_out=G)
+    assert torch.equal(dx, dx_ref)
+    G_ref = ops.rpad_fold(dyp, dypad, add=add) if dypad else dyp + add
+    assert rel(G, G_ref) < 1e-6          # border voxels: the same terms summed in another order
 
 
 def test_instnorm_single_voxel_raises(ops):

@@ -62,7 +62,10 @@ def main():
     x_dn2 = rnd(N, s2, s2, s2, 2 * ngf)
     dy_dn2 = rnd(N, s4, s4, s4, c4)
     gw_dn2 = torch.empty(27 * 2 * ngf * c4, device=dev)
+    dy_df = rnd(N, s2, s2, s2, ngf)                      # D first layer output gradient (ndf = ngf)
+    w_df = rnd(64 * ngf) * 0.01
     table = {
+        "dfirst_dgrad": lambda: ops.conv3d(dy_df, w_df, 1, 4, 2, 1, (S, S, S), transposed=True),
         "down1_wgrad": lambda: ops.conv3d_wgrad(dy_dn1, x_dn1, 3, 2, 1, gw_dn1, False),
         "down2_wgrad": lambda: ops.conv3d_wgrad(dy_dn2, x_dn2, 3, 2, 1, gw_dn2, False),
         "dlast_fwd": lambda: ops.conv3d(x_dl, w_dl, 1, 4, 1, 1, (S // 8 - 2,) * 3),
