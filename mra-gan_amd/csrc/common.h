@@ -67,6 +67,11 @@ __device__ __forceinline__ float4 buf_load_f32x4(__amdgpu_buffer_rsrc_t r, uint3
   const buf_f32x4 v = llvm_raw_buffer_load_f32x4(r, (int)byte_off, 0, 0);
   return make_float4(v.x, v.y, v.z, v.w);
 }
+// 16 bytes at voffset (per lane, VGPR) + soffset (wave-uniform, SGPR): a streamed operand whose
+// per-step offset is uniform costs no VALU address arithmetic
+__device__ __forceinline__ buf_f32x4 buf_load_16b(__amdgpu_buffer_rsrc_t r, int voffset, int soffset) {
+  return llvm_raw_buffer_load_f32x4(r, voffset, soffset, 0);
+}
 
 }  // namespace mragan
 

@@ -138,20 +138,26 @@ conv_brick_x3_kernel(BrickArgs a) {
     const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
     abase[i] = ((bd * a.HH + bh) * a.HW + bw) * kRow + lh * 16;
   }
-  // B: this lane's 16-B fragment inside each (tap, chunk, half, hi|lo) block of the packed weights
-  const __bf16* wx = reinterpret_cast<const __bf16*>(a.wx3);
+  // B: this lane's 16-B fragment inside each (tap, chunk, half, hi|lo) block of the packed weights,
+  // read through a buffer descriptor: the lane part of the offset is fixed (VGPR), the step part
+  // is wave-uniform (SGPR soffset) — no per-step 64-bit address arithmetic in VALU (the flat-
+  // pointer form spent ~5 VALU instructions per weight load)
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.wx3, __builtin_amdgcn_readfirstlane(kTaps * a.C * a.ny * 4));
   int boff[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) boff[j] = (n0 + wn0 + j * 32 + li) * 16 + lh * 8;
-  const int nch_ = a.C / kBK;
-  const int64_t blk = (int64_t)a.ny * 16;       // one (hi|lo) block
+  for (int j = 0; j < TN; ++j) boff[j] = ((n0 + wn0 + j * 32 + li) * 16 + lh * 8) * 2;
+  // uniform scalars (readfirstlane: the compiler otherwise keeps the chunk loop's bound in a VGPR
+  // and every offset derived from the chunk index with it)
+  const int nch_ = __builtin_amdgcn_readfirstlane(a.C / kBK);
+  const int flip = __builtin_amdgcn_readfirstlane(a.flip);
+  const int blkb = a.ny * 16 * 2;               // bytes of one (hi|lo) block
   // halo loads through the instance's range-checked descriptor: an out-of-volume position gets
   // an offset past the end and reads 0, with no select on the loaded value (a conditional
   // overwrite made hipcc drain the memory counter — the 9-step weight prefetch included — at
   // every halo load)
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C,
                                               (uint32_t)a.Di * a.Hi * a.Wi * a.C * 4u);
-  const int nchunks = a.C / kBK;
+  const int nchunks = nch_;
   __syncthreads();
 
   // whole halo of chunk 0
@@ -174,12 +180,12 @@ conv_brick_x3_kernel(BrickArgs a) {
   bf16x8 rb[kPF][TN][2];
   auto b_load = [&](int chunk, int u, bf16x8 (&dst)[TN][2]) __attribute__((always_inline)) {
     const int t = u >> 1, kk = u & 1;
-    const int tap = a.flip ? kTaps - 1 - t : t;
-    const __bf16* src = wx + (((int64_t)tap * nch_ + chunk) * 2 + kk) * 2 * blk;
+    const int tap = flip ? kTaps - 1 - t : t;
+    const int sb = __builtin_amdgcn_readfirstlane(((tap * nch_ + chunk) * 2 + kk) * 2 * blkb);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      dst[j][0] = *reinterpret_cast<const bf16x8*>(src + boff[j]);
-      if constexpr (prec::has_lo<PM>()) dst[j][1] = *reinterpret_cast<const bf16x8*>(src + blk + boff[j]);
+      dst[j][0] = __builtin_bit_cast(bf16x8, buf_load_16b(wr, boff[j], sb));
+      if constexpr (prec::has_lo<PM>()) dst[j][1] = __builtin_bit_cast(bf16x8, buf_load_16b(wr, boff[j], sb + blkb));
     }
   };
 #pragma unroll

@@ -62,6 +62,8 @@ def main():
     x_dn2 = rnd(N, s2, s2, s2, 2 * ngf)
     dy_dn2 = rnd(N, s4, s4, s4, c4)
     gw_dn2 = torch.empty(27 * 2 * ngf * c4, device=dev)
+    x_in16 = rnd(N, s4, s4, s4, c4)                      # res-block InstanceNorm [N x 16^3 x 128]
+    dy_in16 = rnd(N, s4 + 2, s4 + 2, s4 + 2, c4)
     dy_df = rnd(N, s2, s2, s2, ngf)                      # D first layer output gradient (ndf = ngf)
     w_df = rnd(64 * ngf) * 0.01
     table = {
@@ -81,6 +83,9 @@ def main():
         "res_dgrad": lambda: ops.conv3d(dy_res, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, transposed=True),
         "res_wgrad": lambda: ops.conv3d_wgrad(dy_res, x_res, 3, 1, 0, gw_res, False),
         "in_fwd": lambda: ops.instnorm_fwd(x_in, act="relu", ypad=3),
+        "in_fwd16": lambda: ops.instnorm_fwd(x_in16, act="relu", ypad=1),
+        "in_bwd16": lambda: ops.instnorm_bwd(x_in16, *ops.instnorm_fwd(x_in16, act="relu")[1:], dy_in16, 1, None,
+                                             act="relu"),
         "in_bwd": lambda: ops.instnorm_bwd(x_in, *ops.instnorm_fwd(x_in, act="relu")[1:], dy_in, 3, None, act="relu"),
     }
     names = list(table) if args.ops == "all" else args.ops.split(",")
