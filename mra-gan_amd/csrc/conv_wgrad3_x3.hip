@@ -110,33 +110,49 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   const int uw2 = 16 + tid / GQ;
 
   float4 rd[kR], rg[kR], rg2[kR];
-  // (n, d, h, w-segment) of the stage's first row segment, advanced with carries (the per-segment
-  // divisions cost ~600 scalar instructions per stage)
+  // dY / X through buffer descriptors: the segment part of each offset is wave-uniform (SGPR
+  // soffset), the lane part fixed per thread (VGPR) — no per-load 64-bit address arithmetic
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * 4));
+  const __amdgpu_buffer_rsrc_t xgr = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * 4));
+  const int dlane = (uw * a.Cd + co0 + 4 * cq) * 4;
+  const int glane = ((g1 ? gw : 0) * a.Cg + ci0 + 4 * gcq) * 4;
+  const int glane2 = ((g2 ? uw2 : gw) * a.Cg + ci0 + 4 * gcq) * 4;
+  // Segments are 16-voxel runs of dY in (n, d, h, w) order, so a segment's dY offset is linear in
+  // its index; its X offset (padded volume, shifted by (kd, kh)) is carried along with (h, d, n)
+  // carries — no per-segment index arithmetic (divisions cost ~600 scalar instructions per
+  // stage, the recomputed products ~100)
+  const int dseg = kSegW * a.Cd * 4;                          // dY bytes per segment
+  const int gw16 = kSegW * a.Cg * 4, grow = (Wg - a.W) * a.Cg * 4;
+  const int gplane = (Hg - a.H) * Wg * a.Cg * 4, gvol = (Dg - a.D) * Hg * Wg * a.Cg * 4;
+  const int gkdh = (kd * Hg + kh) * Wg * a.Cg * 4;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
-  auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
-    if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
+  int sxo = (((sn * Dg + sd) * Hg + sh) * Wg + sw * kSegW) * a.Cg * 4;
+  auto bump = [&](int& w_, int& h_, int& d_, int& xo) __attribute__((always_inline)) {
+    xo += gw16;
+    if (++w_ == nsw) {
+      w_ = 0; xo += grow;
+      if (++h_ == a.H) { h_ = 0; xo += gplane; if (++d_ == a.D) { d_ = 0; xo += gvol; } }
+    }
   };
   auto load = [&](int st) __attribute__((always_inline)) {
-    int cw = sw, chh = sh, cdd = sd, cn = sn;
+    int cw = sw, chh = sh, cdd = sd, cxo = sxo;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int seg = seg_lo + st * kR + r;
       const bool ok = seg < seg_hi;
-      // past the split's end: re-read segment (cw, …) clamped to a valid row (masked to zero)
-      const int n = ok ? cn : 0, d = ok ? cdd : 0, h = ok ? chh : 0;
-      const int w0 = (ok ? cw : 0) * kSegW;
-      bump(cw, chh, cdd, cn);
-      const float4 dv = *reinterpret_cast<const float4*>(
-          a.dy + ((((n * a.D + d) * a.H + h) * a.W + w0 + uw) * a.Cd + co0 + 4 * cq));
-      const int gbase = ((n * Dg + d + kd) * Hg + h + kh) * Wg + w0;
-      const float4 gv = *reinterpret_cast<const float4*>(a.x + ((gbase + (g1 ? gw : 0)) * a.Cg + ci0 + 4 * gcq));
+      // past the split's end: re-read segment 0 (a valid row, masked to zero)
+      const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
+      const int gso = __builtin_amdgcn_readfirstlane((ok ? cxo : 0) + gkdh);
+      bump(cw, chh, cdd, cxo);
+      const buf_f32x4 dv = buf_load_16b(dyr, dlane, dso);
+      const buf_f32x4 gv = buf_load_16b(xgr, glane, gso);
       // per-component selects (a float4 `ok ? v : zero` is lowered through scratch memory)
       rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
       rg[r] = make_float4(ok ? gv.x : 0.f, ok ? gv.y : 0.f, ok ? gv.z : 0.f, ok ? gv.w : 0.f);
       // w' = 16, 17 (threads < 2·GQ; the others re-read their own unit: keeps rg2 a plain register
       // array, a conditionally written one goes to scratch)
       if constexpr (kSplitG) {
-        const float4 g = *reinterpret_cast<const float4*>(a.x + ((gbase + (g2 ? uw2 : gw)) * a.Cg + ci0 + 4 * gcq));
+        const buf_f32x4 g = buf_load_16b(xgr, glane2, gso);
         rg2[r] = make_float4(ok ? g.x : 0.f, ok ? g.y : 0.f, ok ? g.z : 0.f, ok ? g.w : 0.f);
       }
     }
@@ -179,7 +195,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
     __syncthreads();
     if (st + 1 < nstage) {                          // lands during this stage's MFMAs
 #pragma unroll
-      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
+      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
       load(st + 1);
     }
     const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
@@ -229,8 +245,8 @@ static bool w3_wide(const WgradArgs& a) { return a.Cd % 128 == 0 && a.Cg % 64 ==
 bool wgrad3_x3_applicable(const WgradArgs& a) {
   return a.x3 && a.k == 3 && a.s == 1 && a.p == 0 && a.Wd % kSegW == 0 && a.Dg == a.Dd + 2 && a.Hg == a.Hd + 2 &&
          a.Wg == a.Wd + 2 && a.Cd % kTile == 0 && a.Cg % kTile == 0 &&
-         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31) &&
-         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd < ((int64_t)1 << 31);
+         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg * 4 < ((int64_t)1 << 31) &&     // byte offsets are 32-bit
+         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd * 4 < ((int64_t)1 << 31);
 }
 
 // splits: at most 2 blocks per CU in total (one round: a 513th block doubles the time),
