@@ -144,16 +144,16 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
       const int gso = __builtin_amdgcn_readfirstlane((ok ? cxo : 0) + gkdh);
       bump(cw, chh, cdd, cxo);
-      const buf_f32x4 dv = buf_load_16b(dyr, dlane, dso);
-      const buf_f32x4 gv = buf_load_16b(xgr, glane, gso);
-      // per-component selects (a float4 `ok ? v : zero` is lowered through scratch memory)
-      rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
-      rg[r] = make_float4(ok ? gv.x : 0.f, ok ? gv.y : 0.f, ok ? gv.z : 0.f, ok ? gv.w : 0.f);
+      // past the split's end: an out-of-range voffset reads zeros (no select on the values)
+      const buf_f32x4 dv = buf_load_16b(dyr, ok ? dlane : (int)kOobOffset, dso);
+      const buf_f32x4 gv = buf_load_16b(xgr, ok ? glane : (int)kOobOffset, gso);
+      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      rg[r] = make_float4(gv.x, gv.y, gv.z, gv.w);
       // w' = 16, 17 (threads < 2·GQ; the others re-read their own unit: keeps rg2 a plain register
       // array, a conditionally written one goes to scratch)
       if constexpr (kSplitG) {
-        const buf_f32x4 g = buf_load_16b(xgr, glane2, gso);
-        rg2[r] = make_float4(ok ? g.x : 0.f, ok ? g.y : 0.f, ok ? g.z : 0.f, ok ? g.w : 0.f);
+        const buf_f32x4 g = buf_load_16b(xgr, ok ? glane2 : (int)kOobOffset, gso);
+        rg2[r] = make_float4(g.x, g.y, g.z, g.w);
       }
     }
   };

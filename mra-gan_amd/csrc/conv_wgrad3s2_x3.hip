@@ -105,6 +105,13 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const bool gx = gqx < kGPos;
 
   float4 rd[kR], rg[2][kR], rgx[kR];
+  // D / G rows through buffer descriptors: segment / row parts of the offsets are wave-uniform
+  // (SGPR soffset); out-of-range rows and positions read zeros through an out-of-range voffset
+  // (no select on the loaded values, no 64-bit address arithmetic)
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.d, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * 4));
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.g, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * 4));
+  const int dlane = (uw * a.Cd + dn0 + 4 * cq) * 4;
+  const int dseg = kSegW * a.Cd * 4;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
   auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
     if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
@@ -118,16 +125,18 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       const int n = ok ? cn : 0, d = ok ? cdd : 0, h = ok ? chh : 0;
       const int w0 = (ok ? cw : 0) * kSegW;
       bump(cw, chh, cdd, cn);
-      const float4 dv = *reinterpret_cast<const float4*>(a.d + ((((n * a.D + d) * a.H + h) * a.W + w0 + uw) * a.Cd + dn0 + 4 * cq));
-      rd[r] = make_float4(ok ? dv.x : 0.f, ok ? dv.y : 0.f, ok ? dv.z : 0.f, ok ? dv.w : 0.f);
+      // D segments are contiguous 16-voxel runs: offset linear in the segment index
+      const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
+      const buf_f32x4 dv = buf_load_16b(dr, ok ? dlane : (int)kOobOffset, dso);
+      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
       const int gd = 2 * d - 1 + kd, gh = 2 * h - 1 + kh;
       const bool rok = ok && (unsigned)gd < (unsigned)Dg && (unsigned)gh < (unsigned)Hg;
-      const int grow = ((n * Dg + (rok ? gd : 0)) * Hg + (rok ? gh : 0)) * Wg;
+      const int gso = __builtin_amdgcn_readfirstlane(rok ? ((n * Dg + gd) * Hg + gh) * Wg * a.Cg * 4 : 0);
       auto gload = [&](int q) __attribute__((always_inline)) {
         const int p = 2 * w0 - 1 + q;
         const bool pok = rok && (unsigned)p < (unsigned)Wg;
-        const float4 v = *reinterpret_cast<const float4*>(a.g + ((int64_t)(grow + (pok ? p : 0)) * a.Cg + gn0 + 4 * gcq));
-        return make_float4(pok ? v.x : 0.f, pok ? v.y : 0.f, pok ? v.z : 0.f, pok ? v.w : 0.f);
+        const buf_f32x4 v = buf_load_16b(gr, pok ? (p * a.Cg + gn0 + 4 * gcq) * 4 : (int)kOobOffset, gso);
+        return make_float4(v.x, v.y, v.z, v.w);
       };
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass) rg[pass][r] = gload(pass * GP + gq);
@@ -228,8 +237,8 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
 bool wgrad3s2_x3_applicable(const WgradArgs& a) {
   return a.x3 && a.k == 3 && a.s == 2 && a.p == 1 && a.Wd % kSegW == 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
          a.Wg == 2 * a.Wd && a.Cd % kTD == 0 && (a.Cg % 64 == 0 || a.Cg == 32) &&
-         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31) &&
-         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd < ((int64_t)1 << 31);
+         (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg * 4 < ((int64_t)1 << 31) &&     // byte offsets are 32-bit
+         (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd * 4 < ((int64_t)1 << 31);
 }
 
 static int s2_tg(const WgradArgs& a) { return a.Cg % 64 == 0 ? 64 : 32; }
