@@ -116,36 +116,54 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int nK = min(nK_all, ks0 + kper) - ks0;       // steps of this slice: ks0 … ks0+nK−1
   float4 ra[A_LOADS], rb[B_LOADS];
 
-  auto load_tiles = [&](int ksl) {
-    const int ks = ks0 + ksl;
-    int tap = ks / kchunks;
-    int c0 = (ks - tap * kchunks) * BK;
-    int jw = tap % gw.ntap; int tt = tap / gw.ntap;
-    int jh = tt % gh.ntap; int jd = tt / gh.ntap;
-    int td = gd.t0 + gd.tstep * jd, th = gh.t0 + gh.tstep * jh, tw = gw.t0 + gw.tstep * jw;
-    int wt = (td * a.k + th) * a.k + tw;
-    int dd = gd.sign * jd, dh = gh.sign * jh, dw = gw.sign * jw;
+  // Operands through buffer descriptors (byte offsets are 32-bit: the host checks the sizes).
+  // A: per thread and row a fixed base offset of its (nb, bd, bh, bw) voxel + channel quad; a
+  // K-step adds a wave-uniform tap / channel offset, and a tap outside the input (padding) reads
+  // zeros through an out-of-range voffset.  B: the lane part is fixed, the step part is the
+  // SGPR soffset.  K-steps advance (channel chunk, kw, kh, kd) with carries: no per-step
+  // divisions, no 64-bit address arithmetic.
+  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * 4));
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4));
+  int a_base[A_LOADS];
+#pragma unroll
+  for (int i = 0; i < A_LOADS; ++i)
+    a_base[i] = ((((a_nb[i] < 0 ? 0 : a_nb[i]) * a.Di + a_bd[i]) * a.Hi + a_bh[i]) * a.Wi + a_bw[i]) * a.cx * 4 + 16 * q;
+  int b_voff[B_LOADS];
+#pragma unroll
+  for (int i = 0; i < B_LOADS; ++i) {
+    const int r = tid / LPR + i * ROWS_PER_PASS, n = n0 + r;
+    b_voff[i] = (r < BN && n < a.ny) ? (n * a.cx * 4 + 16 * q) : (int)kOobOffset;
+  }
+  int kc = ks0 % kchunks, tap0 = ks0 / kchunks;
+  int kjw = tap0 % gw.ntap, kjh = (tap0 / gw.ntap) % gh.ntap, kjd = tap0 / gw.ntap / gh.ntap;
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (++kc == kchunks) {
+      kc = 0;
+      if (++kjw == gw.ntap) { kjw = 0; if (++kjh == gh.ntap) { kjh = 0; ++kjd; } }
+    }
+  };
+
+  auto load_tiles = [&]() __attribute__((always_inline)) {
+    const int c0 = kc * BK;
+    const int td = gd.t0 + gd.tstep * kjd, th = gh.t0 + gh.tstep * kjh, tw = gw.t0 + gw.tstep * kjw;
+    const int wt = (td * a.k + th) * a.k + tw;
+    const int dd = gd.sign * kjd, dh = gh.sign * kjh, dw = gw.sign * kjw;
+    const int toff = __builtin_amdgcn_readfirstlane((((dd * a.Hi + dh) * a.Wi + dw) * a.cx + c0) * 4);
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
-      int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
-      bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
-                (unsigned)iw < (unsigned)a.Wi;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
-        const float* src = a.x + ((((int64_t)a_nb[i] * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 + 4 * q;
-        v = *reinterpret_cast<const float4*>(src);
-      }
-      ra[i] = v;
+      const int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
+      const bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
+                      (unsigned)iw < (unsigned)a.Wi;
+      const buf_f32x4 v = buf_load_16b(xrs, ok ? a_base[i] + toff : (int)kOobOffset, 0);
+      ra[i] = make_float4(v.x, v.y, v.z, v.w);
     }
+    const int wso = __builtin_amdgcn_readfirstlane((wt * a.ny * a.cx + c0) * 4);
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
-      int r = tid / LPR + i * ROWS_PER_PASS;
-      int n = n0 + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < BN && n < a.ny)
-        v = *reinterpret_cast<const float4*>(a.w + ((int64_t)wt * a.ny + n) * a.cx + c0 + 4 * q);
-      rb[i] = v;
+      const buf_f32x4 v = buf_load_16b(wrs, b_voff[i], wso);
+      rb[i] = make_float4(v.x, v.y, v.z, v.w);
     }
+    advance();
   };
   auto store_tiles = [&](int buf) {
     __bf16* st = smem + buf * STAGE;
@@ -179,7 +197,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   if (nK > 0) {
-    load_tiles(0);
+    load_tiles();
     store_tiles(0);
   }
   __syncthreads();
@@ -188,7 +206,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int lh = lane >> 5;
   for (int ks = 0; ks < nK; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nK) load_tiles(ks + 1);
+    if (ks + 1 < nK) load_tiles();
     const __bf16* Ah = smem + buf * STAGE;
     const __bf16* Al = Ah + PLANE_A;
     const __bf16* Bh = Ah + 2 * PLANE_A;
@@ -327,6 +345,11 @@ static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int cfg, int splits, 
 }
 
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  // operand byte offsets are 32-bit (buffer descriptors)
+  MRAGAN_CHECK_ARG((int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx * 4 < ((int64_t)1 << 31) &&
+                       (int64_t)a.k * a.k * a.k * a.ny * a.cx * 4 < ((int64_t)1 << 31),
+                   "conv (16-bit MFMA modes): input of %d×%d×%d×%d×%d too large for one launch", a.N, a.Di, a.Hi, a.Wi,
+                   a.cx);
   X3Plan pl = x3_plan(a, total_m);
   if (pl.splits > 1) {
     const size_t need = (size_t)pl.splits * total_m * a.ny * sizeof(float);

@@ -66,7 +66,15 @@ def main():
     dy_in16 = rnd(N, s4 + 2, s4 + 2, s4 + 2, c4)
     dy_df = rnd(N, s2, s2, s2, ngf)                      # D first layer output gradient (ndf = ngf)
     w_df = rnd(64 * ngf) * 0.01
+    x_up1 = rnd(N, s4, s4, s4, c4)                        # G up1 ConvTranspose3d(128 -> 64, k3 s2) input
+    w_up1 = rnd(27 * c4 * 2 * ngf) * 0.01
+    w_dn2 = rnd(27 * 2 * ngf * c4) * 0.01
+    x_d2 = rnd(N, s2, s2, s2, ngf)                        # PatchGAN layer 2 Conv3d(ndf -> 2ndf, k4 s2 p1) input
+    w_d2 = rnd(64 * ngf * 2 * ngf) * 0.01
     table = {
+        "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
+        "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
+        "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
         "dfirst_dgrad": lambda: ops.conv3d(dy_df, w_df, 1, 4, 2, 1, (S, S, S), transposed=True),
         "down1_wgrad": lambda: ops.conv3d_wgrad(dy_dn1, x_dn1, 3, 2, 1, gw_dn1, False),
         "down2_wgrad": lambda: ops.conv3d_wgrad(dy_dn2, x_dn2, 3, 2, 1, gw_dn2, False),
