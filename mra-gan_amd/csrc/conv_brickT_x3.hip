@@ -137,8 +137,10 @@ brickT_x3_kernel(BrickTArgs a) {
   const int vol_bytes = a.Di * a.Hi * a.Wi * a.C * 4;     // < 2^31 (brickT_x3_applicable)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C, 0, vol_bytes, 0x00020000);
-  const int nch = a.C / kBK;
-  const int blkw = a.ny * 32;                                        // one (hi|lo) block, bytes
+  // uniform scalars (readfirstlane: otherwise the chunk loop bound and every offset derived
+  // from the chunk index live in VGPRs)
+  const int nch = __builtin_amdgcn_readfirstlane(a.C / kBK);
+  const int blkw = __builtin_amdgcn_readfirstlane(a.ny * 32);        // one (hi|lo) block, bytes
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<__bf16*>(a.wx), 0, K * K * K * nch * 4 * blkw, 0x00020000);
   __syncthreads();
@@ -185,7 +187,7 @@ brickT_x3_kernel(BrickTArgs a) {
   // weights of step i: tap ts.s[i/2], half i&1 — one 16-B hi and lo fragment per lane; the step
   // offset is wave-uniform (soffset), the lane part a constant voffset
   auto b_load = [&](int chunk, int i, bf16x8 (&dst)[2]) __attribute__((always_inline)) {
-    const int so = (((ts.s[i >> 1].tap * nch + chunk) * 2 + (i & 1)) * 2) * blkw;
+    const int so = __builtin_amdgcn_readfirstlane((((ts.s[i >> 1].tap * nch + chunk) * 2 + (i & 1)) * 2) * blkw);
     dst[0] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so));
     if constexpr (prec::has_lo<PM>()) dst[1] = __builtin_bit_cast(bf16x8, bload(wr, wlane, so + blkw));
     else dst[1] = dst[0];
@@ -215,7 +217,7 @@ brickT_x3_kernel(BrickTArgs a) {
       // a branch here makes the compiler unswitch the loop and serialize the copy without it)
       if (i == 0) {
 #pragma unroll
-        for (int sl = 0; sl < kSL; ++sl) pv[sl] = xload(halo_off(sl), cn * kBK * 4);
+        for (int sl = 0; sl < kSL; ++sl) pv[sl] = xload(halo_off(sl), __builtin_amdgcn_readfirstlane(cn * kBK * 4));
       }
       if (i == kHD) {
 #pragma unroll

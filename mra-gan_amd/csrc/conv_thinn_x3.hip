@@ -157,7 +157,10 @@ thinn_x3_kernel(ThinnArgs a) {
     for (int i = 0; i < 5; ++i) acc[sl][i] = f32x4{};
   const int n16 = lane & 15, g = lane >> 4;
   const int a_hi = 16 * ((g & 1) ^ thinn_rot(n16)), a_lo = 16 * ((2 + (g & 1)) ^ thinn_rot(n16));
-  const __bf16* wx = a.wx;
+  // weight fragments through a buffer descriptor: lane part fixed (VGPR), (plane, half, step)
+  // part wave-uniform (SGPR soffset) — no 64-bit address arithmetic per fragment
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.wx, 8 * 2 * 4 * 2 * 64 * 8 * 2);
+  const int wlane = lane * 16;
   const float bias = a.bias ? a.bias[0] : 0.f;
   const int oh = oh0 + wave;
 
@@ -202,9 +205,9 @@ thinn_x3_kernel(ThinnArgs a) {
       for (int sl = 0; sl < 4; ++sl) {
         const int j = jlo + ((sl - jlo) & 3);
         const int kdp = j <= jhi ? kk - 2 * j : 0;
-        const __bf16* wt = wx + ((int64_t)((kdp * 2 + half) * 4 + s) * 2) * 64 * 8 + lane * 8;
-        bh[sl] = *reinterpret_cast<const bf16x8*>(wt);
-        bl[sl] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(wt + 64 * 8) : bh[sl];
+        const int wso = __builtin_amdgcn_readfirstlane((((kdp * 2 + half) * 4 + s) * 2) * 64 * 8 * 2);
+        bh[sl] = __builtin_bit_cast(bf16x8, buf_load_16b(wr, wlane, wso));
+        bl[sl] = prec::has_lo<PM>() ? __builtin_bit_cast(bf16x8, buf_load_16b(wr, wlane, wso + 64 * 8 * 2)) : bh[sl];
       }
       int kh = 2 * s + (g >> 1);
       kh = kh < kK ? kh : kK - 1;               // the padding kh = 7 has zero weights
