@@ -383,17 +383,27 @@ class CycleGANModel(BaseModel):
         self._A, self._B, self._b = A, B, b
         self._idt = self.opt.lambda_identity > 0
         pGA, pGB = self.netG_A.plan, self.netG_B.plan
-        # both lanes read both generators' packed weights: pack before the fork
-        for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
-            n.plan.ensure_packed()
+        # each lane packs the networks it runs first (G_A, D_A on lane 0; G_B, D_B on lane 1) and
+        # waits for the other lane's generator pack only before its cycle pass: the four repacks
+        # no longer run serially ahead of the fork
         ln = self._lanes()
+        with ln.on(0):
+            pGA.ensure_packed()
+            self.netD_A.plan.ensure_packed()
+            packed_0 = ln.mark(0)
+        with ln.on(1):
+            pGB.ensure_packed()
+            self.netD_B.plan.ensure_packed()
+            packed_1 = ln.mark(1)
         with ln.on(0):          # lane 0: G_A(real_A) → G_B(fake_B)
             self._cGA1 = pGA.forward(torch.cat([A, B], 0) if self._idt else A)   # [fake_B; idt_A]
             fake_B = self._cGA1.out[:b]
+            ln.wait(0, packed_1)
             self._cGB2 = pGB.forward(fake_B)                     # rec_A
         with ln.on(1):          # lane 1: G_B(real_B) → G_A(fake_A)
             self._cGB1 = pGB.forward(torch.cat([B, A], 0) if self._idt else B)   # [fake_A; idt_B]
             fake_A = self._cGB1.out[:b]
+            ln.wait(1, packed_0)
             self._cGA2 = pGA.forward(fake_A)                     # rec_B
         ln.join()
         self._fake_B, self._fake_A = fake_B, fake_A
