@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 8
+#define MRAGAN_ABI_VERSION 9
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -79,6 +79,15 @@ int mragan_conv3d_transposed(const float* x, int N, int Di, int Hi, int Wi, int 
 int mragan_conv3d_presplit(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
                            const void* wsplit, const float* bias, int cout, int k, int stride, int pad, int act,
                            float* y, int Do, int Ho, int Wo, int transposed, void* ws, size_t ws_bytes, void* stream);
+/* Same, and when the convolution runs on the brick kernel (k3 s1, 16-bit MFMA modes) also the
+ * statistics partials of the InstanceNorm that follows it (networks3D.py:241-257: Conv3d →
+ * InstanceNorm3d in every ResnetBlock): part[N][chunks][cout][2] = fp64 Σy, Σy² of the written
+ * output per brick, *chunks = bricks per instance; *chunks = 0 when another kernel ran (the
+ * caller then runs mragan_instnorm_fwd).  part_bytes ≥ 16·N·Do·⌈Ho/4⌉·⌈Wo/6⌉·cout.  ABI 9. */
+int mragan_conv3d_presplit_in_stats(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                                    const void* wsplit, const float* bias, int cout, int k, int stride, int pad, int act,
+                                    float* y, int Do, int Ho, int Wo, int transposed, void* ws, size_t ws_bytes,
+                                    double* part, size_t part_bytes, int* chunks, void* stream);
 
 /* Workspace (bytes) the two calls above need for these shapes in the current precision mode:
  * split-K partial tiles of small-M / large-K dense convolutions (PatchGAN layers 2-4 and their
@@ -119,6 +128,12 @@ int mragan_instnorm_fwd(const float* x, int N, int D, int H, int W, int C, float
 int mragan_instnorm_bwd(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                         const float* dy, int dypad, const float* dy_add, int act, float* dx, void* ws, size_t ws_bytes,
                         void* stream);
+/* InstanceNorm forward from statistics partials a producer already accumulated (written by
+ * mragan_conv3d_presplit_in_stats: [N][chunks][C][2] fp64 Σy, Σy² per brick): finalize + apply
+ * only, no statistics pass over x.  ABI 9. */
+int mragan_instnorm_fwd_partials(const float* x, int N, int D, int H, int W, int C, float* y, int ypad, int act,
+                                 const float* resid, int rpad, float* mean, float* rstd, const double* part, int chunks,
+                                 void* stream);
 /* Same, and also writes g_out = fold(dy, dypad) + dy_add (before act') — the gradient w.r.t. a
  * ResnetBlock's input, x + conv_block(x) (networks3D.py:262-263), which the block's skip path
  * adds again one block earlier: the ReplicationPad3d backward and the skip-gradient add of the

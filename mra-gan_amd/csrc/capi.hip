@@ -47,7 +47,8 @@ static bool thin_side(int kc, int ny) { return kc <= 4 || ny <= 4 || kc % 8 != 0
 
 static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias, int cout,
                        int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* ws,
-                       size_t ws_bytes, void* stream, const void* wx3 = nullptr) {
+                       size_t ws_bytes, void* stream, const void* wx3 = nullptr, double* in_part = nullptr,
+                       int* in_chunks = nullptr) {
   MRAGAN_CHECK_ARG(x && w && y, "conv: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv: bad input shape");
   MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv: bad output shape");
@@ -62,7 +63,7 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
     return conv_thin(a, st);
   }
   IgemmArgs a{x, w, bias, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, trans, act, 1,
-              g_conv_precision, static_cast<float*>(ws), ws_bytes, wx3};
+              g_conv_precision, static_cast<float*>(ws), ws_bytes, wx3, in_part, in_chunks};
   return conv_igemm(a, st);
 }
 
@@ -109,6 +110,28 @@ int mragan_conv3d_presplit(const float* x, int N, int Di, int Hi, int Wi, int ci
   MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_presplit: transposed must be 0/1");
   return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, transposed, ws, ws_bytes,
                      stream, wsplit);
+}
+
+int mragan_conv3d_presplit_in_stats(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                    const void* wsplit, const float* bias, int cout, int k, int stride, int pad, int act,
+                                    float* y, int Do, int Ho, int Wo, int transposed, void* ws, size_t ws_bytes,
+                                    double* part, size_t part_bytes, int* chunks, void* stream) {
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_presplit_in_stats: transposed must be 0/1");
+  MRAGAN_CHECK_ARG(part && chunks, "conv3d_presplit_in_stats: null partials");
+  // every brick shape has bd ≥ 1, bh ≥ 4, bw ≥ 6 (conv_brick.hip choose_brick)
+  const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+  MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_presplit_in_stats: partials %zu < %zu bytes", part_bytes, bound);
+  *chunks = 0;
+  return conv_common(x, N, Di, Hi, Wi, cin, w, bias, cout, k, stride, pad, act, y, Do, Ho, Wo, transposed, ws, ws_bytes,
+                     stream, wsplit, part, chunks);
+}
+
+int mragan_instnorm_fwd_partials(const float* x, int N, int D, int H, int W, int C, float* y, int ypad, int act,
+                                 const float* resid, int rpad, float* mean, float* rstd, const double* part, int chunks,
+                                 void* stream) {
+  MRAGAN_CHECK_ARG(x && y && mean && rstd && part, "instnorm_fwd_partials: null pointer");
+  return instnorm_fwd_partials(x, InShape{N, D, H, W, C}, y, ypad, act, resid, rpad, mean, rstd, part, chunks,
+                               static_cast<hipStream_t>(stream));
 }
 
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,

@@ -387,7 +387,13 @@ int conv_brick(const IgemmArgs& g, hipStream_t st) {
   a.ntiles = (int)c.blocks;
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, c.bm, a.rowvox);
-  if (conv_brick_x3_active(g)) return conv_brick_x3_launch(a, c.bm, c.bn, g.ws, g.ws_bytes, g.wx3, g.x3, st);
+  if (conv_brick_x3_active(g)) {
+    if (g.in_part) {
+      a.part = g.in_part;
+      if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
+    }
+    return conv_brick_x3_launch(a, c.bm, c.bn, g.ws, g.ws_bytes, g.wx3, g.x3, st);
+  }
   // 8 waves (two per SIMD) for the 128-row bricks: one wave's LDS reads and staging overlap the
   // other's MFMAs
   if (c.bm == 128 && c.bn == 128)

@@ -262,18 +262,57 @@ conv_brick_x3_kernel(BrickArgs a) {
     __syncthreads();
   }
 
+  double ps[TN], pq[TN];                 // InstanceNorm statistics of the written values
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn0 + j * 32 + li;
     const float bsum = a.bias ? a.bias[col] : 0.f;
+    ps[j] = 0.0;
+    pq[j] = 0.0;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const int off = out_off[row];
-        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+        if (off >= 0) {
+          const float v = act_fwd(acc[i][j][r] + bsum, a.act);
+          a.y[(int64_t)off * a.ny + col] = v;
+          ps[j] += v;
+          pq[j] += (double)v * v;
+        }
       }
+    }
+  }
+  // the consumer InstanceNorm's per-(instance, channel) Σy / Σy² partial of this brick (the
+  // separate statistics pass over y disappears): lanes li / li + 32 share a column, the WM waves
+  // of a column group add through LDS (the halo buffers are idle), one double2 per column
+  if (a.part) {
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(halo_buf);        // [WM][BN][2]
+    const int wmi = wave / WN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const double s2 = ps[j] + __shfl_xor(ps[j], 32);
+      const double q2 = pq[j] + __shfl_xor(pq[j], 32);
+      if (lh == 0) {
+        red[(wmi * BN + wn0 + j * 32 + li) * 2] = s2;
+        red[(wmi * BN + wn0 + j * 32 + li) * 2 + 1] = q2;
+      }
+    }
+    __syncthreads();
+    const int chunks = a.nbd * a.nbh * a.nbw;
+    const int brick = (bd_i * a.nbh + bh_i) * a.nbw + bw_i;
+    for (int c = tid; c < BN; c += NT) {
+      double s2 = 0.0, q2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s2 += red[(w * BN + c) * 2];
+        q2 += red[(w * BN + c) * 2 + 1];
+      }
+      double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + n0 + c) * 2;
+      dst[0] = s2;
+      dst[1] = q2;
     }
   }
 }

@@ -352,6 +352,27 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   return check_launch("in_apply");
 }
 
+// Forward from statistics partials a producer conv already accumulated (conv_brick_x3 epilogue:
+// [N][chunks][C][2] = Σy, Σy² per brick): the statistics pass is skipped.
+int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
+                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st) {
+  MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm: C=%d must be a multiple of 4 (≤1024)", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, ypad > rpad ? ypad : rpad), "instnorm: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
+  MRAGAN_CHECK_ARG(part && chunks > 0, "instnorm_fwd_partials: no partials");
+  if (s.S() <= 1) {
+    set_error("Expected more than 1 spatial element when training, got input size [%d, %d, %d, %d, %d]", s.N, s.C, s.D,
+              s.H, s.W);
+    return kBadArg;
+  }
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
+  int rc = check_launch("in_finalize");
+  if (rc) return rc;
+  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
+  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
+                     rpad, y, ypad);
+  return check_launch("in_apply");
+}
+
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st) {
   MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm_bwd: C=%d must be a multiple of 4", s.C);
   MRAGAN_CHECK_ARG(in_fits(s, a.dypad), "instnorm_bwd: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);

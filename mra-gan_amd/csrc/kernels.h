@@ -19,6 +19,8 @@ struct IgemmArgs {
   float* ws;        // split-K partial tiles (conv_igemm_ws_bytes)
   size_t ws_bytes;
   const void* wx3;  // optional: w pre-split in bf16x3 brick fragment order (pack tr 2/3), or null
+  double* in_part;  // optional: per-(instance, brick, channel) Σy, Σy² of the output (brick_x3 only)
+  int* in_chunks;   // set to the bricks per instance when in_part was filled, else 0
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
@@ -37,6 +39,7 @@ struct BrickArgs {
   int BD, BH, BW;   // output brick
   int HD, HH, HW;   // its input halo
   int nbd, nbh, nbw, gn, ntiles;
+  double* part;     // optional InstanceNorm statistics partials [N][nbd·nbh·nbw][ny][2] (Σy, Σy²)
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st);
@@ -117,6 +120,8 @@ struct InBwdArgs {
 int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
                  float* rstd, void* ws, size_t ws_bytes, hipStream_t st);
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st);
+int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
+                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st);
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C);
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st);
 size_t instnorm_running_entry_bytes();

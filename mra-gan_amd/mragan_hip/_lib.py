@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -46,6 +46,9 @@ SIGNATURES = {
     "mragan_instnorm_workspace": (sz, [i32, i32, i32, i32, i32]),
     "mragan_instnorm_fwd": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, vp, vp, vp, sz, vp]),
     "mragan_instnorm_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, sz, vp]),
+    "mragan_conv3d_presplit_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32,
+                                              i32, i32, i32, vp, sz, vp, sz, vp, vp]),
+    "mragan_instnorm_fwd_partials": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, vp, vp, vp, i32, vp]),
     "mragan_instnorm_bwd_g": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, sz, vp]),
     "mragan_instnorm_running_update": (i32, [vp, i32, f32, vp]),
     "mragan_running_entry_size": (sz, []),

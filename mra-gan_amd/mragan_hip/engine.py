@@ -25,6 +25,10 @@ import torch
 from . import ops
 from ._lib import call
 
+# A/B switch: MRAGAN_NO_IN_STATS=1 runs the ResnetBlock InstanceNorms with their own statistics
+# pass instead of the brick conv's epilogue partials
+_NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") or "0"))
+
 IN_MOMENTUM = 0.1
 
 
@@ -96,6 +100,18 @@ class ConvLayer:
         N, D, H, W, _ = x.shape
         return ops.conv3d(x, self.wp_fwd, self.cout, self.k, self.s, self.p, self.out_spatial(D, H, W),
                           bias=bias, act=act, transposed=self.transposed, wsplit=self.ws_fwd)
+
+    def forward_in_stats(self, x):
+        """forward() of a bias-free conv feeding an InstanceNorm; on the brick kernel (k3 s1,
+        16-bit MFMA modes) it also leaves the IN statistics partials.  Returns (y, part, chunks);
+        chunks = 0 when no partials were produced."""
+        if self.ws_fwd is None or self.transposed or self.k != 3 or self.s != 1 or _NO_IN_STATS:
+            return self.forward(x), None, 0
+        N, D, H, W, _ = x.shape
+        osp = self.out_spatial(D, H, W)
+        part = ops.in_partials_buffer(N, osp, self.cout, x.device)
+        y, chunks = ops.conv3d_in_stats(x, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
+        return y, part, chunks
 
     def dgrad(self, dy, in_spatial):
         """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
@@ -210,10 +226,12 @@ class NetPlan:
             sc = StageCtx(inp=cur)
             ypad = self._next_prepad(i)
             if st.kind == "block":
-                sc.h1 = st.conv1.forward(cur)
-                sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd(sc.h1, act="relu", ypad=1)
-                sc.h = st.conv2.forward(sc.z1)
-                sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1)
+                # the brick conv accumulates its InstanceNorm's statistics in its epilogue
+                sc.h1, part, chunks = st.conv1.forward_in_stats(cur)
+                sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd(sc.h1, act="relu", ypad=1, part=part, chunks=chunks)
+                sc.h, part, chunks = st.conv2.forward_in_stats(sc.z1)
+                sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1, part=part,
+                                                            chunks=chunks)
             else:
                 bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
                 if st.norm is not None:

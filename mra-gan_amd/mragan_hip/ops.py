@@ -3,6 +3,7 @@ Activations are NDHWC tensors of shape [N, D, H, W, C].  Every call runs on the 
 torch stream; no call allocates inside the library (workspaces come from `Workspace`)."""
 from __future__ import annotations
 
+import ctypes as _ct
 from typing import Optional, Sequence
 
 import torch
@@ -205,6 +206,44 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     return out
 
 
+def in_partials_buffer(N: int, out_spatial: Sequence[int], cout: int, device) -> torch.Tensor:
+    """fp64 buffer for conv3d_in_stats' InstanceNorm statistics partials (the header's bound)."""
+    Do, Ho, Wo = out_spatial
+    return torch.empty(N * Do * (-(-Ho // 4)) * (-(-Wo // 6)) * cout * 2, device=device, dtype=torch.float64)
+
+
+def conv3d_in_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
+                    wsplit: torch.Tensor, part: torch.Tensor, transposed: bool = False):
+    """conv3d (presplit weights, no bias / act) that also leaves the following InstanceNorm's
+    statistics partials in `part` when the brick kernel runs it (ABI 9).  Returns (out, chunks);
+    chunks = 0: no partials, run instnorm_fwd as usual."""
+    _check(x, "conv3d.x")
+    N, Di, Hi, Wi, cin = x.shape
+    Do, Ho, Wo = out_spatial
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    if wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("conv3d: wsplit size does not match the packed weight")
+    if part.dtype != torch.float64 or not part.is_cuda:
+        raise ValueError("conv3d_in_stats: part must be a float64 device tensor")
+    out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
+    tm = None
+    if TIMER.match:
+        vox = Di * Hi * Wi if transposed else Do * Ho * Wo
+        tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
+                              in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo),
+                              cls=f"{'convT' if transposed else 'conv'} {cin}->{cout} k{k} s{s} [{N}x{Di}x{Hi}x{Wi}]",
+                              flops=2.0 * N * vox * cin * cout * k ** 3))
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
+    chunks = _ct.c_int(0)
+    call("mragan_conv3d_presplit_in_stats", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), None, cout, k, s, p,
+         ACT[None], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(part), part.numel() * 8,
+         _ct.byref(chunks), _stream())
+    TIMER.end(tm)
+    return out, chunks.value
+
+
 def conv3d_wgrad(dense: torch.Tensor, gathered: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
                  accumulate: bool) -> torch.Tensor:
     _check(dense, "wgrad.dense")
@@ -268,7 +307,9 @@ class PackTable:
 
 def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch.Tensor] = None, rpad: int = 0,
                  out: Optional[torch.Tensor] = None, mean: Optional[torch.Tensor] = None,
-                 rstd: Optional[torch.Tensor] = None):
+                 rstd: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None, chunks: int = 0):
+    """InstanceNorm forward (+act, residual, replication pad of the output).  With `part` /
+    `chunks` from conv3d_in_stats the statistics pass is skipped (ABI 9)."""
     _check(x, "instnorm.x")
     N, D, H, W, C = x.shape
     shp = (N, D + 2 * ypad, H + 2 * ypad, W + 2 * ypad, C)
@@ -287,8 +328,12 @@ def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch
     # essential HBM bytes: read x (+ the residual), write y (padded)
     tm = TIMER.begin(dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad}",
                           bytes=4.0 * (x.numel() * (2 if resid is not None else 1) + out.numel()))) if TIMER.match else None
-    call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad, _ptr(mean),
-         _ptr(rstd), _ptr(ws), ws.numel(), _stream())
+    if part is not None and chunks > 0:
+        call("mragan_instnorm_fwd_partials", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad,
+             _ptr(mean), _ptr(rstd), _ptr(part), chunks, _stream())
+    else:
+        call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad, _ptr(mean),
+             _ptr(rstd), _ptr(ws), ws.numel(), _stream())
     TIMER.end(tm)
     return out, mean, rstd
 

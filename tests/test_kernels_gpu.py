@@ -362,6 +362,31 @@ def test_instnorm_bwd_g_out(ops, C, dypad, act):
     assert rel(G, G_ref) < 1e-6          # border voxels: the same terms summed in another order
 
 
+@pytest.mark.parametrize("N,C,S", [(2, 128, 16), (1, 64, 9), (3, 64, 7)])
+def test_brick_in_stats_partials(x3, N, C, S):
+    """ABI 9: the brick conv's epilogue InstanceNorm partials (mragan_conv3d_presplit_in_stats)
+    feed mragan_instnorm_fwd_partials; output, mean / rstd and the normalised tensor match the
+    statistics-pass path (partial bricks included: 9³ and 7³ outputs leave padding rows)."""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 7 + C + S)
+    x = torch.randn(N, C, S + 2, S + 3, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    xg = ndhwc(x.float()).cuda()
+    wp = pack(ops, w, False, False)
+    wsplit = torch.empty(wp.numel(), device="cuda", dtype=torch.float32)
+    ops.pack_weight(w.float().cuda().contiguous(), C, C, 27, 4 if ops.get_conv_precision() == "fp16" else 2, wsplit)
+    osp = (S, S + 1, S)
+    y_ref = ops.conv3d(xg, wp, C, 3, 1, 0, osp, wsplit=wsplit)
+    part = ops.in_partials_buffer(N, osp, C, "cuda")
+    y, chunks = ops.conv3d_in_stats(xg, wp, C, 3, 1, 0, osp, wsplit, part)
+    assert chunks > 0
+    assert torch.equal(y, y_ref)
+    z_ref, m_ref, r_ref = ops.instnorm_fwd(y_ref, act="relu", ypad=1)
+    z, m, r = ops.instnorm_fwd(y, act="relu", ypad=1, part=part, chunks=chunks)
+    assert rel(m, m_ref) < 1e-6 and rel(r, r_ref) < 1e-6
+    assert rel(z, z_ref) < 1e-6
+
+
 def test_instnorm_single_voxel_raises(ops):
     from mragan_hip import MraganError
     with pytest.raises(MraganError, match="more than 1 spatial element"):
