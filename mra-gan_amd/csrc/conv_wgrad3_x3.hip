@@ -250,13 +250,13 @@ bool wgrad3_x3_applicable(const WgradArgs& a) {
 }
 
 // splits: at most 2 blocks per CU in total (one round: a 513th block doubles the time),
-// ≥ 6 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
+// ≥ 4 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
 int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
   const bool wide = w3_wide(a);
   const int tiles = (a.Cd / (wide ? 128 : kTile)) * (a.Cg / kTile) * 9;
   int s = (wide ? 256 : 512) / tiles;
-  const int by_len = nseg / (6 * kR);
+  const int by_len = nseg / (4 * kR);
   if (s > by_len) s = by_len;
   if (s > max_splits) s = max_splits;
   if (s < 1) s = 1;

@@ -17,7 +17,7 @@ if [ -n "$KEXPR" ]; then
 fi
 for side in base new; do
   if [ $side = base ]; then export MRAGAN_HIP_LIB=$R/mra-gan_amd/lib/ab/libmragan_hip.so; else unset MRAGAN_HIP_LIB; fi
-  step "kbench $side" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$side" -o run -- python3 tools/kbench.py --ops "$OPS" --reps 20 --precision bf16x3 > "$O/kbench_$side.log" 2>&1
+  step "kbench $side" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$side" -o run -- python3 tools/kbench.py --ops "$OPS" --reps 20 --precision bf16x3 ${KB_ARGS:-} > "$O/kbench_$side.log" 2>&1
   python3 - "$O/kt_$side" "$side" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + '/**/run_kernel_stats.csv', recursive=True)[0]
