@@ -321,8 +321,93 @@ __device__ void pack_split_entry(const PackEntry& e) {
 
 __global__ void pack_split_kernel(PackEntry e) { pack_split_entry(e); }
 
+// Tiled form of one entry (A % 8 == 0, B % 16 == 0, T ≤ 64): a block stages src[a0 .. a0+8)
+// [b0 .. b0+16)[0 .. T) — 8 contiguous runs of 16·T floats — in LDS, then writes every output
+// it feeds with contiguous runs (fp32: 16 or 8 floats; split: one 16-B hi / lo fragment per
+// (tap, n, 8 channels)).  The element-wise form reads src with a stride of T floats and re-reads
+// each line T times through L2 (86 µs for a generator's repack).  Same conversions, so the
+// output is bit-identical.
+constexpr int kPkA = 8, kPkB = 16, kPkTMax = 64;
+__device__ __forceinline__ bool pack_tiled_ok(const PackEntry& e) {
+  if (e.A % kPkA || e.B % kPkB || e.T > kPkTMax) return false;
+  if (e.tr >= 2) {
+    const int C = (e.tr & 1) ? e.A : e.B;
+    return e.T == 27 && C % 32 == 0;
+  }
+  return true;
+}
+
+__device__ void pack_tiled_entry(const PackEntry& e, float* S) {
+  const int T = e.T, TP = T + 1;
+  const int nbt = e.B / kPkB, tiles = (e.A / kPkA) * nbt;
+  const int tid = threadIdx.x;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int a0 = (tile / nbt) * kPkA, b0 = (tile % nbt) * kPkB;
+    __syncthreads();                                   // the previous tile's reads of S are done
+    for (int i = tid; i < kPkA * kPkB * T; i += blockDim.x) {
+      const int la = i / (kPkB * T), rem = i - la * (kPkB * T);
+      const int lb = rem / T, t = rem - lb * T;
+      S[(la * kPkB + lb) * TP + t] = e.src[((a0 + la) * e.B + b0) * T + rem];
+    }
+    __syncthreads();
+    if (e.tr == 0) {                                   // dst[t][a][b]
+      for (int i = tid; i < T * kPkA * kPkB; i += blockDim.x) {
+        const int t = i / (kPkA * kPkB), la = (i / kPkB) % kPkA, lb = i % kPkB;
+        e.dst[(t * e.A + a0 + la) * e.B + b0 + lb] = S[(la * kPkB + lb) * TP + t];
+      }
+    } else if (e.tr == 1) {                            // dst[t][b][a]
+      for (int i = tid; i < T * kPkA * kPkB; i += blockDim.x) {
+        const int t = i / (kPkA * kPkB), lb = (i / kPkA) % kPkB, la = i % kPkA;
+        e.dst[(t * e.B + b0 + lb) * e.A + a0 + la] = S[(la * kPkB + lb) * TP + t];
+      }
+    } else {                                           // split fragments, as pack_split_entry
+      const int trs = e.tr & 1;
+      const int ny = trs ? e.B : e.A, C = trs ? e.A : e.B, nch = C / 32;
+      __bf16* out = reinterpret_cast<__bf16*>(e.dst);
+      // fragments in this tile: tr 2 — (tap, n = a0 + la, g = (b0 + 8h) / 8): 27 × 8 × 2;
+      //                         tr 3 — (tap, n = b0 + lb, g = a0 / 8):      27 × 16 × 1
+      for (int i = tid; i < T * 16; i += blockDim.x) {
+        const int tap = i / 16, f = i % 16;
+        pk_f32x8 v;
+        int n, g;
+        if (!trs) {
+          const int la = f >> 1, h = f & 1;
+          n = a0 + la;
+          g = (b0 + 8 * h) >> 3;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = S[(la * kPkB + 8 * h + j) * TP + tap];
+        } else {
+          const int lb = f;
+          n = b0 + lb;
+          g = a0 >> 3;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = S[(j * kPkB + lb) * TP + tap];
+        }
+        pk_bf16x8 hi, lo;
+        if (e.tr >= 4) {
+          const pk_f16x8 h16 = __builtin_convertvector(v, pk_f16x8);
+          hi = __builtin_bit_cast(pk_bf16x8, h16);
+          lo = __builtin_bit_cast(pk_bf16x8, __builtin_convertvector(v - __builtin_convertvector(h16, pk_f32x8), pk_f16x8));
+        } else {
+          hi = __builtin_convertvector(v, pk_bf16x8);
+          lo = __builtin_convertvector(v - __builtin_convertvector(hi, pk_f32x8), pk_bf16x8);
+        }
+        const int chunk = g >> 2, kk = (g >> 1) & 1, lh = g & 1;
+        const int base = (((tap * nch + chunk) * 2 + kk) * 2) * ny * 16 + n * 16 + lh * 8;
+        *reinterpret_cast<pk_bf16x8*>(out + base) = hi;
+        *reinterpret_cast<pk_bf16x8*>(out + base + ny * 16) = lo;
+      }
+    }
+  }
+}
+
 __global__ void pack_batched_kernel(const PackEntry* __restrict__ tab) {
+  __shared__ float S[kPkA * kPkB * (kPkTMax + 1)];
   const PackEntry e = tab[blockIdx.y];
+  if (pack_tiled_ok(e)) {
+    pack_tiled_entry(e, S);
+    return;
+  }
   if (e.tr >= 2) {
     pack_split_entry(e);
     return;

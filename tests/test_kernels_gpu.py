@@ -626,7 +626,11 @@ def test_pack_weights_batched_equals_single(ops):
     """mragan_pack_weights (one launch for a network's packs) = mragan_pack_weight per pack."""
     g = torch.Generator().manual_seed(21)
     packs, ref = [], []
-    for (A, B, T, tr) in [(128, 128, 27, False), (32, 1, 343, True), (64, 32, 27, True), (1, 32, 64, False)]:
+    # tiled LDS path (A % 8, B % 16, T ≤ 64) and element-wise path; fp32 tr 0/1 and the bf16 / fp16
+    # split fragment orders tr 2..5 (T = 27, channels % 32)
+    for (A, B, T, tr) in [(128, 128, 27, 0), (32, 1, 343, 1), (64, 32, 27, 1), (1, 32, 64, 0), (64, 128, 64, 1),
+                          (256, 128, 64, 0), (128, 64, 27, 2), (64, 128, 27, 3), (128, 128, 27, 4),
+                          (64, 96, 27, 5), (40, 32, 27, 2)]:
         src = torch.randn(A * B * T, generator=g).cuda()
         dst = torch.empty_like(src)
         want = torch.empty_like(src)
