@@ -15,9 +15,16 @@ if [ -z "$SKIP" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -60 "$O/pytest.log"; exit 1; }
   tail -2 "$O/pytest.log"
 fi
+echo "[head] smoke"
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -30 "$O/smoke.log"; exit 1; }
+tail -2 "$O/smoke.log"
 echo "[head] bench default"
 timeout -k 10 600 python3 bench.py > "$O/bench_default.json" 2> "$O/bench_default.err" || { tail -30 "$O/bench_default.err"; exit 1; }
 cat "$O/bench_default.json"
+echo "[head] bench dp2 rehearsal (gloo, same device)"
+timeout -k 10 300 python3 bench.py --gpus 2 --dist-backend gloo --same-device --steps 5 --warmup 2 --no-cpu-baseline \
+    --alt-precisions "" > "$O/bench_dp2.json" 2> "$O/bench_dp2.err" || { tail -30 "$O/bench_dp2.err"; exit 1; }
+grep '^{' "$O/bench_dp2.json" | cut -c1-200
 cd /tmp && export TMPDIR=/tmp
 echo "[head] kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o bench \
