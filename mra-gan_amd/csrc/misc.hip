@@ -503,8 +503,10 @@ int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const floa
 int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st) {
   if (n <= 0) return kOk;
   if (max_elems >= ((int64_t)1 << 31)) { set_error("pack_weights: entry too large"); return kBadArg; }
-  int gx = (int)((max_elems + 255) / 256);             // the largest entry in one pass
-  if (gx > 2048) gx = 2048;
+  // ≤ 256 blocks per entry: the tiled entries have ≤ 128 tiles at these shapes and the
+  // element-wise ones grid-stride; every extra (empty) block still reserves the tile's LDS
+  int gx = (int)((max_elems + 2047) / 2048);
+  if (gx > 256) gx = 256;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(pack_batched_kernel, dim3(gx, n), dim3(256), 0, st, table);
   return check_launch("pack_batched");

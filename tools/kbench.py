@@ -71,7 +71,12 @@ def main():
     w_dn2 = rnd(27 * 2 * ngf * c4) * 0.01
     x_d2 = rnd(N, s2, s2, s2, ngf)                        # PatchGAN layer 2 Conv3d(ndf -> 2ndf, k4 s2 p1) input
     w_d2 = rnd(64 * ngf * 2 * ngf) * 0.01
+    # a generator's repack: 18 res-block convs x (fp32 fwd / bwd packs + bf16 split fwd / bwd)
+    w_g = [rnd(c4 * c4 * 27) for _ in range(18)]
+    pk = [(w, c4, c4, 27, tr, torch.empty_like(w)) for w in w_g for tr in (0, 1, 2, 3)]
+    pack_tab = ops.PackTable()
     table = {
+        "pack_g": lambda: pack_tab.run(pk),
         "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
         "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
