@@ -298,9 +298,13 @@ static X3Plan x3_plan(const IgemmArgs& a, int64_t total_m) {
   auto blocks = [&](int c) {
     return (int64_t)ceil_div(total_m, kX3Cfg[c].bm) * ceil_div(a.ny, kX3Cfg[c].bn);
   };
+  // the largest tile with ≥ 512 blocks (two rounds of the 256 CUs at up to 3 blocks per CU: a
+  // 256-block 128×64 grid left G's down2 at 61–66 µs, 64×64 tiles 49.6 µs); without one, 64×64
+  // for > 64 outputs, and for ≤ 64 outputs the 128×64 tile whose short M is then split in K
+  // (PatchGAN layer 2: 37.5 µs split 4 ways vs 47.1 µs on 64×64 tiles; tools/gpu_igcfg.sh)
   int cfg;
-  if (a.ny > 64) cfg = blocks(0) >= 256 ? 0 : blocks(1) >= 256 ? 1 : 2;
-  else if (a.ny > 32) cfg = blocks(1) >= 256 ? 1 : 2;
+  if (a.ny > 64) cfg = blocks(0) >= 512 ? 0 : blocks(1) >= 512 ? 1 : 2;
+  else if (a.ny > 32) cfg = blocks(1) >= 512 ? 1 : blocks(2) >= 512 ? 2 : 1;
   else cfg = blocks(3) >= 256 ? 3 : 4;
   X3Plan pl{cfg, 1};
   const int64_t b = blocks(cfg);
