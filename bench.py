@@ -14,14 +14,19 @@ With --gpus N > 1 and no torch.distributed environment, the script launches its 
 touching the GPU and exits with its status.
 
 Prints ONE JSON line on rank 0 (contract in the task description), with:
-  roofline      — the dominant kernel BY TIME: every instrumented C-ABI call of two eager steps
-                  (right after the timed region) is bracketed by HIP events on its stream and
-                  grouped by launch class (op + shape); the class with the largest total time is
-                  reported with its algorithmic FLOP (or bytes) per launch ÷ its mean duration;
+  roofline      — the dominant kernel BY TIME: one eager single-stream step (right after the timed
+                  region) records every instrumented C-ABI call by launch class (op + shape); each
+                  class's call is re-issued 10× back to back between HIP events on its stream, so
+                  the class mean is the kernels' own duration; the class with the largest
+                  per-step total is reported with its algorithmic FLOP (or bytes) per launch ÷ that
+                  mean;
   step_roofline — SURVEY §8(d)'s whole-step figure, (F/P_mfma + B_ew/BW_hbm) / T_step;
+  alt_precisions — the same workload and protocol in the other contraction precisions;
+  legs          — further workloads (default: 128³ b1, BASELINE configs[2]'s per-GPU unit), each
+                  with its own ms_per_step, roofline and step_roofline;
   cpu_baseline  — the CPU oracle (oracle/cyclegan_oracle.py, the reference's algorithm restated
-                  in PyTorch-CPU) timed on this host, median of --cpu-steps steps of the same
-                  workload.
+                  in PyTorch-CPU) timed on this host: --cpu-warmup untimed steps, then the median
+                  of --cpu-steps steps of the headline workload.
 """
 import argparse
 import json
@@ -57,9 +62,16 @@ def parse():
                          "operands (one MFMA per product); fp32 accumulation, fp32 tensors and master weights")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: median of this many oracle steps")
     ap.add_argument("--nc", type=int, default=1, help="image channels (input_nc = output_nc)")
-    ap.add_argument("--alt-precisions", default="bf16",
+    ap.add_argument("--alt-precisions", default="bf16,f32",
                     help="comma list of further precisions timed in the same run (same workload, same protocol) "
                          "and reported under alt_precisions; '' for none")
+    ap.add_argument("--legs", default="128:1",
+                    help="comma list of further workloads SIZE:BATCH timed in the same run (BASELINE configs[2]'s "
+                         "per-GPU unit 128^3 b1 by default), reported under legs; '' for none")
+    ap.add_argument("--leg-alt-precisions", default="bf16", help="alt precisions timed for each extra leg")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the per-launch-class timing (profiled runs: the trace then holds only the steps)")
+    ap.add_argument("--cpu-warmup", type=int, default=2, help="CPU baseline: untimed oracle steps first")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels from Python every step (default: replay the step as HIP graphs)")
     ap.add_argument("--single-stream", action="store_true",
@@ -135,11 +147,12 @@ def cpu_baseline(args):
                          pool_rng=random.Random(0))
     shape = (args.batch, args.nc, args.size, args.size, args.size)
     times = []
-    for i in range(args.cpu_steps):
+    for i in range(args.cpu_warmup + args.cpu_steps):
         A, B = synthetic_pair(shape, 1000 + i)
         t0 = time.perf_counter()
         orc.optimize_parameters(A, B)
-        times.append(time.perf_counter() - t0)
+        if i >= args.cpu_warmup:
+            times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
     cpu_model = ""
     try:
@@ -150,7 +163,7 @@ def cpu_baseline(args):
     except OSError:
         pass
     return {"value": args.batch / t, "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"median of {len(times)} optimize_parameters() steps of the CPU oracle (PyTorch-CPU fp32) on "
+            "sample": f"{args.cpu_warmup} warm-up steps, then median of {len(times)} optimize_parameters() steps of the CPU oracle (PyTorch-CPU fp32) on "
                       f"{args.batch}x{args.nc}x{args.size}^3: {t:.2f} s (all: "
                       + ", ".join(f"{x:.2f}" for x in times) + f" s), {threads} threads, {cpu_model}"}
 
@@ -160,7 +173,7 @@ def cpu_baseline_child(args, timeout_s=300):
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--size", str(args.size),
            "--batch", str(args.batch), "--ngf", str(args.ngf), "--netG", args.netG, "--cpu-steps", str(args.cpu_steps),
-           "--nc", str(args.nc)]
+           "--cpu-warmup", str(args.cpu_warmup), "--nc", str(args.nc)]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
         for line in r.stdout.splitlines():
@@ -203,13 +216,13 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
-def build_model(args, precision):
+def build_model(args, precision, batch=None):
     from models import create_model
     from options.train_options import TrainOptions
     sys_argv = sys.argv
     sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
                 "--input_nc", str(args.nc), "--output_nc", str(args.nc),
-                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(args.batch),
+                "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(batch or args.batch),
                 "--conv_precision", precision] + (["--no_cuda_graph"] if args.no_graph else []) + \
         (["--single_stream"] if args.single_stream else [])
     opt = TrainOptions().gather_options()
@@ -225,30 +238,6 @@ def build_model(args, precision):
     return model
 
 
-def time_alt_precision(args, precision, inputs, barrier, dist):
-    """The same workload and timing protocol in another contraction precision (a fresh model,
-    W warm-up steps, K timed steps between barriers, max over ranks)."""
-    model = build_model(args, precision)
-    for i in range(args.warmup):
-        model.set_input(inputs[i])
-        model.optimize_parameters()
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        model.set_input(inputs[args.warmup + i])
-        model.optimize_parameters()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    del model
-    torch.cuda.empty_cache()
-    return {"ms_per_step": round(1e3 * elapsed / args.steps, 3), "dtype": precision,
-            "timing": "same protocol as the headline (barrier + synchronize around K steps, max over ranks)"}
-
-
 def ew_bytes_per_patch(S, netG, elem_bytes=4):
     """SURVEY §8(d) secondary HBM term: the InstanceNorm/activation/pad/residual traffic of one
     patch's step, ≈ 8 passes × 118·S³ elements per G fwd+bwd × 6 G passes = 5664·S³ elements
@@ -256,6 +245,152 @@ def ew_bytes_per_patch(S, netG, elem_bytes=4):
     if netG.startswith("unet"):
         return None
     return 5664.0 * S ** 3 * elem_bytes
+
+
+
+
+DTYPE = {"f32": "f32", "bf16x3": "bf16x3", "bf16": "bf16", "fp16": "fp16"}
+DTYPE_DETAIL = {"f32": "exact f32 products (f32 MFMA / VALU), f32 accumulate",
+                "bf16x3": "each f32 conv operand split into bf16 hi + lo, a*b as 3 bf16 MFMAs (<= 3*2^-18 per "
+                          "product), f32 accumulate; f32 tensors, InstanceNorm, losses, Adam",
+                "bf16": "bf16 conv operands (every conv's inputs and weights rounded RNE), f32 accumulate; f32 "
+                        "InstanceNorm, losses, Adam, master weights",
+                "fp16": "fp16 conv operands with a static loss scale, f32 accumulate; f32 InstanceNorm, losses, "
+                        "Adam, master weights"}
+
+
+def mfma_peak_of(precision):
+    # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic FLOPs is the
+    # bf16 dense peak / 3; bf16 / fp16 run at the dense 16-bit MFMA peak
+    return {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x3": MFMA_BF16_PEAK_TFLOPS / 3}.get(precision, MFMA_BF16_PEAK_TFLOPS)
+
+
+def make_inputs(shape, n, rank):
+    g = torch.Generator().manual_seed(1000 + rank)
+    return [(torch.randn(shape, generator=g).cuda(), torch.randn(shape, generator=g).cuda()) for _ in range(n)]
+
+
+def time_steps(model, inputs, warmup, steps, barrier, dist):
+    """W untimed steps, then K steps between barrier + synchronize; per-step events on the step's
+    stream give the median.  Returns (elapsed s, median ms) as the max over ranks."""
+    for i in range(warmup):
+        model.set_input(inputs[i])
+        model.optimize_parameters()
+    barrier()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    barrier()
+    t0 = time.perf_counter()
+    marks[0].record()
+    for i in range(steps):
+        model.set_input(inputs[warmup + i])
+        model.optimize_parameters()
+        marks[i + 1].record()
+    barrier()
+    wall = time.perf_counter() - t0
+    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(steps))
+    median_ms = step_ms[len(step_ms) // 2]
+    elapsed = max(marks[0].elapsed_time(marks[-1]) / 1e3, wall)
+    if dist is not None:
+        t = torch.tensor([elapsed, median_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, median_ms = float(t[0]), float(t[1])
+    return elapsed, median_ms
+
+
+def kernel_classes(model, inputs, reps=10):
+    """Launch classes of one step: two eager single-stream steps record every instrumented C-ABI
+    call; each class's call is then re-issued `reps` times back to back between HIP events
+    (ops.KernelTimer).  The second step's records are the ones a step issues (the first one also
+    holds one-off work), so launches per step = records of step 2."""
+    from mragan_hip import ops
+    use_graph, lanes = model._use_graph, model.parallel_lanes
+    model._use_graph, model.parallel_lanes = False, False
+    model.set_input(inputs[0])
+    model.optimize_parameters()
+    ops.TIMER.reset()
+    ops.TIMER.match = lambda info: True
+    model.set_input(inputs[1])
+    model.optimize_parameters()
+    ops.TIMER.match = None
+    model._use_graph, model.parallel_lanes = use_graph, lanes
+    return ops.TIMER.classes(reps)
+
+
+def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_top=40):
+    """One workload: the timed step in `precision`, its launch classes and roofline, and the same
+    protocol in each precision of `alts` (a fresh model each)."""
+    from mragan_hip import ops
+    shape = (batch, args.nc, size, size, size)
+    inputs = make_inputs(shape, args.warmup + args.steps, rank)
+    model = build_model(args, precision, batch)
+    elapsed, median_ms = time_steps(model, inputs, args.warmup, args.steps, barrier, dist)
+    graphed = getattr(model, "_graphs", None) is not None
+    classes = kernel_classes(model, inputs) if not args.no_kernel_timing else None
+    loss_scale = model.loss_scale
+    del model
+    torch.cuda.empty_cache()
+    alt = {}
+    for p in alts:
+        m = build_model(args, p, batch)
+        e, med = time_steps(m, inputs, args.warmup, args.steps, barrier, dist)
+        alt[p] = {"value": round(world * batch * args.steps / e, 3), "ms_per_step": round(1e3 * e / args.steps, 3),
+                  "ms_per_step_median": round(med, 3), "dtype": DTYPE[p], "dtype_detail": DTYPE_DETAIL[p],
+                  "timing": "same protocol as the leg's headline (barrier + synchronize around K steps, max over ranks)"}
+        del m
+        torch.cuda.empty_cache()
+    ops.set_conv_precision(precision)
+    ops.set_loss_scale(loss_scale)
+    barrier()
+    t_step = elapsed / args.steps
+    mfma_peak = mfma_peak_of(precision)
+    step_tf = step_flops(size, batch, args.ngf, args.netG, nc=args.nc) / 1e12
+    ew = ew_bytes_per_patch(size, args.netG)
+    ideal_s = step_tf / mfma_peak + (batch * ew / (HBM_PEAK_GBS * 1e9) if ew else 0.0)
+    leg = {
+        "value": round(world * batch * args.steps / elapsed, 3),
+        "unit": "patches/s",
+        "ms_per_step": round(1e3 * t_step, 3),
+        "ms_per_step_median": round(median_ms, 3),
+        "dtype": DTYPE[precision],
+        "dtype_detail": DTYPE_DETAIL[precision],
+        "workload": f"{args.netG} G + 3-layer PatchGAN D, {args.nc}ch->{args.nc}ch, {size}^3 patch, batch {batch}/GPU",
+        "step_launch": "hip_graph" if graphed else "eager",
+        "step_roofline": {"achieved": round(ideal_s / t_step, 4), "ideal_ms": round(1e3 * ideal_s, 3),
+                          "formula": "(F/P_mfma + B_ew/BW_hbm) / T_step (SURVEY 8d)",
+                          "F_tflop": round(step_tf, 4), "P_mfma_tflops": round(mfma_peak, 1),
+                          "B_ew_gb": round(batch * ew / 1e9, 3) if ew else None, "BW_hbm_gbs": HBM_PEAK_GBS},
+        "step_tflop": round(step_tf, 4),
+        "step_tflops_achieved": round(step_tf / t_step, 2),
+    }
+    if alt:
+        leg["alt_precisions"] = alt
+    if classes:
+        prec = {"bf16x3": "bf16x3 split MFMA", "f32": "f32 MFMA", "bf16": "bf16 MFMA", "fp16": "fp16 MFMA"}[precision]
+        dom_cls, dom = next(iter(classes.items()))
+        if dom["flops"]:
+            achieved = dom["flops"] / (dom["mean_ms"] / 1e3) / 1e12
+            peak, unit, bound = mfma_peak, "TFLOP/s", "mfma"
+        else:
+            achieved = dom["bytes"] / (dom["mean_ms"] / 1e3) / 1e9
+            peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
+        traffic, traffic_src = measured_traffic(dom["kernels"], dom_cls)
+        leg["roofline"] = {
+            "bound": bound, "kernel": f"{dom['kernels']} ({prec}) — {dom_cls}",
+            "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit, "frac": round(achieved / peak, 4),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "launch_ms": round(dom["mean_ms"], 4), "launches_per_step": dom["n"],
+            "ms_per_step": round(dom["total_ms"], 4),
+            "flop_per_launch": dom["flops"], "bytes_per_launch": dom["bytes"],
+            "timing": f"dominant launch class by time; its C-ABI call re-issued {dom['reps']}x back to back "
+                      "between HIP events on the step's stream (after one warm launch), mean per launch"}
+        leg["top_kernels"] = [
+            dict(cls=c, kernels=v["kernels"], launches_per_step=v["n"], ms_per_step=round(v["total_ms"], 4),
+                 mean_us=round(1e3 * v["mean_ms"], 2),
+                 frac=round((v["flops"] / (v["mean_ms"] / 1e3) / 1e12) / mfma_peak if v["flops"] else
+                            (v["bytes"] / (v["mean_ms"] / 1e3) / 1e9) / HBM_PEAK_GBS, 4))
+            for c, v in list(classes.items())[:n_top]]
+        leg["kernel_ms_per_step_serial"] = round(sum(v["total_ms"] for v in classes.values()), 3)
+    return leg
 
 
 def main():
@@ -282,113 +417,39 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    from mragan_hip import ops
-    model = build_model(args, args.precision)
-
-    g = torch.Generator().manual_seed(1000 + rank)
-    shape = (args.batch, args.nc, args.size, args.size, args.size)
-    n_in = args.warmup + args.steps
-    inputs = [(torch.randn(shape, generator=g).cuda(), torch.randn(shape, generator=g).cuda()) for _ in range(n_in)]
-
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        model.set_input(inputs[i])
-        model.optimize_parameters()
-    barrier()
-    # per-step events on the step's stream (no host sync inside the timed region): the median
-    # step time; the JSON's value is the whole region's throughput
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    barrier()
-    t0 = time.perf_counter()
-    marks[0].record()
-    for i in range(args.steps):
-        model.set_input(inputs[args.warmup + i])
-        model.optimize_parameters()
-        marks[i + 1].record()
-    barrier()
-    wall = time.perf_counter() - t0
-    graphed = getattr(model, "_graphs", None) is not None
-    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
-    median_ms = step_ms[len(step_ms) // 2]
-    elapsed = max(marks[0].elapsed_time(marks[-1]) / 1e3, wall)
-    if dist is not None:
-        t = torch.tensor([elapsed, median_ms], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, median_ms = float(t[0]), float(t[1])
-
-    alt = {}
-    for prec_alt in [p for p in args.alt_precisions.split(",") if p and p != args.precision]:
-        alt[prec_alt] = time_alt_precision(args, prec_alt, inputs, barrier, dist)
-        ops.set_conv_precision(args.precision)
-        ops.set_loss_scale(model.loss_scale)
-
-    # dominant kernel by time: two eager steps right after the timed region, every instrumented
-    # C-ABI call bracketed by HIP events (ROCm refuses timing events inside a captured graph)
-    ops.TIMER.reset()
-    ops.TIMER.match = lambda info: True
-    # (one stream: a kernel's interval must not include the other lane's concurrent kernels)
-    use_graph, lanes = model._use_graph, model.parallel_lanes
-    model._use_graph, model.parallel_lanes = False, False
-    for i in range(2):
-        model.set_input(inputs[args.warmup + i])
-        model.optimize_parameters()
-    model._use_graph, model.parallel_lanes = use_graph, lanes
-    ops.TIMER.match = None
-    classes = ops.TIMER.classes()
-    barrier()
-
+    alts = [p for p in args.alt_precisions.split(",") if p and p != args.precision]
+    head = run_leg(args, args.size, args.batch, args.precision, alts, barrier, dist, world, rank)
+    legs = {}
+    for spec in [s for s in args.legs.split(",") if s]:
+        S, bsz = (int(v) for v in spec.split(":"))
+        if (S, bsz) == (args.size, args.batch):
+            continue
+        legs[f"{S}^3 b{bsz}"] = run_leg(args, S, bsz, args.precision,
+                                        [p for p in args.leg_alt_precisions.split(",") if p and p != args.precision],
+                                        barrier, dist, world, rank, n_top=12)
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
         return
 
-    patches = world * args.batch * args.steps
-    value = patches / elapsed
-    x3 = args.precision == "bf16x3"
-    # bf16x3 issues 3 bf16 MFMAs per fp32 product: its ceiling for the algorithmic FLOPs is the
-    # bf16 dense peak / 3; bf16 / fp16 run at the dense 16-bit MFMA peak
-    mfma_peak = {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x3": MFMA_BF16_PEAK_TFLOPS / 3}.get(args.precision,
-                                                                                       MFMA_BF16_PEAK_TFLOPS)
-    prec = {"bf16x3": "bf16x3 split MFMA", "f32": "f32 MFMA", "bf16": "bf16 MFMA", "fp16": "fp16 MFMA"}[args.precision]
-    dom_cls, dom = next(iter(classes.items()))
-    per_step_ms = dom["total_ms"] / 2
-    if dom["flops"]:
-        achieved = dom["flops"] / (dom["mean_ms"] / 1e3) / 1e12
-        peak, unit, bound = mfma_peak, "TFLOP/s", "mfma"
-    else:
-        achieved = dom["bytes"] / (dom["mean_ms"] / 1e3) / 1e9
-        peak, unit, bound = HBM_PEAK_GBS, "GB/s", "hbm"
-    traffic, traffic_src = measured_traffic(dom["kernels"], dom_cls)
-    top = [dict(cls=c, kernels=v["kernels"], launches_per_step=v["n"] // 2, ms_per_step=round(v["total_ms"] / 2, 4),
-                mean_us=round(1e3 * v["mean_ms"], 2),
-                frac=round((v["flops"] / (v["mean_ms"] / 1e3) / 1e12) / mfma_peak if v["flops"] else
-                           (v["bytes"] / (v["mean_ms"] / 1e3) / 1e9) / HBM_PEAK_GBS, 4))
-           for c, v in list(classes.items())[:40]]
-    step_tf = step_flops(args.size, args.batch, args.ngf, args.netG, nc=args.nc) / 1e12
-    ew = ew_bytes_per_patch(args.size, args.netG)
-    t_step = elapsed / args.steps
-    ideal_s = step_tf / mfma_peak + (args.batch * ew / (HBM_PEAK_GBS * 1e9) if ew else 0.0)
     res = {
         "metric": "3D patches/sec per CycleGAN step (G+D fwd+bwd)",
-        "value": round(value, 3),
+        "value": head["value"],
         "unit": "patches/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * t_step, 3),
-        "ms_per_step_median": round(median_ms, 3),
+        "ms_per_step": head["ms_per_step"],
+        "ms_per_step_median": head["ms_per_step_median"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"f32": "f32", "bf16x3": "f32", "bf16": "bf16", "fp16": "fp16"}[args.precision],
-        "dtype_detail": {"f32": "exact f32 products",
-                         "bf16x3": "f32-grade products as 3 split-bf16 MFMAs, f32 accumulate",
-                         "bf16": "bf16 conv operands, f32 accumulate; f32 tensors, InstanceNorm, losses, Adam",
-                         "fp16": "fp16 conv operands with a static loss scale, f32 accumulate; f32 tensors, "
-                                 "InstanceNorm, losses, Adam"}[args.precision],
+        "dtype": head["dtype"],
+        "dtype_detail": head["dtype_detail"],
         "data": "synthetic N(0,1) volumes, random init (seed 0)",
         "config": {"workload": f"CycleGAN optimize_parameters(), {args.netG} G + 3-layer PatchGAN D, "
                                f"{args.nc}ch->{args.nc}ch, {args.size}^3 patch, batch {args.batch}/GPU ("
@@ -398,26 +459,15 @@ def main():
                    "conv_precision": args.precision,
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}",
-                   "step_launch": "hip_graph" if graphed else "eager",
+                   "step_launch": head["step_launch"],
                    "streams": 1 if args.single_stream else 2},
-        "roofline": {"bound": bound, "kernel": f"{dom['kernels']} ({prec}) — {dom_cls}",
-                     "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
-                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                     "launch_ms": round(dom["mean_ms"], 4), "launches_per_step": dom["n"] // 2,
-                     "ms_per_step": round(per_step_ms, 4),
-                     "flop_per_launch": dom["flops"], "bytes_per_launch": dom["bytes"],
-                     "timing": "HIP events around each C-ABI call, 2 eager steps right after the timed region"},
-        "top_kernels": top,
-        "step_roofline": {"achieved": round(ideal_s / t_step, 4), "ideal_ms": round(1e3 * ideal_s, 3),
-                          "formula": "(F/P_mfma + B_ew/BW_hbm) / T_step (SURVEY 8d)",
-                          "F_tflop": round(step_tf, 4), "P_mfma_tflops": round(mfma_peak, 1),
-                          "B_ew_gb": round(args.batch * ew / 1e9, 3) if ew else None, "BW_hbm_gbs": HBM_PEAK_GBS},
-        "step_tflop": round(step_tf, 4),
-        "step_tflops_achieved": round(step_tf / t_step, 2),
     }
-    if alt:
-        res["alt_precisions"] = {p: dict(v, value=round(world * args.batch / (v["ms_per_step"] / 1e3), 3))
-                                 for p, v in alt.items()}
+    for k in ("roofline", "step_roofline", "step_tflop", "step_tflops_achieved", "alt_precisions", "top_kernels",
+              "kernel_ms_per_step_serial"):
+        if k in head:
+            res[k] = head[k]
+    if legs:
+        res["legs"] = legs
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_child(args)
     print(json.dumps(res), flush=True)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 9
+#define MRAGAN_ABI_VERSION 10
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -45,8 +45,12 @@ const char* mragan_last_error(void);
  *                      accumulation (BASELINE configs[1]/[2] "bf16"), 2.5 PF peak;     (ABI 7)
  *   MRAGAN_PREC_F16    operands rounded to fp16, one v_mfma_f32_32x32x16_f16 per product, fp32
  *                      accumulation (configs[4] "fp16"); use with a loss scale.          (ABI 7)
- * The non-MFMA thin convolutions (D first/last layers) and their weight gradients stay exact
- * fp32 in every mode.                                                                         */
+ * In the bf16 / fp16 modes EVERY convolution operand is rounded (RNE) to that type — the MFMA
+ * kernels' fragments, and the operands the fp32-computing kernels load (the thin VALU convolutions
+ * of the image-channel layers: D first / last, the nc > 1 G stem / head; the fp32 fallbacks for
+ * channel counts the MFMA kernels do not tile): forward x and W, data-gradient dY and W,
+ * weight-gradient X and dY.  Products accumulate in fp32 (the thin D-first data gradient in
+ * fp64).  The fp32-grade modes (f32, bf16x3) never round.                              (ABI 10) */
 enum mragan_precision { MRAGAN_PREC_F32 = 0, MRAGAN_PREC_BF16X3 = 1, MRAGAN_PREC_BF16 = 2, MRAGAN_PREC_F16 = 3 };
 int mragan_set_conv_precision(int mode);
 int mragan_get_conv_precision(void);
@@ -192,6 +196,16 @@ int mragan_adam(float* p, const float* g, float* m, float* v, int64_t n, float l
  * as mragan_adam derives them, so both entry points produce identical parameters.            */
 int mragan_adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out6);
 int mragan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, void* stream);
+/* fp16 loss scaling without silent divergence (what torch.cuda.amp.GradScaler.step does for the
+ * reference's Adam, cycle_gan_model.py:107-110): mragan_nonfinite_flag ORs 1 into the DEVICE int
+ * *flag when g[0:n] holds an inf or NaN (call it on every flat gradient buffer of an optimizer);
+ * mragan_adam_dev_checked is mragan_adam_dev that leaves p, m and v untouched when *flag != 0;
+ * mragan_skip_count then adds (*flag != 0) to the DEVICE int *counter and clears *flag for the
+ * next step.  All graph-replayable.  (ABI 10)                                                   */
+int mragan_nonfinite_flag(const float* g, int64_t n, int* flag, void* stream);
+int mragan_adam_dev_checked(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* flag,
+                            void* stream);
+int mragan_skip_count(int* flag, int* counter, void* stream);
 int mragan_fill(float* p, int64_t n, float value, void* stream);
 /* ---- sliding-window inference (test.py:38-207 + TestModel, models/test_model.py) -------------
  * The normalised volume vol[X][Y][Z] (fp32, resident) is cut into the reference's patches and the

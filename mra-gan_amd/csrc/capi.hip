@@ -55,7 +55,7 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
   MRAGAN_CHECK_ARG(k >= 1 && stride >= 1 && pad >= 0, "conv: bad k/stride/pad");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
-    ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act};
+    ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act, g_conv_precision};
     if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride))
       return conv_thin1_x3(a, g_conv_precision, ws, ws_bytes, st);
     if (g_conv_precision != MRAGAN_PREC_F32 && thinn_x3_applicable(cin, cout, k, stride))
@@ -169,6 +169,7 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
     ThinWgradArgs a{};
     a.D = dense; a.N = N; a.Dd = Dd; a.Hd = Hd; a.Wd = Wd; a.Cd = Cd;
     a.G = gathered; a.Dg = Dg; a.Hg = Hg; a.Wg = Wg; a.Cg = Cg; a.k = k; a.s = stride; a.p = pad;
+    a.rnd = g_conv_precision;
     return conv_thin_wgrad(a, dw, accumulate, static_cast<float*>(ws), ws_bytes, st);
   }
   WgradArgs a{dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0,
@@ -284,7 +285,23 @@ int mragan_adam_hyper(float lr, float beta1, float beta2, float eps, int step, f
 
 int mragan_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, void* stream) {
   MRAGAN_CHECK_ARG(p && g && m && v && hyper, "adam_dev: bad args");
-  return adam_dev(p, g, m, v, n, hyper, static_cast<hipStream_t>(stream));
+  return adam_dev(p, g, m, v, n, hyper, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int mragan_adam_dev_checked(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* flag,
+                            void* stream) {
+  MRAGAN_CHECK_ARG(p && g && m && v && hyper && flag, "adam_dev_checked: bad args");
+  return adam_dev(p, g, m, v, n, hyper, flag, static_cast<hipStream_t>(stream));
+}
+
+int mragan_nonfinite_flag(const float* g, int64_t n, int* flag, void* stream) {
+  MRAGAN_CHECK_ARG(g && flag && n >= 0, "nonfinite_flag: bad args");
+  return nonfinite_flag(g, n, flag, static_cast<hipStream_t>(stream));
+}
+
+int mragan_skip_count(int* flag, int* counter, void* stream) {
+  MRAGAN_CHECK_ARG(flag && counter, "skip_count: bad args");
+  return skip_count(flag, counter, static_cast<hipStream_t>(stream));
 }
 
 int mragan_debug_stamps(unsigned long long* host, int n) { return thin1_debug_stamps(host, n); }

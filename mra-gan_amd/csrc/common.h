@@ -39,6 +39,21 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
   }
 }
 
+// Operand rounding of the 16-bit contraction modes in the kernels that compute in fp32 (the
+// thin VALU convolutions and the fp32 implicit-GEMM / weight-gradient fallbacks), so that a
+// bf16 / fp16 mode rounds EVERY convolution operand exactly as the MFMA kernels' fragment
+// conversion does (RNE): `mode` is the precision code (prec.h, kPrecBf16 = 2, kPrecF16 = 3);
+// the fp32-grade modes (f32, bf16x3 = 1) keep the value.
+__device__ __forceinline__ float op_round(float v, int mode) {
+  if (mode == 2) return (float)(__bf16)v;
+  if (mode == 3) return (float)(_Float16)v;
+  return v;
+}
+__device__ __forceinline__ float4 op_round4(float4 v, int mode) {
+  if (mode != 2 && mode != 3) return v;
+  return make_float4(op_round(v.x, mode), op_round(v.y, mode), op_round(v.z, mode), op_round(v.w, mode));
+}
+
 struct Vol {   // batch + spatial extents of an NDHWC tensor
   int n, d, h, w;
   __host__ __device__ int64_t spatial() const { return (int64_t)d * h * w; }

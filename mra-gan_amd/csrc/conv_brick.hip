@@ -367,7 +367,10 @@ bool conv_brick_x3_active(const IgemmArgs& a) {
 }
 
 bool conv_brick_applicable(const IgemmArgs& a) {
-  return a.k == 3 && a.s == 1 && a.cx % kBrickBK == 0 && a.ny % 64 == 0 && a.Di > 0;
+  // the x3 kernel's per-instance input descriptor has 32-bit byte offsets and reads its padding
+  // taps at kOobOffset = 2^31, which must lie outside the instance
+  return a.k == 3 && a.s == 1 && a.cx % kBrickBK == 0 && a.ny % 64 == 0 && a.Di > 0 &&
+         (int64_t)a.Di * a.Hi * a.Wi * a.cx * 4 < ((int64_t)1 << 31);
 }
 
 int conv_brick(const IgemmArgs& g, hipStream_t st) {

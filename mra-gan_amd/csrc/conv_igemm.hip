@@ -137,12 +137,12 @@ conv_igemm_f32_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
       int r = tid / LPR + i * ROWS_PER_PASS;
-      if (r < BM) *reinterpret_cast<float4*>(As + (buf * BM + r) * LDK + 4 * q) = ra[i];
+      if (r < BM) *reinterpret_cast<float4*>(As + (buf * BM + r) * LDK + 4 * q) = op_round4(ra[i], a.x3);
     }
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
       int r = tid / LPR + i * ROWS_PER_PASS;
-      if (r < BN) *reinterpret_cast<float4*>(Bs + (buf * BN + r) * LDK + 4 * q) = rb[i];
+      if (r < BN) *reinterpret_cast<float4*>(Bs + (buf * BN + r) * LDK + 4 * q) = op_round4(rb[i], a.x3);
     }
   };
 
@@ -241,6 +241,17 @@ static void igemm_geometry(IgemmArgs& a, int64_t& max_mc, int64_t& total_m) {
   total_m = (int64_t)a.N * a.Do * a.Ho * a.Wo;
 }
 
+// conv_igemm_x3 addresses its input through a buffer descriptor with 32-bit byte offsets: the
+// instances one launch may cover (0 when a single instance is already too large).  Larger batches
+// run as several launches on consecutive instance ranges (exact: every op is per instance).
+static int x3_instances_per_launch(const IgemmArgs& a) {
+  const int64_t per = (int64_t)a.Di * a.Hi * a.Wi * a.cx * 4;
+  const int64_t lim = ((int64_t)1 << 31) - 1;
+  if (per > lim) return 0;
+  const int64_t nb = lim / per;
+  return (int)(nb < a.N ? nb : a.N);
+}
+
 size_t conv_igemm_ws_bytes(IgemmArgs a) {
   int64_t max_mc, total_m;
   igemm_geometry(a, max_mc, total_m);
@@ -248,8 +259,33 @@ size_t conv_igemm_ws_bytes(IgemmArgs a) {
   if (!g_brick_off && conv_brick_applicable(a))
     return conv_brick_x3_active(a) ? conv_brick_x3_ws_bytes(a.cx, a.ny) : 0;
   if (!g_brick_off && brickT_x3_applicable(a)) return brickT_x3_ws_bytes(a);
-  if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_ws_bytes(a, max_mc, total_m);
+  if (a.x3 && a.cx % 16 == 0) {
+    const int nb = x3_instances_per_launch(a);
+    if (nb > 0 && nb < a.N) {
+      a.N = nb;
+      igemm_geometry(a, max_mc, total_m);
+    }
+    return conv_igemm_x3_ws_bytes(a, max_mc, total_m);
+  }
   return 0;
+}
+
+static int conv_igemm_x3_chunked(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  const int nb = x3_instances_per_launch(a);
+  MRAGAN_CHECK_ARG(nb > 0, "conv (16-bit MFMA modes): one %d×%d×%d×%d instance exceeds 2 GiB", a.Di, a.Hi, a.Wi, a.cx);
+  if (nb >= a.N) return conv_igemm_x3(a, max_mc, total_m, st);
+  const int64_t in_vol = (int64_t)a.Di * a.Hi * a.Wi * a.cx, out_vol = (int64_t)a.Do * a.Ho * a.Wo * a.ny;
+  for (int n0 = 0; n0 < a.N; n0 += nb) {
+    IgemmArgs c = a;
+    c.N = nb < a.N - n0 ? nb : a.N - n0;
+    c.x = a.x + n0 * in_vol;
+    c.y = a.y + n0 * out_vol;
+    int64_t mc, tm;
+    igemm_geometry(c, mc, tm);
+    const int rc = conv_igemm_x3(c, mc, tm, st);
+    if (rc) return rc;
+  }
+  return kOk;
 }
 
 int conv_igemm(IgemmArgs a, hipStream_t st) {
@@ -260,7 +296,7 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   if (max_mc == 0 || a.ny == 0) return kOk;
   if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
   if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
-  if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3(a, max_mc, total_m, st);
+  if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_chunked(a, max_mc, total_m, st);
   if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);
   if (a.cx % 16 == 0) return dispatch_tile<16>(a, max_mc, total_m, st);
   return dispatch_tile<8>(a, max_mc, total_m, st);

@@ -3,7 +3,8 @@
 //   * G head   Conv3d(ngf→nc, k7) + Tanh                   (networks3D.py:211-213)  fwd: thin_n
 //   * D first  Conv3d(nc→ndf, k4 s2 p1) + LeakyReLU        (networks3D.py:389-390)  fwd: thin_k
 //   * D last   Conv3d(8ndf→1, k4 s1 p1) (+ Sigmoid)        (networks3D.py:417-420)  fwd: thin_dot
-// and their data / weight gradients.  On fp32 the VALU FMA rate equals the f32 MFMA rate
+// and their data / weight gradients.  In the bf16 / fp16 modes every operand is rounded to that
+// type as it is loaded (op_round), like the MFMA kernels' fragments.  On fp32 the VALU FMA rate equals the f32 MFMA rate
 // (157 TF both), and these GEMMs have N or K of 1-2, so they are written as VALU direct
 // convolutions with the input halo staged in LDS and the per-tap weights read as
 // wave-uniform (scalar) loads.
@@ -44,14 +45,14 @@ __global__ void __launch_bounds__(256) thin_k_kernel(ThinArgs a, int tiles_d, in
     bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
     const float* src = a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * CX;
 #pragma unroll
-    for (int c = 0; c < CX; ++c) xs[e * CX + c] = ok ? src[c] : 0.f;
+    for (int c = 0; c < CX; ++c) xs[e * CX + c] = ok ? op_round(src[c], a.rnd) : 0.f;
   }
   // the block's weight slice for every tap, [t][32][CX], zero beyond ny (broadcast reads)
   const int T = a.k * a.k * a.k;
   float* wsl = xs + ((R * CX + 3) & ~3);
   for (int e = tid; e < T * TK_NB * CX; e += 256) {
     const int c = e % CX, j = (e / CX) % TK_NB, t = e / (CX * TK_NB);
-    wsl[e] = (n0 + j < a.ny) ? a.w[((int64_t)t * a.ny + n0 + j) * CX + c] : 0.f;
+    wsl[e] = (n0 + j < a.ny) ? op_round(a.w[((int64_t)t * a.ny + n0 + j) * CX + c], a.rnd) : 0.f;
   }
   __syncthreads();
   const int ow = tid % TK_OW, oh = (tid / TK_OW) % TK_OH, od = tid / (TK_OW * TK_OH);
@@ -140,8 +141,9 @@ __global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, in
         const int half = e & 1, n = (e >> 1) % NY, jj = (e >> 1) / NY;
         const int jw = jj % K, jh = jj / K;
         const int th = a.trans ? K - 1 - jh : jh, tw = a.trans ? K - 1 - jw : jw;
-        wsl[e] = *reinterpret_cast<const float4*>(a.w + ((int64_t)((td * K + th) * K + tw) * NY + n) * a.cx + c0 +
-                                                  4 * half);
+        wsl[e] = op_round4(*reinterpret_cast<const float4*>(a.w + ((int64_t)((td * K + th) * K + tw) * NY + n) * a.cx +
+                                                            c0 + 4 * half),
+                           a.rnd);
       }
       for (int e = tid; e < R; e += 256) {
         const int half = e & 1, pos = e >> 1;
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(256) thin_n_kernel(ThinArgs a, int tiles_h, in
         if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
           v = *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c0 +
                                                4 * half);
-        slab[rh * RS + tn_slot(rw) + half] = v;
+        slab[rh * RS + tn_slot(rw) + half] = op_round4(v, a.rnd);
       }
       __syncthreads();
       for (int jh = 0; jh < K; ++jh) {
@@ -229,11 +231,11 @@ __global__ void __launch_bounds__(256) thin_n_class_kernel(ThinArgs a) {
         const float* xr = a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx;
         const float* wt = a.w + (int64_t)((td * k + th) * k + tw) * NY * a.cx;
         for (int c = 0; c < a.cx; c += 4) {
-          const float4 xv = *reinterpret_cast<const float4*>(xr + c);
+          const float4 xv = op_round4(*reinterpret_cast<const float4*>(xr + c), a.rnd);
 #pragma unroll
           for (int n = 0; n < NY; ++n) {
-            const float* wn = wt + n * a.cx + c;
-            acc[n] = fmaf(xv.x, wn[0], fmaf(xv.y, wn[1], fmaf(xv.z, wn[2], fmaf(xv.w, wn[3], acc[n]))));
+            const float4 wn = op_round4(*reinterpret_cast<const float4*>(wt + n * a.cx + c), a.rnd);
+            acc[n] = fmaf(xv.x, wn.x, fmaf(xv.y, wn.y, fmaf(xv.z, wn.z, fmaf(xv.w, wn.w, acc[n]))));
           }
         }
       }
@@ -275,7 +277,7 @@ __global__ void __launch_bounds__(256) thin_n_class8_kernel(ThinArgs a) {
       const int q = j + 8 * u;
 #pragma unroll
       for (int n = 0; n < NY; ++n)
-        wr[t][u][n] = (tok && q < CQ) ? *reinterpret_cast<const float4*>(wt + n * a.cx + 4 * q)
+        wr[t][u][n] = (tok && q < CQ) ? op_round4(*reinterpret_cast<const float4*>(wt + n * a.cx + 4 * q), a.rnd)
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
@@ -302,7 +304,7 @@ __global__ void __launch_bounds__(256) thin_n_class8_kernel(ThinArgs a) {
       for (int u = 0; u < QPL; ++u) {
         const int q = j + 8 * u;
         if (q < CQ) {
-          const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * q);
+          const float4 xv = op_round4(*reinterpret_cast<const float4*>(xr + 4 * q), a.rnd);
 #pragma unroll
           for (int n = 0; n < NY; ++n) {
             const float4 wv = wr[t][u][n];
@@ -352,7 +354,8 @@ __global__ void __launch_bounds__(256) thin_naive_kernel(ThinArgs a) {
         id = nd / a.s; ih = nh / a.s; iw = nw / a.s;
       }
       if ((unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi || (unsigned)iw >= (unsigned)a.Wi) continue;
-      s = fmaf(a.x[((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c], a.w[((int64_t)t * a.ny + n) * a.cx + c], s);
+      s = fmaf(op_round(a.x[((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c], a.rnd),
+               op_round(a.w[((int64_t)t * a.ny + n) * a.cx + c], a.rnd), s);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -385,10 +388,11 @@ __global__ void __launch_bounds__(256) thin_dot_kernel(ThinArgs a) {
     const int tw = t % k, th = (t / k) % k, td = t / (k * k);
     const int id = od * a.s - a.p + td, ih = oh * a.s - a.p + th, iw = ow * a.s - a.p + tw;
     if ((unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi || (unsigned)iw >= (unsigned)a.Wi) continue;
-    const float4 xv = *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c);
+    const float4 xv = op_round4(
+        *reinterpret_cast<const float4*>(a.x + ((((int64_t)nb * a.Di + id) * a.Hi + ih) * a.Wi + iw) * a.cx + c), a.rnd);
 #pragma unroll
     for (int n = 0; n < NY; ++n) {
-      const float4 wv = *reinterpret_cast<const float4*>(a.w + ((int64_t)t * NY + n) * a.cx + c);
+      const float4 wv = op_round4(*reinterpret_cast<const float4*>(a.w + ((int64_t)t * NY + n) * a.cx + c), a.rnd);
       acc[n] = fmaf(xv.x, wv.x, fmaf(xv.y, wv.y, fmaf(xv.z, wv.z, fmaf(xv.w, wv.w, acc[n]))));
     }
   }
@@ -549,7 +553,7 @@ __global__ void __launch_bounds__(512) thin_wgrad_kernel(ThinWgradArgs a) {
       const int mw = mi % TW_W, mh = (mi / TW_W) % TW_H, md = mi / (TW_W * TW_H);
       const int gd = m0d + md, gh = m0h + mh, gw = m0w + mw;
       const bool ok = gd < a.Dd && gh < a.Hd && gw < a.Wd;
-      Dt[e] = ok ? a.D[((((int64_t)nb * a.Dd + gd) * a.Hd + gh) * a.Wd + gw) * a.Cd + c] : 0.f;
+      Dt[e] = ok ? op_round(a.D[((((int64_t)nb * a.Dd + gd) * a.Hd + gh) * a.Wd + gw) * a.Cd + c], a.rnd) : 0.f;
     }
     const int r0d = m0d * S - a.p, r0h = m0h * S - a.p, r0w = m0w * S - a.p;
     for (int e = tid; e < Rn * GCH; e += nthr) {
@@ -557,7 +561,7 @@ __global__ void __launch_bounds__(512) thin_wgrad_kernel(ThinWgradArgs a) {
       const int rw = ri % RW, rh = (ri / RW) % RH, rd = ri / (RW * RH);
       const int id = r0d + rd, ih = r0h + rh, iw = r0w + rw;
       const bool ok = (unsigned)id < (unsigned)a.Dg && (unsigned)ih < (unsigned)a.Hg && (unsigned)iw < (unsigned)a.Wg;
-      Gt[e] = ok ? a.G[((((int64_t)nb * a.Dg + id) * a.Hg + ih) * a.Wg + iw) * a.Cg + goff + c] : 0.f;
+      Gt[e] = ok ? op_round(a.G[((((int64_t)nb * a.Dg + id) * a.Hg + ih) * a.Wg + iw) * a.Cg + goff + c], a.rnd) : 0.f;
     }
     __syncthreads();
     if (!active) continue;

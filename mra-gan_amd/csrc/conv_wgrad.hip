@@ -95,12 +95,12 @@ conv_wgrad_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < D_LOADS; ++i) {
       int r = tid / LPR_D + i * RPP_D;
-      if (r < BKm) *reinterpret_cast<float4*>(Ds + (buf * BKm + r) * BM + 4 * qd) = rd[i];
+      if (r < BKm) *reinterpret_cast<float4*>(Ds + (buf * BKm + r) * BM + 4 * qd) = op_round4(rd[i], a.x3);
     }
 #pragma unroll
     for (int i = 0; i < G_LOADS; ++i) {
       int r = tid / LPR_G + i * RPP_G;
-      if (r < BKm) *reinterpret_cast<float4*>(Gs + (buf * BKm + r) * BN + 4 * qg) = rg[i];
+      if (r < BKm) *reinterpret_cast<float4*>(Gs + (buf * BKm + r) * BN + 4 * qg) = op_round4(rg[i], a.x3);
     }
   };
 
@@ -383,6 +383,25 @@ size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k)
 
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st) {
   MRAGAN_CHECK_ARG(a.Cd % 4 == 0 && a.Cg % 4 == 0, "conv_wgrad: channels must be multiples of 4 (%d,%d)", a.Cd, a.Cg);
+  if (a.x3 && a.N > 1) {
+    // the 16-bit MFMA kernels address their operands with 32-bit byte offsets: a batch whose
+    // tensors exceed 2 GiB runs as consecutive instance ranges accumulating into `out` (each
+    // range's plan needs at most the whole batch's workspace)
+    const int64_t dper = (int64_t)a.Dd * a.Hd * a.Wd * a.Cd, gper = (int64_t)a.Dg * a.Hg * a.Wg * a.Cg;
+    const int64_t per = 4 * (dper > gper ? dper : gper), lim = ((int64_t)1 << 31) - 1;
+    if (per * a.N > lim && per <= lim) {
+      const int nb = (int)(lim / per);
+      for (int n0 = 0; n0 < a.N; n0 += nb) {
+        WgradArgs c = a;
+        c.N = nb < a.N - n0 ? nb : a.N - n0;
+        c.D = a.D + n0 * dper;
+        c.G = a.G + n0 * gper;
+        const int rc = conv_wgrad(c, out, n0 == 0 ? accumulate : 1, ws_bytes, st);
+        if (rc) return rc;
+      }
+      return kOk;
+    }
+  }
   const int T = a.k * a.k * a.k;
   const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
   bool big;
@@ -403,7 +422,8 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   }
   const bool idx32 = M * a.Cd < ((int64_t)1 << 31) &&
                      (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31);
-  if (a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0 && idx32) {
+  const bool x3 = a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0 && idx32;
+  if (x3) {
     auto grid_of = [&](int bm, int bn) { return dim3(ceil_div(a.Cd, bm) * ceil_div(a.Cg, bn), T, a.splits); };
     MRAGAN_PREC_DISPATCH(a.x3, {
       if (a.Cd >= 128 && a.Cg >= 128)
@@ -429,7 +449,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
     dim3 grid(ceil_div(a.Cd, 64) * ceil_div(a.Cg, 64), T, a.splits);
     hipLaunchKernelGGL((conv_wgrad_f32_kernel<2, 2, 1, 1>), grid, dim3(256), 0, st, a);
   }
-  int rc = check_launch("conv_wgrad_f32");
+  int rc = check_launch(x3 ? "conv_wgrad_x3" : "conv_wgrad_f32");
   if (rc) return rc;
   return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, a.splits, accumulate, st);
 }

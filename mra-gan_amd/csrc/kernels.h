@@ -58,6 +58,7 @@ struct ThinArgs {
   const float* bias;
   float* y; int Do, Ho, Wo, ny;
   int k, s, p, trans, act;
+  int rnd;             // operand rounding (op_round): the precision mode, set by the C ABI
 };
 int conv_thin(ThinArgs a, hipStream_t st);
 // bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)
@@ -103,6 +104,7 @@ struct ThinWgradArgs {
   int tiles_d, tiles_h, tiles_w, ntiles;
   int nroles, RS;
   float* slab;     // [gridDim.x][Cd*Cg*k³]
+  int rnd;         // operand rounding (op_round): the precision mode, set by the C ABI
 };
 int conv_thin_wgrad(ThinWgradArgs a, float* out, int accumulate, float* ws, size_t ws_bytes, hipStream_t st);
 size_t conv_thin_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int s);
@@ -142,7 +144,10 @@ size_t channel_sum_ws_bytes(int64_t M, int C);
 int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, int step,
          float grad_scale, hipStream_t st);
 void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out);
-int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st);
+int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* skip,
+             hipStream_t st);
+int nonfinite_flag(const float* g, int64_t n, int* flag, hipStream_t st);
+int skip_count(int* flag, int* counter, hipStream_t st);
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);
 struct PackEntry {          // layout shared with include/mragan_hip.h (mragan_pack_entry)
   const float* src;

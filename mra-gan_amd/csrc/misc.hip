@@ -245,7 +245,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 // {step_size, beta1, beta2, eps, sqrt(bc2), grad_scale} (adam_hyper computes them exactly as
 // adam() does, so both paths produce identical bits)
 __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                float* __restrict__ v, int64_t n, const float* __restrict__ hyper) {
+                                float* __restrict__ v, int64_t n, const float* __restrict__ hyper,
+                                const int* __restrict__ skip) {
+  if (skip && *skip) return;        // a non-finite gradient this step: no update (GradScaler's skip)
   const float step_size = hyper[0], beta1 = hyper[1], beta2 = hyper[2], eps = hyper[3], bc2_sqrt = hyper[4],
               grad_scale = hyper[5];
   const float w1 = 1.f - beta1;
@@ -496,9 +498,35 @@ void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float g
   out[4] = (float)sqrt(bc2);
   out[5] = grad_scale;
 }
-int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, hipStream_t st) {
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, hyper);
+int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* skip,
+             hipStream_t st) {
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, hyper, skip);
   return check_launch("adam_dev");
+}
+
+// ---- found-inf (fp16 loss scaling) ----------------------------------------------------------
+// flag |= 1 when any of g[0:n] is inf / NaN: one vector atomic per wave that saw one
+__global__ void nonfinite_kernel(const float* __restrict__ g, int64_t n, int* flag) {
+  bool bad = false;
+  GRID_STRIDE(i, n) bad |= !isfinite(g[i]);
+  if (__builtin_amdgcn_ballot_w64(bad) != 0 && (threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_ballot_w64(bad)))
+    atomicOr(flag, 1);
+}
+int nonfinite_flag(const float* g, int64_t n, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_cap(n, 2048)), dim3(256), 0, st, g, n, flag);
+  return check_launch("nonfinite");
+}
+// after the step's updates: counter += (flag != 0); flag = 0
+__global__ void skip_count_kernel(int* flag, int* counter) {
+  if (threadIdx.x == 0) {
+    const int f = *flag;
+    *counter += f != 0;
+    *flag = 0;
+  }
+}
+int skip_count(int* flag, int* counter, hipStream_t st) {
+  hipLaunchKernelGGL(skip_count_kernel, dim3(1), dim3(64), 0, st, flag, counter);
+  return check_launch("skip_count");
 }
 int pack_weights_batched(const PackEntry* table, int n, int64_t max_elems, hipStream_t st) {
   if (n <= 0) return kOk;

@@ -105,8 +105,8 @@ class BaseModel:
     def save_networks(self, which_epoch):
         """Writes '<epoch>_net_<name>.pth' = the net's state_dict on CPU (reference :89-112).
         The net itself is not moved (its parameters live in flat device buffers).  Data parallel:
-        the running statistics are averaged over the ranks first (every rank must call this)."""
-        self.sync_running_stats()
+        average the running statistics with sync_running_stats() on EVERY rank first (a
+        collective), then save from one rank (train.py does both)."""
         os.makedirs(self.save_dir, exist_ok=True)
         for name in self.model_names:
             if isinstance(name, str):

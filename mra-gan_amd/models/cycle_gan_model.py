@@ -209,6 +209,11 @@ class FusedAdam(torch.optim.Optimizer):
         self._v = {}
         self.step_count = 0
         self.grad_scale = 1.0
+        # loss-scaled (fp16) training: skip the update of a step whose gradients overflowed, like
+        # torch.cuda.amp.GradScaler.step (device flag, graph-replayable; count in `skipped()`)
+        self.check_finite = False
+        self._flag = None
+        self._skipped = None
 
     def zero_grad(self, set_to_none: bool = True):
         from mragan_hip import ops
@@ -234,13 +239,31 @@ class FusedAdam(torch.optim.Optimizer):
     def step_dev(self, hyper):
         """Device half: one fused Adam kernel per flat buffer with the scalars in `hyper`
         (written by the host before the kernels run; graph-replayable)."""
+        ops = ops_mod()
+        if self.check_finite:
+            if self._flag is None:
+                dev = self.nets[0]._flat_grad.device
+                self._flag = torch.zeros(1, dtype=torch.int32, device=dev)
+                self._skipped = torch.zeros(1, dtype=torch.int32, device=dev)
+            for n in self.nets:
+                networks3D.ensure_flat(n)
+                ops.nonfinite_flag(n._flat_grad, self._flag)
         for n in self.nets:
             networks3D.ensure_flat(n)
             m, v = self._state(n)
-            ops_mod().adam_dev(n._flat_param, n._flat_grad, m, v, hyper)
+            if self.check_finite:
+                ops.adam_dev_checked(n._flat_param, n._flat_grad, m, v, hyper, self._flag)
+            else:
+                ops.adam_dev(n._flat_param, n._flat_grad, m, v, hyper)
             n.mark_params_dirty()
+        if self.check_finite:
+            ops.skip_count(self._flag, self._skipped)
         # what torch's step wrapper records for an LR scheduler (it warns otherwise)
         self._opt_called = True
+
+    def skipped(self) -> int:
+        """Steps whose update was skipped for a non-finite gradient (synchronizes)."""
+        return 0 if self._skipped is None else int(self._skipped.item())
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -315,6 +338,7 @@ class CycleGANModel(BaseModel):
             self.optimizer_G = FusedAdam([self.netG_A, self.netG_B], lr=opt.lr, betas=(opt.beta1, 0.999))
             self.optimizer_D = FusedAdam([self.netD_A, self.netD_B], lr=opt.lr, betas=(opt.beta1, 0.999))
             self.optimizers = [self.optimizer_G, self.optimizer_D]
+            self.optimizer_G.check_finite = self.optimizer_D.check_finite = self.loss_scale != 1.0
             self._loss_buf = torch.zeros(8, device=self.device, dtype=torch.float32)
             for i, n in enumerate(self.loss_names):
                 setattr(self, 'loss_' + n, self._loss_buf[i])

@@ -77,60 +77,64 @@ WS = Workspace()
 
 
 class KernelTimer:
-    """Optional per-launch HIP-event timing of selected C-ABI calls (bench.py measures the
-    dominant kernel with it, on the stream the kernels run on).  Each instrumented wrapper passes
-    an info dict with a launch-class key `cls`, its algorithmic `flops` (MFMA-bound calls) or
-    `bytes` (HBM-bound calls); the library's launch log names the kernels the call launched."""
+    """Per-launch-class timing of the instrumented C-ABI calls (bench.py's dominant-kernel
+    roofline).  While `match` is set, each instrumented wrapper hands its call to `run(info, fn)`:
+    the call is issued as usual and recorded — launch class `cls`, algorithmic `flops`
+    (MFMA-bound) or `bytes` (HBM-bound), the kernels it launched (library launch log) and the
+    call itself.  `classes(reps)` then re-issues ONE recorded call of each class `reps` times back
+    to back on the current stream between two HIP events (one warm launch first), so a class's
+    mean is the kernels' own duration: no host submission gap inside the interval and no spin
+    kernel in a profile of the run."""
 
     def __init__(self):
         self.match = None       # callable(info: dict) -> bool
-        self.events = []        # (info, start, end, kernel names)
+        self.calls = []         # (info, kernel names, fn)
 
-    def begin(self, info):
-        if self.match is None or not self.match(info):
-            return None
-        if torch.cuda.is_current_stream_capturing():
-            return None         # ROCm cannot time event nodes of a graph: eager launches only
+    def run(self, info, fn):
+        if self.match is None or not self.match(info) or torch.cuda.is_current_stream_capturing():
+            fn()
+            return
         from ._lib import lib
         lib().mragan_launch_log(1)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        # keep the GPU busy until the launch below is queued: otherwise the interval also holds
-        # the host's submission latency (the GPU reaches the start event, then idles)
-        torch.cuda._sleep(100000)
-        s.record()
-        return (info, s, e)
-
-    def end(self, tok):
-        if tok is not None:
-            tok[2].record()
-            from ._lib import lib
-            self.events.append((tok[0], tok[1], tok[2], lib().mragan_launch_log(1).decode()))
+        fn()
+        self.calls.append((info, lib().mragan_launch_log(1).decode(), fn))
 
     def reset(self):
-        self.events = []
+        self.calls = []
 
-    def mean_ms(self):
-        if not self.events:
-            return None
-        torch.cuda.synchronize()
-        return sum(s.elapsed_time(e) for _, s, e, _ in self.events) / len(self.events)
-
-    def classes(self):
-        """{cls: dict(n, total_ms, mean_ms, flops|bytes per launch, kernels)} over the recorded
-        launches, largest total time first."""
-        torch.cuda.synchronize()
+    def classes(self, reps: int = 10):
+        """{cls: dict(n, total_ms, mean_ms, flops|bytes per launch, kernels)} for the recorded
+        calls (n = launches recorded, total_ms = n × mean_ms), largest total time first."""
         out = {}
-        for info, s, e, names in self.events:
-            c = out.setdefault(info["cls"], dict(n=0, total_ms=0.0, flops=info.get("flops"), bytes=info.get("bytes"),
-                                                 kernels=names, info=info))
+        for info, names, fn in self.calls:
+            c = out.setdefault(info["cls"], dict(n=0, flops=info.get("flops"), bytes=info.get("bytes"), kernels=names,
+                                                 info=info, fn=fn))
             c["n"] += 1
-            c["total_ms"] += s.elapsed_time(e)
         for c in out.values():
-            c["mean_ms"] = c["total_ms"] / c["n"]
+            fn = c.pop("fn")
+            fn()                                    # warm: first-touch of the operands, code load
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                fn()
+            e.record()
+            e.synchronize()
+            c["mean_ms"] = s.elapsed_time(e) / reps
+            c["total_ms"] = c["mean_ms"] * c["n"]
+            c["reps"] = reps
+        self.calls = []
         return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_ms"]))
 
 
 TIMER = KernelTimer()
+
+
+def _timed(info_fn, fn):
+    """Issue fn(); when the timer records, under the launch class info_fn() describes."""
+    if TIMER.match is None:
+        fn()
+    else:
+        TIMER.run(info_fn(), fn)
 
 
 PRECISION = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
@@ -185,25 +189,26 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     elif tuple(out.shape) != (N, Do, Ho, Wo, cout):
         raise ValueError(f"conv3d: out shape {tuple(out.shape)} != {(N, Do, Ho, Wo, cout)}")
     name = "mragan_conv3d_transposed" if transposed else "mragan_conv3d_fwd"
-    tm = None
-    if TIMER.match:
-        vox = Di * Hi * Wi if transposed else Do * Ho * Wo       # algorithmic: every tap of every voxel
-        tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
-                              in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo),
-                              cls=f"{'convT' if transposed else 'conv'} {cin}->{cout} k{k} s{s} [{N}x{Di}x{Hi}x{Wi}]",
-                              flops=2.0 * N * vox * cin * cout * k ** 3))
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
     ws = WS.get(nbytes) if nbytes else None
     if wsplit is not None:
         if wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
             raise ValueError("conv3d: wsplit size does not match the packed weight")
-        call("mragan_conv3d_presplit", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), _ptr(bias), cout, k, s, p,
-             ACT[act], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _stream())
+        fn = lambda: call("mragan_conv3d_presplit", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), _ptr(bias),
+                          cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _stream())
     else:
-        call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo,
-             _ptr(ws), nbytes, _stream())
-    TIMER.end(tm)
+        fn = lambda: call(name, _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p, ACT[act], _ptr(out),
+                          Do, Ho, Wo, _ptr(ws), nbytes, _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
     return out
+
+
+def _conv_info(cin, cout, k, s, p, transposed, N, in_sp, out_sp):
+    vox = in_sp[0] * in_sp[1] * in_sp[2] if transposed else out_sp[0] * out_sp[1] * out_sp[2]   # every tap of every voxel
+    Di, Hi, Wi = in_sp
+    return dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N, in_spatial=in_sp,
+                out_spatial=out_sp, cls=f"{'convT' if transposed else 'conv'} {cin}->{cout} k{k} s{s} [{N}x{Di}x{Hi}x{Wi}]",
+                flops=2.0 * N * vox * cin * cout * k ** 3)
 
 
 def in_partials_buffer(N: int, out_spatial: Sequence[int], cout: int, device) -> torch.Tensor:
@@ -227,20 +232,13 @@ def conv3d_in_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("conv3d_in_stats: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
-    tm = None
-    if TIMER.match:
-        vox = Di * Hi * Wi if transposed else Do * Ho * Wo
-        tm = TIMER.begin(dict(op="conv", cin=cin, cout=cout, k=k, s=s, p=p, transposed=transposed, N=N,
-                              in_spatial=(Di, Hi, Wi), out_spatial=(Do, Ho, Wo),
-                              cls=f"{'convT' if transposed else 'conv'} {cin}->{cout} k{k} s{s} [{N}x{Di}x{Hi}x{Wi}]",
-                              flops=2.0 * N * vox * cin * cout * k ** 3))
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
     ws = WS.get(nbytes) if nbytes else None
     chunks = _ct.c_int(0)
-    call("mragan_conv3d_presplit_in_stats", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), None, cout, k, s, p,
-         ACT[None], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(part), part.numel() * 8,
-         _ct.byref(chunks), _stream())
-    TIMER.end(tm)
+    fn = lambda: call("mragan_conv3d_presplit_in_stats", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), None,
+                      cout, k, s, p, ACT[None], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(part),
+                      part.numel() * 8, _ct.byref(chunks), _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
     return out, chunks.value
 
 
@@ -256,11 +254,10 @@ def conv3d_wgrad(dense: torch.Tensor, gathered: torch.Tensor, k: int, s: int, p:
         raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
     nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
     ws = WS.get(nbytes)
-    tm = TIMER.begin(dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
-                          flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3)) if TIMER.match else None
-    call("mragan_conv3d_wgrad", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered), Dg, Hg, Wg, Cg, k, s, p, _ptr(dw),
-         int(accumulate), _ptr(ws), ws.numel(), _stream())
-    TIMER.end(tm)
+    fn = lambda: call("mragan_conv3d_wgrad", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered), Dg, Hg, Wg, Cg, k, s, p,
+                      _ptr(dw), int(accumulate), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
+                        flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)
     return dw
 
 
@@ -325,16 +322,15 @@ def instnorm_fwd(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch
             raise ValueError("instnorm: residual shape mismatch")
     nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
     ws = WS.get(nbytes)
-    # essential HBM bytes: read x (+ the residual), write y (padded)
-    tm = TIMER.begin(dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad}",
-                          bytes=4.0 * (x.numel() * (2 if resid is not None else 1) + out.numel()))) if TIMER.match else None
     if part is not None and chunks > 0:
-        call("mragan_instnorm_fwd_partials", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad,
-             _ptr(mean), _ptr(rstd), _ptr(part), chunks, _stream())
+        fn = lambda: call("mragan_instnorm_fwd_partials", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act],
+                          _ptr(resid), rpad, _ptr(mean), _ptr(rstd), _ptr(part), chunks, _stream())
     else:
-        call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad, _ptr(mean),
-             _ptr(rstd), _ptr(ws), ws.numel(), _stream())
-    TIMER.end(tm)
+        fn = lambda: call("mragan_instnorm_fwd", _ptr(x), N, D, H, W, C, _ptr(out), ypad, ACT[act], _ptr(resid), rpad,
+                          _ptr(mean), _ptr(rstd), _ptr(ws), ws.numel(), _stream())
+    # essential HBM bytes: read x (+ the residual), write y (padded)
+    _timed(lambda: dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad}",
+                        bytes=4.0 * (x.numel() * (2 if resid is not None else 1) + out.numel())), fn)
     return out, mean, rstd
 
 
@@ -351,21 +347,19 @@ def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: to
         out = torch.empty_like(x)
     nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
     ws = WS.get(nbytes)
-    # essential HBM bytes: read x, dy (padded) (+ dy_add), write dx
-    tm = TIMER.begin(dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad}",
-                          bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
-                                           + (x.numel() if g_out is not None else 0))))\
-        if TIMER.match else None
     if g_out is None:
-        call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
-             ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
+        fn = lambda: call("mragan_instnorm_bwd", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad,
+                          _ptr(dy_add), ACT[act], _ptr(out), _ptr(ws), ws.numel(), _stream())
     else:
         _check(g_out, "instnorm_bwd.g_out")
         if tuple(g_out.shape) != tuple(x.shape):
             raise ValueError("instnorm_bwd: g_out shape mismatch")
-        call("mragan_instnorm_bwd_g", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad, _ptr(dy_add),
-             ACT[act], _ptr(out), _ptr(g_out), _ptr(ws), ws.numel(), _stream())
-    TIMER.end(tm)
+        fn = lambda: call("mragan_instnorm_bwd_g", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad,
+                          _ptr(dy_add), ACT[act], _ptr(out), _ptr(g_out), _ptr(ws), ws.numel(), _stream())
+    # essential HBM bytes: read x, dy (padded) (+ dy_add), write dx
+    _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad}",
+                        bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                     + (x.numel() if g_out is not None else 0))), fn)
     return out
 
 
@@ -470,6 +464,24 @@ def adam_dev(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
     if hyper.dtype != torch.float32 or hyper.numel() < 6 or not hyper.is_cuda:
         raise ValueError("adam_dev: hyper must be a device float32 tensor of 6 values")
     call("mragan_adam_dev", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(hyper), _stream())
+
+
+def adam_dev_checked(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, hyper: torch.Tensor,
+                     flag: torch.Tensor):
+    """adam_dev that leaves p, m, v untouched when the device int `flag` is non-zero."""
+    if flag.dtype != torch.int32 or not flag.is_cuda:
+        raise ValueError("adam_dev_checked: flag must be a device int32 tensor")
+    call("mragan_adam_dev_checked", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(hyper), _ptr(flag), _stream())
+
+
+def nonfinite_flag(g: torch.Tensor, flag: torch.Tensor):
+    """flag |= 1 (device int32) when g holds an inf / NaN."""
+    call("mragan_nonfinite_flag", _ptr(g), g.numel(), _ptr(flag), _stream())
+
+
+def skip_count(flag: torch.Tensor, counter: torch.Tensor):
+    """counter += (flag != 0); flag = 0 (both device int32)."""
+    call("mragan_skip_count", _ptr(flag), _ptr(counter), _stream())
 
 
 def fill(t: torch.Tensor, value: float):

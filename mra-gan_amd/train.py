@@ -19,6 +19,20 @@ from options.train_options import TrainOptions  # noqa: E402
 from utils.visualizer import Visualizer  # noqa: E402
 
 
+def _rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def save(model, *tags):
+    """Checkpoint: every rank averages the InstanceNorm running statistics (a collective, so all
+    ranks call this at the same iteration), rank 0 writes the files."""
+    model.sync_running_stats()
+    if _rank() == 0:
+        for t in tags:
+            model.save_networks(t)
+
+
 def train(opt, sampler, model=None, log=print):
     """train.py:70-147 over `sampler` (yields dict(image=..., label=...) batches)."""
     if model is None:
@@ -47,12 +61,11 @@ def train(opt, sampler, model=None, log=print):
                 visualizer.print_current_losses(epoch, epoch_iter, losses, t, t_data)
             if total_steps % opt.save_latest_freq == 0:
                 log('saving the latest model (epoch %d, total_steps %d)' % (epoch, total_steps))
-                model.save_networks('latest')
+                save(model, 'latest')
             iter_data_time = time.time()
         if epoch % opt.save_epoch_freq == 0:
             log('saving the model at the end of epoch %d, iters %d' % (epoch, total_steps))
-            model.save_networks('latest')
-            model.save_networks(epoch)
+            save(model, 'latest', epoch)
         log('End of epoch %d / %d \t Time Taken: %d sec' %
             (epoch, opt.niter + opt.niter_decay, time.time() - epoch_start_time))
         model.update_learning_rate()

@@ -172,14 +172,40 @@ def test_conv_transpose3d_fwd_dgrad_wgrad(ops, N, cin, cout, S, k, s, p, op):
 
 
 X3_TOL = 2e-5     # bf16x3: ≤ 3·2⁻¹⁸ relative per product, random → ~5e-6 rel-L2 measured scale
-# rel-L2 gates of the MFMA modes on random operands: bf16x3 as above; bf16 / fp16 round each
-# operand once (unit roundoff 2⁻⁸ / 2⁻¹¹ → ~3e-3 / ~4e-4 rel-L2 expected for a long random sum)
-MODE_TOL = {"bf16x3": X3_TOL, "bf16": 1e-2, "fp16": 1.5e-3}
+# bf16 / fp16: every operand is rounded once (RNE) and the products of the rounded operands are
+# exact in fp32, so the kernel must equal the fp64 convolution of the ROUNDED operands up to fp32
+# accumulation order (~1e-6 rel-L2): same gate as bf16x3.  The unrounded fp64 result is a further
+# check that the rounding happened (unit roundoff 2⁻⁸ / 2⁻¹¹ moves a long random sum by ≥ 1e-3 /
+# 1e-4 rel-L2).
+MODE_TOL = {"bf16x3": X3_TOL, "bf16": X3_TOL, "fp16": X3_TOL}
+ROUNDED_MIN_DIFF = {"bf16": 1e-3, "fp16": 1e-4}
 
 
 def xtol():
     from mragan_hip import ops
     return MODE_TOL[ops.get_conv_precision()]
+
+
+def R(t):
+    """An operand as the current contraction mode feeds it to the products: bf16 / fp16 round
+    (RNE) the fp32 value, the fp32-grade modes keep it (include/mragan_hip.h, ABI 10)."""
+    from mragan_hip import ops
+    mode = ops.get_conv_precision()
+    t32 = t.detach().float()
+    if mode == "bf16":
+        return t32.to(torch.bfloat16).double()
+    if mode == "fp16":
+        return t32.to(torch.float16).double()
+    return t32.double()
+
+
+def check_rounded(got, ref_rounded, ref_exact):
+    """got vs the fp64 result on rounded operands; in bf16 / fp16 also far from the unrounded one."""
+    from mragan_hip import ops
+    mode = ops.get_conv_precision()
+    assert rel(got, ref_rounded) < MODE_TOL[mode]
+    if mode in ROUNDED_MIN_DIFF:
+        assert rel(got, ref_exact) > ROUNDED_MIN_DIFF[mode], "operands were not rounded"
 
 X3_CASES = [
     # N, cin, cout, S, k, s, p   (every tile shape of conv_igemm_x3.hip's dispatch)
@@ -209,17 +235,19 @@ def x3(ops, request):
 def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
     ops = x3
     g = torch.Generator().manual_seed(5 + N * 100 + cin + cout)
-    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
     w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
     b = torch.randn(cout, generator=g, dtype=torch.float64)
     y = F.conv3d(x, w, b, stride=s, padding=p)
+    yr = F.conv3d(R(x), R(w), b.float().double(), stride=s, padding=p)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
-    (dx_ref,) = torch.autograd.grad(y, x, dy)
-    out = ops.conv3d(ndhwc(x.detach().float()).cuda(), pack(ops, w, False, False), cout, k, s, p, y.shape[2:],
+    dx_ref = torch.nn.grad.conv3d_input(x.shape, w, dy, stride=s, padding=p)
+    dx_rnd = torch.nn.grad.conv3d_input(x.shape, R(w), R(dy), stride=s, padding=p)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), cout, k, s, p, y.shape[2:],
                      bias=b.float().cuda(), act="lrelu")
-    assert rel(ncdhw(out), F.leaky_relu(y.detach(), 0.2)) < xtol()
+    check_rounded(ncdhw(out), F.leaky_relu(yr, 0.2), F.leaky_relu(y, 0.2))
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w, False, True), cin, k, s, p, x.shape[2:], transposed=True)
-    assert rel(ncdhw(dx), dx_ref) < xtol()
+    check_rounded(ncdhw(dx), dx_rnd, dx_ref)
 
 
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1),
@@ -228,15 +256,16 @@ def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
     ops = x3
     g = torch.Generator().manual_seed(13 + N * 10 + cin + cout)
     x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
-    w = (torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
     y = F.conv3d(x, w, stride=s, padding=p)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
-    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw_ref = torch.nn.grad.conv3d_weight(x, w.shape, dy, stride=s, padding=p)
+    dw_rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), stride=s, padding=p)
     dw = torch.full((cout, cin, k, k, k), 3.0, device="cuda")
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=False)
-    assert rel(dw, dw_ref) < xtol()
+    check_rounded(dw, dw_rnd, dw_ref)
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=True)
-    assert rel(dw, 2 * dw_ref) < xtol()
+    check_rounded(dw, 2 * dw_rnd, 2 * dw_ref)
 
 
 @pytest.mark.parametrize("N,cin,cout,dims", [(1, 32, 64, (8, 10, 32)), (2, 64, 128, (6, 4, 64)), (1, 32, 128, (4, 2, 32)),
@@ -249,13 +278,14 @@ def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
     ops = x3
     g = torch.Generator().manual_seed(17 + N + cin + cout)
     x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
-    w = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1
     y = F.conv3d(x, w, stride=2, padding=1)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
-    (dw_ref,) = torch.autograd.grad(y, w, dy)
+    dw_ref = torch.nn.grad.conv3d_weight(x, w.shape, dy, stride=2, padding=1)
+    dw_rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), stride=2, padding=1)
     dw = torch.full((cout, cin, 3, 3, 3), 3.0, device="cuda")
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 2, 1, dw, accumulate=False)
-    assert rel(dw, dw_ref) < xtol()
+    check_rounded(dw, dw_rnd, dw_ref)
     # transposed: ConvTranspose3d(cout → cin) on the coarse grid of y, output padding 1
     xt = torch.randn(y.shape, generator=g, dtype=torch.float64)
     wt = (torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
@@ -263,9 +293,12 @@ def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
     assert tuple(yt.shape[2:]) == tuple(dims)
     dyt = torch.randn(yt.shape, generator=g, dtype=torch.float64)
     (dwt_ref,) = torch.autograd.grad(yt, wt, dyt)
+    xr = R(xt).requires_grad_()
+    wr = R(wt).requires_grad_()
+    (dwt_rnd,) = torch.autograd.grad(F.conv_transpose3d(xr, wr, stride=2, padding=1, output_padding=1), wr, R(dyt))
     dwt = torch.zeros((cout, cin, 3, 3, 3), device="cuda")
     ops.conv3d_wgrad(ndhwc(xt.float()).cuda(), ndhwc(dyt.float()).cuda(), 3, 2, 1, dwt, accumulate=False)
-    assert rel(dwt, dwt_ref) < xtol()
+    check_rounded(dwt, dwt_rnd, dwt_ref)
 
 
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
@@ -277,11 +310,40 @@ def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
     y = F.conv_transpose3d(x, w, stride=s, padding=p, output_padding=op)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     (dx_ref,) = torch.autograd.grad(y, x, dy)
+    xr = R(x).requires_grad_()
+    yr = F.conv_transpose3d(xr, R(w), stride=s, padding=p, output_padding=op)
+    (dx_rnd,) = torch.autograd.grad(F.conv_transpose3d(xr, R(w), stride=s, padding=p, output_padding=op), xr, R(dy))
     out = ops.conv3d(ndhwc(x.detach().float()).cuda(), pack(ops, w, True, False), cout, k, s, p, y.shape[2:],
                      transposed=True)
-    assert rel(ncdhw(out), y.detach()) < xtol()
+    check_rounded(ncdhw(out), yr.detach(), y.detach())
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w, True, True), cin, k, s, p, x.shape[2:])
-    assert rel(ncdhw(dx), dx_ref) < xtol()
+    check_rounded(ncdhw(dx), dx_rnd, dx_ref)
+
+
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p", CONV_CASES)
+def test_conv_all_paths_rounding(x3, N, cin, cout, S, k, s, p):
+    """Every dispatch path — the thin VALU kernels of the image-channel layers and the fp32
+    fallbacks included — rounds its operands in the bf16 / fp16 modes exactly like the MFMA
+    kernels (ABI 10): forward, data gradient and weight gradient each equal the fp64 convolution
+    of the rounded operands up to fp32 accumulation order."""
+    ops = x3
+    g = torch.Generator().manual_seed(23 + N * 1000 + cin * 7 + cout)
+    x = torch.randn(N, cin, S, S + 1, S + 2, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64)
+    y = F.conv3d(x, w, b.float().double(), stride=s, padding=p)
+    yr = F.conv3d(R(x), R(w), b.float().double(), stride=s, padding=p)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), cout, k, s, p, y.shape[2:],
+                     bias=b.float().cuda())
+    check_rounded(ncdhw(out), yr, y)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, w, False, True), cin, k, s, p, x.shape[2:], transposed=True)
+    check_rounded(ncdhw(dx), torch.nn.grad.conv3d_input(x.shape, R(w), R(dy), stride=s, padding=p),
+                  torch.nn.grad.conv3d_input(x.shape, w, dy, stride=s, padding=p))
+    dw = torch.zeros((cout, cin, k, k, k), device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), k, s, p, dw, accumulate=False)
+    check_rounded(dw, torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), stride=s, padding=p),
+                  torch.nn.grad.conv3d_weight(x, w.shape, dy, stride=s, padding=p))
 
 
 def test_conv_precision_modes(ops):
@@ -522,14 +584,14 @@ def test_thin1_bf16x3_stem_fwd_head_dgrad(x3, N, ngf, S, p):
     y = F.conv3d(x, w, b, padding=p)
     out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), ngf, 7, 1, p, y.shape[2:],
                      bias=b.float().cuda(), act="lrelu")
-    assert rel(ncdhw(out), F.leaky_relu(y, 0.2)) < xtol()
+    check_rounded(ncdhw(out), F.leaky_relu(F.conv3d(R(x), R(w), b, padding=p), 0.2), F.leaky_relu(y, 0.2))
     xh = torch.randn(N, ngf, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
     wh = torch.randn(1, ngf, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1
     yh = F.conv3d(xh, wh, padding=p)
     dy = torch.randn(yh.shape, generator=g, dtype=torch.float64)
     (dx_ref,) = torch.autograd.grad(yh, xh, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wh, False, True), ngf, 7, 1, p, xh.shape[2:], transposed=True)
-    assert rel(ncdhw(dx), dx_ref) < xtol()
+    check_rounded(ncdhw(dx), torch.nn.grad.conv3d_input(xh.shape, R(wh), R(dy), padding=p), dx_ref)
 
 
 @pytest.mark.parametrize("N,ngf,S,p", [(2, 32, 12, 0), (1, 32, 37, 0), (2, 32, 9, 3)])
@@ -544,10 +606,11 @@ def test_thin1_bf16x3_wgrad(x3, N, ngf, S, p):
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     (dw_ref,) = torch.autograd.grad(y, w, dy)
     dw = torch.full((ngf, 1, 7, 7, 7), 3.0, device="cuda")
+    dw_rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), padding=p)
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 7, 1, p, dw, accumulate=False)
-    assert rel(dw, dw_ref) < xtol()
+    check_rounded(dw, dw_rnd, dw_ref)
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 7, 1, p, dw, accumulate=True)
-    assert rel(dw, 2 * dw_ref) < xtol()
+    check_rounded(dw, 2 * dw_rnd, 2 * dw_ref)
     xh = torch.randn(N, ngf, S, S + 1, S + 2, generator=g, dtype=torch.float64)
     wh = (torch.randn(1, ngf, 7, 7, 7, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
     yh = F.conv3d(xh, wh, padding=p)
@@ -555,7 +618,7 @@ def test_thin1_bf16x3_wgrad(x3, N, ngf, S, p):
     (dwh_ref,) = torch.autograd.grad(yh, wh, dz)
     dwh = torch.empty(1, ngf, 7, 7, 7, device="cuda")
     ops.conv3d_wgrad(ndhwc(dz.float()).cuda(), ndhwc(xh.float()).cuda(), 7, 1, p, dwh, accumulate=False)
-    assert rel(dwh, dwh_ref) < xtol()
+    check_rounded(dwh, torch.nn.grad.conv3d_weight(R(xh), wh.shape, R(dz), padding=p), dwh_ref)
 
 
 @pytest.mark.parametrize("N,S,p", [(2, 12, 0), (1, 37, 0), (2, 9, 3), (1, 70, 0)])
@@ -570,14 +633,14 @@ def test_thinn_bf16x3_head_fwd_stem_dgrad(x3, N, S, p):
     y = torch.tanh(F.conv3d(x, w, b, padding=p))
     out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), 1, 7, 1, p, y.shape[2:],
                      bias=b.float().cuda(), act="tanh")
-    assert rel(ncdhw(out), y) < xtol()
+    check_rounded(ncdhw(out), torch.tanh(F.conv3d(R(x), R(w), b, padding=p)), y)
     xs = torch.randn(N, 1, S, S + 1, S + 2, generator=g, dtype=torch.float64, requires_grad=True)
     ws = torch.randn(32, 1, 7, 7, 7, generator=g, dtype=torch.float64) * 0.05
     ys = F.conv3d(xs, ws, padding=p)
     dy = torch.randn(ys.shape, generator=g, dtype=torch.float64)
     (dx_ref,) = torch.autograd.grad(ys, xs, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, ws, False, True), 1, 7, 1, p, xs.shape[2:], transposed=True)
-    assert rel(ncdhw(dx), dx_ref) < xtol()
+    check_rounded(ncdhw(dx), torch.nn.grad.conv3d_input(xs.shape, R(ws), R(dy), padding=p), dx_ref)
 
 
 @pytest.mark.parametrize("N,cin,S,k,op", [(2, 64, 8, 3, 1), (1, 64, 13, 3, 1), (2, 128, 6, 4, 0), (1, 32, 9, 4, 0)])
@@ -591,7 +654,7 @@ def test_brickT_bf16x3(x3, N, cin, S, k, op):
     w = torch.randn(cin, 32, k, k, k, generator=g, dtype=torch.float64) * 0.1
     y = F.conv_transpose3d(x, w, stride=2, padding=1, output_padding=op)
     out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, True, False), 32, k, 2, 1, y.shape[2:], transposed=True)
-    assert rel(ncdhw(out), y) < xtol()
+    check_rounded(ncdhw(out), F.conv_transpose3d(R(x), R(w), stride=2, padding=1, output_padding=op), y)
     # the same form as the data gradient of Conv3d(32 → cin, k, s2, p1)
     xc = torch.randn(N, 32, 2 * S, 2 * S + 1, 2 * S + 2, generator=g, dtype=torch.float64, requires_grad=True)
     wc = torch.randn(cin, 32, k, k, k, generator=g, dtype=torch.float64) * 0.1
@@ -599,7 +662,7 @@ def test_brickT_bf16x3(x3, N, cin, S, k, op):
     dy = torch.randn(yc.shape, generator=g, dtype=torch.float64)
     (dx_ref,) = torch.autograd.grad(yc, xc, dy)
     dx = ops.conv3d(ndhwc(dy.float()).cuda(), pack(ops, wc, False, True), 32, k, 2, 1, xc.shape[2:], transposed=True)
-    assert rel(ncdhw(dx), dx_ref) < xtol()
+    check_rounded(ncdhw(dx), torch.nn.grad.conv3d_input(xc.shape, R(wc), R(dy), stride=2, padding=1), dx_ref)
 
 
 @pytest.mark.parametrize("N,cin,cout,D,H,W", [(4, 128, 128, 16, 16, 16), (2, 128, 128, 8, 9, 16), (1, 64, 192, 5, 3, 32),
@@ -616,10 +679,11 @@ def test_wgrad3_bf16x3(x3, N, cin, cout, D, H, W):
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
     (dw_ref,) = torch.autograd.grad(y, w, dy)
     dw = torch.full((cout, cin, 3, 3, 3), 3.0, device="cuda")
+    dw_rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy))
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 1, 0, dw, accumulate=False)
-    assert rel(dw, dw_ref) < xtol()
+    check_rounded(dw, dw_rnd, dw_ref)
     ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 3, 1, 0, dw, accumulate=True)
-    assert rel(dw, 2 * dw_ref) < xtol()
+    check_rounded(dw, 2 * dw_rnd, 2 * dw_ref)
 
 
 def test_pack_weights_batched_equals_single(ops):
@@ -675,3 +739,74 @@ def test_brick_presplit_equals_per_call_split(ops, N, cin, cout, S, transposed):
         assert torch.equal(got, want)
     finally:
         ops.set_conv_precision(prev)
+
+
+def test_x3_batch_over_2gib(ops):
+    """A 16-bit-mode convolution whose batch tensor exceeds 2 GiB (the MFMA kernels address their
+    operands with 32-bit byte offsets): conv_igemm runs it as consecutive instance ranges, the
+    weight gradient accumulates over them (bf16 training at 128³ batch 2 reached
+    2^31 bytes in G's batched down1 pass).  Checked against per-instance launches (the ops are per
+    instance) and, for two instances, the fp32 CPU convolution of the rounded operands."""
+    prev = ops.get_conv_precision()
+    ops.set_conv_precision("bf16")
+    try:
+        N, S, cin, cout = 9, 128, 32, 64
+        assert N * S ** 3 * cin * 4 > 2 ** 31
+        gen = torch.Generator(device="cuda").manual_seed(3)
+        x = torch.randn(N, S, S, S, cin, device="cuda", generator=gen)
+        w = torch.randn(cout, cin, 3, 3, 3, device="cuda", generator=gen) * 0.05
+        wp = pack(ops, w, False, False)
+        osp = (S // 2,) * 3
+        y = ops.conv3d(x, wp, cout, 3, 2, 1, osp)
+        for n in (0, N - 1):
+            yn = ops.conv3d(x[n:n + 1].contiguous(), wp, cout, 3, 2, 1, osp)
+            assert rel(y[n:n + 1], yn) < 1e-6
+        xr = R(x[N - 1:N].permute(0, 4, 1, 2, 3).cpu()).float()
+        ref = F.conv3d(xr, R(w.cpu()).float(), stride=2, padding=1)
+        assert rel(ncdhw(y[N - 1:N]), ref.double()) < 2e-5
+        # weight gradient over the whole batch = the sum of two sub-batch gradients
+        dy = torch.randn(N, *osp, cout, device="cuda", generator=gen)
+        dw = torch.zeros(cout, cin, 3, 3, 3, device="cuda")
+        ops.conv3d_wgrad(dy, x, 3, 2, 1, dw, accumulate=False)
+        dw2 = torch.zeros_like(dw)
+        ops.conv3d_wgrad(dy[:4].contiguous(), x[:4].contiguous(), 3, 2, 1, dw2, accumulate=False)
+        ops.conv3d_wgrad(dy[4:].contiguous(), x[4:].contiguous(), 3, 2, 1, dw2, accumulate=True)
+        assert rel(dw, dw2) < 1e-5
+    finally:
+        ops.set_conv_precision(prev)
+
+
+def test_fp16_found_inf_skips_adam(ops):
+    """fp16 loss scaling: a non-finite gradient anywhere in an optimizer's flat buffers leaves
+    every parameter and both moments untouched and counts one skipped step."""
+    g = torch.Generator().manual_seed(4)
+    n = 100_003
+    p = [torch.randn(n, generator=g).cuda() for _ in range(2)]
+    gr = [torch.randn(n, generator=g).cuda() for _ in range(2)]
+    m = [torch.zeros(n, device="cuda") for _ in range(2)]
+    v = [torch.zeros(n, device="cuda") for _ in range(2)]
+    hyper = torch.tensor(ops.adam_hyper(2e-4, 0.5, 0.999, 1e-8, 1, 1.0 / 1024), device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    count = torch.zeros(1, dtype=torch.int32, device="cuda")
+    # clean step: updates, no skip
+    p0 = [t.clone() for t in p]
+    for t in gr:
+        ops.nonfinite_flag(t, flag)
+    for i in range(2):
+        ops.adam_dev_checked(p[i], gr[i], m[i], v[i], hyper, flag)
+    ops.skip_count(flag, count)
+    torch.cuda.synchronize()
+    assert int(count) == 0 and int(flag) == 0
+    assert all(not torch.equal(a, b) for a, b in zip(p, p0))
+    # overflow in the second buffer: nothing moves
+    gr[1][n // 2] = float("inf")
+    gr[1][7] = float("nan")
+    snap = [t.clone() for t in p + m + v]
+    for t in gr:
+        ops.nonfinite_flag(t, flag)
+    for i in range(2):
+        ops.adam_dev_checked(p[i], gr[i], m[i], v[i], hyper, flag)
+    ops.skip_count(flag, count)
+    torch.cuda.synchronize()
+    assert int(count) == 1 and int(flag) == 0
+    assert all(torch.equal(a, b) for a, b in zip(p + m + v, snap))

@@ -100,6 +100,9 @@ class _StubModel:
     def save_networks(self, which):
         self.calls.append(("save", which))
 
+    def sync_running_stats(self):
+        self.calls.append(("sync",))
+
     def update_learning_rate(self):
         self.calls.append(("lr",))
 
@@ -118,6 +121,9 @@ def test_epoch_loop_cadence(tmp_path):
     # 'latest' every 3 iterations (12 in all), 'latest' + '2' at the end of epoch 2
     assert saves == ["latest", "latest", "latest", 2, "latest", "latest"]   # steps 3, 6, end of epoch 2, 9, 12
     assert sum(1 for c in m.calls if c[0] == "lr") == 3
+    # the data-parallel running-statistics average precedes every save point (one collective each)
+    assert [c[0] for c in m.calls if c[0] in ("sync", "save")] == \
+        ["sync", "save", "sync", "save", "sync", "save", "save", "sync", "save", "sync", "save"]
     log = open(os.path.join(tmp_path, "loop", "loss_log.txt")).read().splitlines()
     assert len(log) == 1 + 6                         # header + one line every 2 iterations
     assert log[1].startswith("(epoch: 1, iters: 2, time: ")
