@@ -346,9 +346,10 @@ class CycleGANModel(BaseModel):
         self._use_graph = self.isTrain and not getattr(opt, 'no_cuda_graph', False) and self.device.type == 'cuda'
         self.parallel_lanes = not getattr(opt, 'single_stream', False)
         self._aux_stream = None
-        self._graphs = None          # (G-phase graph, D-phase graph) once captured
-        self._rs_tables = None       # running-stat update tables of the captured step
+        self._graphs = None          # (G-phase graph, D-phase graph) of the step being replayed
+        self._rs_tables = None       # running-stat update tables of that capture
         self._graph_key = None
+        self._graph_cache = OrderedDict()   # capture key → captured step (LRU, GRAPH_CACHE entries)
         self._eager_steps = 0
         self._eager_shapes = set()   # input shapes stepped eagerly (workspaces sized for them)
         self._in = {}                # persistent input buffers (the graphs read them)
@@ -584,9 +585,41 @@ class CycleGANModel(BaseModel):
                 tuple(n._flat_param.data_ptr() for n in nets), tuple(n._flat_grad.data_ptr() for n in nets),
                 self._step_idx.data_ptr(), self._step_hyper.data_ptr(), bool(self._dist))
 
+    # attributes a captured step's tensors live in (re-published when a cached capture replays)
+    _CAPTURE_ATTRS = ('_cGA1', '_cGA2', '_cGB1', '_cGB2', '_cDA1', '_cDA2', '_cDB1', '_cDB2', '_fake_A', '_fake_B',
+                      '_A', '_B', '_b', '_idt', 'fake_A', 'fake_B', 'rec_A', 'rec_B', 'idt_A', 'idt_B')
+    GRAPH_CACHE = 4
+
+    def _use_capture(self):
+        """Make the capture for the current key the replayed one: from the cache (alternating batch
+        shapes — an epoch's smaller last batch — replay without recapturing), or a new
+        capture (the least recently used one beyond GRAPH_CACHE entries is released)."""
+        key = self._capture_key()
+        # a capture whose pool buffers were reallocated (a larger batch grew them) points at freed
+        # memory: drop it (key fields 4, 5 are the pool buffers' addresses)
+        for k in [k for k in self._graph_cache if k[4:6] != key[4:6]]:
+            del self._graph_cache[k]
+        ent = self._graph_cache.get(key)
+        if ent is None:
+            self._capture()
+            from mragan_hip import engine
+            self._rs_tables = [(engine.running_table(e, self._A.device), len(e)) for e in self._running_entries() if e]
+            ent = dict(graphs=self._graphs, rs=self._rs_tables,
+                       attrs={k: getattr(self, k) for k in self._CAPTURE_ATTRS if hasattr(self, k)})
+            self._graph_cache[key] = ent
+            while len(self._graph_cache) > self.GRAPH_CACHE:
+                self._graph_cache.popitem(last=False)
+        else:
+            self._graph_cache.move_to_end(key)
+            self._graphs, self._rs_tables = ent["graphs"], ent["rs"]
+            for k, v in ent["attrs"].items():
+                setattr(self, k, v)
+        self._graph_key = key
+
     def _capture(self):
         """Record the G phase and the D phase as two HIP graphs (one memory pool).  Capturing
         launches nothing; the caller replays them for this step."""
+        self._n_captures = getattr(self, '_n_captures', 0) + 1
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
             n.mark_params_dirty()            # the graphs must contain the weight repacks
         torch.cuda.synchronize()
@@ -628,7 +661,7 @@ class CycleGANModel(BaseModel):
         # (a capture must not allocate them)
         if self._use_graph and shape_key in self._eager_shapes:
             if self._graphs is None or self._graph_key != self._capture_key():
-                self._capture()
+                self._use_capture()
             graphed = True
         run_G = self._graphs[0].replay if graphed else self._phase_G
         run_D = self._graphs[1].replay if graphed else self._phase_D

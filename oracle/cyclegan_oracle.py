@@ -209,25 +209,115 @@ def _rpad(x, p):
     return F.pad(x, (p,) * 6, mode="replicate") if p else x   # nn.ReplicationPad3d(p)
 
 
-def generator_forward(state: dict, params: dict, layers: List[dict], x: torch.Tensor) -> torch.Tensor:
+# --------------------------------------------------------------------------------------
+# Convolution arithmetic: exact (the reference's ATen convs), or with the operands rounded to
+# bf16 / fp16 where the engine's 16-bit contraction modes round them
+# --------------------------------------------------------------------------------------
+
+class ExactConv:
+    """The reference's convolutions (nn.Conv3d / nn.ConvTranspose3d → ATen) in the oracle's dtype."""
+
+    def conv3d(self, x, w, b=None, stride=1, padding=0):
+        return F.conv3d(x, w, b, stride=stride, padding=padding)
+
+    def conv_transpose3d(self, x, w, b=None, stride=1, padding=0, output_padding=0):
+        return F.conv_transpose3d(x, w, b, stride=stride, padding=padding, output_padding=output_padding)
+
+
+EXACT = ExactConv()
+
+
+class RoundedConv:
+    """The reference's convolutions with every operand rounded the way the engine's bf16 / fp16
+    contraction modes round it (include/mragan_hip.h, ABI 10 — every convolution, every kernel):
+
+      forward          y  = conv(R(x), R(W)) + b              (bias added unrounded, fp32 epilogue)
+      data gradient    dx = conv_input(R(dY), R(W))
+      weight gradient  dW = conv_weight(R(X), R(dY));  db = Σ dY  (unrounded, channel_sum)
+
+    R rounds the fp32 value (the engine's tensors are fp32; an fp64 oracle value is first rounded
+    to fp32) to bf16 or fp16, round-to-nearest-even, as v_cvt_pk_bf16_f32 / v_cvt_f16_f32 and the
+    MFMA fragment conversion do.  Gradients enter the engine's backward multiplied by the static
+    loss scale (mragan_set_loss_scale), so a gradient operand is R(s·dY)/s — an exact power-of-two
+    rescaling except where fp16's range clips.  The products and sums are then evaluated in the
+    oracle's dtype (fp64: "emulated", no accumulation error; fp32: the calibration twin)."""
+
+    def __init__(self, mode: str, loss_scale: float = 1.0):
+        if mode not in ("bf16", "fp16"):
+            raise ValueError(f"operand rounding must be 'bf16' or 'fp16', got {mode!r}")
+        self.mode = mode
+        self.dt = torch.bfloat16 if mode == "bf16" else torch.float16
+        self.scale = float(loss_scale)
+
+    def op(self, t: torch.Tensor) -> torch.Tensor:
+        return t.detach().float().to(self.dt).to(t.dtype)
+
+    def grad(self, g: torch.Tensor) -> torch.Tensor:
+        if self.scale == 1.0:
+            return self.op(g)
+        return (g.detach().float() * self.scale).to(self.dt).to(g.dtype) / self.scale
+
+    def conv3d(self, x, w, b=None, stride=1, padding=0):
+        return _RoundedConvFn.apply(x, w, b, self, False, stride, padding, 0)
+
+    def conv_transpose3d(self, x, w, b=None, stride=1, padding=0, output_padding=0):
+        return _RoundedConvFn.apply(x, w, b, self, True, stride, padding, output_padding)
+
+
+class _RoundedConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, rnd, transposed, stride, padding, output_padding):
+        xr, wr = rnd.op(x), rnd.op(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.cfg = (rnd, transposed, stride, padding, output_padding, b is not None)
+        y = _conv_any(xr, wr, transposed, stride, padding, output_padding)
+        return y + b.view(1, -1, 1, 1, 1) if b is not None else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xr, wr = ctx.saved_tensors
+        rnd, transposed, stride, padding, output_padding, has_b = ctx.cfg
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        gx = gw = gb = None
+        if need_x or need_w:
+            with torch.enable_grad():
+                xl = xr.detach().requires_grad_(need_x)
+                wl = wr.detach().requires_grad_(need_w)
+                y = _conv_any(xl, wl, transposed, stride, padding, output_padding)
+                want = [t for t, n in ((xl, need_x), (wl, need_w)) if n]
+                got = list(torch.autograd.grad(y, want, rnd.grad(gy)))
+            gx = got.pop(0) if need_x else None
+            gw = got.pop(0) if need_w else None
+        if has_b and ctx.needs_input_grad[2]:
+            gb = gy.sum(dim=(0, 2, 3, 4))
+        return gx, gw, gb, None, None, None, None, None
+
+
+def _conv_any(x, w, transposed, stride, padding, output_padding):
+    if transposed:
+        return F.conv_transpose3d(x, w, None, stride=stride, padding=padding, output_padding=output_padding)
+    return F.conv3d(x, w, None, stride=stride, padding=padding)
+
+
+def generator_forward(state: dict, params: dict, layers: List[dict], x: torch.Tensor, conv=EXACT) -> torch.Tensor:
     """ResnetGenerator.forward (networks3D.py:219-220): the Sequential of layers."""
     h = x
     for L in layers:
         if L["kind"] == "conv":
-            h = F.conv3d(_rpad(h, L["prepad"]), params[L["name"] + ".weight"], params[L["name"] + ".bias"],
-                         stride=L["s"], padding=L["p"])
+            h = conv.conv3d(_rpad(h, L["prepad"]), params[L["name"] + ".weight"], params[L["name"] + ".bias"],
+                            stride=L["s"], padding=L["p"])
             if L["norm"]:
                 h = instance_norm_train(h, state, L["norm"])
             h = _act(h, L["act"])
         elif L["kind"] == "convT":
-            h = F.conv_transpose3d(h, params[L["name"] + ".weight"], params[L["name"] + ".bias"],
-                                   stride=L["s"], padding=L["p"], output_padding=L["op"])
+            h = conv.conv_transpose3d(h, params[L["name"] + ".weight"], params[L["name"] + ".bias"],
+                                      stride=L["s"], padding=L["p"], output_padding=L["op"])
             h = instance_norm_train(h, state, L["norm"])
             h = _act(h, L["act"])
         else:  # ResnetBlock.forward: x + conv_block(x)   networks3D.py:261-263
-            r = F.conv3d(_rpad(h, 1), params[L["conv1"] + ".weight"], params[L["conv1"] + ".bias"])
+            r = conv.conv3d(_rpad(h, 1), params[L["conv1"] + ".weight"], params[L["conv1"] + ".bias"])
             r = F.relu(instance_norm_train(r, state, L["norm1"]))
-            r = F.conv3d(_rpad(r, 1), params[L["conv2"] + ".weight"], params[L["conv2"] + ".bias"])
+            r = conv.conv3d(_rpad(r, 1), params[L["conv2"] + ".weight"], params[L["conv2"] + ".bias"])
             r = instance_norm_train(r, state, L["norm2"])
             h = h + r
     return h
@@ -366,7 +456,7 @@ def init_unet_state(spec: dict, init_gain: float = 0.02, dtype=torch.float32) ->
     return state
 
 
-def unet_forward(state: dict, params: dict, spec: dict, x: torch.Tensor) -> torch.Tensor:
+def unet_forward(state: dict, params: dict, spec: dict, x: torch.Tensor, conv=EXACT) -> torch.Tensor:
     """UnetGenerator.forward with the reference's in-place activations made explicit: a
     non-outermost block's `downrelu` (inplace) rewrites its input, so the skip half of
     torch.cat([x, model(x)], 1) is LeakyReLU(x) (networks3D.py:340-343)."""
@@ -376,16 +466,16 @@ def unet_forward(state: dict, params: dict, spec: dict, x: torch.Tensor) -> torc
         lv = levels[i]
         wd, wu = params[lv["down"] + ".weight"], params[lv["up"] + ".weight"]
         if lv["kind"] == "outer":
-            s = block(i + 1, F.conv3d(h, wd, None, stride=2, padding=1))
-            y = F.conv_transpose3d(F.relu(s), wu, params[lv["up"] + ".bias"], stride=2, padding=1)
+            s = block(i + 1, conv.conv3d(h, wd, None, stride=2, padding=1))
+            y = conv.conv_transpose3d(F.relu(s), wu, params[lv["up"] + ".bias"], stride=2, padding=1)
             return torch.tanh(y)
         a = F.leaky_relu(h, LRELU_SLOPE)
-        d = F.conv3d(a, wd, None, stride=2, padding=1)
+        d = conv.conv3d(a, wd, None, stride=2, padding=1)
         if lv["kind"] == "mid":
             r = F.relu(block(i + 1, instance_norm_train(d, state, lv["dnorm"])))
         else:
             r = F.relu(d)
-        u = instance_norm_train(F.conv_transpose3d(r, wu, None, stride=2, padding=1), state, lv["unorm"])
+        u = instance_norm_train(conv.conv_transpose3d(r, wu, None, stride=2, padding=1), state, lv["unorm"])
         return torch.cat([a, u], 1)
 
     return block(0, x)
@@ -403,8 +493,13 @@ class CycleGANOracle:
     def __init__(self, input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, n_layers_D=3, netG=None,
                  use_lsgan=False, lambda_A=10.0, lambda_B=10.0, lambda_identity=0.5,
                  lr=2e-4, beta1=0.5, pool_size=50, init_gain=0.02, dtype=torch.float32,
-                 states: Dict[str, dict] = None, pool_rng: random.Random = None):
+                 states: Dict[str, dict] = None, pool_rng: random.Random = None,
+                 operand_rounding: str = None, loss_scale: float = 1.0):
+        """operand_rounding: None (the reference's arithmetic) or 'bf16' / 'fp16' — every
+        convolution operand rounded as the engine's 16-bit contraction modes round it
+        (RoundedConv), fp16 gradients under the static `loss_scale`."""
         self.dtype = dtype
+        self.conv = EXACT if operand_rounding is None else RoundedConv(operand_rounding, loss_scale)
         self.use_lsgan = use_lsgan
         self.lambda_A, self.lambda_B, self.lambda_idt = lambda_A, lambda_B, lambda_identity
         self.lr, self.beta1 = lr, beta1
@@ -441,8 +536,8 @@ class CycleGANOracle:
     def _net(self, name, x, params):
         spec = self.layers[name]
         if isinstance(spec, dict):
-            return unet_forward(self.state[name], params, spec, x)
-        return generator_forward(self.state[name], params, spec, x)
+            return unet_forward(self.state[name], params, spec, x, self.conv)
+        return generator_forward(self.state[name], params, spec, x, self.conv)
 
     def _leaf_params(self, names, requires_grad):
         out = {}

@@ -20,6 +20,10 @@ CASE_KW = {
     "step_unet_s64_b1_ngf32": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, netG="unet_custom", use_lsgan=False),
     "step_r9_s96_b1_nc2": dict(input_nc=2, output_nc=2, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
     "step_r9_s128_b1": dict(input_nc=1, output_nc=1, ngf=32, ndf=32, n_blocks=9, use_lsgan=False),
+    # pool of one image: the step takes the ImagePool swap path from step 2 on
+    "step_r6_s24_b1_pool1": dict(input_nc=1, output_nc=1, ngf=4, ndf=4, n_blocks=6, use_lsgan=False, pool_size=1),
+    # --netG unet_256 (8 downsamplings) at the smallest size it trains at
+    "step_unet256_s256_b1_ngf4": dict(input_nc=1, output_nc=1, ngf=4, ndf=4, netG="unet_256", use_lsgan=False),
 }
 
 

@@ -70,13 +70,15 @@ def test_graph_step_bit_identical_to_eager(tmp_path, precision):
 
 def test_graph_step_changing_batch_and_no_identity(tmp_path):
     """An epoch's smaller last batch (train.py:52, no drop_last) between full ones, with
-    --lambda_identity 0 (no identity passes): the graphed step re-captures per batch shape, the
+    --lambda_identity 0 (no identity passes): the graphed step captures once per batch shape and replays the cached captures, the
     pool keeps its images across the change, and everything stays bit-identical to eager."""
     batches = [2, 2, 1, 2, 2, 1, 2]
     extra = ["--lambda_identity", "0"]
     le, se, ve, me = _run(tmp_path / "e", False, len(batches), "f32", batches, extra)
     lg, sg, vg, mg = _run(tmp_path / "g", True, len(batches), "f32", batches, extra)
     assert mg._graphs is not None and not hasattr(mg, "idt_A")
+    # one capture per batch shape: the alternation replays cached captures (no recapture)
+    assert mg._n_captures == 2 and len(mg._graph_cache) == 2
     assert mg.fake_B_pool.num_imgs == 2
     assert torch.equal(le, lg), (le - lg).abs().max()
     assert float(le[:, 3].abs().max()) == 0.0 and float(le[:, 7].abs().max()) == 0.0   # loss_idt_*

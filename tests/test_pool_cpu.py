@@ -70,3 +70,40 @@ def test_query_returns_tensor_like_reference():
         want = ref.query(x.clone())
         got = dev.query(x.clone())
         assert isinstance(got, torch.Tensor) and got.shape == want.shape and torch.equal(got, want), q
+
+
+def _pool_seq():
+    import os
+    import numpy as np
+    from golden_util import GOLDEN
+    return np.load(os.path.join(GOLDEN, "pool_seq_p2.npz"), allow_pickle=False)
+
+
+def _replay(pool_query, z):
+    """Feed the fixture's batches (images carrying their running id) through `pool_query` after
+    seeding the global `random` like the reference run; returns the ids it hands back."""
+    random.seed(int(z["seed"]))
+    got, nid = [], 0
+    for b in z["sizes"]:
+        b = int(b)
+        imgs = torch.arange(nid, nid + b, dtype=torch.float32).view(b, 1, 1, 1, 1).expand(b, 1, 2, 2, 2).contiguous()
+        nid += b
+        out = pool_query(imgs)
+        got.extend(int(v) for v in out[:, 0, 0, 0, 0])
+    return got
+
+
+def test_pool_sequence_pinned_to_reference():
+    """48 queries of batch 1/2/3 through the REFERENCE's ImagePool(2) (tools/gen_fixtures.py
+    pool_seq_p2, seeded `random`): the oracle's ImagePool and the engine's host ImagePool and
+    DeviceImagePool return the same images (swaps included) in the same order."""
+    from models.cycle_gan_model import DeviceImagePool
+    from models.cycle_gan_model import ImagePool as EngineImagePool
+    z = _pool_seq()
+    want = [int(v) for v in z["ids"]]
+    assert sum(w != i for i, w in enumerate(want)) > 20          # the sequence exercises the swap path
+    P = int(z["pool_size"])
+    orc = ImagePool(P)                                            # global `random`, like the reference
+    assert _replay(orc.query, z) == want
+    assert _replay(EngineImagePool(P).query, z) == want
+    assert _replay(DeviceImagePool(P).query, z) == want

@@ -1,14 +1,22 @@
 """Whole-step parity on the GPU: the drop-in CycleGANModel (HIP engine) against the golden
 fixtures produced by the reference itself (tools/gen_fixtures.py) and against the oracle.
 
-Gates (calibrated on the reference's own fp32-vs-fp64 error):
+fp32-grade modes (f32, bf16x3) — gates calibrated on the reference's own fp32-vs-fp64 error
+(SURVEY §8c):
   * initial weights: bit-exact (same torch seed → same RNG consumption);
-  * losses and generated volumes at step 1: rel ≤ 1e-4 vs the fp64 reference;
+  * losses and generated volumes at step 1: rel ≤ 1e-4 (f32) / 1e-3 (bf16x3) vs the fp64 reference;
   * step-1 gradients: ‖g − g64‖ ≤ max(1e-3‖g64‖, 2‖g_ref32 − g64‖) on the sampled elements;
     pre-InstanceNorm conv biases: exactly 0 (their true gradient is identically zero);
-  * InstanceNorm running statistics after step 1: rel ≤ 1e-4;
+  * InstanceNorm running statistics after step 1: rel ≤ 1e-4 / 1e-3;
   * later steps: losses within max(1e-3, k × the reference's own fp32-vs-fp64 divergence at that
     step) — fp32 noise amplified by Adam, as for the reference (k = 4 exact f32, 10 bf16x3).
+
+Reduced modes (bf16, fp16: every conv operand rounded) — against the oracle's rounded-operand
+step (tests/golden/prec_<case>.npz, tools/gen_precision_fixtures.py): "emu64" is the step with
+the engine's operand rounding evaluated in fp64, "emu32" the same in fp32.  The same calibrated
+rule as above with emu32 in the reference-fp32 role: every quantity within max(1e-3, 2 × the
+emu32-vs-emu64 gap) of emu64 (gradients per tensor with the same outlier budget, and for the whole
+network with none).
 """
 import random
 import sys
@@ -103,22 +111,129 @@ def test_init_bit_exact(stepped):
 
 # forward-value gates: exact-f32 MFMA 1e-4 (measured 1e-6…2e-5); bf16x3 split MFMA (≤ 3·2⁻¹⁸ per
 # product) the north star's 1e-3 (measured ≤ 1.5e-4)
-VALUE_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
-# reduced precisions: losses / generated volumes / running statistics (measured maxima over the
-# fixtures at 24³-64³: bf16 8.0e-4 / 8.8e-2 / 1.8e-2, fp16 1.4e-4 / 1.15e-2 / 5.2e-3)
-LOSS_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 2e-3, "fp16": 5e-4}
-VOL_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 0.15, "fp16": 2.5e-2}
-RS_TOL = {"f32": 1e-4, "bf16x3": 1e-3, "bf16": 4e-2, "fp16": 1.2e-2}
-# whole-network gradient rel-L2 of the reduced precisions (measured maxima 0.39 / 0.145)
-GRAD_TOL = {"bf16": 0.6, "fp16": 0.3}
+LOSS_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
+VOL_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
+RS_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
 # later-step losses: multiple of the reference's own fp32-vs-fp64 divergence at that step, and at
-# least LATER_MIN (reduced precisions: measured maxima 3.0e-3 bf16, 1.3e-3 fp16)
-LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0, "bf16": 10.0, "fp16": 10.0}
-LATER_MIN = {"f32": 1e-3, "bf16x3": 1e-3, "bf16": 1e-2, "fp16": 4e-3}
+# least LATER_MIN
+LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0}
+LATER_MIN = {"f32": 1e-3, "bf16x3": 1e-3}
 
+
+# ---- reduced precisions: against the rounded-operand oracle ----------------------------------
+
+def prec_fixture(name):
+    import os
+    from golden_util import GOLDEN
+    path = os.path.join(GOLDEN, f"prec_{name}.npz")
+    return np.load(path, allow_pickle=False) if os.path.exists(path) else None
+
+
+def _pgap(p, mode, key, got):
+    """(rel err of `got` vs emu64, rel gap emu32 vs emu64) at the fixture's sampled indices."""
+    flat = got.detach().reshape(-1).double().cpu()
+    w64 = p[f"{mode}/emu64/{key}/val"]
+    w32 = p[f"{mode}/emu32/{key}/val"]
+    g = flat[torch.from_numpy(p[f"{mode}/emu64/{key}/idx"])].numpy()
+    return rel_err(g, w64), rel_err(w32, w64), g, w64, w32
+
+
+REDUCED_MIN = 1e-3        # the north star's gate; the calibrated term can only widen it
+
+
+def _reduced(stepped):
+    name, z, meta, _, history, snap = stepped
+    p = prec_fixture(name)
+    mode = meta["precision"]
+    if p is None or f"{mode}/emu64/steps" not in p.files or f"{mode}/emu32/steps" not in p.files:
+        pytest.skip(f"no rounded-operand fixture for {name} {mode} (tools/gen_precision_fixtures.py)")
+    return name, mode, p, history, snap
+
+
+def test_reduced_losses(stepped):
+    if stepped[2]["precision"] not in REDUCED:
+        pytest.skip("fp32-grade mode")
+    name, mode, p, history, _ = _reduced(stepped)
+    for step in range(int(p[f"{mode}/emu64/steps"])):
+        w64 = p[f"{mode}/emu64/step{step}/losses"]
+        w32 = p[f"{mode}/emu32/step{step}/losses"]
+        err, gap = rel_err(history[step], w64), rel_err(w32, w64)
+        # after the first Adam step the runs separate like the reference's fp32 and fp64 (±lr steps
+        # of round-off-sized gradients): the later-step factor of the fp32-grade modes
+        env = max(REDUCED_MIN, (2.0 if step == 0 else 10.0) * gap)
+        print(f"{name} {mode} step {step}: loss rel err {err:.2e} (emu32 gap {gap:.2e}, gate {env:.2e})")
+        assert err < env, (step, history[step], w64)
+
+
+def test_reduced_volumes_and_running_stats(stepped):
+    if stepped[2]["precision"] not in REDUCED:
+        pytest.skip("fp32-grade mode")
+    name, mode, p, _, snap = _reduced(stepped)
+    for vis, t in snap["vis"].items():
+        err, gap, *_ = _pgap(p, mode, f"step0/{vis}", t)
+        print(f"{name} {mode} {vis}: rel err {err:.2e} (emu32 gap {gap:.2e})")
+        assert err < max(REDUCED_MIN, 2 * gap), vis
+    for net, bufs in snap["bufs"].items():
+        for k, b in bufs.items():
+            err, gap, *_ = _pgap(p, mode, f"step0/buf/{net}/{k}", b)
+            assert err < max(REDUCED_MIN, 2 * gap), (net, k, err, gap)
+
+
+def test_reduced_gradients(stepped):
+    if stepped[2]["precision"] not in REDUCED:
+        pytest.skip("fp32-grade mode")
+    name, mode, p, _, snap = _reduced(stepped)
+    bad, n_params = [], 0
+    ours, r32, r64 = [], [], []
+    for net, grads in snap["grads"].items():
+        for k, gr in grads.items():
+            if is_pre_in_bias(net, k):
+                assert float(gr.abs().max()) == 0.0, (net, k)
+                continue
+            err, gap, g, w64, w32 = _pgap(p, mode, f"step0/grad/{net}/{k}", gr)
+            env = max(REDUCED_MIN, 2 * gap)
+            n_params += 1
+            if err > env:
+                bad.append((net, k, err, env))
+            scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
+            ours.append(g * scale)
+            r64.append(w64 * scale)
+            r32.append(w32 * scale)
+    print(f"{name} {mode}: {len(bad)}/{n_params} parameters over their envelope: {bad}")
+    assert len(bad) <= max(2, int(0.2 * n_params)), bad
+    assert all(r <= 20 * env for _, _, r, env in bad), bad
+    whole = rel_err(np.concatenate(ours), np.concatenate(r64))
+    whole_ref = rel_err(np.concatenate(r32), np.concatenate(r64))
+    print(f"{name} {mode}: whole-net grad rel err {whole:.2e} (emu32 gap {whole_ref:.2e})")
+    assert whole <= max(REDUCED_MIN, 2 * whole_ref), (whole, whole_ref)
+
+
+def test_reduced_params_after_adam(stepped):
+    """Adam's first step is ≈ ±lr·sign(g): count the sampled weights that stepped differently from
+    emu64, against twice the emu32 run's count (and at least 2 %)."""
+    if stepped[2]["precision"] not in REDUCED:
+        pytest.skip("fp32-grade mode")
+    name, mode, p, _, snap = _reduced(stepped)
+    total = bad = bad32 = 0
+    for net, params in snap["params"].items():
+        for k, t in params.items():
+            if is_pre_in_bias(net, k):
+                continue
+            _, _, g, w64, w32 = _pgap(p, mode, f"step0/param/{net}/{k}", t)
+            assert np.abs(g - w64).max() <= 2.05 * 2e-4, (net, k)
+            total += g.size
+            bad += int((np.abs(g - w64) > 1e-6).sum())
+            bad32 += int((np.abs(w32 - w64) > 1e-6).sum())
+    print(f"{name} {mode}: {bad}/{total} sampled weights stepped differently (emu32: {bad32})")
+    assert bad <= max(0.02 * total, 2 * bad32), (bad, bad32, total)
+
+
+# ---- fp32-grade modes: against the reference's own fp32 / fp64 runs ------------------------
 
 def test_losses(stepped):
     name, z, meta, _, history, _ = stepped
+    if meta["precision"] in REDUCED:
+        pytest.skip("reduced precision: test_reduced_losses")
     got = history[0]
     want = z["fp64/step0/losses"]
     assert rel_err(got, want) < LOSS_TOL[meta["precision"]], (got, want)
@@ -135,6 +250,8 @@ def test_losses(stepped):
 
 def test_generated_volumes(stepped):
     name, z, meta, _, _, snap = stepped
+    if meta["precision"] in REDUCED:
+        pytest.skip("reduced precision: test_reduced_volumes_and_running_stats")
     for vis, t in snap["vis"].items():
         g, w = sampled(z, f"fp64/step0/{vis}", t)
         assert rel_err(g, w) < VOL_TOL[meta["precision"]], vis
@@ -154,7 +271,7 @@ def conditioning(stepped):
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
     if meta["precision"] in REDUCED:
-        return None                 # reduced precisions: whole-network envelope gate only
+        return None                 # reduced precisions: test_reduced_gradients
     eps = PERTURB[meta["precision"]]
     pre = {4e-6: "fp64p4e-6", 4e-5: "fp64p4e-5"}[eps]
     if any(k.startswith(pre + "/") for k in z.files):
@@ -181,20 +298,7 @@ def test_gradients(stepped, conditioning):
     exactly 0.  Whole network: the same rule on all sampled elements together, no exceptions."""
     name, z, meta, _, _, snap = stepped
     if meta["precision"] in REDUCED:
-        ours, ref64 = [], []
-        for net, grads in snap["grads"].items():
-            for k, gr in grads.items():
-                if is_pre_in_bias(net, k):
-                    assert float(gr.abs().max()) == 0.0, (net, k)
-                    continue
-                g, w64 = sampled(z, f"fp64/step0/grad/{net}/{k}", gr)
-                scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
-                ours.append(g * scale)
-                ref64.append(w64 * scale)
-        whole = rel_err(np.concatenate(ours), np.concatenate(ref64))
-        print(f"{name} {meta['precision']}: whole-net grad rel err {whole:.2e}")
-        assert whole < GRAD_TOL[meta["precision"]], whole
-        return
+        pytest.skip("reduced precision: test_reduced_gradients")
     bad = []
     n_params = 0
     ours, ref32, ref64, pert = [], [], [], [[] for _ in conditioning]
@@ -236,6 +340,8 @@ def test_gradients(stepped, conditioning):
 
 def test_running_stats(stepped):
     name, z, meta, _, _, snap = stepped
+    if meta["precision"] in REDUCED:
+        pytest.skip("reduced precision: test_reduced_volumes_and_running_stats")
     for net, bufs in snap["bufs"].items():
         for k, b in bufs.items():
             g, w = sampled(z, f"fp64/step0/buf/{net}/{k}", b)
@@ -246,6 +352,8 @@ def test_params_after_adam(stepped):
     """Adam's first step moves each weight by ≈ lr·sign(g); elements whose reference gradient
     is at fp32 round-off may flip sign, so gate on the fraction that moved differently."""
     name, z, meta, _, _, snap = stepped
+    if meta["precision"] in REDUCED:
+        pytest.skip("reduced precision: test_reduced_params_after_adam")
     lr = 2e-4
     total = bad = 0
     for net, params in snap["params"].items():
@@ -262,6 +370,5 @@ def test_params_after_adam(stepped):
 
 
 # fraction of weights whose first Adam step (≈ ±lr) went the other way: f32-grade modes flip only
-# round-off-sized gradients (measured 0.2-0.3 %); the reduced modes flip every element whose
-# gradient their operand rounding moved across zero
-ADAM_FLIP_TOL = {"f32": 0.02, "bf16x3": 0.02, "bf16": 0.35, "fp16": 0.2}
+# round-off-sized gradients (measured 0.2-0.3 %)
+ADAM_FLIP_TOL = {"f32": 0.02, "bf16x3": 0.02}

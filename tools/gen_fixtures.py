@@ -45,6 +45,16 @@ CASES = {
     # the running statistics then see only the four cycle passes
     "step_r6_s24_b1_noidt": (["--netG", "resnet_6blocks", "--ngf", "8", "--ndf", "8", "--lambda_identity", "0"],
                              24, 1, 1, ["fp32", "fp64"], 2, 9),
+    # ImagePool of one image (cycle_gan_model.py:8-35): from the second step on every D query
+    # draws random.uniform and, half the time, swaps the stored fake — the step itself takes the
+    # swap path (the pool-50 cases never leave the pass-through phase)
+    "step_r6_s24_b1_pool1": (["--netG", "resnet_6blocks", "--ngf", "4", "--ndf", "4", "--pool_size", "1"],
+                             24, 1, 1, ["fp32", "fp64"], 6, 11),
+    # UnetGenerator with 8 downsamplings (--netG unet_256, BASELINE configs[3]'s generator): it
+    # trains only from 256³ (a 1³ bottleneck InstanceNorm raises below), so at 256³
+    # with narrow widths
+    "step_unet256_s256_b1_ngf4": (["--netG", "unet_256", "--ngf", "4", "--ndf", "4"], 256, 1, 1,
+                                  ["fp32", "fp64", "fp64p4e-6", "fp64p4e-5"], 1, 12),
 }
 # reference-written checkpoint (base_model.py:89-112) of a tiny model after one step, plus the
 # losses of the step the reference takes right after it (ckpt_* cases, see run_checkpoint)
@@ -229,11 +239,39 @@ def run_checkpoint(name, argv, S, B, nc, seed):
     print("wrote", os.path.join(ck, name))
 
 
+def run_pool_sequence(name="pool_seq_p2", pool_size=2, seed=123, queries=48):
+    """The reference's ImagePool(pool_size) on a sequence of batches (sizes 1, 2, 3 cycling) whose
+    images carry their running id: stores the ids it returns, per query, in order."""
+    import random
+    import itertools
+    sys.modules["monai"] = types.ModuleType("monai")
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from models.cycle_gan_model import ImagePool     # noqa: E402  (the reference's)
+    random.seed(seed)
+    pool = ImagePool(pool_size)
+    sizes, ids, nid = [], [], 0
+    for q, b in zip(range(queries), itertools.cycle((1, 2, 3))):
+        imgs = torch.arange(nid, nid + b, dtype=torch.float32).view(b, 1, 1, 1, 1).expand(b, 1, 2, 2, 2).contiguous()
+        nid += b
+        out = pool.query(imgs)
+        sizes.append(b)
+        ids.extend(int(v) for v in out[:, 0, 0, 0, 0])
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, sizes=np.array(sizes), ids=np.array(ids), pool_size=np.array(pool_size),
+                        seed=np.array(seed))
+    print("wrote", path, "returned ids differ from inputs at", int((np.array(ids) != np.arange(len(ids))).sum()),
+          "of", len(ids))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(os.cpu_count())
-    which = sys.argv[1:] or list(CASES) + list(CKPT_CASES)
+    which = sys.argv[1:] or list(CASES) + list(CKPT_CASES) + ["pool_seq_p2"]
     for name in which:
+        if name == "pool_seq_p2":
+            run_pool_sequence()
+            continue
         if name in CKPT_CASES:
             run_checkpoint(name, *CKPT_CASES[name])
             continue
