@@ -102,7 +102,7 @@ conv_brick_kernel(BrickArgs a) {
     if (v >= 0) {
       int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
       int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
-      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Yd + od + a.ye) * a.Yh + oh + a.ye) * a.Yw + ow + a.ye);
     }
     out_off[r] = off;
   }
@@ -373,19 +373,25 @@ bool conv_brick_applicable(const IgemmArgs& a) {
          (int64_t)a.Di * a.Hi * a.Wi * a.cx * 4 < ((int64_t)1 << 31);
 }
 
-int conv_brick(const IgemmArgs& g, hipStream_t st) {
+int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   BrickArgs a{};
   a.x = g.x; a.N = g.N; a.Di = g.Di; a.Hi = g.Hi; a.Wi = g.Wi; a.C = g.cx;
   a.w = g.w; a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
   a.act = g.act;
+  a.ye = 0; a.Yd = g.Do; a.Yh = g.Ho; a.Yw = g.Wo;
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
   a.flip = g.trans ? 1 : 0;
   a.p = g.trans ? g.k - 1 - g.p : g.p;
+  if (interior) {
+    // interior of a full transposed conv (output = input + 2): y[o + 1] = Σ_j x[o − 1 + j] Wp[2 − j]
+    // for o in the input grid — a "same" forward conv (pad 1, flipped taps) written one voxel in
+    a.p = 1; a.Do = g.Di; a.Ho = g.Hi; a.Wo = g.Wi; a.ye = 1;
+  }
   const bool x3 = g.x3 != 0;
-  BrickChoice c = choose_brick(g.N, g.Do, g.Ho, g.Wo, g.ny, x3);
+  BrickChoice c = choose_brick(g.N, a.Do, a.Ho, a.Wo, g.ny, x3);
   a.BD = c.bd; a.BH = c.bh; a.BW = c.bw;
   a.HD = c.bd + 2; a.HH = c.bh + 2; a.HW = c.bw + 2;
-  a.nbd = ceil_div(g.Do, c.bd); a.nbh = ceil_div(g.Ho, c.bh); a.nbw = ceil_div(g.Wo, c.bw);
+  a.nbd = ceil_div(a.Do, c.bd); a.nbh = ceil_div(a.Ho, c.bh); a.nbw = ceil_div(a.Wo, c.bw);
   a.gn = ceil_div(g.ny, c.bn);
   a.ntiles = (int)c.blocks;
   if (a.ntiles == 0) return kOk;

@@ -119,7 +119,7 @@ conv_brick_x3_kernel(BrickArgs a) {
     if (v >= 0) {
       const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
       const int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
-      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow);
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Yd + od + a.ye) * a.Yh + oh + a.ye) * a.Yw + ow + a.ye);
     }
     out_off[r] = off;
   }

@@ -36,4 +36,25 @@ __device__ __forceinline__ DimGeo dim_geo(int c, int O, int k, int s, int p, int
   return g;
 }
 
+// Shell classes of a full transposed k×k×k stride-1 convolution (the data gradient of a valid
+// conv on a replication-padded input: output extent O = input + k − 1 per dim, y[o] = Σ_t
+// x[o − t]·Wp[t]).  The brick kernel computes the interior (every output with ≥ 1 real tap along
+// each dim's full range, 1 … O−2 for k = 3); the shell — the outputs on the first / last plane of
+// some dim — is split into 6 classes: class 2f + side has dim f on the low (side 0, o = 0, tap 0
+// only) or high (side 1, o = O−1, tap k−1 only) plane, the dims before f interior, the dims after
+// f over their full range.  Every shell output is in exactly one class (Σ = O³ − (O−2)³ for k = 3).
+__device__ __forceinline__ DimGeo shell_geo(int cls, int dim, int O, int k) {
+  const int f = cls >> 1, hi = cls & 1;
+  DimGeo g;
+  g.tstep = 1; g.a_mul = 1; g.sign = -1; g.o_mul = 1;
+  if (dim == f) {
+    g.Q = 1; g.ntap = 1; g.t0 = hi ? k - 1 : 0; g.base_add = hi ? O - k : 0; g.o_add = hi ? O - 1 : 0;
+  } else if (dim < f) {
+    g.Q = O - 2; g.ntap = k; g.t0 = 0; g.base_add = 1; g.o_add = 1;
+  } else {
+    g.Q = O; g.ntap = k; g.t0 = 0; g.base_add = 0; g.o_add = 0;
+  }
+  return g;
+}
+
 }  // namespace mragan

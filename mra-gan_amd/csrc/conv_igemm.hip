@@ -232,6 +232,17 @@ static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hi
 }
 
 static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
+static const bool g_split_off = getenv("MRAGAN_NO_DGRAD_SPLIT") != nullptr;   // A/B switch
+static int x3_instances_per_launch(const IgemmArgs& a);
+
+// data gradient of a valid k3 s1 conv (transposed form p = 0, output = input + 2): the 16-bit
+// modes compute it as interior + shell (the whole-grid brick spent 42 % of its rows on outputs
+// whose taps mostly read zero padding and on padded brick rows)
+bool full_dgrad_split_applicable(const IgemmArgs& a) {
+  return !g_brick_off && !g_split_off && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
+         a.Ho == a.Hi + 2 && a.Wo == a.Wi + 2 && a.Do == a.Ho && a.Ho == a.Wo && a.Di >= 2 && a.cx % 16 == 0 &&
+         conv_brick_x3_active(a) && x3_instances_per_launch(a) >= a.N;
+}
 
 // class count and row counts (class 0 is the largest along every dim)
 static void igemm_geometry(IgemmArgs& a, int64_t& max_mc, int64_t& total_m) {
@@ -294,6 +305,11 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   int64_t max_mc, total_m;
   igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return kOk;
+  if (full_dgrad_split_applicable(a)) {
+    // the 16-bit brick kernel on the interior (no padded rows, no all-zero taps) + the shell pass
+    const int rc = conv_brick(a, st, true);
+    return rc ? rc : conv_igemm_x3_shell(a, st);
+  }
   if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
   if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_chunked(a, max_mc, total_m, st);

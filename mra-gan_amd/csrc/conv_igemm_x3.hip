@@ -68,9 +68,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
 
   int cw = cls % a.s, ch = (cls / a.s) % a.s, cd = cls / (a.s * a.s);
   if (a.nclass == 1) { cd = ch = cw = 0; }
-  const DimGeo gd = dim_geo(cd, a.Do, a.k, a.s, a.p, a.trans);
-  const DimGeo gh = dim_geo(ch, a.Ho, a.k, a.s, a.p, a.trans);
-  const DimGeo gw = dim_geo(cw, a.Wo, a.k, a.s, a.p, a.trans);
+  const DimGeo gd = a.shell ? shell_geo(cls, 0, a.Do, a.k) : dim_geo(cd, a.Do, a.k, a.s, a.p, a.trans);
+  const DimGeo gh = a.shell ? shell_geo(cls, 1, a.Ho, a.k) : dim_geo(ch, a.Ho, a.k, a.s, a.p, a.trans);
+  const DimGeo gw = a.shell ? shell_geo(cls, 2, a.Wo, a.k) : dim_geo(cw, a.Wo, a.k, a.s, a.p, a.trans);
   const int64_t Mc = (int64_t)a.N * gd.Q * gh.Q * gw.Q;
   const int64_t m0 = (int64_t)mb_idx * BM;
   const int n0 = nb_idx * BN;
@@ -346,6 +346,18 @@ static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int cfg, int splits, 
     case 3: return launch_x3<4, 1, 2, 1, BK>(a, max_mc, splits, st);
     default: return launch_x3<4, 1, 1, 1, BK>(a, max_mc, splits, st);
   }
+}
+
+// the shell pass of a full k3 s1 transposed conv (see shell_geo): 6 classes, rows = shell outputs
+int conv_igemm_x3_shell(IgemmArgs a, hipStream_t st) {
+  a.shell = 1;
+  a.nclass = 6;
+  const int O = a.Do;
+  const int64_t max_mc = (int64_t)a.N * O * O;                       // classes 0/1: one plane
+  const int64_t total_m = (int64_t)a.N * ((int64_t)O * O * O - (int64_t)(O - 2) * (O - 2) * (O - 2));
+  X3Plan pl = x3_plan(a, total_m);
+  // no split-K: its reduce would rewrite every output of the grid, not only the shell
+  return a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, 1, st) : dispatch_x3<16>(a, max_mc, pl.cfg, 1, st);
 }
 
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {

@@ -21,10 +21,12 @@ struct IgemmArgs {
   const void* wx3;  // optional: w pre-split in bf16x3 brick fragment order (pack tr 2/3), or null
   double* in_part;  // optional: per-(instance, brick, channel) Σy, Σy² of the output (brick_x3 only)
   int* in_chunks;   // set to the bricks per instance when in_part was filled, else 0
+  int shell;        // conv_igemm_x3 only: the 6 shell-face classes of a full (k3 s1 p0) transposed conv
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st);
+int conv_igemm_x3_shell(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_m);
 
 // k3 s1 convolutions with an LDS-resident input halo (conv_brick.hip)
@@ -40,9 +42,14 @@ struct BrickArgs {
   int HD, HH, HW;   // its input halo
   int nbd, nbh, nbw, gn, ntiles;
   double* part;     // optional InstanceNorm statistics partials [N][nbd·nbh·nbw][ny][2] (Σy, Σy²)
+  int ye;           // output embedding: y is [N][Yd][Yh][Yw][ny], output voxel o written at o + ye
+  int Yd, Yh, Yw;
 };
 bool conv_brick_applicable(const IgemmArgs& a);
-int conv_brick(const IgemmArgs& a, hipStream_t st);
+int conv_brick(const IgemmArgs& a, hipStream_t st, bool interior = false);
+// the data gradient of a valid k3 s1 conv (transposed form, output = input + 2 per dim) as the
+// interior brick pass plus the shell pass (conv_igemm.hip)
+bool full_dgrad_split_applicable(const IgemmArgs& a);
 int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, int mode,
                          hipStream_t st);
 size_t conv_brick_x3_ws_bytes(int C, int ny);
