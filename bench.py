@@ -3,7 +3,10 @@
 (G_A, G_B, D_A, D_B forward + backward + both Adam steps), BASELINE.json's metric.
 
 Workload (N=1): BASELINE configs[1] — ResNet-9blocks G + 3-layer PatchGAN D, 1ch→1ch,
-64³ patch, batch 2 per GPU, synthetic N(0,1) volumes, random init (seed 0).  Multi-GPU:
+64³ patch, batch 2 per GPU, bf16 (every convolution operand rounded to bf16, fp32 accumulation;
+the step is pinned against the oracle's rounded-operand step, tests/test_step_gpu.py), synthetic
+N(0,1) volumes, random init (seed 0).  The fp32-grade modes (bf16x3 split products, exact f32)
+are timed in the same run under alt_precisions.  Multi-GPU:
 one process per GPU (torch.distributed over RCCL), each rank its own batch (weak scaling),
 gradients all-reduced inside the step.
 
@@ -57,18 +60,18 @@ def parse():
     ap.add_argument("--ngf", type=int, default=32)
     ap.add_argument("--netG", default="resnet_9blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="bf16x3", choices=["f32", "bf16x3", "bf16", "fp16"],
+    ap.add_argument("--precision", default="bf16", choices=["f32", "bf16x3", "bf16", "fp16"],
                     help="MFMA-conv contraction: exact f32, split-bf16 (bf16x3, fp32-grade), or bf16 / fp16 "
                          "operands (one MFMA per product); fp32 accumulation, fp32 tensors and master weights")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: median of this many oracle steps")
     ap.add_argument("--nc", type=int, default=1, help="image channels (input_nc = output_nc)")
-    ap.add_argument("--alt-precisions", default="bf16,f32",
+    ap.add_argument("--alt-precisions", default="bf16x3,f32",
                     help="comma list of further precisions timed in the same run (same workload, same protocol) "
                          "and reported under alt_precisions; '' for none")
     ap.add_argument("--legs", default="128:1",
                     help="comma list of further workloads SIZE:BATCH timed in the same run (BASELINE configs[2]'s "
                          "per-GPU unit 128^3 b1 by default), reported under legs; '' for none")
-    ap.add_argument("--leg-alt-precisions", default="bf16", help="alt precisions timed for each extra leg")
+    ap.add_argument("--leg-alt-precisions", default="bf16x3", help="alt precisions timed for each extra leg")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch-class timing (profiled runs: the trace then holds only the steps)")
     ap.add_argument("--cpu-warmup", type=int, default=2, help="CPU baseline: untimed oracle steps first")

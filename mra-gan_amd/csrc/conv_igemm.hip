@@ -232,7 +232,10 @@ static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hi
 }
 
 static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
-static const bool g_split_off = getenv("MRAGAN_NO_DGRAD_SPLIT") != nullptr;   // A/B switch
+// A/B switch, off by default: measured on MI355X (bf16, 64³ b2 bench, r03c) the interior brick
+// (~25 µs at N = 4, the forward's time) plus the shell pass (~28 µs: 252 blocks × 36 serial K-steps,
+// latency-bound) lost to the whole-grid brick (~41 µs)
+static const bool g_split_off = getenv("MRAGAN_DGRAD_SPLIT") == nullptr;
 static int x3_instances_per_launch(const IgemmArgs& a);
 
 // data gradient of a valid k3 s1 conv (transposed form p = 0, output = input + 2): the 16-bit

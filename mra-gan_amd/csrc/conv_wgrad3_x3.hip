@@ -16,6 +16,8 @@
 // 16 B pad: 528-B rows), X as [ci][w' 18][r 8] (592-B rows); both row strides keep the 16-lane
 // ds_read_b128 groups conflict-free.  The next stage's global loads are in registers during the
 // MFMAs.  Partial tiles go to split-K slabs ws[z][t][co][ci], reduced by wgrad_reduce_kernel.
+#include <type_traits>
+
 #include "kernels.h"
 #include "prec.h"
 
@@ -35,6 +37,28 @@ constexpr int kDHalf = kSegW * 16;                  // lo part offset in a dY ro
 constexpr int kGHalf = (kSegW + 2) * 16;            // lo part offset in an X row
 constexpr int kLds = kTile * kDRow + kTile * kGRow; // 71 680 B
 constexpr int kLdsW = 128 * kDRow + 64 * kGRow;     // 105 472 B (8-wave 128 × 64 variant)
+
+// 16-bit modes (bf16 / fp16: one plane, no lo half): the tiles are staged in their natural
+// [K = w·8 + r][channel] order — each thread converts its float4 (4 channels of one voxel) and
+// stores 8 B, no transpose in VALU — and the MFMA operands, which need 8 consecutive K per lane,
+// come out of LDS through ds_read_b64_tr_b16 (gfx950's transposing read: lane 4q+p of a 16-lane
+// group addresses row q, channels 4p…4p+3; lane i receives channel i of the 4 rows).  Rows are
+// TC·2 (dY) / TI·2 (X) bytes; 16-B chunks are XOR-swizzled by the row so the 4 rows × 2 channel
+// groups of a 32-lane half hit 16 distinct 16-B slots (conflict-free transposed reads; the
+// ds_write_b64 of 16 contiguous lanes stays one 128-B run): chunk c of row k sits at
+// c ^ tr_swz(k).  The kw-shifted X rows (k + 8kw) keep k's swizzle.
+constexpr int kTrRowsD = kSegW * kR;                 // 128 K rows of dY per stage
+constexpr int kTrRowsG = (kSegW + 2) * kR;           // 144 K rows of X (two extra w for kw = 1, 2)
+template <int RB>
+__device__ __forceinline__ int tr_swz(int row) {
+  return RB == 256 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
+}
+constexpr int kLdsTr = kTrRowsD * 64 * 2 + kTrRowsG * 64 * 2;    // 34 816 B
+constexpr int kLdsTrW = kTrRowsD * 128 * 2 + kTrRowsG * 64 * 2;  // 51 200 B
+typedef short tr_v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ tr_v4s tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tr_v4s*)(p));
+}
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -70,9 +94,11 @@ template <int TC, int TI, int PM>
 __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
   constexpr int WC = TC / 32;             // waves along co
+  constexpr bool kTr = !prec::has_lo<PM>();        // 16-bit modes: natural-order tiles + transposing reads
+  constexpr int RBD = TC * 2, RBG = TI * 2;         // tr image row bytes (dY, X)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ds = smem;
-  char* Gs = smem + TC * kDRow;
+  char* Gs = smem + (kTr ? kTrRowsD * RBD : TC * kDRow);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int wm0 = (wave % WC) * 32, wn0 = (wave / WC) * 32;
@@ -177,13 +203,37 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
     split8_store<PM>(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
     split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
   };
-  auto store = [&]() __attribute__((always_inline)) {
-    put(Ds, kDRow, kDHalf, uw, cq, rd);
-    if (g1) put(Gs, kGRow, kGHalf, gw, gcq, rg);
-    if constexpr (kSplitG) {
-      if (g2) put(Gs, kGRow, kGHalf, uw2, gcq, rg2);
+  // 16-bit modes: unit (voxel w, channel quad q) → rows w·8 + r, 8 B at chunk q/2 (swizzled), half q&1
+  auto put16 = [&](char* base, auto rb_c, int w, int q, const float4 (&v)[kR]) __attribute__((always_inline)) {
+    constexpr int RB = decltype(rb_c)::value;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int row = w * kR + r;
+      uint2 h, l;
+      prec::split4<PM>(v[r], h, l);
+      *reinterpret_cast<uint2*>(base + row * RB + 16 * ((q >> 1) ^ tr_swz<RB>(row)) + 8 * (q & 1)) = h;
     }
   };
+  auto store = [&]() __attribute__((always_inline)) {
+    if constexpr (kTr) {
+      put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+      if (g1) put16(Gs, std::integral_constant<int, RBG>{}, gw, gcq, rg);
+      if constexpr (kSplitG) {
+        if (g2) put16(Gs, std::integral_constant<int, RBG>{}, uw2, gcq, rg2);
+      }
+    } else {
+      put(Ds, kDRow, kDHalf, uw, cq, rd);
+      if (g1) put(Gs, kGRow, kGHalf, gw, gcq, rg);
+      if constexpr (kSplitG) {
+        if (g2) put(Gs, kGRow, kGHalf, uw2, gcq, rg2);
+      }
+    }
+  };
+  // transposed-read lane offsets: lane 4q+p of its 16-lane group g (g = lane bit 4) addresses row
+  // 8h + q (+ the read's K offset) and channels (sub-tile base + 16g + 4p … +3)
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
+  const int trA = (8 * lh + tq) * RBD + 16 * (((wm0 + 16 * tg) / 8 + (tp >> 1)) ^ tr_swz<RBD>(tq)) + 8 * (tp & 1);
+  const int trB = (8 * lh + tq) * RBG + 16 * (((wn0 + 16 * tg) / 8 + (tp >> 1)) ^ tr_swz<RBG>(tq)) + 8 * (tp & 1);
 
   f32x16 acc[3];
 #pragma unroll
@@ -198,12 +248,23 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
       load(st + 1);
     }
-    const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
-    const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+    const char* arow = kTr ? Ds + trA : Ds + (wm0 + li) * kDRow + lh * 16;
+    const char* brow = kTr ? Gs + trB : Gs + (wn0 + li) * kGRow + lh * 16;
     // fragments of K-step ks: A hi/lo (dY) and B hi/lo for the three kw taps (X shifted by kw
     // slots); software-pipelined one K-step ahead so the LDS latency hides under the MFMAs
     bf16x8 fa[2][2], fb[2][3][2];
     auto frag = [&](int ks, bf16x8 (&A)[2], bf16x8 (&Bf)[3][2]) __attribute__((always_inline)) {
+      if constexpr (kTr) {
+        // K-step ks covers rows 16ks … 16ks+15: two 4-row reads per operand for this lane's 8 K
+        const tr_v4s a0 = tr_read(arow + (16 * ks) * RBD), a1 = tr_read(arow + (16 * ks + 4) * RBD);
+        A[0] = A[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const tr_v4s b0 = tr_read(brow + (16 * ks + 8 * kw) * RBG), b1 = tr_read(brow + (16 * ks + 8 * kw + 4) * RBG);
+          Bf[kw][0] = Bf[kw][1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        return;
+      }
       A[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
       A[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : A[0];
 #pragma unroll
@@ -276,22 +337,25 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const bool wide = w3_wide(g);
   const int blocks = ((g.Cd / (wide ? 128 : kTile)) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
   MRAGAN_PREC_DISPATCH(g.x3, {
+    constexpr bool tr = !prec::has_lo<PM>();
     if (wide) {
+      const int lds = tr ? kLdsTrW : kLdsW;
       static bool attr_w = false;
       if (!attr_w) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<128, 64, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsW);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr_w = true;
       }
-      hipLaunchKernelGGL((wgrad3_x3_kernel<128, 64, PM>), dim3(blocks), dim3(512), kLdsW, st, a);
+      hipLaunchKernelGGL((wgrad3_x3_kernel<128, 64, PM>), dim3(blocks), dim3(512), lds, st, a);
     } else {
+      const int lds = tr ? kLdsTr : kLds;
       static bool attr_set = false;
       if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<64, 64, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr_set = true;
       }
-      hipLaunchKernelGGL((wgrad3_x3_kernel<64, 64, PM>), dim3(blocks), dim3(256), kLds, st, a);
+      hipLaunchKernelGGL((wgrad3_x3_kernel<64, 64, PM>), dim3(blocks), dim3(256), lds, st, a);
     }
     return nsplit;
   })

@@ -13,10 +13,14 @@ fp32-grade modes (f32, bf16x3) — gates calibrated on the reference's own fp32-
 
 Reduced modes (bf16, fp16: every conv operand rounded) — against the oracle's rounded-operand
 step (tests/golden/prec_<case>.npz, tools/gen_precision_fixtures.py): "emu64" is the step with
-the engine's operand rounding evaluated in fp64, "emu32" the same in fp32.  The same calibrated
-rule as above with emu32 in the reference-fp32 role: every quantity within max(1e-3, 2 × the
-emu32-vs-emu64 gap) of emu64 (gradients per tensor with the same outlier budget, and for the whole
-network with none).
+the engine's operand rounding evaluated in fp64, "emu32" the same in fp32 (and "emu32p1/p2" at
+inputs moved by ~2 fp32 ulps: further realisations).  The same calibrated rule as above with the
+fp32 realisations in the reference-fp32 role: every quantity within max(1e-3, 2 × the largest
+fp32-vs-emu64 gap) of emu64 (gradients per tensor with the same outlier budget, and for the whole
+network with none).  Measured (r03c, MI355X): the GPU's distance to emu64 tracks emu32's within
+0.7-1.3× for every volume, loss vector and whole-network gradient at 24³-256³ — bf16 operand
+rounding is chaotic at the 1e-2 level (rec_A 4e-2, whole-network gradient 0.2-0.3), for ANY
+accumulation order, so a fixed 1e-3 gate on volumes is below the arithmetic's reproducibility.
 """
 import random
 import sys
@@ -129,13 +133,23 @@ def prec_fixture(name):
     return np.load(path, allow_pickle=False) if os.path.exists(path) else None
 
 
+CAL_RUNS = ("emu32", "emu32p1", "emu32p2")
+
+
+def _cal_runs(p, mode):
+    """The fp32 calibration realisations the fixture holds (emu32, and the input-perturbed twins)."""
+    return [r for r in CAL_RUNS if f"{mode}/{r}/steps" in p.files]
+
+
 def _pgap(p, mode, key, got):
-    """(rel err of `got` vs emu64, rel gap emu32 vs emu64) at the fixture's sampled indices."""
+    """(rel err of `got` vs emu64, largest rel gap of an fp32 realisation vs emu64, got, emu64,
+    emu32) at the fixture's sampled indices."""
     flat = got.detach().reshape(-1).double().cpu()
     w64 = p[f"{mode}/emu64/{key}/val"]
     w32 = p[f"{mode}/emu32/{key}/val"]
+    gap = max(rel_err(p[f"{mode}/{r}/{key}/val"], w64) for r in _cal_runs(p, mode))
     g = flat[torch.from_numpy(p[f"{mode}/emu64/{key}/idx"])].numpy()
-    return rel_err(g, w64), rel_err(w32, w64), g, w64, w32
+    return rel_err(g, w64), gap, g, w64, w32
 
 
 REDUCED_MIN = 1e-3        # the north star's gate; the calibrated term can only widen it
@@ -156,8 +170,8 @@ def test_reduced_losses(stepped):
     name, mode, p, history, _ = _reduced(stepped)
     for step in range(int(p[f"{mode}/emu64/steps"])):
         w64 = p[f"{mode}/emu64/step{step}/losses"]
-        w32 = p[f"{mode}/emu32/step{step}/losses"]
-        err, gap = rel_err(history[step], w64), rel_err(w32, w64)
+        err = rel_err(history[step], w64)
+        gap = max(rel_err(p[f"{mode}/{r}/step{step}/losses"], w64) for r in _cal_runs(p, mode))
         # after the first Adam step the runs separate like the reference's fp32 and fp64 (±lr steps
         # of round-off-sized gradients): the later-step factor of the fp32-grade modes
         env = max(REDUCED_MIN, (2.0 if step == 0 else 10.0) * gap)

@@ -35,9 +35,16 @@ from oracle.cyclegan_oracle import CycleGANOracle  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden")
 MODES = {"bf16": 1.0, "fp16": 1024.0}        # mode → the engine's loss scale (CycleGANModel default)
-SMALL = ["step_r9_s32_b1", "step_r6_s24_b2_nc2_lsgan", "step_unet_s32_b2_ngf8", "step_r6_s24_b1_noidt"]
-BIG = ["step_r9_s64_b2", "step_r9_s96_b1_nc2", "step_r9_s128_b1"]
-RUNS = ("emu64", "emu32")
+SMALL = ["step_r9_s32_b1", "step_r6_s24_b2_nc2_lsgan", "step_unet_s32_b2_ngf8", "step_r6_s24_b1_noidt",
+         "step_r6_s24_b1_pool1"]
+BIG = ["step_r9_s64_b2", "step_unet_s64_b1_ngf32", "step_r9_s96_b1_nc2", "step_r9_s128_b1",
+       "step_unet256_s256_b1_ngf4"]
+# emu32p1 / emu32p2: the fp32 twin at inputs perturbed by ~2 fp32 ulps (relative 1e-7 N(0,1) noise):
+# further independent realisations of how far fp32 accumulation alone moves a rounded-operand step
+# (the tests gate on the largest of the three gaps — one realisation under-states it for
+# few-element quantities like the 8 losses)
+RUNS = ("emu64", "emu32", "emu32p1", "emu32p2")
+PERTURB = 1e-7
 
 
 def sample(t, key, out, n):
@@ -60,6 +67,10 @@ def run(case, mode, run_name, out):
     pre = f"{mode}/{run_name}"
     for step in range(steps):
         A, B = inputs(meta, step)
+        if run_name.startswith("emu32p"):
+            g = torch.Generator().manual_seed(90 + int(run_name[-1]) * 1000 + step)
+            A = A * (1 + PERTURB * torch.randn(A.shape, generator=g))
+            B = B * (1 + PERTURB * torch.randn(B.shape, generator=g))
         losses = orc.optimize_parameters(A, B)
         out[f"{pre}/step{step}/losses"] = np.array(list(losses.values()), dtype=np.float64)
         if step:
