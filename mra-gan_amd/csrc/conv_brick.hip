@@ -19,6 +19,9 @@
 // [hi 32 × bf16][lo 32 × bf16], split once when staged.  Both row formats are 144 B (36 dwords:
 // 16 consecutive rows of a ds_read_b128 phase land on distinct bank quads).
 #include "conv_geo.h"
+#include <cstdio>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace mragan {
@@ -323,10 +326,22 @@ static BrickChoice choose_brick(int N, int Do, int Ho, int Wo, int ny, bool x3) 
     if (cost < best.cost * 0.999 || (cost < best.cost * 1.001 && blocks < best.blocks))
       best = BrickChoice{bm, bn, s[0], s[1], s[2], blocks, cost};
   };
-  for (auto& s : shapes128) consider(128, 64, s);
-  for (auto& s : shapes128) consider(128, 128, s);
-  for (auto& s : shapes64) consider(64, 128, s);
-  for (auto& s : shapes64) consider(64, 64, s);
+  // A/B switch: MRAGAN_BRICK_CFG="bm,bn" restricts the choice to that tile (the best shape for it)
+  static int force_bm = -1, force_bn = -1;
+  if (force_bm < 0) {
+    const char* e = getenv("MRAGAN_BRICK_CFG");
+    force_bm = force_bn = 0;
+    if (e && sscanf(e, "%d,%d", &force_bm, &force_bn) != 2) force_bm = force_bn = 0;
+  }
+  auto allowed = [&](int bm, int bn) { return force_bm == 0 || (bm == force_bm && bn == force_bn); };
+  for (auto& s : shapes128) if (allowed(128, 64)) consider(128, 64, s);
+  for (auto& s : shapes128) if (allowed(128, 128)) consider(128, 128, s);
+  for (auto& s : shapes64) if (allowed(64, 128)) consider(64, 128, s);
+  for (auto& s : shapes64) if (allowed(64, 64)) consider(64, 64, s);
+  if (best.bm == 0) {                    // the forced tile does not fit this conv: the free choice
+    for (auto& s : shapes128) consider(128, 64, s);
+    for (auto& s : shapes64) consider(64, 64, s);
+  }
   return best;
 }
 

@@ -53,8 +53,12 @@ template <int RB>
 __device__ __forceinline__ int tr_swz(int row) {
   return RB == 256 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
 }
-constexpr int kLdsTr = kTrRowsD * 64 * 2 + kTrRowsG * 64 * 2;    // 34 816 B
-constexpr int kLdsTrW = kTrRowsD * 128 * 2 + kTrRowsG * 64 * 2;  // 51 200 B
+// two stage buffers: the stage after next is loaded while this one's MFMAs run and stored right
+// after them, so a load has a whole stage (not only the MFMA phase) to land
+constexpr int kTrStage = kTrRowsD * 64 * 2 + kTrRowsG * 64 * 2;    // 34 816 B
+constexpr int kTrStageW = kTrRowsD * 128 * 2 + kTrRowsG * 64 * 2;  // 51 200 B
+constexpr int kLdsTr = 2 * kTrStage;
+constexpr int kLdsTrW = 2 * kTrStageW;
 typedef short tr_v4s __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ tr_v4s tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tr_v4s*)(p));
@@ -97,6 +101,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   constexpr bool kTr = !prec::has_lo<PM>();        // 16-bit modes: natural-order tiles + transposing reads
   constexpr int RBD = TC * 2, RBG = TI * 2;         // tr image row bytes (dY, X)
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kStage = kTrRowsD * RBD + kTrRowsG * RBG;            // tr: bytes of one stage buffer
   char* Ds = smem;
   char* Gs = smem + (kTr ? kTrRowsD * RBD : TC * kDRow);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -239,14 +244,36 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
 
-  if (nstage > 0) load(0);
-  for (int st = 0; st < nstage; ++st) {
-    store();
-    __syncthreads();
-    if (st + 1 < nstage) {                          // lands during this stage's MFMAs
+  auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
+    Ds = smem + b * kStage;
+    Gs = Ds + kTrRowsD * RBD;
+  };
+  if constexpr (kTr) {
+    // prologue: stage 0 staged, stage 1 in registers
+    if (nstage > 0) {
+      load(0);
+      store();
+    }
+    if (nstage > 1) {
 #pragma unroll
       for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
-      load(st + 1);
+      load(1);
+    }
+  } else if (nstage > 0) {
+    load(0);
+  }
+  for (int st = 0; st < nstage; ++st) {
+    if constexpr (kTr) {
+      use_buf(st & 1);
+      __syncthreads();              // stage st staged by every wave; buffer (st+1)&1 read by nobody now
+    } else {
+      store();
+      __syncthreads();
+      if (st + 1 < nstage) {                        // lands during this stage's MFMAs
+#pragma unroll
+        for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+        load(st + 1);
+      }
     }
     const char* arow = kTr ? Ds + trA : Ds + (wm0 + li) * kDRow + lh * 16;
     const char* brow = kTr ? Gs + trB : Gs + (wn0 + li) * kGRow + lh * 16;
@@ -284,7 +311,19 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+    if constexpr (kTr) {
+      if (st + 1 < nstage) {
+        use_buf((st + 1) & 1);
+        store();                    // stage st+1 (loaded one stage ago) into the other buffer
+        if (st + 2 < nstage) {
+#pragma unroll
+          for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+          load(st + 2);
+        }
+      }
+    } else {
+      __syncthreads();
+    }
   }
 
   // slab[z][t][co][ci]: lane li = ci column, register r = co row (r & 3) + 8 (r >> 2) + 4 lh

@@ -27,6 +27,8 @@ from . import networks3D
 from .base_model import BaseModel
 
 device = networks3D.device
+# A/B switch: MRAGAN_NO_GRAPH_CACHE=1 keeps only the latest capture (round-2 behaviour)
+_NO_GRAPH_CACHE = bool(int(__import__("os").environ.get("MRAGAN_NO_GRAPH_CACHE", "0") or "0"))
 
 
 class ImagePool():
@@ -361,11 +363,13 @@ class CycleGANModel(BaseModel):
         self.real_B = self._stage_input('B', input[1 if AtoB else 0])
 
     def _stage_input(self, key, x):
-        """Copy into a persistent device buffer (same values; a captured step reads it)."""
-        buf = self._in.get(key)
-        if buf is None or buf.shape != x.shape or buf.dtype != x.dtype:
+        """Copy into a persistent device buffer per input shape (same values; a captured step reads
+        it, and alternating batch shapes keep their buffers — and their cached captures)."""
+        k = (key, tuple(x.shape), x.dtype)
+        buf = self._in.get(k)
+        if buf is None:
             buf = torch.empty(x.shape, dtype=x.dtype, device=self.device)
-            self._in[key] = buf
+            self._in[k] = buf
         buf.copy_(x, non_blocking=True)
         return buf
 
@@ -595,6 +599,8 @@ class CycleGANModel(BaseModel):
         shapes — an epoch's smaller last batch — replay without recapturing), or a new
         capture (the least recently used one beyond GRAPH_CACHE entries is released)."""
         key = self._capture_key()
+        if _NO_GRAPH_CACHE:
+            self._graph_cache.clear()
         # a capture whose pool buffers were reallocated (a larger batch grew them) points at freed
         # memory: drop it (key fields 4, 5 are the pool buffers' addresses)
         for k in [k for k in self._graph_cache if k[4:6] != key[4:6]]:

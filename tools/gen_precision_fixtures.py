@@ -52,7 +52,8 @@ def sample(t, key, out, n):
     name = key.split("/", 2)[2]              # strip "<mode>/<run>/": same indices in every run
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     idx = np.sort(rng.choice(flat.numel(), size=min(n, flat.numel()), replace=False))
-    out[key + "/idx"] = idx.astype(np.int64)
+    if key.split("/")[1] == "emu64":         # the other runs share the emu64 run's positions
+        out[key + "/idx"] = idx.astype(np.int64)
     out[key + "/val"] = flat[torch.from_numpy(idx)].numpy()
     out[key + "/norm"] = np.array(flat.norm().item())
 

@@ -54,8 +54,16 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--source", default=None, help="what was profiled (recorded in the entry)")
     a = ap.parse_args()
-    fetch_kib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
-    write_kib, nw = per_launch(a.write, "WRITE_SIZE", a.kernel)
+    # a launch class may be several kernels (e.g. "wgrad3_x3_kernel,wgrad_reduce_kernel"): per-launch
+    # averages of each, summed
+    fetch_kib = write_kib = 0.0
+    nf = nw = 0
+    for k in a.kernel.split(","):
+        f, n1 = per_launch(a.fetch, "FETCH_SIZE", k)
+        w, n2 = per_launch(a.write, "WRITE_SIZE", k)
+        fetch_kib += f
+        write_kib += w
+        nf, nw = max(nf, n1), max(nw, n2)
     entry = {
         "kernel": a.kernel,
         "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
