@@ -37,7 +37,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;                 // channels per chunk
-constexpr int kRow = 144;               // LDS row bytes: hi 64 B, lo 64 B, 16 B pad
+// LDS row bytes of one halo position (32 channels): bf16x3 hi 64 B | lo 64 B | 16 B pad; the
+// one-plane modes (bf16, fp16) hi 64 B | 16 B pad — half the halo, so two blocks fit a CU.  Both
+// strides are an odd number of 16-B slots (9, 5): rows distinct mod 16 land on distinct slots, so
+// brick_row_perm's conflict-free assignment holds for either.
+template <int PM>
+constexpr int row_bytes() { return prec::has_lo<PM>() ? 144 : 80; }
 constexpr int kTaps = 27;
 constexpr int kSteps = 2 * kTaps;       // (tap, 16-channel half) steps per chunk
 
@@ -91,6 +96,7 @@ conv_brick_x3_kernel(BrickArgs a) {
   constexpr int kP = 18;                             // unrolled period: ring slots compile-time
   static_assert(kSteps % kP == 0 && kP % kPF == 0 && kP % 9 == 0 && kHD < kPF, "step period");
 
+  constexpr int kRow = row_bytes<PM>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* halo_buf = smem;                                                // [2][HMAX][kRow]
   int* out_off = reinterpret_cast<int*>(smem + 2 * HMAX * kRow);       // [BM]
@@ -320,7 +326,7 @@ conv_brick_x3_kernel(BrickArgs a) {
 template <int WM, int WN, int TM, int TN, int HMAX, int PM>
 static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
   constexpr int BM = WM * TM * 32;
-  const size_t lds = (size_t)2 * HMAX * kRow + (size_t)(BM + HMAX) * sizeof(int);
+  const size_t lds = (size_t)2 * HMAX * row_bytes<PM>() + (size_t)(BM + HMAX) * sizeof(int);
   auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM>;
   static bool attr_set = false;
   if (!attr_set) {

@@ -558,9 +558,15 @@ class CycleGANModel(BaseModel):
         hyp = self.optimizer_G.advance() + self.optimizer_D.advance()
         idx = torch.tensor([retB, stB, retA, stA], dtype=torch.int64).pin_memory()
         hyp = torch.tensor(hyp, dtype=torch.float32).pin_memory()
-        if getattr(self, '_step_idx', None) is None or self._step_idx.shape != idx.shape:
-            self._step_idx = torch.empty(idx.shape, dtype=torch.int64, device=self.device)
+        # one persistent index buffer per batch size (a captured step reads it: alternating batch
+        # sizes keep their buffers and so their cached captures)
+        if not hasattr(self, '_step_idx_bufs'):
+            self._step_idx_bufs = {}
             self._step_hyper = torch.empty(12, dtype=torch.float32, device=self.device)
+        self._step_idx = self._step_idx_bufs.get(tuple(idx.shape))
+        if self._step_idx is None:
+            self._step_idx = torch.empty(idx.shape, dtype=torch.int64, device=self.device)
+            self._step_idx_bufs[tuple(idx.shape)] = self._step_idx
         self._step_idx.copy_(idx, non_blocking=True)
         self._step_hyper.copy_(hyp, non_blocking=True)
 
@@ -592,7 +598,7 @@ class CycleGANModel(BaseModel):
     # attributes a captured step's tensors live in (re-published when a cached capture replays)
     _CAPTURE_ATTRS = ('_cGA1', '_cGA2', '_cGB1', '_cGB2', '_cDA1', '_cDA2', '_cDB1', '_cDB2', '_fake_A', '_fake_B',
                       '_A', '_B', '_b', '_idt', 'fake_A', 'fake_B', 'rec_A', 'rec_B', 'idt_A', 'idt_B')
-    GRAPH_CACHE = 4
+    GRAPH_CACHE = 2          # the full batch and an epoch's smaller last batch
 
     def _use_capture(self):
         """Make the capture for the current key the replayed one: from the cache (alternating batch
