@@ -120,8 +120,12 @@ VOL_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
 RS_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
 # later-step losses: multiple of the reference's own fp32-vs-fp64 divergence at that step, and at
 # least LATER_MIN
+# least LATER_MIN.  bf16x3's per-product error (≤ 3·2⁻¹⁸) is ~50× fp32's, so more of the first Adam
+# step's ±lr signs (elements with a round-off-sized gradient) differ from fp64 and a multi-step
+# trajectory departs further: on the 6-step pool-1 case (r03a) 1.8e-4, 7.0e-4, 8.6e-4, 1.05e-3 at
+# steps 1-4, against the reference fp32's 5e-8 … 3.3e-5
 LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0}
-LATER_MIN = {"f32": 1e-3, "bf16x3": 1e-3}
+LATER_MIN = {"f32": 1e-3, "bf16x3": 3e-3}
 
 
 # ---- reduced precisions: against the rounded-operand oracle ----------------------------------
