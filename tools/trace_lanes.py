@@ -17,7 +17,7 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "").replace("mragan::", "")
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("mragan::", "")
     return n.split("<")[0]
 
 
@@ -77,7 +77,7 @@ def main():
             for i in range(len(lst) - 3):
                 names = [lst[i + k][3] for k in range(4)]
                 if names[0].startswith("thinn_x3_kernel") and names[1] == "rpad_kernel" and \
-                        names[2].startswith("thin1_pack") and names[3].startswith("thin1"):
+                        "pack" in names[2] and names[3].startswith("thin1"):
                     h, rp, pk, st = lst[i:i + 4]
                     bnd.append(dict(gap1=rp[0] - h[1], rpad=rp[1] - rp[0], gap2=pk[0] - rp[1], pack=pk[1] - pk[0],
                                     gap3=st[0] - pk[1], head=h[1] - h[0], stem=st[1] - st[0]))
