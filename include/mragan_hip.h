@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 10
+#define MRAGAN_ABI_VERSION 11
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -145,6 +145,40 @@ int mragan_instnorm_fwd_partials(const float* x, int N, int D, int H, int W, int
 int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                           const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out, void* ws,
                           size_t ws_bytes, void* stream);
+
+/* ---- 16-bit operand planes (bf16 / fp16 modes only; ABI 11) --------------------------------
+ * The "operand plane" of an fp32 NDHWC tensor is the same tensor as the 16-bit words (bf16 in
+ * MRAGAN_PREC_BF16, fp16 in MRAGAN_PREC_F16, round-to-nearest-even) every MFMA convolution of that
+ * mode rounds its fp32 operands to — so a convolution reading the plane computes exactly the
+ * products it computes from the fp32 tensor, from half the bytes and with no conversion.  A
+ * producer writes the plane of a tensor that is only ever a convolution operand (a ResnetBlock's
+ * relu(IN(conv1(x))) and the InstanceNorm-backward outputs that are the dY of its two convs,
+ * networks3D.py:241-257) instead of the fp32 tensor, and beside it for a tensor that also feeds
+ * fp32 math (a block's output: the next block's skip add, :262-263).  Every entry fails with
+ * MRAGAN_EBADARG in the fp32-grade modes.
+ *   instnorm_fwd_op16 / _partials_op16: mragan_instnorm_fwd / _fwd_partials writing y (fp32,
+ *       nullable) and / or y16 (its plane, nullable, same padded layout);
+ *   instnorm_bwd_op16: mragan_instnorm_bwd_g writing dx only as its plane dx16 (g_out nullable);
+ *   conv3d_op16: mragan_conv3d_presplit_in_stats (no bias, no activation) on the plane x16 of
+ *       the input — the k3 s1 brick kernel (ResnetBlock convs and their whole-grid data
+ *       gradients); part / chunks nullable (no InstanceNorm partials);
+ *   conv3d_wgrad_op16: mragan_conv3d_wgrad on the planes of dense and gathered — the k3 s1 valid
+ *       weight gradient of the ResnetBlock convs (wgrad3_x3).                                   */
+int mragan_instnorm_fwd_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
+                             const float* resid, int rpad, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                             void* stream);
+int mragan_instnorm_fwd_partials_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad,
+                                      int act, const float* resid, int rpad, float* mean, float* rstd,
+                                      const double* part, int chunks, void* stream);
+int mragan_instnorm_bwd_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                             const float* dy, int dypad, const float* dy_add, int act, void* dx16, float* g_out, void* ws,
+                             size_t ws_bytes, void* stream);
+int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, const void* wsplit,
+                       int cout, int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
+                       size_t ws_bytes, double* part, size_t part_bytes, int* chunks, void* stream);
+int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
+                             int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                             size_t ws_bytes, void* stream);
 
 /* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
  * entry listing the per-instance statistics of the reference's sequential calls in call order. */

@@ -134,6 +134,72 @@ int mragan_instnorm_fwd_partials(const float* x, int N, int D, int H, int W, int
                                static_cast<hipStream_t>(stream));
 }
 
+static int op16_mode_ok() {
+  MRAGAN_CHECK_ARG(g_conv_precision == MRAGAN_PREC_BF16 || g_conv_precision == MRAGAN_PREC_F16,
+                   "16-bit operand planes need the bf16 or fp16 precision mode (current: %d)", g_conv_precision);
+  return kOk;
+}
+
+int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit, int cout,
+                       int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
+                       size_t ws_bytes, double* part, size_t part_bytes, int* chunks, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x16 && w && wsplit && y, "conv3d_op16: null pointer");
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_op16: transposed must be 0/1");
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && Do > 0 && Ho > 0 && Wo > 0,
+                   "conv3d_op16: bad shape");
+  MRAGAN_CHECK_ARG(!thin_side(cin, cout), "conv3d_op16: channel counts %d -> %d are not a brick convolution", cin, cout);
+  if (part) {
+    MRAGAN_CHECK_ARG(chunks, "conv3d_op16: null chunks");
+    const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+    MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_op16: partials %zu < %zu bytes", part_bytes, bound);
+    *chunks = 0;
+  }
+  IgemmArgs a{static_cast<const float*>(x16), w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad,
+              transposed, kActNone, 1, g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
+  a.x16 = 1;
+  return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
+int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
+                             int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                             size_t ws_bytes, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(dense16 && gathered16 && dw && ws, "wgrad_op16: null pointer");
+  MRAGAN_CHECK_ARG(!thin_wgrad_side(Cd, Cg) && k >= 1 && stride >= 1 && pad >= 0, "wgrad_op16: bad args");
+  WgradArgs a{static_cast<const float*>(dense16), N, Dd, Hd, Wd, Cd, static_cast<const float*>(gathered16), Dg, Hg, Wg,
+              Cg, k, stride, pad, static_cast<float*>(ws), 0, 0, g_conv_precision, 1};
+  return conv_wgrad(a, dw, accumulate, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_fwd_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
+                             const float* resid, int rpad, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && (y || y16) && mean && rstd && ws, "instnorm_fwd_op16: null pointer");
+  return instnorm_fwd(x, InShape{N, D, H, W, C}, y, ypad, act, resid, rpad, mean, rstd, ws, ws_bytes,
+                      static_cast<hipStream_t>(stream), y16, g_conv_precision);
+}
+
+int mragan_instnorm_fwd_partials_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad,
+                                      int act, const float* resid, int rpad, float* mean, float* rstd,
+                                      const double* part, int chunks, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && (y || y16) && mean && rstd && part, "instnorm_fwd_partials_op16: null pointer");
+  return instnorm_fwd_partials(x, InShape{N, D, H, W, C}, y, ypad, act, resid, rpad, mean, rstd, part, chunks,
+                               static_cast<hipStream_t>(stream), y16, g_conv_precision);
+}
+
+int mragan_instnorm_bwd_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                             const float* dy, int dypad, const float* dy_add, int act, void* dx16, float* g_out, void* ws,
+                             size_t ws_bytes, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx16 && ws, "instnorm_bwd_op16: null pointer");
+  MRAGAN_CHECK_ARG(!g_out || (g_out != dy && g_out != dy_add), "instnorm_bwd_op16: g_out aliases an operand");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, nullptr, g_out, dx16, g_conv_precision};
+  return instnorm_bwd(a, InShape{N, D, H, W, C}, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
 size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout, int k, int stride, int pad, int Do,
                                int Ho, int Wo, int transposed) {
   if (thin_side(cin, cout)) {

@@ -87,6 +87,13 @@ __device__ __forceinline__ float4 buf_load_f32x4(__amdgpu_buffer_rsrc_t r, uint3
 __device__ __forceinline__ buf_f32x4 buf_load_16b(__amdgpu_buffer_rsrc_t r, int voffset, int soffset) {
   return llvm_raw_buffer_load_f32x4(r, voffset, soffset, 0);
 }
+// 8 bytes (four 16-bit operand words of a 16-bit operand plane), same addressing
+typedef float buf_f32x2 __attribute__((ext_vector_type(2)));
+__device__ buf_f32x2 llvm_raw_buffer_load_f32x2(__amdgpu_buffer_rsrc_t r, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.ptr.buffer.load.v2f32");
+__device__ __forceinline__ uint2 buf_load_8b(__amdgpu_buffer_rsrc_t r, int voffset, int soffset) {
+  return __builtin_bit_cast(uint2, llvm_raw_buffer_load_f32x2(r, voffset, soffset, 0));
+}
 
 }  // namespace mragan
 

@@ -394,6 +394,7 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   a.w = g.w; a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
   a.act = g.act;
   a.ye = 0; a.Yd = g.Do; a.Yh = g.Ho; a.Yw = g.Wo;
+  a.x16 = g.x16;
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
   a.flip = g.trans ? 1 : 0;
   a.p = g.trans ? g.k - 1 - g.p : g.p;
@@ -411,6 +412,7 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   a.ntiles = (int)c.blocks;
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, c.bm, a.rowvox);
+  MRAGAN_CHECK_ARG(!g.x16 || conv_brick_x3_active(g), "conv_brick: a 16-bit operand plane needs the 16-bit MFMA brick");
   if (conv_brick_x3_active(g)) {
     if (g.in_part) {
       a.part = g.in_part;

@@ -75,15 +75,29 @@ __device__ __forceinline__ void split4_store(char* row, int q, const float4& v) 
   if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(row + 64 + 8 * q) = l;
 }
 
+// one 16-B slice q of a halo position: fp32 input → 4 channels split into the row; a 16-bit
+// operand plane (X16) → 8 channels already in MFMA format, copied as they are
+template <int PM, int X16>
+__device__ __forceinline__ void halo_store(char* row, int q, const float4& v) {
+  if constexpr (X16) *reinterpret_cast<float4*>(row + 16 * q) = v;
+  else split4_store<PM>(row, q, v);
+}
+
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int HMAX, int PM>
+template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16>
 __global__ void __launch_bounds__(WM * WN * 64)
 conv_brick_x3_kernel(BrickArgs a) {
+  static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
   constexpr int NT = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  constexpr int NSL = (HMAX * 8 + NT - 1) / NT;      // halo float4 slices per thread per chunk
+  // input: fp32 NDHWC, or (X16) the producer's 16-bit operand plane of it (bf16 / fp16 words,
+  // already rounded as this kernel would round them): half the halo bytes, no conversion
+  constexpr int ES = X16 ? 2 : 4;                    // bytes per input element
+  constexpr int SPP = X16 ? 4 : 8;                   // 16-B slices per halo position (32 channels)
+  constexpr int CPS = kBK / SPP;                     // channels per slice
+  constexpr int NSL = (HMAX * SPP + NT - 1) / NT;    // halo slices per thread per chunk
   // next-chunk halo: slice s is loaded at step 3s and split + stored kHD steps later (a ring of
   // 3 float4); vmcnt drains in issue order, so a load's real deadline is the next weight wait
   // kPF steps on — kHD < kPF keeps the store inside that window
@@ -161,8 +175,8 @@ conv_brick_x3_kernel(BrickArgs a) {
   // an offset past the end and reads 0, with no select on the loaded value (a conditional
   // overwrite made hipcc drain the memory counter — the 9-step weight prefetch included — at
   // every halo load)
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C,
-                                              (uint32_t)a.Di * a.Hi * a.Wi * a.C * 4u);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const char*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C * ES,
+                                              (uint32_t)a.Di * a.Hi * a.Wi * a.C * (uint32_t)ES);
   const int nchunks = nch_;
   __syncthreads();
 
@@ -171,14 +185,14 @@ conv_brick_x3_kernel(BrickArgs a) {
     float4 pv[NSL];                      // all loads in flight before the first store
 #pragma unroll
     for (int sl = 0; sl < NSL; ++sl) {
-      const int e = sl * NT + tid, pos = e >> 3;
+      const int e = sl * NT + tid, pos = e / SPP;
       const int o = pos < HP ? hoff[pos] : -1;
-      pv[sl] = buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + 4 * (e & 7)) * 4u);
+      pv[sl] = buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + CPS * (e % SPP)) * (uint32_t)ES);
     }
 #pragma unroll
     for (int sl = 0; sl < NSL; ++sl) {
-      const int e = sl * NT + tid, pos = e >> 3;
-      if (pos < HP) split4_store<PM>(halo_buf + pos * kRow, e & 7, pv[sl]);
+      const int e = sl * NT + tid, pos = e / SPP;
+      if (pos < HP) halo_store<PM, X16>(halo_buf + pos * kRow, e % SPP, pv[sl]);
     }
   }
 
@@ -229,15 +243,16 @@ conv_brick_x3_kernel(BrickArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       // next chunk's halo: slice s = u/3 loaded into ring slot s mod 3 (u0/3 ≡ 0 mod 3) …
       if (du % 3 == 0 && u / 3 < NSL) {
-        const int e = (u / 3) * NT + tid, hpos = e >> 3;
+        const int e = (u / 3) * NT + tid, hpos = e / SPP;
         const int o = (stream && hpos < HP) ? hoff[hpos] : -1;
         rh[(du / 3) % 3] = buf_load_f32x4(
-            xr, o < 0 ? kOobOffset : (uint32_t)(o + (c + 1 < nchunks ? c + 1 : c) * kBK + 4 * (e & 7)) * 4u);
+            xr, o < 0 ? kOobOffset
+                      : (uint32_t)(o + (c + 1 < nchunks ? c + 1 : c) * kBK + CPS * (e % SPP)) * (uint32_t)ES);
       }
       // … and split + stored kHD steps later
       if ((du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
-        const int e = ((u - kHD) / 3) * NT + tid, hpos = e >> 3;
-        if (stream && hpos < HP) split4_store<PM>(Hn + hpos * kRow, e & 7, rh[((du + kP - kHD) / 3) % 3]);
+        const int e = ((u - kHD) / 3) * NT + tid, hpos = e / SPP;
+        if (stream && hpos < HP) halo_store<PM, X16>(Hn + hpos * kRow, e % SPP, rh[((du + kP - kHD) / 3) % 3]);
       }
       // B fragments of this step (loaded kPF steps ago), then refill the slot with step u + kPF
       bf16x8 bh[TN], bl[TN];
@@ -323,18 +338,29 @@ conv_brick_x3_kernel(BrickArgs a) {
   }
 }
 
-template <int WM, int WN, int TM, int TN, int HMAX, int PM>
-static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
+template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16>
+static int launch_brick_x3_as(const BrickArgs& a, hipStream_t st) {
   constexpr int BM = WM * TM * 32;
   const size_t lds = (size_t)2 * HMAX * row_bytes<PM>() + (size_t)(BM + HMAX) * sizeof(int);
-  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM>;
+  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM, X16>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3(a.ntiles), dim3(WM * WN * 64), lds, st, a);
-  return check_launch("conv_brick_x3");
+  return check_launch(X16 ? "conv_brick_x3(op16)" : "conv_brick_x3");
+}
+
+template <int WM, int WN, int TM, int TN, int HMAX, int PM>
+static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
+  if (!a.x16) return launch_brick_x3_as<WM, WN, TM, TN, HMAX, PM, 0>(a, st);
+  if constexpr (prec::has_lo<PM>()) {
+    set_error("conv_brick_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
+    return kBadArg;
+  } else {
+    return launch_brick_x3_as<WM, WN, TM, TN, HMAX, PM, 1>(a, st);
+  }
 }
 
 // bm ∈ {64, 128}, bn ∈ {64, 128}: 4 waves (one per SIMD), wave tile (bm/2)×(bn/2) — the
@@ -360,6 +386,12 @@ static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_b
   }
   // 128-row bricks on 8 waves (two per SIMD): one wave's halo staging and LDS waits overlap the
   // other's MFMAs (the LDS-resident halo allows only one block per CU)
+  static const int var = [] {
+    const char* e = getenv("MRAGAN_BRICK_VAR");
+    return e ? atoi(e) : 0;
+  }();
+  if (bm == 128 && bn == 128 && var == 1) return launch_brick_x3<1, 4, 4, 1, 400, PM>(a, st);
+  if (bm == 128 && bn == 128 && var == 2) return launch_brick_x3<2, 2, 2, 2, 400, PM>(a, st);
   if (bm == 128 && bn == 128) return launch_brick_x3<2, 4, 2, 1, 400, PM>(a, st);
   if (bm == 128) return launch_brick_x3<4, 2, 1, 1, 400, PM>(a, st);
   if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300, PM>(a, st);

@@ -308,6 +308,12 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   int64_t max_mc, total_m;
   igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return kOk;
+  if (a.x16) {
+    // 16-bit operand planes: the ResnetBlock convs (forward and whole-grid data gradient) only
+    MRAGAN_CHECK_ARG(!g_brick_off && conv_brick_applicable(a), "conv: a 16-bit operand plane input is supported by the "
+                     "k3 s1 brick kernel only");
+    return conv_brick(a, st);
+  }
   if (full_dgrad_split_applicable(a)) {
     // the 16-bit brick kernel on the interior (no padded rows, no all-zero taps) + the shell pass
     const int rc = conv_brick(a, st, true);

@@ -390,6 +390,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
     const int64_t dper = (int64_t)a.Dd * a.Hd * a.Wd * a.Cd, gper = (int64_t)a.Dg * a.Hg * a.Wg * a.Cg;
     const int64_t per = 4 * (dper > gper ? dper : gper), lim = ((int64_t)1 << 31) - 1;
     if (per * a.N > lim && per <= lim) {
+      MRAGAN_CHECK_ARG(!a.in16, "conv_wgrad: 16-bit operand planes of more than 2 GiB");
       const int nb = (int)(lim / per);
       for (int n0 = 0; n0 < a.N; n0 += nb) {
         WgradArgs c = a;
@@ -413,10 +414,13 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   }
   static const bool no_w3 = getenv("MRAGAN_NO_WGRAD3") != nullptr;   // A/B switch
   const bool w3 = !no_w3 && wgrad3_x3_applicable(a), w3s2 = !no_w3 && !w3 && wgrad3s2_x3_applicable(a);
+  MRAGAN_CHECK_ARG(!a.in16 || w3, "conv_wgrad: 16-bit operand planes are supported by the k3 s1 valid weight "
+                   "gradient (wgrad3_x3) only");
   if (w3 || w3s2) {
     const int used = w3 ? conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st)
                         : conv_wgrad3s2_x3(a, wgrad3s2_x3_splits(a, a.splits), st);
-    int rc = check_launch("wgrad3_x3");
+    if (used < 0) return -used;
+    int rc = check_launch(a.in16 ? "wgrad3_x3(op16)" : "wgrad3_x3");
     if (rc) return rc;
     return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, used, accumulate, st);
   }

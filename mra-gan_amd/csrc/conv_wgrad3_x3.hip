@@ -94,11 +94,16 @@ struct Wgrad3Args {
 // 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
 // the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
 // kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
-template <int TC, int TI, int PM>
+template <int TC, int TI, int PM, int X16>
 __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
   constexpr int WC = TC / 32;             // waves along co
   constexpr bool kTr = !prec::has_lo<PM>();        // 16-bit modes: natural-order tiles + transposing reads
+  // X16: dY and X are the producers' 16-bit operand planes (bf16 / fp16 words, rounded as the
+  // staging below would round them): 8-B loads stored as they are, no conversion
+  static_assert(!X16 || kTr, "16-bit operand planes exist in the one-plane modes only");
+  constexpr int ES = X16 ? 2 : 4;         // bytes per operand element
+  using RegT = std::conditional_t<X16 != 0, uint2, float4>;
   constexpr int RBD = TC * 2, RBG = TI * 2;         // tr image row bytes (dY, X)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kStage = kTrRowsD * RBD + kTrRowsG * RBG;            // tr: bytes of one stage buffer
@@ -140,24 +145,24 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   const bool g2 = kSplitG && tid < 2 * GQ;         // second X unit (w' 16, 17) in rg2
   const int uw2 = 16 + tid / GQ;
 
-  float4 rd[kR], rg[kR], rg2[kR];
+  RegT rd[kR], rg[kR], rg2[kR];
   // dY / X through buffer descriptors: the segment part of each offset is wave-uniform (SGPR
   // soffset), the lane part fixed per thread (VGPR) — no per-load 64-bit address arithmetic
-  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * 4));
-  const __amdgpu_buffer_rsrc_t xgr = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * 4));
-  const int dlane = (uw * a.Cd + co0 + 4 * cq) * 4;
-  const int glane = ((g1 ? gw : 0) * a.Cg + ci0 + 4 * gcq) * 4;
-  const int glane2 = ((g2 ? uw2 : gw) * a.Cg + ci0 + 4 * gcq) * 4;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * ES));
+  const __amdgpu_buffer_rsrc_t xgr = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * ES));
+  const int dlane = (uw * a.Cd + co0 + 4 * cq) * ES;
+  const int glane = ((g1 ? gw : 0) * a.Cg + ci0 + 4 * gcq) * ES;
+  const int glane2 = ((g2 ? uw2 : gw) * a.Cg + ci0 + 4 * gcq) * ES;
   // Segments are 16-voxel runs of dY in (n, d, h, w) order, so a segment's dY offset is linear in
   // its index; its X offset (padded volume, shifted by (kd, kh)) is carried along with (h, d, n)
   // carries — no per-segment index arithmetic (divisions cost ~600 scalar instructions per
   // stage, the recomputed products ~100)
-  const int dseg = kSegW * a.Cd * 4;                          // dY bytes per segment
-  const int gw16 = kSegW * a.Cg * 4, grow = (Wg - a.W) * a.Cg * 4;
-  const int gplane = (Hg - a.H) * Wg * a.Cg * 4, gvol = (Dg - a.D) * Hg * Wg * a.Cg * 4;
-  const int gkdh = (kd * Hg + kh) * Wg * a.Cg * 4;
+  const int dseg = kSegW * a.Cd * ES;                         // dY bytes per segment
+  const int gw16 = kSegW * a.Cg * ES, grow = (Wg - a.W) * a.Cg * ES;
+  const int gplane = (Hg - a.H) * Wg * a.Cg * ES, gvol = (Dg - a.D) * Hg * Wg * a.Cg * ES;
+  const int gkdh = (kd * Hg + kh) * Wg * a.Cg * ES;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
-  int sxo = (((sn * Dg + sd) * Hg + sh) * Wg + sw * kSegW) * a.Cg * 4;
+  int sxo = (((sn * Dg + sd) * Hg + sh) * Wg + sw * kSegW) * a.Cg * ES;
   auto bump = [&](int& w_, int& h_, int& d_, int& xo) __attribute__((always_inline)) {
     xo += gw16;
     if (++w_ == nsw) {
@@ -176,15 +181,21 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       const int gso = __builtin_amdgcn_readfirstlane((ok ? cxo : 0) + gkdh);
       bump(cw, chh, cdd, cxo);
       // past the split's end: an out-of-range voffset reads zeros (no select on the values)
-      const buf_f32x4 dv = buf_load_16b(dyr, ok ? dlane : (int)kOobOffset, dso);
-      const buf_f32x4 gv = buf_load_16b(xgr, ok ? glane : (int)kOobOffset, gso);
-      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
-      rg[r] = make_float4(gv.x, gv.y, gv.z, gv.w);
-      // w' = 16, 17 (threads < 2·GQ; the others re-read their own unit: keeps rg2 a plain register
-      // array, a conditionally written one goes to scratch)
-      if constexpr (kSplitG) {
-        const buf_f32x4 g = buf_load_16b(xgr, ok ? glane2 : (int)kOobOffset, gso);
-        rg2[r] = make_float4(g.x, g.y, g.z, g.w);
+      if constexpr (X16) {
+        rd[r] = buf_load_8b(dyr, ok ? dlane : (int)kOobOffset, dso);
+        rg[r] = buf_load_8b(xgr, ok ? glane : (int)kOobOffset, gso);
+        if constexpr (kSplitG) rg2[r] = buf_load_8b(xgr, ok ? glane2 : (int)kOobOffset, gso);
+      } else {
+        const buf_f32x4 dv = buf_load_16b(dyr, ok ? dlane : (int)kOobOffset, dso);
+        const buf_f32x4 gv = buf_load_16b(xgr, ok ? glane : (int)kOobOffset, gso);
+        rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+        rg[r] = make_float4(gv.x, gv.y, gv.z, gv.w);
+        // w' = 16, 17 (threads < 2·GQ; the others re-read their own unit: keeps rg2 a plain register
+        // array, a conditionally written one goes to scratch)
+        if constexpr (kSplitG) {
+          const buf_f32x4 g = buf_load_16b(xgr, ok ? glane2 : (int)kOobOffset, gso);
+          rg2[r] = make_float4(g.x, g.y, g.z, g.w);
+        }
       }
     }
   };
@@ -209,13 +220,18 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
     split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
   };
   // 16-bit modes: unit (voxel w, channel quad q) → rows w·8 + r, 8 B at chunk q/2 (swizzled), half q&1
-  auto put16 = [&](char* base, auto rb_c, int w, int q, const float4 (&v)[kR]) __attribute__((always_inline)) {
+  auto put16 = [&](char* base, auto rb_c, int w, int q, const RegT (&v)[kR]) __attribute__((always_inline)) {
     constexpr int RB = decltype(rb_c)::value;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int row = w * kR + r;
-      uint2 h, l;
-      prec::split4<PM>(v[r], h, l);
+      uint2 h;
+      if constexpr (X16) {
+        h = v[r];
+      } else {
+        uint2 l;
+        prec::split4<PM>(v[r], h, l);
+      }
       *reinterpret_cast<uint2*>(base + row * RB + 16 * ((q >> 1) ^ tr_swz<RB>(row)) + 8 * (q & 1)) = h;
     }
   };
@@ -363,6 +379,24 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
+template <int TC, int TI, int PM, int X16>
+static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
+  if constexpr (X16 && prec::has_lo<PM>()) {
+    return;                                     // rejected by the caller
+  } else {
+    constexpr bool tr = !prec::has_lo<PM>();
+    constexpr bool wide = TC == 128;
+    const int lds = wide ? (tr ? kLdsTrW : kLdsW) : (tr ? kLdsTr : kLds);
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
+  }
+}
+
 int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   Wgrad3Args a{};
   a.dy = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
@@ -375,26 +409,17 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const int nsplit = (a.nseg + per - 1) / per;
   const bool wide = w3_wide(g);
   const int blocks = ((g.Cd / (wide ? 128 : kTile)) * (g.Cg / kTile) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
+  if (g.in16 && g.x3 != kPrecBf16 && g.x3 != kPrecF16) {
+    set_error("wgrad3_x3: 16-bit operand planes need the bf16 or fp16 mode");
+    return -kBadArg;
+  }
   MRAGAN_PREC_DISPATCH(g.x3, {
-    constexpr bool tr = !prec::has_lo<PM>();
     if (wide) {
-      const int lds = tr ? kLdsTrW : kLdsW;
-      static bool attr_w = false;
-      if (!attr_w) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<128, 64, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr_w = true;
-      }
-      hipLaunchKernelGGL((wgrad3_x3_kernel<128, 64, PM>), dim3(blocks), dim3(512), lds, st, a);
+      if (g.in16) launch_wgrad3<128, 64, PM, 1>(a, blocks, st);
+      else launch_wgrad3<128, 64, PM, 0>(a, blocks, st);
     } else {
-      const int lds = tr ? kLdsTr : kLds;
-      static bool attr_set = false;
-      if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<64, 64, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL((wgrad3_x3_kernel<64, 64, PM>), dim3(blocks), dim3(256), lds, st, a);
+      if (g.in16) launch_wgrad3<64, 64, PM, 1>(a, blocks, st);
+      else launch_wgrad3<64, 64, PM, 0>(a, blocks, st);
     }
     return nsplit;
   })

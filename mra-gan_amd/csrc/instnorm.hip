@@ -79,6 +79,17 @@ __device__ void in_finalize_group(const double* __restrict__ part, const InShape
   }
 }
 
+// four values → the 16-bit operand words a bf16 (mode 2) / fp16 (mode 3) MFMA consumer would
+// round them to (RNE, as prec.h's staging conversion): the 16-bit operand plane of a tensor
+__device__ __forceinline__ uint2 f4_op16(float4 v, int mode) {
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+  const f32x4_t f = {v.x, v.y, v.z, v.w};
+  if (mode == 3) return __builtin_bit_cast(uint2, __builtin_convertvector(f, f16x4_t));
+  return __builtin_bit_cast(uint2, __builtin_convertvector(f, bf16x4_t));
+}
+
 __device__ __forceinline__ float4 f4_act(float4 v, int act) {
   return make_float4(act_fwd(v.x, act), act_fwd(v.y, act), act_fwd(v.z, act), act_fwd(v.w, act));
 }
@@ -143,10 +154,11 @@ __global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restri
 // ---- forward apply: y (padded by ypad) = act((x − μ)·rstd) + resid(interior of rpad-padded) --
 // One output row (n, dp, hp) of the padded y per block iteration; source row and the residual
 // row are fixed per row, each thread walks its float4s (q fixed per thread).
+// y (fp32) and / or y16 (the 16-bit operand plane, precision mode `mode`) may be written
 __global__ void __launch_bounds__(256) in_apply_kernel(const float* __restrict__ x, InShape s, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, int act,
                                                        const float* __restrict__ resid, int rpad, float* __restrict__ y,
-                                                       int ypad) {
+                                                       int ypad, uint2* __restrict__ y16, int mode) {
   const int CQ = s.C / 4, tid = threadIdx.x, q = tid % CQ, WS = 256 / CQ;
   const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
   const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad;
@@ -163,6 +175,7 @@ __global__ void __launch_bounds__(256) in_apply_kernel(const float* __restrict__
     const float4* xrow = xv + (size_t)((n * s.D + sd) * s.H + sh) * s.W * CQ;
     const float4* rrow = resid ? rv + ((size_t)((n * Dr + sd + rpad) * Hr + sh + rpad) * Wr + rpad) * CQ : nullptr;
     float4* yrow = yv + (size_t)row * rowq + q;
+    uint2* y16row = y16 + (size_t)row * rowq + q;
     for (int wp = wt; wp < Wp; wp += WS) {
       const int sw = min(max(wp - ypad, 0), s.W - 1);
       float4 v = xrow[sw * CQ + q];
@@ -172,7 +185,8 @@ __global__ void __launch_bounds__(256) in_apply_kernel(const float* __restrict__
         const float4 r = rrow[sw * CQ + q];
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
       }
-      yrow[wp * CQ] = v;
+      if (y) yrow[wp * CQ] = v;
+      if (y16) y16row[wp * CQ] = f4_op16(v, mode);
     }
   }
 }
@@ -308,6 +322,7 @@ __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape 
     const float4 c0 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[0];   // (mg0, mgx0, mg1, mgx1)
     const float4 c1 = reinterpret_cast<const float4*>(coef + 2 * (n * s.C + 4 * q))[1];
     float4* out = dx + (size_t)rr * s.W * CQ + q;
+    uint2* out16 = reinterpret_cast<uint2*>(a.dx16) + (size_t)rr * s.W * CQ + q;
     float4* gout = a.g_out ? reinterpret_cast<float4*>(a.g_out) + (size_t)rr * s.W * CQ + q : nullptr;
     for (int w = wt; w < s.W; w += WS) {
       float4 g, xh, graw;
@@ -318,7 +333,8 @@ __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape 
       o.y = row.rs.y * (g.y - c0.z - xh.y * c0.w);
       o.z = row.rs.z * (g.z - c1.x - xh.z * c1.y);
       o.w = row.rs.w * (g.w - c1.z - xh.w * c1.w);
-      out[w * CQ] = o;
+      if (dx) out[w * CQ] = o;
+      if (a.dx16) out16[w * CQ] = f4_op16(o, a.mode16);
     }
   }
 }
@@ -366,7 +382,7 @@ static int grid_for(int64_t work, int cap = 8192) {
 }
 
 int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
-                 float* rstd, void* ws, size_t ws_bytes, hipStream_t st) {
+                 float* rstd, void* ws, size_t ws_bytes, hipStream_t st, void* y16, int mode16) {
   MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm: C=%d must be a multiple of 4 (≤1024)", s.C);
   MRAGAN_CHECK_ARG(in_fits(s, ypad > rpad ? ypad : rpad), "instnorm: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
   if (s.S() <= 1) {
@@ -384,14 +400,15 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   if ((rc = check_launch("in_finalize"))) return rc;
   const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
   hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
-                     rpad, y, ypad);
+                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
   return check_launch("in_apply");
 }
 
 // Forward from statistics partials a producer conv already accumulated (conv_brick_x3 epilogue:
 // [N][chunks][C][2] = Σy, Σy² per brick): the statistics pass is skipped.
 int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
-                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st) {
+                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st, void* y16,
+                          int mode16) {
   MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm: C=%d must be a multiple of 4 (≤1024)", s.C);
   MRAGAN_CHECK_ARG(in_fits(s, ypad > rpad ? ypad : rpad), "instnorm: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
   MRAGAN_CHECK_ARG(part && chunks > 0, "instnorm_fwd_partials: no partials");
@@ -405,8 +422,8 @@ int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act
   if (rc) return rc;
   const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
   hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
-                     rpad, y, ypad);
-  return check_launch("in_apply");
+                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
+  return check_launch(y16 ? "in_apply(op16)" : "in_apply");
 }
 
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -436,7 +453,7 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
     case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
     default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
   }
-  return check_launch("in_bwd_apply");
+  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
 }
 
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st) {

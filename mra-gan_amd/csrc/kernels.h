@@ -22,6 +22,7 @@ struct IgemmArgs {
   double* in_part;  // optional: per-(instance, brick, channel) Σy, Σy² of the output (brick_x3 only)
   int* in_chunks;   // set to the bricks per instance when in_part was filled, else 0
   int shell;        // conv_igemm_x3 only: the 6 shell-face classes of a full (k3 s1 p0) transposed conv
+  int x16;          // x is a 16-bit operand plane (bf16 / fp16 words of the precision mode), not fp32
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
@@ -44,6 +45,7 @@ struct BrickArgs {
   double* part;     // optional InstanceNorm statistics partials [N][nbd·nbh·nbw][ny][2] (Σy, Σy²)
   int ye;           // output embedding: y is [N][Yd][Yh][Yw][ny], output voxel o written at o + ye
   int Yd, Yh, Yw;
+  int x16;          // x is a 16-bit operand plane (conv_brick_x3 in the bf16 / fp16 modes)
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st, bool interior = false);
@@ -91,6 +93,7 @@ struct WgradArgs {
   int64_t chunk;   // set by conv_wgrad
   int splits;
   int x3;          // precision mode (prec.h): 0 f32; 1 bf16x3 / 2 bf16 / 3 fp16 MFMA (Cd, Cg multiples of 32)
+  int in16;        // D and G are 16-bit operand planes (wgrad3_x3 in the bf16 / fp16 modes only)
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
 // bf16x3 weight gradient of valid k3 s1 convs on padded inputs, 3 kw taps per block (conv_wgrad3_x3.hip)
@@ -123,14 +126,18 @@ struct InShape {
 struct InBwdArgs {
   const float* x; const float* mean; const float* rstd;
   const float* dy; int dypad; const float* dy_add; int act;
-  float* dx;
+  float* dx;           // fp32 dx, or null when only dx16 is wanted
   float* g_out;        // optional: g = fold(dy) + dy_add before act' (the ResnetBlock's input gradient)
+  void* dx16;          // optional: dx as the 16-bit operand plane of precision mode mode16 (2 bf16, 3 fp16)
+  int mode16;
 };
+// y and / or y16 (the 16-bit operand plane of y in precision mode mode16) are written
 int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad, float* mean,
-                 float* rstd, void* ws, size_t ws_bytes, hipStream_t st);
+                 float* rstd, void* ws, size_t ws_bytes, hipStream_t st, void* y16 = nullptr, int mode16 = 0);
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st);
 int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
-                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st);
+                          float* mean, float* rstd, const double* part, int chunks, hipStream_t st, void* y16 = nullptr,
+                          int mode16 = 0);
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C);
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st);
 size_t instnorm_running_entry_bytes();

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -73,6 +73,15 @@ SIGNATURES = {
     "mragan_crop_patches": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
     "mragan_patch_gather": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
     "mragan_patch_combine": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+    # ABI 11: 16-bit operand planes (bf16 / fp16 modes)
+    "mragan_instnorm_fwd_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, i32, vp, vp, vp, sz, vp]),
+    "mragan_instnorm_fwd_partials_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, i32, vp, vp, vp, i32,
+                                                vp]),
+    "mragan_instnorm_bwd_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, sz, vp]),
+    "mragan_conv3d_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp, sz,
+                                 vp, sz, vp, vp]),
+    "mragan_conv3d_wgrad_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
+                                       sz, vp]),
 }
 
 _lock = threading.Lock()

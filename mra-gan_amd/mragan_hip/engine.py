@@ -28,6 +28,9 @@ from ._lib import call
 # A/B switch: MRAGAN_NO_IN_STATS=1 runs the ResnetBlock InstanceNorms with their own statistics
 # pass instead of the brick conv's epilogue partials
 _NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") or "0"))
+# A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
+# 16-bit operand planes, ABI 11)
+_NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
 
 IN_MOMENTUM = 0.1
 
@@ -113,6 +116,28 @@ class ConvLayer:
         y, chunks = ops.conv3d_in_stats(x, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
         return y, part, chunks
 
+    def forward_in_stats_op16(self, x16):
+        """forward_in_stats on the operand plane of the input (brick kernel, 16-bit modes)."""
+        N, D, H, W, _ = x16.shape
+        osp = self.out_spatial(D, H, W)
+        part = None if _NO_IN_STATS else ops.in_partials_buffer(N, osp, self.cout, x16.device)
+        y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
+        return y, part, chunks
+
+    def dgrad_op16(self, dy16, in_spatial):
+        """dgrad from the operand plane of dy (brick kernel, 16-bit modes)."""
+        return ops.conv3d_op16(dy16, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial, self.ws_bwd,
+                               transposed=not self.transposed)[0]
+
+    def wgrad_op16(self, x16, dy16, accumulate=True):
+        """wgrad of a forward-form conv from the operand planes of X and dY (wgrad3, 16-bit modes)."""
+        ops.conv3d_wgrad_op16(dy16, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
+
+    def op16_ok(self, W):
+        """Can this k3 s1 conv run on operand planes (brick both ways, wgrad3) at output width W?"""
+        return (not self.transposed and self.k == 3 and self.s == 1 and self.ws_fwd is not None
+                and self.ws_bwd is not None and self.cin % 64 == 0 and self.cout % 64 == 0 and W % 16 == 0)
+
     def dgrad(self, dy, in_spatial):
         """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
         return ops.conv3d(dy, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial,
@@ -151,7 +176,8 @@ class StageCtx:
     h1: torch.Tensor = None
     mean1: torch.Tensor = None
     rstd1: torch.Tensor = None
-    z1: torch.Tensor = None         # block: relu(IN(h1)) padded by 1
+    z1: torch.Tensor = None         # block: relu(IN(h1)) padded by 1 (its operand plane on the op16 path)
+    inp16: torch.Tensor = None      # block on the op16 path: the operand plane of inp
 
 
 @dataclass
@@ -222,28 +248,60 @@ class NetPlan:
         ctx = NetCtx(N=N, spatial=(D, H, W))
         first = self.stages[0]
         cur = ops.rpad(x, first.prepad) if first.prepad else x
+        cur16 = None            # operand plane of cur (16-bit modes, ResnetBlock inputs)
+        op16 = self._op16_active()
         for i, st in enumerate(self.stages):
-            sc = StageCtx(inp=cur)
+            sc = StageCtx(inp=cur, inp16=cur16)
             ypad = self._next_prepad(i)
+            # a ResnetBlock next: its input's operand plane beside the fp32 tensor (the skip add)
+            want16 = op16 and i + 1 < len(self.stages) and self.stages[i + 1].kind == "block"
+            out16 = None
             if st.kind == "block":
-                # the brick conv accumulates its InstanceNorm's statistics in its epilogue
-                sc.h1, part, chunks = st.conv1.forward_in_stats(cur)
-                sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd(sc.h1, act="relu", ypad=1, part=part, chunks=chunks)
-                sc.h, part, chunks = st.conv2.forward_in_stats(sc.z1)
-                sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1, part=part,
-                                                            chunks=chunks)
+                if cur16 is not None:
+                    # 16-bit operand planes (ABI 11): conv1 reads the block input's plane, IN1 writes
+                    # only the plane of relu(IN(h1)) (conv2's operand), IN2 both copies of the output
+                    sc.h1, part, chunks = st.conv1.forward_in_stats_op16(cur16)
+                    _, sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd_op16(sc.h1, act="relu", ypad=1, part=part,
+                                                                          chunks=chunks)
+                    sc.h, part, chunks = st.conv2.forward_in_stats_op16(sc.z1)
+                    if want16:
+                        sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=None, ypad=ypad, resid=cur,
+                                                                                rpad=1, part=part, chunks=chunks,
+                                                                                want_f32=True)
+                    else:
+                        sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1,
+                                                                    part=part, chunks=chunks)
+                else:
+                    # the brick conv accumulates its InstanceNorm's statistics in its epilogue
+                    sc.h1, part, chunks = st.conv1.forward_in_stats(cur)
+                    sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd(sc.h1, act="relu", ypad=1, part=part, chunks=chunks)
+                    sc.h, part, chunks = st.conv2.forward_in_stats(sc.z1)
+                    sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1, part=part,
+                                                                chunks=chunks)
             else:
                 bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
                 if st.norm is not None:
                     sc.h = st.conv.forward(cur)
-                    sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad)
+                    if want16 and self._op16_blocks_ok(sc.h.shape[3]):
+                        sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad,
+                                                                                want_f32=True)
+                    else:
+                        sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad)
                 else:
                     sc.h = st.conv.forward(cur, bias=bias, act=st.act)     # activated output
                     sc.out = ops.rpad(sc.h, ypad) if ypad else sc.h
             ctx.stages.append(sc)
-            cur = sc.out
+            cur, cur16 = sc.out, out16
         ctx.out = cur
         return ctx
+
+    def _op16_active(self):
+        """16-bit operand planes for the ResnetBlock section: bf16 / fp16 mode, not switched off."""
+        return not _NO_OP16 and ops.op16_dtype() is not None
+
+    def _op16_blocks_ok(self, W):
+        """Every ResnetBlock conv can run on operand planes at block width W."""
+        return all(st.conv1.op16_ok(W) and st.conv2.op16_ok(W) for st in self.stages if st.kind == "block")
 
     # ---- backward ----------------------------------------------------------------------
     def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,
@@ -257,6 +315,23 @@ class NetPlan:
         for i in range(last, -1, -1):
             st, sc = self.stages[i], ctx.stages[i]
             want_dgrad = i > 0 or need_input_grad
+            if st.kind == "block" and sc.inp16 is not None:
+                # 16-bit operand planes: the IN backwards write dY only as planes (the convs' sole use)
+                if gpad == 0 and gadd is None:
+                    G = g
+                    dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                else:
+                    G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
+                    dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
+                if need_wgrad:
+                    st.conv2.wgrad_op16(sc.z1, dh2)
+                dz1 = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4])
+                dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
+                if need_wgrad:
+                    st.conv1.wgrad_op16(sc.inp16, dh1)
+                g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
+                gpad, gadd = 1, G
+                continue
             if st.kind == "block":
                 if gpad == 0 and gadd is None:
                     G = g

@@ -363,6 +363,124 @@ def instnorm_bwd(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: to
     return out
 
 
+# ---- 16-bit operand planes (bf16 / fp16 modes, ABI 11) ----------------------------------------
+# The plane of an fp32 tensor holds the bf16 (fp16) words every MFMA convolution of the mode rounds
+# it to, as a torch.bfloat16 (float16) tensor of the same shape; see include/mragan_hip.h.
+
+def op16_dtype() -> Optional[torch.dtype]:
+    """dtype of the operand planes in the current precision mode (None in the fp32-grade modes)."""
+    return {"bf16": torch.bfloat16, "fp16": torch.float16}.get(get_conv_precision())
+
+
+def _check16(t: torch.Tensor, name: str):
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError(f"{name}: 16-bit operand planes need the bf16 or fp16 precision mode")
+    if not t.is_cuda or t.dtype != dt or not t.is_contiguous() or t.dim() != 5:
+        raise ValueError(f"{name}: expected a contiguous 5-d {dt} device tensor, got {t.dtype} {tuple(t.shape)}")
+
+
+def instnorm_fwd_op16(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch.Tensor] = None, rpad: int = 0,
+                      part: Optional[torch.Tensor] = None, chunks: int = 0, want_f32: bool = False):
+    """instnorm_fwd writing the output's operand plane (and the fp32 output too when want_f32).
+    Returns (out or None, out16, mean, rstd)."""
+    _check(x, "instnorm.x")
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError("instnorm_fwd_op16: 16-bit operand planes need the bf16 or fp16 precision mode")
+    N, D, H, W, C = x.shape
+    shp = (N, D + 2 * ypad, H + 2 * ypad, W + 2 * ypad, C)
+    out = torch.empty(shp, device=x.device, dtype=torch.float32) if want_f32 else None
+    out16 = torch.empty(shp, device=x.device, dtype=dt)
+    mean = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    rstd = torch.empty((N, C), device=x.device, dtype=torch.float32)
+    if resid is not None:
+        _check(resid, "instnorm.resid")
+        if tuple(resid.shape) != (N, D + 2 * rpad, H + 2 * rpad, W + 2 * rpad, C):
+            raise ValueError("instnorm: residual shape mismatch")
+    if part is not None and chunks > 0:
+        fn = lambda: call("mragan_instnorm_fwd_partials_op16", _ptr(x), N, D, H, W, C, _ptr(out), _ptr(out16), ypad,
+                          ACT[act], _ptr(resid), rpad, _ptr(mean), _ptr(rstd), _ptr(part), chunks, _stream())
+    else:
+        nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+        ws = WS.get(nbytes)
+        fn = lambda: call("mragan_instnorm_fwd_op16", _ptr(x), N, D, H, W, C, _ptr(out), _ptr(out16), ypad, ACT[act],
+                          _ptr(resid), rpad, _ptr(mean), _ptr(rstd), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad} op16",
+                        bytes=4.0 * x.numel() * (2 if resid is not None else 1) + out16.numel() * (6 if want_f32 else 2)),
+           fn)
+    return out, out16, mean, rstd
+
+
+def instnorm_bwd_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int = 0,
+                      dy_add: Optional[torch.Tensor] = None, act=None, g_out: Optional[torch.Tensor] = None):
+    """instnorm_bwd writing dx only as its operand plane (returned); g_out as in instnorm_bwd."""
+    _check(x, "instnorm_bwd.x")
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError("instnorm_bwd_op16: 16-bit operand planes need the bf16 or fp16 precision mode")
+    N, D, H, W, C = x.shape
+    if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
+        raise ValueError(f"instnorm_bwd: dy shape {tuple(dy.shape)} does not match pad {dypad}")
+    if g_out is not None:
+        _check(g_out, "instnorm_bwd.g_out")
+        if tuple(g_out.shape) != tuple(x.shape):
+            raise ValueError("instnorm_bwd: g_out shape mismatch")
+    dx16 = torch.empty(x.shape, device=x.device, dtype=dt)
+    nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_instnorm_bwd_op16", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad,
+                      _ptr(dy_add), ACT[act], _ptr(dx16), _ptr(g_out), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad} op16",
+                        bytes=4.0 * (x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                     + (x.numel() if g_out is not None else 0)) + 2.0 * x.numel()), fn)
+    return dx16
+
+
+def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
+                wsplit: torch.Tensor, part: Optional[torch.Tensor] = None, transposed: bool = False):
+    """conv3d (pre-split weights, no bias / act) on the operand plane x16 of its input (the k3 s1
+    brick kernel); with `part` also the InstanceNorm statistics partials.  Returns (out, chunks)."""
+    _check16(x16, "conv3d_op16.x16")
+    N, Di, Hi, Wi, cin = x16.shape
+    Do, Ho, Wo = out_spatial
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    if wsplit is None or wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("conv3d_op16: wsplit missing or its size does not match the packed weight")
+    if part is not None and (part.dtype != torch.float64 or not part.is_cuda):
+        raise ValueError("conv3d_op16: part must be a float64 device tensor")
+    out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
+    chunks = _ct.c_int(0)
+    fn = lambda: call("mragan_conv3d_op16", _ptr(x16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), cout, k, s, p,
+                      _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(part),
+                      0 if part is None else part.numel() * 8, None if part is None else _ct.byref(chunks), _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
+    return out, chunks.value
+
+
+def conv3d_wgrad_op16(dense16: torch.Tensor, gathered16: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
+                      accumulate: bool) -> torch.Tensor:
+    """conv3d_wgrad on the operand planes of dense and gathered (the k3 s1 valid weight gradient)."""
+    _check16(dense16, "wgrad_op16.dense")
+    _check16(gathered16, "wgrad_op16.gathered")
+    N, Dd, Hd, Wd, Cd = dense16.shape
+    Ng, Dg, Hg, Wg, Cg = gathered16.shape
+    if Ng != N:
+        raise ValueError("wgrad: batch mismatch")
+    if dw.numel() != Cd * Cg * k ** 3 or not dw.is_contiguous():
+        raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
+    nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_conv3d_wgrad_op16", _ptr(dense16), N, Dd, Hd, Wd, Cd, _ptr(gathered16), Dg, Hg, Wg, Cg,
+                      k, s, p, _ptr(dw), int(accumulate), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
+                        flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)
+    return dw
+
+
 def rpad(x: torch.Tensor, p: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _check(x, "rpad.x")
     N, D, H, W, C = x.shape

@@ -449,6 +449,104 @@ def test_brick_in_stats_partials(x3, N, C, S):
     assert rel(z, z_ref) < 1e-6
 
 
+@pytest.fixture(params=["bf16", "fp16"])
+def op16(ops, request):
+    """The two modes with 16-bit operand planes (ABI 11)."""
+    ops.set_conv_precision(request.param)
+    yield ops
+    ops.set_conv_precision("f32")
+
+
+def _presplit(ops, w, C_in, C_out, transposed_pack):
+    wsplit = torch.empty(w.numel(), device="cuda", dtype=torch.float32)
+    base = 4 if ops.get_conv_precision() == "fp16" else 2
+    ops.pack_weight(w.float().cuda().contiguous(), C_out, C_in, 27, base + int(transposed_pack), wsplit)
+    return wsplit
+
+
+@pytest.mark.parametrize("N,C,S,ypad,act,resid", [(2, 128, 16, 1, "relu", False), (1, 64, 9, 1, None, True),
+                                                  (3, 64, 7, 0, "relu", True)])
+def test_op16_instnorm_fwd_planes(op16, N, C, S, ypad, act, resid):
+    """ABI 11: the InstanceNorm forward's operand plane is exactly its fp32 output rounded RNE to
+    the mode's 16-bit type (torch's .to() rounds RNE); the fp32 copy is bit-identical to the fp32
+    entry's; the statistics-pass and the brick-partials forms both."""
+    ops = op16
+    g = torch.Generator().manual_seed(N + C + S)
+    x = ndhwc(torch.randn(N, C, S, S + 1, S, generator=g).float()).cuda()
+    r = ndhwc(torch.randn(N, C, S + 2, S + 3, S + 2, generator=g).float()).cuda() if resid else None
+    y_ref, m_ref, s_ref = ops.instnorm_fwd(x, act=act, ypad=ypad, resid=r, rpad=1 if resid else 0)
+    y, y16, m, rs = ops.instnorm_fwd_op16(x, act=act, ypad=ypad, resid=r, rpad=1 if resid else 0, want_f32=True)
+    assert torch.equal(y, y_ref) and torch.equal(m, m_ref) and torch.equal(rs, s_ref)
+    assert y16.dtype == ops.op16_dtype() and torch.equal(y16, y_ref.to(ops.op16_dtype()))
+    none, y16b, _, _ = ops.instnorm_fwd_op16(x, act=act, ypad=ypad, resid=r, rpad=1 if resid else 0)
+    assert none is None and torch.equal(y16b, y16)
+
+
+@pytest.mark.parametrize("C,dypad,act,with_g", [(128, 1, None, True), (128, 1, "relu", False), (64, 0, "relu", False)])
+def test_op16_instnorm_bwd_plane(op16, C, dypad, act, with_g):
+    """ABI 11: the InstanceNorm backward's dx plane = its fp32 dx rounded RNE; g_out unchanged."""
+    ops = op16
+    g = torch.Generator().manual_seed(C + dypad)
+    N, S = 2, 9
+    x = ndhwc(torch.randn(N, C, S, S, S + 1, generator=g).float()).cuda()
+    _, mean, rstd = ops.instnorm_fwd(x, act=act)
+    dy = ndhwc(torch.randn(N, C, S + 2 * dypad, S + 2 * dypad, S + 1 + 2 * dypad, generator=g).float()).cuda()
+    add = ndhwc(torch.randn(N, C, S, S, S + 1, generator=g).float()).cuda()
+    G_ref = torch.empty_like(x)
+    dx_ref = ops.instnorm_bwd(x, mean, rstd, dy, dypad, add, act=act, g_out=G_ref)
+    G = torch.full_like(x, float("nan")) if with_g else None
+    dx16 = ops.instnorm_bwd_op16(x, mean, rstd, dy, dypad, add, act=act, g_out=G)
+    assert torch.equal(dx16, dx_ref.to(ops.op16_dtype()))
+    if with_g:
+        assert torch.equal(G, G_ref)
+
+
+@pytest.mark.parametrize("N,C,S,W", [(2, 128, 16, 16), (1, 64, 9, 16), (1, 128, 5, 32)])
+def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
+    """ABI 11: the brick forward (with its InstanceNorm partials), the whole-grid data gradient and
+    the k3 s1 weight gradient on operand planes equal the same kernels on the fp32 tensors in the
+    same mode bit for bit (the fp32 path rounds each operand to the very words the planes hold)."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 11 + C + S)
+    x = ndhwc(torch.randn(N, C, S + 2, S + 2, W + 2, generator=g).float()).cuda()     # padded block input
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_f, wp_b = pack(ops, w, False, False), pack(ops, w, False, True)
+    ws_f, ws_b = _presplit(ops, w, C, C, False), _presplit(ops, w, C, C, True)
+    osp = (S, S, W)
+    part_ref = ops.in_partials_buffer(N, osp, C, "cuda")
+    y_ref, ch_ref = ops.conv3d_in_stats(x, wp_f, C, 3, 1, 0, osp, ws_f, part_ref)
+    part = ops.in_partials_buffer(N, osp, C, "cuda")
+    y, ch = ops.conv3d_op16(x.to(dt), wp_f, C, 3, 1, 0, osp, ws_f, part)
+    assert ch == ch_ref > 0
+    assert torch.equal(y, y_ref)
+    n = N * ch * C * 2
+    assert torch.equal(part[:n], part_ref[:n])
+    dy = ndhwc(torch.randn(N, C, S, S, W, generator=g).float()).cuda()
+    dx_ref = ops.conv3d(dy, wp_b, C, 3, 1, 0, (S + 2, S + 2, W + 2), transposed=True, wsplit=ws_b)
+    dx, _ = ops.conv3d_op16(dy.to(dt), wp_b, C, 3, 1, 0, (S + 2, S + 2, W + 2), ws_b, transposed=True)
+    assert torch.equal(dx, dx_ref)
+    gw_ref = torch.empty(C * C * 27, device="cuda")
+    ops.conv3d_wgrad(dy, x, 3, 1, 0, gw_ref, False)
+    gw = torch.full_like(gw_ref, float("nan"))
+    ops.conv3d_wgrad_op16(dy.to(dt), x.to(dt), 3, 1, 0, gw, False)
+    assert torch.equal(gw, gw_ref)
+    # and against fp64 on the rounded operands (the mode's definition)
+    gw64 = F.conv3d(ncdhw(x.to(dt).double().cpu()).transpose(0, 1), ncdhw(dy.to(dt).double().cpu()).transpose(0, 1))
+    assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
+
+
+def test_op16_rejected_outside_16bit_modes(ops):
+    from mragan_hip import MraganError
+    ops.set_conv_precision("bf16x3")
+    try:
+        x = torch.zeros(1, 4, 4, 4, 64, device="cuda")
+        with pytest.raises((MraganError, ValueError)):
+            ops.instnorm_fwd_op16(x)
+    finally:
+        ops.set_conv_precision("f32")
+
+
 def test_instnorm_single_voxel_raises(ops):
     from mragan_hip import MraganError
     with pytest.raises(MraganError, match="more than 1 spatial element"):

@@ -75,7 +75,20 @@ def main():
     w_g = [rnd(c4 * c4 * 27) for _ in range(18)]
     pk = [(w, c4, c4, 27, tr, torch.empty_like(w)) for w in w_g for tr in (0, 1, 2, 3)]
     pack_tab = ops.PackTable()
+    # 16-bit operand planes (ABI 11; bf16 / fp16 modes): the res-block convs on planes
+    dt16 = ops.op16_dtype()
+    if dt16 is not None:
+        x_res16, dy_res16 = x_res.to(dt16), dy_res.to(dt16)
+        ws_res_f = torch.empty(w_res.numel(), device=dev)
+        ws_res_b = torch.empty(w_res.numel(), device=dev)
+        base = 4 if args.precision == "fp16" else 2
+        ops.pack_weight(w_res, c4, c4, 27, base, ws_res_f)
+        ops.pack_weight(w_res, c4, c4, 27, base + 1, ws_res_b)
+        part_res = ops.in_partials_buffer(N, (s4, s4, s4), c4, dev)
     table = {
+        "res_fwd16": lambda: ops.conv3d_op16(x_res16, w_res, c4, 3, 1, 0, (s4, s4, s4), ws_res_f, part_res),
+        "res_dgrad16": lambda: ops.conv3d_op16(dy_res16, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, ws_res_b, transposed=True),
+        "res_wgrad16": lambda: ops.conv3d_wgrad_op16(dy_res16, x_res16, 3, 1, 0, gw_res, False),
         "pack_g": lambda: pack_tab.run(pk),
         "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
@@ -101,7 +114,7 @@ def main():
                                              act="relu"),
         "in_bwd": lambda: ops.instnorm_bwd(x_in, *ops.instnorm_fwd(x_in, act="relu")[1:], dy_in, 3, None, act="relu"),
     }
-    names = list(table) if args.ops == "all" else args.ops.split(",")
+    names = [n for n in table if not n.endswith("16")] if args.ops == "all" else args.ops.split(",")
     for name in names:
         fn = table[name]
         fn()

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-KB="python3 $R/tools/kbench.py --ops $OPS --reps 5 --precision bf16x3"
+KB="python3 $R/tools/kbench.py --ops $OPS --reps 5 --precision ${PREC:-bf16x3} --N ${KN:-4}"
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS --output-format csv -d "$O/p1" -o run -- $KB > "$O/p1.log" 2>&1
 timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv -d "$O/p2" -o run -- $KB > "$O/p2.log" 2>&1
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/p3" -o run -- $KB > "$O/p3.log" 2>&1
