@@ -179,6 +179,23 @@ int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, 
 int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
                              int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
                              size_t ws_bytes, void* stream);
+/* InstanceNorm backward statistics in the data-gradient epilogue (ABI 11).  In a
+ * ResnetBlock (networks3D.py:241-257) conv2's input is z1 = relu(IN(h1)) padded by 1, so the IN
+ * backward of h1 reads g = fold(dz1)·relu'(x̂) with dz1 = conv2's padded data gradient.  Its two
+ * statistics are sums over the padded grid: Σ_i g_i = Σ_p dz_p·act'(x̂_c(p)), Σ_i g_i·x̂_i =
+ * Σ_p dz_p·act'(x̂_c(p))·x̂_c(p) (c = the fold's clamp).  mragan_conv3d_op16_dgrad_in_stats is the
+ * whole-grid data gradient (k3 s1 p0, transposed form, output (Di+2)·(Hi+2)·(Wi+2)) from the
+ * plane dy16 that also leaves these per-brick partials, reading x_in (h1, [N][Di][Hi][Wi][cout]
+ * fp32) and its IN statistics in the epilogue; mragan_instnorm_bwd_partials_op16 is
+ * mragan_instnorm_bwd_op16 from them (finalize + apply: no statistics pass over dy and x). */
+int mragan_conv3d_op16_dgrad_in_stats(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                                      const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
+                                      const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                      int* chunks, void* stream);
+int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,
+                                      int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
+                                      float* g_out, const double* part, int chunks, void* ws, size_t ws_bytes,
+                                      void* stream);
 
 /* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
  * entry listing the per-instance statistics of the reference's sequential calls in call order. */

@@ -161,6 +161,38 @@ int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, 
   return conv_igemm(a, static_cast<hipStream_t>(stream));
 }
 
+int mragan_conv3d_op16_dgrad_in_stats(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                      const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
+                                      const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                      int* chunks, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(dy16 && w && wsplit && y && x_in && mean && rstd && part && chunks,
+                   "conv3d_op16_dgrad_in_stats: null pointer");
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && !thin_side(cin, cout),
+                   "conv3d_op16_dgrad_in_stats: bad shape");
+  MRAGAN_CHECK_ARG(act == kActNone || act == kActRelu || act == kActLrelu, "conv3d_op16_dgrad_in_stats: act %d", act);
+  const int Do = Di + 2, Ho = Hi + 2, Wo = Wi + 2;
+  const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+  MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_op16_dgrad_in_stats: partials %zu < %zu bytes", part_bytes, bound);
+  *chunks = 0;
+  IgemmArgs a{static_cast<const float*>(dy16), w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, 3, 1, 0, 1, kActNone,
+              1, g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
+  a.x16 = 1;
+  a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act;
+  return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,
+                                      int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
+                                      float* g_out, const double* part, int chunks, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx16 && part && ws, "instnorm_bwd_partials_op16: null pointer");
+  MRAGAN_CHECK_ARG(!g_out || (g_out != dy && g_out != dy_add), "instnorm_bwd_partials_op16: g_out aliases an operand");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, nullptr, g_out, dx16, g_conv_precision};
+  return instnorm_bwd_partials(a, InShape{N, D, H, W, C}, part, chunks, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
 int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
                              int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
                              size_t ws_bytes, void* stream) {

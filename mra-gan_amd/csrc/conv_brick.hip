@@ -395,6 +395,12 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   a.act = g.act;
   a.ye = 0; a.Yd = g.Do; a.Yh = g.Ho; a.Yw = g.Wo;
   a.x16 = g.x16;
+  if (g.bs_x) {
+    // backward statistics (see BrickArgs::sx): only for the whole-grid data gradient (output = input + 2)
+    MRAGAN_CHECK_ARG(g.in_part && g.trans && g.Do == g.Di + 2 && g.Ho == g.Hi + 2 && g.Wo == g.Wi + 2 && g.bs_mean &&
+                     g.bs_rstd && !interior, "conv_brick: backward statistics need the whole-grid data gradient");
+    a.sx = g.bs_x; a.smean = g.bs_mean; a.srstd = g.bs_rstd; a.sact = g.bs_act;
+  }
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
   a.flip = g.trans ? 1 : 0;
   a.p = g.trans ? g.k - 1 - g.p : g.p;
@@ -413,6 +419,7 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, c.bm, a.rowvox);
   MRAGAN_CHECK_ARG(!g.x16 || conv_brick_x3_active(g), "conv_brick: a 16-bit operand plane needs the 16-bit MFMA brick");
+  MRAGAN_CHECK_ARG(!g.bs_x || conv_brick_x3_active(g), "conv_brick: backward statistics need the 16-bit MFMA brick");
   if (conv_brick_x3_active(g)) {
     if (g.in_part) {
       a.part = g.in_part;

@@ -108,6 +108,8 @@ conv_brick_x3_kernel(BrickArgs a) {
   // residue in every chunk
   constexpr int kPF = 9;
   constexpr int kP = 18;                             // unrolled period: ring slots compile-time
+  constexpr int kAD = prec::has_lo<PM>() ? 1 : 2;    // A-fragment read distance (steps)
+  static_assert(kP % (kAD + 1) == 0, "A ring period");
   static_assert(kSteps % kP == 0 && kP % kPF == 0 && kP % 9 == 0 && kHD < kPF, "step period");
 
   constexpr int kRow = row_bytes<PM>();
@@ -115,6 +117,7 @@ conv_brick_x3_kernel(BrickArgs a) {
   char* halo_buf = smem;                                                // [2][HMAX][kRow]
   int* out_off = reinterpret_cast<int*>(smem + 2 * HMAX * kRow);       // [BM]
   int* hoff = out_off + BM;                                            // [HMAX]
+  int* xoff = hoff + HMAX;                                             // [BM] (backward statistics)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * TM * 32, wn0 = (wave % WN) * TN * 32;
@@ -139,7 +142,15 @@ conv_brick_x3_kernel(BrickArgs a) {
     if (v >= 0) {
       const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
       const int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
-      if (od < a.Do && oh < a.Ho && ow < a.Wo) off = (int)((((int64_t)nb * a.Yd + od + a.ye) * a.Yh + oh + a.ye) * a.Yw + ow + a.ye);
+      if (od < a.Do && oh < a.Ho && ow < a.Wo) {
+        off = (int)((((int64_t)nb * a.Yd + od + a.ye) * a.Yh + oh + a.ye) * a.Yw + ow + a.ye);
+        // backward statistics: the interior voxel this padded output folds into (clamp of o − 1)
+        if (a.sx) {
+          const int cd = min(max(od - 1, 0), a.Do - 3), ch = min(max(oh - 1, 0), a.Ho - 3),
+                    cw = min(max(ow - 1, 0), a.Wo - 3);
+          xoff[r] = (int)((((int64_t)nb * (a.Do - 2) + cd) * (a.Ho - 2) + ch) * (a.Wo - 2) + cw);
+        }
+      }
     }
     out_off[r] = off;
   }
@@ -223,7 +234,9 @@ conv_brick_x3_kernel(BrickArgs a) {
     char* Hn = halo_buf + ((c + 1) & 1) * HMAX * kRow;
     const bool stream = c + 1 < nchunks;
     float4 rh[3];
-    bf16x8 af[2][2][TM];       // [step parity][hi|lo][fragment]
+    // A fragments kAD steps ahead (ring of kAD + 1): one LDS round trip (~120 cycles under load)
+    // outlasts a one-plane mode's step (1–2 MFMAs), so those read two steps ahead
+    bf16x8 af[kAD + 1][2][TM];   // [step mod kAD+1][hi|lo][fragment]
     auto a_read = [&](int u, bf16x8 (&dst)[2][TM]) __attribute__((always_inline)) {
       const int t = u >> 1, kk = u & 1;
       const int tap_off = (((t / 9) * a.HH + (t / 3) % 3) * a.HW + t % 3) * kRow + kk * 32;
@@ -233,7 +246,8 @@ conv_brick_x3_kernel(BrickArgs a) {
         if constexpr (prec::has_lo<PM>()) dst[1][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off + 64);
       }
     };
-    a_read(0, af[0]);
+#pragma unroll
+    for (int v = 0; v < kAD; ++v) a_read(v, af[v]);
     for (int u0 = 0; u0 < kSteps; u0 += kP) {
 #pragma unroll
     for (int du = 0; du < kP; ++du) {
@@ -268,10 +282,10 @@ conv_brick_x3_kernel(BrickArgs a) {
       }
       // A fragments of the NEXT step from the halo (software pipelined: the LDS latency hides
       // under this step's MFMAs; the chunk's first step is read after its barrier)
-      if (u + 1 < kSteps) a_read(u + 1, af[(du + 1) & 1]);
+      if (u + kAD < kSteps) a_read(u + kAD, af[(du + kAD) % (kAD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 (&ah)[TM] = af[du & 1][0];
-      const bf16x8 (&al)[TM] = af[du & 1][1];
+      const bf16x8 (&ah)[TM] = af[du % (kAD + 1)][0];
+      const bf16x8 (&al)[TM] = af[du % (kAD + 1)][1];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -284,6 +298,7 @@ conv_brick_x3_kernel(BrickArgs a) {
   }
 
   double ps[TN], pq[TN];                 // InstanceNorm statistics of the written values
+  if (!a.sx) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn0 + j * 32 + li;
@@ -301,6 +316,34 @@ conv_brick_x3_kernel(BrickArgs a) {
           a.y[(int64_t)off * a.ny + col] = v;
           ps[j] += v;
           pq[j] += (double)v * v;
+        }
+      }
+    }
+  }
+  } else {
+    // backward statistics of the InstanceNorm in front of this conv (the data gradient of a
+    // ResnetBlock conv is the padded dz; IN-backward reads g = fold(dz)·act'(x̂)): Σ_i g_i =
+    // Σ_p dz_p·act'(x̂_c(p)) and Σ_i g_i·x̂_i = Σ_p dz_p·act'(x̂_c(p))·x̂_c(p), c = the fold's clamp
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn0 + j * 32 + li;
+      const float mu = a.smean[nb * a.ny + col], rs = a.srstd[nb * a.ny + col];
+      ps[j] = 0.0;
+      pq[j] = 0.0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int off = out_off[row];
+          if (off >= 0) {
+            const float v = acc[i][j][r];
+            a.y[(int64_t)off * a.ny + col] = v;
+            const float xh = (a.sx[(int64_t)xoff[row] * a.ny + col] - mu) * rs;
+            const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? v * kLreluSlope : v;
+            ps[j] += gv;
+            pq[j] += (double)gv * xh;
+          }
         }
       }
     }
@@ -341,7 +384,7 @@ conv_brick_x3_kernel(BrickArgs a) {
 template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16>
 static int launch_brick_x3_as(const BrickArgs& a, hipStream_t st) {
   constexpr int BM = WM * TM * 32;
-  const size_t lds = (size_t)2 * HMAX * row_bytes<PM>() + (size_t)(BM + HMAX) * sizeof(int);
+  const size_t lds = (size_t)2 * HMAX * row_bytes<PM>() + (size_t)(2 * BM + HMAX) * sizeof(int);
   auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM, X16>;
   static bool attr_set = false;
   if (!attr_set) {

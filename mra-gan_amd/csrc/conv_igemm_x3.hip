@@ -33,7 +33,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int WM, int WN, int TM, int TN, int BK, int PM>
+template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH>
 __global__ void __launch_bounds__(256)
 conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   constexpr int BM = WM * TM * 32;
@@ -114,7 +114,10 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int kper = (nK_all + ksplit - 1) / ksplit;
   const int ks0 = min(nK_all, kz * kper);
   const int nK = min(nK_all, ks0 + kper) - ks0;       // steps of this slice: ks0 … ks0+nK−1
-  float4 ra[A_LOADS], rb[B_LOADS];
+  // two register stages: the tiles of step ks + 2 are loaded while step ks runs and stored to LDS
+  // at the end of step ks + 1, so a load has two steps' MFMAs to land (one step was ~128 MFMA
+  // cycles per wave against a ~1–2 µs L2 / MALL round trip: the stride-2 convs ran at 4–9 % of peak)
+  float4 ra[2][A_LOADS], rb[2][B_LOADS];
 
   // Operands through buffer descriptors (byte offsets are 32-bit: the host checks the sizes).
   // A: per thread and row a fixed base offset of its (nb, bd, bh, bw) voxel + channel quad; a
@@ -143,7 +146,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
   };
 
-  auto load_tiles = [&]() __attribute__((always_inline)) {
+  auto load_tiles = [&](float4 (&ra_)[A_LOADS], float4 (&rb_)[B_LOADS]) __attribute__((always_inline)) {
     const int c0 = kc * BK;
     const int td = gd.t0 + gd.tstep * kjd, th = gh.t0 + gh.tstep * kjh, tw = gw.t0 + gw.tstep * kjw;
     const int wt = (td * a.k + th) * a.k + tw;
@@ -155,24 +158,24 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       const bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
                       (unsigned)iw < (unsigned)a.Wi;
       const buf_f32x4 v = buf_load_16b(xrs, ok ? a_base[i] + toff : (int)kOobOffset, 0);
-      ra[i] = make_float4(v.x, v.y, v.z, v.w);
+      ra_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
     const int wso = __builtin_amdgcn_readfirstlane((wt * a.ny * a.cx + c0) * 4);
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
       const buf_f32x4 v = buf_load_16b(wrs, b_voff[i], wso);
-      rb[i] = make_float4(v.x, v.y, v.z, v.w);
+      rb_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
     advance();
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const float4 (&ra_)[A_LOADS], const float4 (&rb_)[B_LOADS]) {
     __bf16* st = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
       int r = tid / LPR + i * ROWS_PER_PASS;
       if (r < BM) {
         uint2 hi, lo;
-        prec::split4<PM>(ra[i], hi, lo);
+        prec::split4<PM>(ra_[i], hi, lo);
         *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
         if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
       }
@@ -182,7 +185,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       int r = tid / LPR + i * ROWS_PER_PASS;
       if (r < BN) {
         uint2 hi, lo;
-        prec::split4<PM>(rb[i], hi, lo);
+        prec::split4<PM>(rb_[i], hi, lo);
         *reinterpret_cast<uint2*>(st + 2 * PLANE_A + r * LDK + 4 * q) = hi;
         if constexpr (prec::has_lo<PM>())
           *reinterpret_cast<uint2*>(st + 2 * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
@@ -197,8 +200,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   if (nK > 0) {
-    load_tiles();
-    store_tiles(0);
+    load_tiles(ra[0], rb[0]);
+    if (DEPTH == 2 && nK > 1) load_tiles(ra[1], rb[1]);
+    store_tiles(0, ra[0], rb[0]);
   }
   __syncthreads();
 
@@ -206,7 +210,16 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int lh = lane >> 5;
   for (int ks = 0; ks < nK; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nK) load_tiles();
+    // register stage ks & 1 was stored at the end of step ks − 1: refill it with step ks + 2
+    // (DEPTH 1: one stage, step ks + 1 loaded here and stored at the end of this step)
+    if constexpr (DEPTH == 2) {
+      if (ks + 2 < nK) {
+        if (buf) load_tiles(ra[1], rb[1]);
+        else load_tiles(ra[0], rb[0]);
+      }
+    } else {
+      if (ks + 1 < nK) load_tiles(ra[0], rb[0]);
+    }
     const __bf16* Ah = smem + buf * STAGE;
     const __bf16* Al = Ah + PLANE_A;
     const __bf16* Bh = Ah + 2 * PLANE_A;
@@ -235,7 +248,11 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
           acc[i][j] = prec::mma<PM>(ah[i], al[i], bh[j], bl[j], acc[i][j]);
         }
     }
-    if (ks + 1 < nK) store_tiles(buf ^ 1);
+    if (ks + 1 < nK) {
+      if (DEPTH == 1) store_tiles(buf ^ 1, ra[0], rb[0]);
+      else if (buf) store_tiles(0, ra[0], rb[0]);
+      else store_tiles(1, ra[1], rb[1]);
+    }
     __syncthreads();
   }
 
@@ -330,9 +347,14 @@ static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
   int ntiles = gm * gn * a.nclass;
+  static const bool depth1 = getenv("MRAGAN_IG_DEPTH1") != nullptr;   // A/B switch
   MRAGAN_PREC_DISPATCH(a.x3, {
-    hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM>), dim3(ntiles * splits), dim3(256), 0, st, a, gm,
-                       gn, ntiles, splits);
+    if (depth1)
+      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, 1>), dim3(ntiles * splits), dim3(256), 0, st, a,
+                         gm, gn, ntiles, splits);
+    else
+      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, 2>), dim3(ntiles * splits), dim3(256), 0, st, a,
+                         gm, gn, ntiles, splits);
     return check_launch("conv_igemm_x3");
   })
 }

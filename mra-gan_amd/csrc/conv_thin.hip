@@ -329,6 +329,96 @@ __global__ void __launch_bounds__(256) thin_n_class8_kernel(ThinArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// thin_n_tile8: thin_n_class8 for stride 2 with the input halo of an 8×8×8 output tile staged in
+// LDS once (7³ rows: every input row serves up to 64 outputs of the tile, which thin_n_class8 each
+// re-read through L1/L2 — 537 MB of L2 reads for the 64³ b2 D-first data gradient, 75 µs).  Lane
+// groups of 8 (lane j = channel quad j) walk the tile's outputs of one parity class each; taps,
+// skip conditions, fp64 product order and the xor-shuffle sum are thin_n_class8's, so results are
+// bit-identical to it.
+// ---------------------------------------------------------------------------------------
+constexpr int kT8 = 8, kT8Halo = kT8 / 2 + 3;
+
+__device__ __forceinline__ int floor_div2(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+
+template <int NY>
+__global__ void __launch_bounds__(256) thin_n_tile8_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w) {
+  constexpr int s = 2, HE = kT8Halo;
+  extern __shared__ float4 hx[];                      // [HE³][CQ], zero outside the input volume
+  const int k = a.k, CQ = a.cx / 4;
+  int b = blockIdx.x;
+  const int tw_ = b % tiles_w; b /= tiles_w;
+  const int th_ = b % tiles_h; b /= tiles_h;
+  const int td_ = b % tiles_d;
+  const int nb = b / tiles_d;
+  const int o0d = td_ * kT8, o0h = th_ * kT8, o0w = tw_ * kT8;
+  // lowest input index any output of the tile reads: floor((o0 + p − (k − 1)) / 2)
+  const int ild = floor_div2(o0d + a.p - (k - 1)), ilh = floor_div2(o0h + a.p - (k - 1)),
+            ilw = floor_div2(o0w + a.p - (k - 1));
+  const float* xn = a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * a.cx;
+  for (int e = threadIdx.x; e < HE * HE * HE * CQ; e += 256) {
+    const int q = e % CQ, r = e / CQ;
+    const int id = ild + r / (HE * HE), ih = ilh + (r / HE) % HE, iw = ilw + r % HE;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
+      v = op_round4(*reinterpret_cast<const float4*>(xn + ((int64_t)(id * a.Hi + ih) * a.Wi + iw) * a.cx + 4 * q), a.rnd);
+    hx[e] = v;
+  }
+  const int j = threadIdx.x & 7, grp = threadIdx.x >> 3;
+  const int cls = grp & 7, gi = grp >> 3;             // 4 lane groups per parity class
+  const int cw = cls % s, ch = (cls / s) % s, cd = cls / (s * s);
+  const int t0d = (cd + a.p) % s, t0h = (ch + a.p) % s, t0w = (cw + a.p) % s;
+  float4 wr[8][NY];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int td = t0d + s * (t >> 2), th = t0h + s * ((t >> 1) & 1), tw = t0w + s * (t & 1);
+    const bool tok = td < k && th < k && tw < k;
+    const float* wt = a.w + (int64_t)((min(td, k - 1) * k + min(th, k - 1)) * k + min(tw, k - 1)) * NY * a.cx;
+#pragma unroll
+    for (int n = 0; n < NY; ++n)
+      wr[t][n] = (tok && j < CQ) ? op_round4(*reinterpret_cast<const float4*>(wt + n * a.cx + 4 * j), a.rnd)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  constexpr int QT = kT8 / s;                         // class outputs per tile dim
+  for (int idx = gi; idx < QT * QT * QT; idx += 4) {
+    const int od = o0d + s * (idx / (QT * QT)) + cd, oh = o0h + s * ((idx / QT) % QT) + ch,
+              ow = o0w + s * (idx % QT) + cw;
+    if (od >= a.Do || oh >= a.Ho || ow >= a.Wo) continue;        // uniform per lane group
+    double acc[NY];
+#pragma unroll
+    for (int n = 0; n < NY; ++n) acc[n] = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int td = t0d + s * (t >> 2), th = t0h + s * ((t >> 1) & 1), tw = t0w + s * (t & 1);
+      const int id = (od + a.p - td) / s, ih = (oh + a.p - th) / s, iw = (ow + a.p - tw) / s;
+      if (td >= k || th >= k || tw >= k || (unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi ||
+          (unsigned)iw >= (unsigned)a.Wi)
+        continue;
+      if (j < CQ) {
+        const float4 xv = hx[(((id - ild) * HE + (ih - ilh)) * HE + (iw - ilw)) * CQ + j];
+#pragma unroll
+        for (int n = 0; n < NY; ++n) {
+          const float4 wv = wr[t][n];
+          acc[n] = fma((double)xv.x, (double)wv.x, fma((double)xv.y, (double)wv.y,
+                       fma((double)xv.z, (double)wv.z, fma((double)xv.w, (double)wv.w, acc[n]))));
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NY; ++n) {
+      acc[n] += __shfl_xor(acc[n], 4, 8);
+      acc[n] += __shfl_xor(acc[n], 2, 8);
+      acc[n] += __shfl_xor(acc[n], 1, 8);
+    }
+    if (j == 0) {
+      float* dst = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * NY;
+#pragma unroll
+      for (int n = 0; n < NY; ++n) dst[n] = act_fwd((float)acc[n] + (a.bias ? a.bias[n] : 0.f), a.act);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // naive: one wave per output voxel (lanes split taps × channels), any stride / transposed
 // form.  Used for the tiny D-last convolution and the D-first data gradient.
 // ---------------------------------------------------------------------------------------
@@ -467,6 +557,21 @@ int conv_thin(ThinArgs a, hipStream_t st) {
   if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && a.cx <= 32 && ceil_div(a.k, a.s) == 2 &&
       (int64_t)a.N * a.Do * a.Ho * a.Wo < ((int64_t)1 << 31) &&
       (int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx < ((int64_t)1 << 31)) {
+    static const bool no_tile8 = getenv("MRAGAN_NO_TILE8") != nullptr;   // A/B switch
+    if (a.s == 2 && !no_tile8) {
+      const int tiles_d = ceil_div(a.Do, kT8), tiles_h = ceil_div(a.Ho, kT8), tiles_w = ceil_div(a.Wo, kT8);
+      const int64_t blocks = (int64_t)a.N * tiles_d * tiles_h * tiles_w;
+      const size_t lds = (size_t)kT8Halo * kT8Halo * kT8Halo * (a.cx / 4) * sizeof(float4);
+      if (blocks < ((int64_t)1 << 31)) {
+        switch (a.ny) {
+          case 1: hipLaunchKernelGGL((thin_n_tile8_kernel<1>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
+          case 2: hipLaunchKernelGGL((thin_n_tile8_kernel<2>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
+          case 3: hipLaunchKernelGGL((thin_n_tile8_kernel<3>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
+          default: hipLaunchKernelGGL((thin_n_tile8_kernel<4>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
+        }
+        return check_launch("thin_n_tile8");
+      }
+    }
     const int64_t maxq = (int64_t)a.N * ceil_div(a.Do, a.s) * ceil_div(a.Ho, a.s) * ceil_div(a.Wo, a.s);
     int64_t gx = ceil_div(maxq, 32 * 4);             // ≈ 4 voxels per lane group: the weights load once per 4
     if (gx > 4096) gx = 4096;

@@ -94,7 +94,7 @@ struct Wgrad3Args {
 // 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
 // the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
 // kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
-template <int TC, int TI, int PM, int X16>
+template <int TC, int TI, int PM, int X16, int AL>
 __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
   constexpr int WC = TC / 32;             // waves along co
@@ -170,16 +170,83 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       if (++h_ == a.H) { h_ = 0; xo += gplane; if (++d_ == a.D) { d_ = 0; xo += gvol; } }
     }
   };
+  // AL (aligned stages, the host checks): every stage's kR segments are whole w-runs of kR / nsw
+  // consecutive rows of one (n, d) plane and every stage is full — the X offset of segment r is
+  // the stage's plus a per-block constant, and a stage advances with one carry chain instead of
+  // kR (the per-segment carries cost ~9 scalar instructions per MFMA, PMC r03e)
+  const int rps = kR / nsw;                                   // rows per stage (AL)
+  const int grow1 = Wg * a.Cg * ES;                            // X bytes per padded row
+  int xro[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) xro[r] = AL ? __builtin_amdgcn_readfirstlane((r / nsw) * grow1 + (r % nsw) * gw16) : 0;
+  auto adv_stage = [&]() __attribute__((always_inline)) {     // AL: the next stage's first segment
+    if constexpr (AL) {
+      sxo += rps * grow1;
+      sh += rps;
+      if (sh == a.H) {
+        sh = 0; sxo += gplane;
+        if (++sd == a.D) { sd = 0; sxo += gvol; }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+    }
+  };
+  // kW16 (16-bit planes, aligned stages): wave w stages segment(s) w (+ NW) of a stage, 16 B =
+  // 8 channels per load and per LDS store (the 8-B quad units issued 3× the loads at 0.54–0.70×
+  // the 16-B rate: the plane path ran 8 % slower than the fp32 one, r03f)
+  constexpr bool kW16 = X16 && AL;
+  constexpr int NW = NT / 64, SPW = kR / NW;                   // waves, segments per wave
+  constexpr int DO8 = TC / 8, GO8 = TI / 8;                    // 16-B octets per voxel
+  constexpr int DL = 16 * DO8 / 64, GU = 18 * GO8, GL = (GU + 63) / 64;
+  static_assert(kR % NW == 0 && (16 * DO8) % 64 == 0, "wave-per-segment staging");
+  uint4 d16[kW16 ? SPW : 1][kW16 ? DL : 1], g16[kW16 ? SPW : 1][kW16 ? GL : 1];
+  int dlo[kW16 ? DL : 1], glo[kW16 ? GL : 1], rdo[kW16 ? SPW : 1], rgo[kW16 ? SPW : 1];
+  if constexpr (kW16) {
+#pragma unroll
+    for (int j = 0; j < DL; ++j) {
+      const int u = lane + 64 * j;
+      dlo[j] = ((u / DO8) * a.Cd + co0 + 8 * (u % DO8)) * 2;
+    }
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int u = lane + 64 * j;
+      glo[j] = u < GU ? ((u / GO8) * a.Cg + ci0 + 8 * (u % GO8)) * 2 : (int)kOobOffset;
+    }
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+      const int r = wave + NW * q;
+      rdo[q] = __builtin_amdgcn_readfirstlane(r * dseg);
+      rgo[q] = __builtin_amdgcn_readfirstlane((r / nsw) * grow1 + (r % nsw) * gw16);
+    }
+  }
+  auto load16 = [&](int st) __attribute__((always_inline)) {
+    const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
+    const int gso0 = __builtin_amdgcn_readfirstlane(sxo + gkdh);
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+#pragma unroll
+      for (int j = 0; j < DL; ++j) d16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(dyr, dlo[j], dso0 + rdo[q]));
+#pragma unroll
+      for (int j = 0; j < GL; ++j) g16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(xgr, glo[j], gso0 + rgo[q]));
+    }
+  };
   auto load = [&](int st) __attribute__((always_inline)) {
+    if constexpr (kW16) {
+      load16(st);
+      return;
+    }
     int cw = sw, chh = sh, cdd = sd, cxo = sxo;
+    const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
+    const int gso0 = __builtin_amdgcn_readfirstlane(sxo + gkdh);
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int seg = seg_lo + st * kR + r;
-      const bool ok = seg < seg_hi;
+      const bool ok = AL || seg < seg_hi;
       // past the split's end: re-read segment 0 (a valid row, masked to zero)
-      const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
-      const int gso = __builtin_amdgcn_readfirstlane((ok ? cxo : 0) + gkdh);
-      bump(cw, chh, cdd, cxo);
+      const int dso = AL ? dso0 + r * dseg : __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
+      const int gso = AL ? gso0 + xro[r] : __builtin_amdgcn_readfirstlane((ok ? cxo : 0) + gkdh);
+      if constexpr (!AL) bump(cw, chh, cdd, cxo);
       // past the split's end: an out-of-range voffset reads zeros (no select on the values)
       if constexpr (X16) {
         rd[r] = buf_load_8b(dyr, ok ? dlane : (int)kOobOffset, dso);
@@ -235,7 +302,27 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       *reinterpret_cast<uint2*>(base + row * RB + 16 * ((q >> 1) ^ tr_swz<RB>(row)) + 8 * (q & 1)) = h;
     }
   };
+  auto store16 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < SPW; ++q) {
+      const int r = wave + NW * q;
+#pragma unroll
+      for (int j = 0; j < DL; ++j) {
+        const int u = lane + 64 * j, row = (u / DO8) * kR + r;
+        *reinterpret_cast<uint4*>(Ds + row * RBD + 16 * ((u % DO8) ^ tr_swz<RBD>(row))) = d16[q][j];
+      }
+#pragma unroll
+      for (int j = 0; j < GL; ++j) {
+        const int u = lane + 64 * j, row = (u / GO8) * kR + r;
+        if (u < GU) *reinterpret_cast<uint4*>(Gs + row * RBG + 16 * ((u % GO8) ^ tr_swz<RBG>(row))) = g16[q][j];
+      }
+    }
+  };
   auto store = [&]() __attribute__((always_inline)) {
+    if constexpr (kW16) {
+      store16();
+      return;
+    }
     if constexpr (kTr) {
       put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
       if (g1) put16(Gs, std::integral_constant<int, RBG>{}, gw, gcq, rg);
@@ -271,8 +358,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       store();
     }
     if (nstage > 1) {
-#pragma unroll
-      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+      adv_stage();
       load(1);
     }
   } else if (nstage > 0) {
@@ -286,8 +372,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       store();
       __syncthreads();
       if (st + 1 < nstage) {                        // lands during this stage's MFMAs
-#pragma unroll
-        for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+        adv_stage();
         load(st + 1);
       }
     }
@@ -332,8 +417,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
         use_buf((st + 1) & 1);
         store();                    // stage st+1 (loaded one stage ago) into the other buffer
         if (st + 2 < nstage) {
-#pragma unroll
-          for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sxo);
+          adv_stage();
           load(st + 2);
         }
       }
@@ -379,7 +463,7 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TC, int TI, int PM, int X16>
+template <int TC, int TI, int PM, int X16, int AL>
 static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
   if constexpr (X16 && prec::has_lo<PM>()) {
     return;                                     // rejected by the caller
@@ -389,11 +473,11 @@ static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
     const int lds = wide ? (tr ? kLdsTrW : kLdsW) : (tr ? kLdsTr : kLds);
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
+    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
   }
 }
 
@@ -413,13 +497,17 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     set_error("wgrad3_x3: 16-bit operand planes need the bf16 or fp16 mode");
     return -kBadArg;
   }
+  // aligned stages: whole w-runs of rows of one plane per stage, every stage full
+  const int nsw = g.Wd / kSegW;
+  static const bool no_al = getenv("MRAGAN_W3_NO_AL") != nullptr;   // A/B switch
+  const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (wide) {
-      if (g.in16) launch_wgrad3<128, 64, PM, 1>(a, blocks, st);
-      else launch_wgrad3<128, 64, PM, 0>(a, blocks, st);
+      if (g.in16) { if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st); }
+      else { if (al) launch_wgrad3<128, 64, PM, 0, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 0, 0>(a, blocks, st); }
     } else {
-      if (g.in16) launch_wgrad3<64, 64, PM, 1>(a, blocks, st);
-      else launch_wgrad3<64, 64, PM, 0>(a, blocks, st);
+      if (g.in16) { if (al) launch_wgrad3<64, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<64, 64, PM, 1, 0>(a, blocks, st); }
+      else { if (al) launch_wgrad3<64, 64, PM, 0, 1>(a, blocks, st); else launch_wgrad3<64, 64, PM, 0, 0>(a, blocks, st); }
     }
     return nsplit;
   })

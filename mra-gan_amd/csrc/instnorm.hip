@@ -456,6 +456,30 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
 }
 
+// Backward from statistics partials the producer of dy already accumulated (conv_brick_x3's
+// backward-statistics epilogue: [N][chunks][C][2] = Σg, Σg·x̂ per brick): finalize + apply only.
+int instnorm_bwd_partials(const InBwdArgs& a, InShape s, const double* part, int chunks, void* ws, size_t ws_bytes,
+                          hipStream_t st) {
+  MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm_bwd: C=%d must be a multiple of 4", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, a.dypad), "instnorm_bwd: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
+  MRAGAN_CHECK_ARG(part && chunks > 0, "instnorm_bwd_partials: no partials");
+  const size_t need = (size_t)s.N * s.C * 2 * sizeof(float);
+  if (need > ws_bytes) { set_error("instnorm_bwd_partials: workspace too small"); return kWorkspace; }
+  float* coef = static_cast<float*>(ws);
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
+  int rc = check_launch("in_bwd_finalize");
+  if (rc) return rc;
+  const int rows = s.N * s.D * s.H;
+  const dim3 ga(rows < 16384 ? rows : 16384);
+  switch (a.dypad) {
+    case 0: hipLaunchKernelGGL(in_bwd_apply_kernel<0>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 1: hipLaunchKernelGGL(in_bwd_apply_kernel<1>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
+    default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
+  }
+  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
+}
+
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st) {
   if (nentries <= 0) return kOk;
   hipLaunchKernelGGL(in_running_kernel, dim3(nentries), dim3(256), 0, st, static_cast<const RunningEntry*>(table), momentum);

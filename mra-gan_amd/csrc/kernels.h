@@ -23,6 +23,8 @@ struct IgemmArgs {
   int* in_chunks;   // set to the bricks per instance when in_part was filled, else 0
   int shell;        // conv_igemm_x3 only: the 6 shell-face classes of a full (k3 s1 p0) transposed conv
   int x16;          // x is a 16-bit operand plane (bf16 / fp16 words of the precision mode), not fp32
+  // with in_part, backward statistics instead (BrickArgs::sx): the producing IN's x, μ, rstd, act
+  const float* bs_x; const float* bs_mean; const float* bs_rstd; int bs_act;
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
@@ -46,6 +48,11 @@ struct BrickArgs {
   int ye;           // output embedding: y is [N][Yd][Yh][Yw][ny], output voxel o written at o + ye
   int Yd, Yh, Yw;
   int x16;          // x is a 16-bit operand plane (conv_brick_x3 in the bf16 / fp16 modes)
+  // optional (with part): backward-statistics partials instead of forward ones — the output is the
+  // padded data gradient dz of a conv whose input was an InstanceNorm(+act) output of sx
+  // ([N][Do−2][Ho−2][Wo−2][ny] fp32, statistics smean / srstd [N][ny]): part = Σ_p g, Σ_p g·x̂
+  // with g = dz_p·act'(x̂) at the interior voxel p folds into (conv_brick_x3 only)
+  const float* sx; const float* smean; const float* srstd; int sact;
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st, bool interior = false);
@@ -138,6 +145,8 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
 int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
                           float* mean, float* rstd, const double* part, int chunks, hipStream_t st, void* y16 = nullptr,
                           int mode16 = 0);
+int instnorm_bwd_partials(const InBwdArgs& a, InShape s, const double* part, int chunks, void* ws, size_t ws_bytes,
+                          hipStream_t st);
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C);
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st);
 size_t instnorm_running_entry_bytes();

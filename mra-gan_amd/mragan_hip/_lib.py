@@ -82,6 +82,10 @@ SIGNATURES = {
                                  vp, sz, vp, vp]),
     "mragan_conv3d_wgrad_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                                        sz, vp]),
+    "mragan_conv3d_op16_dgrad_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, sz, vp, vp, vp, i32,
+                                                vp, sz, vp, vp]),
+    "mragan_instnorm_bwd_partials_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32,
+                                                vp, sz, vp]),
 }
 
 _lock = threading.Lock()

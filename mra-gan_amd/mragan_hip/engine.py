@@ -129,6 +129,19 @@ class ConvLayer:
         return ops.conv3d_op16(dy16, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial, self.ws_bwd,
                                transposed=not self.transposed)[0]
 
+    def dgrad_op16_in_stats(self, dy16, norm_x, mean, rstd, act):
+        """dgrad_op16 (whole-grid, k3 s1 p0) that also leaves the backward-statistics partials of
+        the InstanceNorm(+act) that produced this conv's input (norm_x its pre-norm input).
+        Returns (dz, part, chunks); chunks = 0: no partials."""
+        if _NO_IN_STATS:
+            N, D, H, W, _ = dy16.shape
+            return self.dgrad_op16(dy16, (D + 2, H + 2, W + 2)), None, 0
+        N, D, H, W, _ = dy16.shape
+        part = ops.in_partials_buffer(N, (D + 2, H + 2, W + 2), self.cin, dy16.device)
+        dz, chunks = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean, rstd, act,
+                                                    part)
+        return dz, part, chunks
+
     def wgrad_op16(self, x16, dy16, accumulate=True):
         """wgrad of a forward-form conv from the operand planes of X and dY (wgrad3, 16-bit modes)."""
         ops.conv3d_wgrad_op16(dy16, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
@@ -325,8 +338,12 @@ class NetPlan:
                     dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
                     st.conv2.wgrad_op16(sc.z1, dh2)
-                dz1 = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4])
-                dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
+                # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
+                dz1, part, chunks = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
+                if chunks:
+                    dh1 = ops.instnorm_bwd_partials_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, "relu", part, chunks)
+                else:
+                    dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
                     st.conv1.wgrad_op16(sc.inp16, dh1)
                 g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])

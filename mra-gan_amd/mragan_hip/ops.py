@@ -461,6 +461,57 @@ def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, 
     return out, chunks.value
 
 
+def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, wsplit: torch.Tensor,
+                               x_in: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, act, part: torch.Tensor):
+    """Whole-grid data gradient (k3 s1 p0 transposed form, output = input + 2 per dim) from the
+    plane dy16 that also leaves, in `part`, the backward-statistics partials of the InstanceNorm
+    (+act) whose output was this conv's input: x_in (pre-norm, [N, D, H, W, cout]), mean, rstd.
+    Returns (dz, chunks); chunks = 0: no partials (run instnorm_bwd_op16)."""
+    _check16(dy16, "dgrad_in_stats.dy16")
+    _check(x_in, "dgrad_in_stats.x_in")
+    N, Di, Hi, Wi, cin = dy16.shape
+    if tuple(x_in.shape) != (N, Di, Hi, Wi, cout):
+        raise ValueError(f"dgrad_in_stats: x_in shape {tuple(x_in.shape)} != {(N, Di, Hi, Wi, cout)}")
+    if wp.numel() != 27 * cin * cout or wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("dgrad_in_stats: packed / pre-split weight size mismatch")
+    if part.dtype != torch.float64 or not part.is_cuda:
+        raise ValueError("dgrad_in_stats: part must be a float64 device tensor")
+    osp = (Di + 2, Hi + 2, Wi + 2)
+    out = torch.empty((N,) + osp + (cout,), device=dy16.device, dtype=torch.float32)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, 3, 1, 0, *osp, 1)
+    ws = WS.get(nbytes) if nbytes else None
+    chunks = _ct.c_int(0)
+    fn = lambda: call("mragan_conv3d_op16_dgrad_in_stats", _ptr(dy16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), cout,
+                      _ptr(out), _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act], _ptr(part),
+                      part.numel() * 8, _ct.byref(chunks), _stream())
+    _timed(lambda: _conv_info(cin, cout, 3, 1, 0, True, N, (Di, Hi, Wi), osp), fn)
+    return out, chunks.value
+
+
+def instnorm_bwd_partials_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int,
+                               dy_add: Optional[torch.Tensor], act, part: torch.Tensor, chunks: int,
+                               g_out: Optional[torch.Tensor] = None):
+    """instnorm_bwd_op16 from backward-statistics partials (conv3d_op16_dgrad_in_stats): no
+    statistics pass.  Returns the dx plane."""
+    _check(x, "instnorm_bwd.x")
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError("instnorm_bwd_partials_op16: 16-bit operand planes need the bf16 or fp16 precision mode")
+    N, D, H, W, C = x.shape
+    if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
+        raise ValueError(f"instnorm_bwd: dy shape {tuple(dy.shape)} does not match pad {dypad}")
+    dx16 = torch.empty(x.shape, device=x.device, dtype=dt)
+    nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_instnorm_bwd_partials_op16", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy),
+                      dypad, _ptr(dy_add), ACT[act], _ptr(dx16), _ptr(g_out), _ptr(part), chunks, _ptr(ws), ws.numel(),
+                      _stream())
+    _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad} op16 partials",
+                        bytes=4.0 * (x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                     + (x.numel() if g_out is not None else 0)) + 2.0 * x.numel()), fn)
+    return dx16
+
+
 def conv3d_wgrad_op16(dense16: torch.Tensor, gathered16: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
                       accumulate: bool) -> torch.Tensor:
     """conv3d_wgrad on the operand planes of dense and gathered (the k3 s1 valid weight gradient)."""

@@ -536,6 +536,35 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
+@pytest.mark.parametrize("N,C,S,W,act", [(2, 128, 16, 16, "relu"), (1, 64, 9, 16, "relu"), (1, 128, 5, 32, "lrelu"),
+                                          (2, 64, 6, 16, None)])
+def test_op16_dgrad_backward_statistics(op16, N, C, S, W, act):
+    """ABI 11: the whole-grid data gradient's epilogue partials of the preceding InstanceNorm's
+    backward statistics give the same IN backward as the statistics pass: dz bit-identical to the
+    plain data gradient, dx within fp32 summation-order noise of the statistics-pass result (the
+    partials sum the fold in fp64 where the statistics pass sums it in fp32 first)."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 13 + C + S)
+    h1 = ndhwc(torch.randn(N, C, S, S, W, generator=g).float()).cuda()             # conv1 output (pre-IN)
+    _, z16, mean, rstd = ops.instnorm_fwd_op16(h1, act=act, ypad=1)
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_b = pack(ops, w, False, True)
+    ws_b = _presplit(ops, w, C, C, True)
+    dh2 = ndhwc(torch.randn(N, C, S, S, W, generator=g).float()).cuda().to(dt)
+    dz_ref, _ = ops.conv3d_op16(dh2, wp_b, C, 3, 1, 0, (S + 2, S + 2, W + 2), ws_b, transposed=True)
+    part = ops.in_partials_buffer(N, (S + 2, S + 2, W + 2), C, "cuda")
+    dz, chunks = ops.conv3d_op16_dgrad_in_stats(dh2, wp_b, C, ws_b, h1, mean, rstd, act, part)
+    assert chunks > 0
+    assert torch.equal(dz, dz_ref)
+    ref = ops.instnorm_bwd(h1, mean, rstd, dz, 1, None, act=act)                     # fp32 statistics pass
+    got = ops.instnorm_bwd_partials_op16(h1, mean, rstd, dz, 1, None, act, part, chunks)
+    assert rel(got.float(), ref) < (4e-3 if dt == torch.bfloat16 else 6e-4)           # one 16-bit rounding
+    plane = ops.instnorm_bwd_op16(h1, mean, rstd, dz, 1, None, act=act)
+    # 16-bit words that differ from the statistics-pass plane: only round-half cases of ~1e-7 shifts
+    assert (got != plane).float().mean().item() < 1e-3
+
+
 def test_op16_rejected_outside_16bit_modes(ops):
     from mragan_hip import MraganError
     ops.set_conv_precision("bf16x3")
