@@ -114,9 +114,8 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int kper = (nK_all + ksplit - 1) / ksplit;
   const int ks0 = min(nK_all, kz * kper);
   const int nK = min(nK_all, ks0 + kper) - ks0;       // steps of this slice: ks0 … ks0+nK−1
-  // two register stages: the tiles of step ks + 2 are loaded while step ks runs and stored to LDS
-  // at the end of step ks + 1, so a load has two steps' MFMAs to land (one step was ~128 MFMA
-  // cycles per wave against a ~1–2 µs L2 / MALL round trip: the stride-2 convs ran at 4–9 % of peak)
+  // DEPTH 2 (A/B only, measured slower): two register stages, the tiles of step ks + 2 loaded
+  // while step ks runs and stored to LDS at the end of step ks + 1; DEPTH 1 (default): one stage
   float4 ra[2][A_LOADS], rb[2][B_LOADS];
 
   // Operands through buffer descriptors (byte offsets are 32-bit: the host checks the sizes).
@@ -347,7 +346,10 @@ static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
   int ntiles = gm * gn * a.nclass;
-  static const bool depth1 = getenv("MRAGAN_IG_DEPTH1") != nullptr;   // A/B switch
+  // A/B switch, off: the two-stage register prefetch measured 15–20 % SLOWER than one stage on
+  // every stride-2 / PatchGAN shape (bf16, r03h: down1 84.3 vs 70.8 µs, down2 52.6 vs 42.2, up1
+  // 87.6 vs 72.8, D layer 2 28.8 vs 25.2 at N = 4) — the extra 24–32 VGPRs cost occupancy
+  static const bool depth1 = getenv("MRAGAN_IG_DEPTH2") == nullptr;
   MRAGAN_PREC_DISPATCH(a.x3, {
     if (depth1)
       hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, 1>), dim3(ntiles * splits), dim3(256), 0, st, a,

@@ -455,7 +455,11 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
   const bool wide = w3_wide(a);
   const int tiles = (a.Cd / (wide ? 128 : kTile)) * (a.Cg / kTile) * 9;
-  int s = (wide ? 256 : 512) / tiles;
+  static const int budget = [] {                              // A/B switch: MRAGAN_W3_BLOCKS
+    const char* e = getenv("MRAGAN_W3_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  int s = (budget > 0 ? budget : (wide ? 256 : 512)) / tiles;
   const int by_len = nseg / (4 * kR);
   if (s > by_len) s = by_len;
   if (s > max_splits) s = max_splits;
