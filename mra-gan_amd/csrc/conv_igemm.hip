@@ -291,6 +291,7 @@ static int conv_igemm_x3_chunked(const IgemmArgs& a, int64_t max_mc, int64_t tot
   const int64_t in_vol = (int64_t)a.Di * a.Hi * a.Wi * a.cx, out_vol = (int64_t)a.Do * a.Ho * a.Wo * a.ny;
   for (int n0 = 0; n0 < a.N; n0 += nb) {
     IgemmArgs c = a;
+    c.in_part = nullptr;                 // instance ranges: no InstanceNorm partials (stats pass instead)
     c.N = nb < a.N - n0 ? nb : a.N - n0;
     c.x = a.x + n0 * in_vol;
     c.y = a.y + n0 * out_vol;

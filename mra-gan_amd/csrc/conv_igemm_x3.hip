@@ -273,9 +273,11 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
     return;
   }
+  double ps[TN], pq[TN];                 // InstanceNorm statistics of the written values
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     int col = n0 + wn0 + j * 32 + li;
+    ps[j] = pq[j] = 0.0;
     if (col >= a.ny) continue;
     float bsum = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
@@ -284,8 +286,48 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       for (int r = 0; r < 16; ++r) {
         int row = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         int off = out_off[row];
-        if (off >= 0) a.y[(int64_t)off * a.ny + col] = act_fwd(acc[i][j][r] + bsum, a.act);
+        if (off >= 0) {
+          const float v = act_fwd(acc[i][j][r] + bsum, a.act);
+          a.y[(int64_t)off * a.ny + col] = v;
+          ps[j] += v;
+          pq[j] += (double)v * v;
+        }
       }
+    }
+  }
+  // the consumer InstanceNorm's Σy / Σy² partial of this tile (the host guarantees that a tile's
+  // rows lie in one instance and one class): chunk = class · (tiles per class and instance) +
+  // tile within them; lanes li / li + 32 share a column, the WM waves of a column add through LDS
+  if (a.in_part) {
+    __syncthreads();                                  // the staging buffers are idle now
+    double* red = reinterpret_cast<double*>(smem);    // [WM][BN][2]
+    const int wmi = wave / WN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const double s2 = ps[j] + __shfl_xor(ps[j], 32);
+      const double q2 = pq[j] + __shfl_xor(pq[j], 32);
+      if (lh == 0) {
+        red[(wmi * BN + wn0 + j * 32 + li) * 2] = s2;
+        red[(wmi * BN + wn0 + j * 32 + li) * 2 + 1] = q2;
+      }
+    }
+    __syncthreads();
+    const int64_t qv = Mc / a.N;                      // rows of this class per instance
+    const int nb = (int)(m0 / qv);
+    const int cpc = (int)(qv / BM);
+    const int chunk = cls * cpc + (int)((m0 - (int64_t)nb * qv) / BM);
+    const int chunks = a.nclass * cpc;
+    for (int c = tid; c < BN; c += 256) {
+      if (n0 + c >= a.ny) continue;
+      double s2 = 0.0, q2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s2 += red[(w * BN + c) * 2];
+        q2 += red[(w * BN + c) * 2 + 1];
+      }
+      double* dst = a.in_part + (((int64_t)nb * chunks + chunk) * a.ny + n0 + c) * 2;
+      dst[0] = s2;
+      dst[1] = q2;
     }
   }
 }
@@ -318,9 +360,13 @@ static X3Plan x3_plan(const IgemmArgs& a, int64_t total_m) {
   // 256-block 128×64 grid left G's down2 at 61–66 µs, 64×64 tiles 49.6 µs); without one, 64×64
   // for > 64 outputs, and for ≤ 64 outputs the 128×64 tile whose short M is then split in K
   // (PatchGAN layer 2: 37.5 µs split 4 ways vs 47.1 µs on 64×64 tiles; tools/gpu_igcfg.sh)
+  static const int64_t want = [] {                            // A/B switch: MRAGAN_IG_MINBLOCKS
+    const char* e = getenv("MRAGAN_IG_MINBLOCKS");
+    return (int64_t)(e ? atoi(e) : 512);
+  }();
   int cfg;
-  if (a.ny > 64) cfg = blocks(0) >= 512 ? 0 : blocks(1) >= 512 ? 1 : 2;
-  else if (a.ny > 32) cfg = blocks(1) >= 512 ? 1 : blocks(2) >= 512 ? 2 : 1;
+  if (a.ny > 64) cfg = blocks(0) >= want ? 0 : blocks(1) >= want ? 1 : 2;
+  else if (a.ny > 32) cfg = blocks(1) >= want ? 1 : blocks(2) >= want ? 2 : 1;
   else cfg = blocks(3) >= 256 ? 3 : 4;
   X3Plan pl{cfg, 1};
   const int64_t b = blocks(cfg);
@@ -396,6 +442,19 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
     if (a.ws == nullptr || a.ws_bytes < need) {
       set_error("conv: split-K workspace %zu < %zu bytes (query mragan_conv3d_workspace)", a.ws_bytes, need);
       return kWorkspace;
+    }
+  }
+  // InstanceNorm partials from the epilogue: no K split, every tile inside one instance and one
+  // class, every class the same row count (forward convs, and transposed ones whose output is a
+  // whole multiple of the stride)
+  if (a.in_part) {
+    const int bm = kX3Cfg[pl.cfg].bm;
+    const int64_t per_cls = total_m / ((int64_t)a.N * a.nclass);
+    const bool even = per_cls * a.N * a.nclass == total_m && per_cls == max_mc / a.N && max_mc % a.N == 0;
+    if (pl.splits == 1 && !a.shell && even && per_cls % bm == 0 && a.bias == nullptr) {
+      if (a.in_chunks) *a.in_chunks = (int)(a.nclass * (per_cls / bm));
+    } else {
+      a.in_part = nullptr;
     }
   }
   int rc = a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)

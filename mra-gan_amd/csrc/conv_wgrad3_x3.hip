@@ -459,7 +459,11 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
     const char* e = getenv("MRAGAN_W3_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  int s = (budget > 0 ? budget : (wide ? 256 : 512)) / tiles;
+  // wide tiles: a 192-block budget (10 splits for the 128-channel ResnetBlock convs) — in the
+  // two-lane step fewer, longer blocks beat one block per CU (same box, r03k: 13.14 ms at 192,
+  // 13.20 at 128, 13.36 at 256: the split-K slabs and their reduce shrink, the other lane
+  // fills the CUs left)
+  int s = (budget > 0 ? budget : (wide ? 192 : 512)) / tiles;
   const int by_len = nseg / (4 * kR);
   if (s > by_len) s = by_len;
   if (s > max_splits) s = max_splits;

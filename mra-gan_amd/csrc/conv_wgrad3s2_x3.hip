@@ -251,7 +251,11 @@ int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   const int tg = s2_tg(a);
   const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
   const int tiles = (a.Cd / kTD) * (a.Cg / tg) * 9;
-  int s = (tg == 64 ? 256 : 512) / tiles;
+  static const int scale = [] {                               // A/B switch: MRAGAN_W3S2_BUDGET (percent)
+    const char* e = getenv("MRAGAN_W3S2_BUDGET");
+    return e ? atoi(e) : 100;
+  }();
+  int s = (tg == 64 ? 256 : 512) * scale / 100 / tiles;
   const int by_len = nseg / (4 * kR);
   if (s > by_len) s = by_len;
   if (s > max_splits) s = max_splits;

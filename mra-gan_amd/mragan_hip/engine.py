@@ -105,15 +105,16 @@ class ConvLayer:
                           bias=bias, act=act, transposed=self.transposed, wsplit=self.ws_fwd)
 
     def forward_in_stats(self, x):
-        """forward() of a bias-free conv feeding an InstanceNorm; on the brick kernel (k3 s1,
-        16-bit MFMA modes) it also leaves the IN statistics partials.  Returns (y, part, chunks);
-        chunks = 0 when no partials were produced."""
-        if self.ws_fwd is None or self.transposed or self.k != 3 or self.s != 1 or _NO_IN_STATS:
+        """forward() of a bias-free conv feeding an InstanceNorm; in the MFMA modes the brick
+        kernel (k3 s1) and the implicit GEMM (no K split) also leave the IN statistics partials.
+        Returns (y, part, chunks); chunks = 0 when no partials were produced."""
+        if _NO_IN_STATS or ops.get_conv_precision() == "f32" or min(self.cin, self.cout) < 8:
             return self.forward(x), None, 0
         N, D, H, W, _ = x.shape
         osp = self.out_spatial(D, H, W)
         part = ops.in_partials_buffer(N, osp, self.cout, x.device)
-        y, chunks = ops.conv3d_in_stats(x, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
+        y, chunks = ops.conv3d_in_stats(x, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part,
+                                        transposed=self.transposed)
         return y, part, chunks
 
     def forward_in_stats_op16(self, x16):
@@ -294,12 +295,15 @@ class NetPlan:
             else:
                 bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
                 if st.norm is not None:
-                    sc.h = st.conv.forward(cur)
+                    # the conv's epilogue leaves the norm's statistics partials where it can
+                    sc.h, part, chunks = st.conv.forward_in_stats(cur)
                     if want16 and self._op16_blocks_ok(sc.h.shape[3]):
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad,
+                                                                                part=part, chunks=chunks,
                                                                                 want_f32=True)
                     else:
-                        sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad)
+                        sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad, part=part,
+                                                                    chunks=chunks)
                 else:
                     sc.h = st.conv.forward(cur, bias=bias, act=st.act)     # activated output
                     sc.out = ops.rpad(sc.h, ypad) if ypad else sc.h

@@ -217,17 +217,19 @@ def in_partials_buffer(N: int, out_spatial: Sequence[int], cout: int, device) ->
     return torch.empty(N * Do * (-(-Ho // 4)) * (-(-Wo // 6)) * cout * 2, device=device, dtype=torch.float64)
 
 
+
 def conv3d_in_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
-                    wsplit: torch.Tensor, part: torch.Tensor, transposed: bool = False):
-    """conv3d (presplit weights, no bias / act) that also leaves the following InstanceNorm's
-    statistics partials in `part` when the brick kernel runs it (ABI 9).  Returns (out, chunks);
+                    wsplit: Optional[torch.Tensor], part: torch.Tensor, transposed: bool = False):
+    """conv3d (presplit weights if any, no bias / act) that also leaves the following
+    InstanceNorm's statistics partials in `part` when the kernel that runs it produces them (the
+    brick, ABI 9; the 16-bit implicit GEMM without a K split, ABI 11).  Returns (out, chunks);
     chunks = 0: no partials, run instnorm_fwd as usual."""
     _check(x, "conv3d.x")
     N, Di, Hi, Wi, cin = x.shape
     Do, Ho, Wo = out_spatial
     if wp.numel() != k ** 3 * cin * cout:
         raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
-    if wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
         raise ValueError("conv3d: wsplit size does not match the packed weight")
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("conv3d_in_stats: part must be a float64 device tensor")

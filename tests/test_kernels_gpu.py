@@ -576,6 +576,41 @@ def test_op16_rejected_outside_16bit_modes(ops):
         ops.set_conv_precision("f32")
 
 
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p,tr,expect", [
+    (2, 32, 64, 16, 3, 2, 1, False, True),      # G down1 (k3 s2 p1)
+    (2, 64, 128, 32, 3, 2, 1, False, True),     # G down2 (16³ outputs: no K split)
+    (2, 128, 64, 8, 3, 2, 1, True, True),       # G up1 (ConvTranspose3d k3 s2 p1 op1)
+    (2, 32, 64, 16, 4, 2, 1, False, False),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
+    (1, 128, 256, 8, 4, 1, 1, False, False),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
+])
+def test_igemm_in_stats_partials(x3, N, cin, cout, S, k, s, p, tr, expect):
+    """ABI 11: the 16-bit implicit GEMM's epilogue InstanceNorm partials (no K split, tiles inside
+    one instance and class) feed mragan_instnorm_fwd_partials; output, mean / rstd and the
+    normalised tensor match the statistics-pass path."""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 7 + cin + cout + S + k)
+    x = torch.randn(N, cin, S, S, S, generator=g, dtype=torch.float64)
+    shape_w = (cin, cout, k, k, k) if tr else (cout, cin, k, k, k)
+    w = torch.randn(*shape_w, generator=g, dtype=torch.float64) * 0.05
+    xg = ndhwc(x.float()).cuda()
+    wp = pack(ops, w, tr, False)
+    if tr:
+        o = ops.convT_out_size(S, k, s, p, 1)
+    else:
+        o = ops.conv_out_size(S, k, s, p)
+    osp = (o, o, o)
+    y_ref = ops.conv3d(xg, wp, cout, k, s, p, osp, transposed=tr)
+    part = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y, chunks = ops.conv3d_in_stats(xg, wp, cout, k, s, p, osp, None, part, transposed=tr)
+    if expect:
+        assert chunks > 0
+    assert torch.equal(y, y_ref)
+    z_ref, m_ref, r_ref = ops.instnorm_fwd(y_ref, act="lrelu", ypad=1)
+    z, m, r = ops.instnorm_fwd(y, act="lrelu", ypad=1, part=part, chunks=chunks)
+    assert rel(m, m_ref) < 1e-6 and rel(r, r_ref) < 1e-6
+    assert rel(z, z_ref) < 1e-6
+
+
 def test_instnorm_single_voxel_raises(ops):
     from mragan_hip import MraganError
     with pytest.raises(MraganError, match="more than 1 spatial element"):
