@@ -54,11 +54,12 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--source", default=None, help="what was profiled (recorded in the entry)")
     a = ap.parse_args()
-    # a launch class may be several kernels (e.g. "wgrad3_x3_kernel,wgrad_reduce_kernel"): per-launch
+    # a launch class may be several kernels (e.g. "wgrad3_x3_kernel;wgrad_reduce_kernel", ';'-separated:
+    # template names hold commas): per-launch
     # averages of each, summed
     fetch_kib = write_kib = 0.0
     nf = nw = 0
-    for k in a.kernel.split(","):
+    for k in a.kernel.split(";"):
         f, n1 = per_launch(a.fetch, "FETCH_SIZE", k)
         w, n2 = per_launch(a.write, "WRITE_SIZE", k)
         fetch_kib += f
