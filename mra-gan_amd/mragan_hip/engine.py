@@ -31,6 +31,11 @@ _NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") 
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
+# A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
+_FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") or "0"))
+               # the library's A/B switches that send those convs to the fp32-pack kernels
+               or any(v in __import__("os").environ for v in ("MRAGAN_NO_BRICK", "MRAGAN_BRICK_STAGED",
+                                                              "MRAGAN_DGRAD_SPLIT")))
 
 IN_MOMENTUM = 0.1
 
@@ -77,15 +82,23 @@ class ConvLayer:
         # pre-split 16-bit fragment copies for the brick kernel, refreshed by the same pack launch
         # (tr 2|3: bf16 hi/lo — the bf16x3 and bf16 modes; tr 4|5: fp16 — the fp16 mode)
         (_, A, B, _, tf, _), (_, _, _, _, tb, _) = out
-        base = 4 if ops.get_conv_precision() == "fp16" else 2
-        if self._splittable(self.k, self.s, self.cout, self.cin):
+        prec = ops.get_conv_precision()
+        base = 4 if prec == "fp16" else 2
+        split_f = self._splittable(self.k, self.s, self.cout, self.cin)
+        split_b = self._splittable(self.k, self.s, self.cin, self.cout)
+        if split_f:
             if self.ws_fwd is None or self.ws_fwd.device != w.device:
                 self.ws_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             out.append((w, A, B, T, base + int(tf), self.ws_fwd))
-        if self._splittable(self.k, self.s, self.cin, self.cout):
+        if split_b:
             if self.ws_bwd is None or self.ws_bwd.device != w.device:
                 self.ws_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             out.append((w, A, B, T, base + int(tb), self.ws_bwd))
+        if prec != "f32" and split_f and split_b and not self.transposed and not _FP32_PACKS:
+            # the MFMA-mode brick kernels read only the pre-split copies of a k3 s1 ResnetBlock
+            # conv (forward and data gradient): its two fp32 packs are not refreshed (the repack
+            # moves half the bytes; a mode switch repacks, ensure_packed)
+            out = out[2:]
         return out
 
     def repack(self):
