@@ -7,11 +7,13 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "lib")
-OBJ = os.path.join(HERE, "build")
+# MRAGAN_LIB_DIR / MRAGAN_OBJ_DIR / MRAGAN_EXTRA_FLAGS: variant builds for same-box A/B
+# (tools/gpu_libs_ab.sh); the default is the in-tree library the package loads
+LIB = os.environ.get("MRAGAN_LIB_DIR", os.path.join(HERE, "lib"))
+OBJ = os.environ.get("MRAGAN_OBJ_DIR", os.path.join(HERE, "build"))
 ARCH = os.environ.get("MRAGAN_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+         "-Wno-unused-variable", "-Wno-unused-but-set-variable"] + os.environ.get("MRAGAN_EXTRA_FLAGS", "").split()
 
 
 def sources():

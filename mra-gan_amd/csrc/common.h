@@ -67,8 +67,18 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // loaded value makes the compiler wait for each load before issuing the next one.
 // Build the descriptor from wave-uniform values only (cdna_hip_programming.md T8 / T20).
 constexpr uint32_t kOobOffset = 0x80000000u;
+// The base and size go through readfirstlane: a descriptor the compiler cannot prove uniform
+// (e.g. a base offset by an instance index derived from blockIdx through divisions) lands in
+// VGPRs, and every load through it becomes a waterfall loop (4 readfirstlane + 64-bit compares +
+// exec juggling per load — found in conv_brick_x3's halo loads).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+#ifdef MRAGAN_RSRC_NO_RFL   // A/B baseline (tools/gpu_libs_ab.sh)
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+#endif
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  void* ub = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 __device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));

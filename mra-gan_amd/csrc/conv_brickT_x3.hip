@@ -98,6 +98,7 @@ struct BrickTArgs {
   float* y; int Do, Ho, Wo, ny;            // ny = 32
   int k, p, act;
   int nbd, nbh, nbw;
+  double* part;                            // optional: the next InstanceNorm's Σy / Σy² per brick
 };
 
 template <int K, int PM>
@@ -246,6 +247,7 @@ brickT_x3_kernel(BrickTArgs a) {
   const int q = lane & 7;                                   // read-back: channel quad 4q … 4q+3
   float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + 4 * q);
+  double ps[4] = {0.0, 0.0, 0.0, 0.0}, pq[4] = {0.0, 0.0, 0.0, 0.0};   // InstanceNorm partials (a.part)
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
@@ -270,9 +272,47 @@ brickT_x3_kernel(BrickTArgs a) {
         // non-temporal: the 134 MB output stream otherwise evicts the weight fragments every
         // block re-reads from L2 (measured 165 → 132 µs at 4 × 64³ × 32)
         __builtin_nontemporal_store(f32x4{r.x, r.y, r.z, r.w}, reinterpret_cast<f32x4*>(dst));
+        if (a.part) {
+          ps[0] += r.x; ps[1] += r.y; ps[2] += r.z; ps[3] += r.w;
+          pq[0] += (double)r.x * r.x; pq[1] += (double)r.y * r.y; pq[2] += (double)r.z * r.z; pq[3] += (double)r.w * r.w;
+        }
       }
     }
     if (half == 0) __syncthreads();
+  }
+  // the consumer InstanceNorm's per-(instance, channel) Σy / Σy² of this brick (its separate
+  // statistics pass over the 64³ output disappears): the 8 lanes of a channel quad add by
+  // shuffles, the 4 waves through LDS past the epilogue rows (4 × 128 rows × kRow)
+  if (a.part) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        ps[k] += __shfl_xor(ps[k], m);
+        pq[k] += __shfl_xor(pq[k], m);
+      }
+    }
+    double* red = reinterpret_cast<double*>(smem + 4 * 128 * kRow);   // [4 waves][32 channels][2]
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        red[(wave * 32 + 4 * q + k) * 2] = ps[k];
+        red[(wave * 32 + 4 * q + k) * 2 + 1] = pq[k];
+      }
+    }
+    __syncthreads();
+    if (tid < 32) {
+      double s2 = 0.0, q2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        s2 += red[(w * 32 + tid) * 2];
+        q2 += red[(w * 32 + tid) * 2 + 1];
+      }
+      const int chunks = a.nbd * a.nbh * a.nbw, brick = (bd_i * a.nbh + bh_i) * a.nbw + bw_i;
+      double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + tid) * 2;
+      dst[0] = s2;
+      dst[1] = q2;
+    }
   }
 }
 
@@ -319,6 +359,11 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, kOH); a.nbw = ceil_div(g.Wo, kOW);
   const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
   if (blocks == 0) return kOk;
+  static const bool no_stats = getenv("MRAGAN_NO_BRICKT_STATS") != nullptr;   // A/B switch
+  if (g.in_part && !no_stats) {           // conv3d_in_stats: the following InstanceNorm's partials
+    a.part = g.in_part;
+    if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
+  }
   if (g.k == 3) launch_brickT<3, PM>(a, (unsigned)blocks, st);
   else launch_brickT<4, PM>(a, (unsigned)blocks, st);
   return check_launch("brickT_x3");

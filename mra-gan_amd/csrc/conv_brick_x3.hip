@@ -26,6 +26,15 @@
 #include "kernels.h"
 #include "prec.h"
 
+// build-time A/B knobs of the one-plane modes (tools/gpu_libs_ab.sh): weight prefetch distance
+// (one n-tile) and A-fragment read distance, in steps
+#ifndef MRAGAN_BRICK_KPF1
+#define MRAGAN_BRICK_KPF1 9
+#endif
+#ifndef MRAGAN_BRICK_KAD1
+#define MRAGAN_BRICK_KAD1 2
+#endif
+
 namespace mragan {
 
 namespace {
@@ -106,9 +115,9 @@ conv_brick_x3_kernel(BrickArgs a) {
   static_assert(BN % 32 == 0 && BM % 32 == 0, "tile");
   // weight prefetch distance in steps; divides kSteps so a ring slot maps to the same step
   // residue in every chunk
-  constexpr int kPF = 9;
+  constexpr int kPF = (!prec::has_lo<PM>() && TN == 1) ? MRAGAN_BRICK_KPF1 : 9;
   constexpr int kP = 18;                             // unrolled period: ring slots compile-time
-  constexpr int kAD = prec::has_lo<PM>() ? 1 : 2;    // A-fragment read distance (steps)
+  constexpr int kAD = prec::has_lo<PM>() ? 1 : MRAGAN_BRICK_KAD1;    // A-fragment read distance (steps)
   static_assert(kP % (kAD + 1) == 0, "A ring period");
   static_assert(kSteps % kP == 0 && kP % kPF == 0 && kP % 9 == 0 && kHD < kPF, "step period");
 
@@ -433,10 +442,21 @@ static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_b
     const char* e = getenv("MRAGAN_BRICK_VAR");
     return e ? atoi(e) : 0;
   }();
+  // one-plane modes (bf16 / fp16): one MFMA per 32×32 tile and step, so the 8-wave tiles' weight
+  // loads (1 KB per wave per MFMA, each fragment loaded by 2–4 waves) outrun the L1 → SIMD return
+  // rate (≈ 64 B per clock per CU) and pace the MFMAs.  These tiles run one wave per SIMD with 64
+  // GEMM rows × 32 columns per wave: half the weight bytes per MFMA (128×64: 24.7 vs 26.1 µs,
+  // res dgrad [2×18³] 22.5 vs 26.2 µs, profiles/r03q/ – r03s/).  var 5 = the 8-wave tiles (A/B).
+  // The 128×128 tile keeps its 8 waves: with 64×32 per wave its weight loads per MFMA already
+  // match these, and the 18³ data gradient at N = 4 runs it in one round (30.2 µs against 32.7 /
+  // 33.0 µs for 432 blocks of 128×64 / 64×128).
+  const bool onep = !prec::has_lo<PM>() && var != 5;
   if (bm == 128 && bn == 128 && var == 1) return launch_brick_x3<1, 4, 4, 1, 400, PM>(a, st);
   if (bm == 128 && bn == 128 && var == 2) return launch_brick_x3<2, 2, 2, 2, 400, PM>(a, st);
   if (bm == 128 && bn == 128) return launch_brick_x3<2, 4, 2, 1, 400, PM>(a, st);
+  if (bm == 128 && (onep || var == 4)) return launch_brick_x3<2, 2, 2, 1, 400, PM>(a, st);
   if (bm == 128) return launch_brick_x3<4, 2, 1, 1, 400, PM>(a, st);
+  if (bn == 128 && (onep || var == 3)) return launch_brick_x3<1, 4, 2, 1, 300, PM>(a, st);
   if (bn == 128) return launch_brick_x3<2, 2, 1, 2, 300, PM>(a, st);
   return launch_brick_x3<2, 2, 1, 1, 300, PM>(a, st);
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box kernel A/B by environment switch: kbench ops under a rocprofv3 kernel trace, once per
-# "VAR=VALUE" setting ("-" = none), printing each kernel's mean.
+# "VAR=VALUE[;VAR=VALUE]" setting ("-" = none), printing each kernel's mean.
 #   bash tools/gpu_ab_env.sh TAG PREC N OPS "- MRAGAN_X=1"
 set -eo pipefail
 TAG=$1; PREC=$2; N=$3; OPS=$4; SETS=${5:-"-"}
@@ -13,7 +13,8 @@ source tools/gpu_step.sh
 i=0
 for e in $SETS; do
   i=$((i + 1))
-  if [ "$e" = "-" ]; then envs=(); else envs=(env "$e"); fi
+  envs=()
+  if [ "$e" != "-" ]; then IFS=';' read -ra envs <<< "$e"; envs=(env "${envs[@]}"); fi
   step "kb $e" 120 "${envs[@]}" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$i" -o run -- \
       python3 tools/kbench.py --ops "$OPS" --reps 20 --precision "$PREC" --N "$N" > "$O/kb_$i.log" 2>&1
   python3 - "$O/kt_$i" "$e" <<'PY'
