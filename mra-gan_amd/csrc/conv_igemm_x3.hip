@@ -44,7 +44,16 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   constexpr int B_LOADS = (BN * LPR + 255) / 256;
   constexpr int ROWS_PER_PASS = 256 / LPR;
   constexpr int PLANE_A = BM * LDK, PLANE_B = BN * LDK;   // bf16 elements per plane
-  constexpr int STAGE = 2 * (PLANE_A + PLANE_B);          // hi+lo of A and B
+  // hi (+ lo in bf16x3) planes of A and B.  The one-plane modes drop the lo planes of the 2-tile
+  // waves' blocks: 128×64 at 31 instead of 62 KB, two more blocks per CU (G down1 [4×64³]: 64.6
+  // vs 71.2 µs); the 64×64 tile keeps them — at 7 blocks per CU it ran 9 % slower
+  // (profiles/r03u/)
+#ifdef MRAGAN_IG_TWO_PLANES   // A/B baseline (build variant)
+  constexpr int NPL = 2;
+#else
+  constexpr int NPL = (prec::has_lo<PM>() || TM * TN == 1) ? 2 : 1;
+#endif
+  constexpr int STAGE = NPL * (PLANE_A + PLANE_B);
   static_assert(WM * WN == 4, "4 waves");
   static_assert(BK % 16 == 0, "bf16 MFMA consumes K in 16s");
 
@@ -185,9 +194,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
       if (r < BN) {
         uint2 hi, lo;
         prec::split4<PM>(rb_[i], hi, lo);
-        *reinterpret_cast<uint2*>(st + 2 * PLANE_A + r * LDK + 4 * q) = hi;
+        *reinterpret_cast<uint2*>(st + NPL * PLANE_A + r * LDK + 4 * q) = hi;
         if constexpr (prec::has_lo<PM>())
-          *reinterpret_cast<uint2*>(st + 2 * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
+          *reinterpret_cast<uint2*>(st + NPL * PLANE_A + PLANE_B + r * LDK + 4 * q) = lo;
       }
     }
   };
@@ -221,7 +230,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
     const __bf16* Ah = smem + buf * STAGE;
     const __bf16* Al = Ah + PLANE_A;
-    const __bf16* Bh = Ah + 2 * PLANE_A;
+    const __bf16* Bh = Ah + NPL * PLANE_A;
     const __bf16* Bl = Bh + PLANE_B;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
