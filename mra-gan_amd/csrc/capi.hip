@@ -56,8 +56,11 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act, g_conv_precision};
-    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride))
+    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride)) {
+      a.in_part = in_part;
+      a.in_chunks = in_chunks;
       return conv_thin1_x3(a, g_conv_precision, ws, ws_bytes, st);
+    }
     if (g_conv_precision != MRAGAN_PREC_F32 && thinn_x3_applicable(cin, cout, k, stride))
       return conv_thinn_x3(a, g_conv_precision, ws, ws_bytes, st);
     return conv_thin(a, st);

@@ -164,6 +164,7 @@ struct Thin1RArgs {
   float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo][32]
   int pe, act;
   int nbh, nbw, L, nch, items;
+  double* part;                           // optional: the next InstanceNorm's Σy / Σy² per item
 };
 
 // forward brick: 16 rows × 16 columns per depth step, 4 rows (2 tiles) per wave
@@ -171,6 +172,7 @@ constexpr int kFH = 16;
 constexpr int kFRH = kFH + kK - 1;      // 22 X8 rows per plane
 constexpr int kFPlaneE = kFRH * kBW;    // 352 entries per plane (hi or lo)
 constexpr int kFLds = 2 * kRing * kFPlaneE * 16 + kGroups * 2 * kC * 16;   // ring + weights: 141 312 B
+constexpr int kFRed = 4 * kC * 2 * 8;   // + [4 waves][32 channels][Σ, Σ²] doubles (a.part)
 
 template <int PM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_fwd_kernel(Thin1RArgs a) {
@@ -219,6 +221,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     __syncthreads();
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
 
+    // InstanceNorm partials of this item (a.part): lane (li, lh) holds channels 16·lh + q of its
+    // voxels; fp32 over the item's ≤ 2·L values per lane, fp64 across lanes and waves
+    float ps[16], pq[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ps[q] = pq[q] = 0.f;
     for (int s = 0; s < nsteps; ++s) {
       const bool more = s + kK < nplanes;
       float n0[8], n1[8];
@@ -261,8 +268,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             if (a.act != kActNone)
               v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
             *reinterpret_cast<float4*>(yv + 4 * q) = v;
+            if (a.part) {
+              ps[4 * q] += v.x; ps[4 * q + 1] += v.y; ps[4 * q + 2] += v.z; ps[4 * q + 3] += v.w;
+              pq[4 * q] += v.x * v.x; pq[4 * q + 1] += v.y * v.y; pq[4 * q + 2] += v.z * v.z; pq[4 * q + 3] += v.w * v.w;
+            }
           }
         }
+      }
+      __syncthreads();
+    }
+    if (a.part) {
+      // item = nb · (items per instance) + (chunk · nbh + chh) · nbw + cw: the partials' chunk order
+      double* red = reinterpret_cast<double*>(smem + kFLds);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        double s2 = ps[q], q2 = pq[q];
+#pragma unroll
+        for (int m = 1; m < 32; m <<= 1) {
+          s2 += __shfl_xor(s2, m);
+          q2 += __shfl_xor(q2, m);
+        }
+        if (li == 0) {
+          red[(wave * kC + 16 * lh + q) * 2] = s2;
+          red[(wave * kC + 16 * lh + q) * 2 + 1] = q2;
+        }
+      }
+      __syncthreads();
+      if (tid < kC) {
+        double s2 = 0.0, q2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          s2 += red[(w * kC + tid) * 2];
+          q2 += red[(w * kC + tid) * 2 + 1];
+        }
+        double* dst = a.part + ((int64_t)item * kC + tid) * 2;
+        dst[0] = s2;
+        dst[1] = q2;
       }
       __syncthreads();
     }
@@ -305,7 +346,12 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   int grid = 1;
   pick_chunk(columns, t.Do, cu_count(), a.L, a.nch, grid);
   a.items = (int)(columns * a.nch);
-  const size_t lds = kFLds;
+  static const bool no_stats = getenv("MRAGAN_NO_THIN1_STATS") != nullptr;   // A/B switch
+  if (t.in_part && !no_stats && !t.trans && t.act == kActNone && !t.bias) {
+    a.part = t.in_part;                   // conv3d_in_stats: the stem InstanceNorm's partials
+    if (t.in_chunks) *t.in_chunks = a.nch * a.nbh * a.nbw;
+  }
+  const size_t lds = kFLds + kFRed;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM>),

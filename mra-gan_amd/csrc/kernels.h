@@ -75,6 +75,8 @@ struct ThinArgs {
   float* y; int Do, Ho, Wo, ny;
   int k, s, p, trans, act;
   int rnd;             // operand rounding (op_round): the precision mode, set by the C ABI
+  double* in_part = nullptr;   // optional (thin1_x3 forward only): the next InstanceNorm's Σy / Σy²
+  int* in_chunks = nullptr;    // set to the items per instance when in_part was filled
 };
 int conv_thin(ThinArgs a, hipStream_t st);
 // bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)

@@ -119,9 +119,11 @@ class ConvLayer:
 
     def forward_in_stats(self, x):
         """forward() of a bias-free conv feeding an InstanceNorm; in the MFMA modes the brick
-        kernel (k3 s1) and the implicit GEMM (no K split) also leave the IN statistics partials.
+        kernel (k3 s1), the implicit GEMM (no K split), brickT (32-channel ConvTranspose3d) and the
+        stem's thin1 kernel (k7, 1 → 32) also leave the IN statistics partials.
         Returns (y, part, chunks); chunks = 0 when no partials were produced."""
-        if _NO_IN_STATS or ops.get_conv_precision() == "f32" or min(self.cin, self.cout) < 8:
+        thin1 = self.cin == 1 and self.k == 7 and self.s == 1 and not self.transposed   # G stem (thin1_x3)
+        if _NO_IN_STATS or ops.get_conv_precision() == "f32" or (min(self.cin, self.cout) < 8 and not thin1):
             return self.forward(x), None, 0
         N, D, H, W, _ = x.shape
         osp = self.out_spatial(D, H, W)

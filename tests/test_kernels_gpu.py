@@ -582,6 +582,8 @@ def test_op16_rejected_outside_16bit_modes(ops):
     (2, 128, 64, 8, 3, 2, 1, True, True),       # G up1 (ConvTranspose3d k3 s2 p1 op1)
     (2, 64, 32, 8, 3, 2, 1, True, True),        # G up2 (32 output channels: brickT epilogue partials)
     (1, 64, 32, 6, 3, 2, 1, True, True),        # up2 form with partial 4×16×16 output bricks (12³)
+    (2, 1, 32, 22, 7, 1, 0, False, True),       # G stem (k7, 1 → 32: thin1 epilogue partials, 16³)
+    (1, 1, 32, 27, 7, 1, 0, False, True),       # stem form with partial 16×16 output columns (21³)
     (2, 32, 64, 16, 4, 2, 1, False, False),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
     (1, 128, 256, 8, 4, 1, 1, False, False),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
 ])
