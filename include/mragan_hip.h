@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 11
+#define MRAGAN_ABI_VERSION 12
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -196,6 +196,21 @@ int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const f
                                       int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
                                       float* g_out, const double* part, int chunks, void* ws, size_t ws_bytes,
                                       void* stream);
+/* The same for the G head (ABI 12; networks3D.py:211-213): the head conv (ngf → 1, k7 p0) reads
+ * ReplicationPad3d(3)(relu(IN(x))) of the last up-conv's output x.  mragan_conv3d_dgrad_in_stats
+ * is its data gradient — the transposed form (stride 1, pad 0) of the packed weight, output
+ * (Di+k−1)·(Hi+k−1)·(Wi+k−1)·cout fp32 — that also leaves the backward-statistics partials of that
+ * InstanceNorm, reading x_in ([N][Di+k−1−2·fold_pad]…[cout]) at the fold's clamp of every padded
+ * voxel, when the kernel that runs it has the epilogue (thin1_x3: cin 1, cout 32, k7, 16-bit
+ * MFMA modes); otherwise it computes the plain data gradient and *chunks = 0.
+ * mragan_instnorm_bwd_partials is mragan_instnorm_bwd (fp32 dx) from such partials. */
+int mragan_conv3d_dgrad_in_stats(const float* dy, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, int cout,
+                                 int k, float* y, void* ws, size_t ws_bytes, const float* x_in, const float* mean,
+                                 const float* rstd, int act, int fold_pad, double* part, size_t part_bytes, int* chunks,
+                                 void* stream);
+int mragan_instnorm_bwd_partials(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                                 const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out,
+                                 const double* part, int chunks, void* ws, size_t ws_bytes, void* stream);
 
 /* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
  * entry listing the per-instance statistics of the reference's sequential calls in call order. */

@@ -196,6 +196,38 @@ int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const f
   return instnorm_bwd_partials(a, InShape{N, D, H, W, C}, part, chunks, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
+int mragan_conv3d_dgrad_in_stats(const float* dy, int N, int Di, int Hi, int Wi, int cin, const float* w, int cout, int k,
+                                 float* y, void* ws, size_t ws_bytes, const float* x_in, const float* mean,
+                                 const float* rstd, int act, int fold_pad, double* part, size_t part_bytes, int* chunks,
+                                 void* stream) {
+  MRAGAN_CHECK_ARG(dy && w && y && x_in && mean && rstd && part && chunks, "conv3d_dgrad_in_stats: null pointer");
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && k >= 1, "conv3d_dgrad_in_stats: bad shape");
+  MRAGAN_CHECK_ARG(act == kActNone || act == kActRelu || act == kActLrelu, "conv3d_dgrad_in_stats: act %d", act);
+  const int Do = Di + k - 1, Ho = Hi + k - 1, Wo = Wi + k - 1;
+  MRAGAN_CHECK_ARG(fold_pad >= 0 && Do > 2 * fold_pad && Ho > 2 * fold_pad && Wo > 2 * fold_pad,
+                   "conv3d_dgrad_in_stats: fold %d does not fit the %d×%d×%d gradient", fold_pad, Do, Ho, Wo);
+  const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+  MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_dgrad_in_stats: partials %zu < %zu bytes", part_bytes, bound);
+  *chunks = 0;
+  if (g_conv_precision != MRAGAN_PREC_F32 && thin_side(cin, cout) && thin1_x3_applicable(cin, cout, k, 1)) {
+    ThinArgs a{dy, N, Di, Hi, Wi, cin, w, nullptr, y, Do, Ho, Wo, cout, k, 1, 0, 1, kActNone, g_conv_precision};
+    a.in_part = part; a.in_chunks = chunks;
+    a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act; a.bs_fold = fold_pad;
+    return conv_thin1_x3(a, g_conv_precision, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  }
+  // no kernel with the statistics epilogue for this shape / mode: the plain data gradient, chunks = 0
+  return conv_common(dy, N, Di, Hi, Wi, cin, w, nullptr, cout, k, 1, 0, kActNone, y, Do, Ho, Wo, 1, ws, ws_bytes, stream);
+}
+
+int mragan_instnorm_bwd_partials(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
+                                 const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out,
+                                 const double* part, int chunks, void* ws, size_t ws_bytes, void* stream) {
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx && part && ws, "instnorm_bwd_partials: null pointer");
+  MRAGAN_CHECK_ARG(!g_out || (g_out != dy && g_out != dy_add), "instnorm_bwd_partials: g_out aliases an operand");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, dx, g_out, nullptr, 0};
+  return instnorm_bwd_partials(a, InShape{N, D, H, W, C}, part, chunks, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
 int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
                              int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
                              size_t ws_bytes, void* stream) {

@@ -165,6 +165,10 @@ struct Thin1RArgs {
   int pe, act;
   int nbh, nbw, L, nch, items;
   double* part;                           // optional: the next InstanceNorm's Σy / Σy² per item
+  // optional (with part, transposed form = a data gradient): backward statistics of the
+  // InstanceNorm(+act) whose output, replication-padded by sfold, was the conv's input — x̂ at the
+  // clamped voxel c(o) = clamp(o − sfold) of every padded output: Σ g, Σ g·x̂ with g = y·act'(x̂)
+  const float* sx; const float* smean; const float* srstd; int sact, sfold;
 };
 
 // forward brick: 16 rows × 16 columns per depth step, 4 rows (2 tiles) per wave
@@ -223,15 +227,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 
     // InstanceNorm partials of this item (a.part): lane (li, lh) holds channels 16·lh + q of its
     // voxels; fp32 over the item's ≤ 2·L values per lane, fp64 across lanes and waves
-    float ps[16], pq[16];
+    float ps[16], pq[16], smu[16], srs[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ps[q] = pq[q] = 0.f;
+    for (int q = 0; q < 16; ++q) ps[q] = pq[q] = smu[q] = srs[q] = 0.f;
+    if (a.part && a.sx) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        smu[q] = a.smean[nb * kC + 16 * lh + q];
+        srs[q] = a.srstd[nb * kC + 16 * lh + q];
+      }
+    }
     for (int s = 0; s < nsteps; ++s) {
       const bool more = s + kK < nplanes;
       float n0[8], n1[8];
       if (more) {
         load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er0, w0 + ep, n0);
         if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er1, w0 + ep, n1);
+      }
+      // backward statistics: this step's x̂ operands, loaded before the MFMAs so their latency hides
+      // under them (loaded in the epilogue they stalled every depth step: +0.17 ms per step)
+      float4 sxv[2][4];
+      if (a.part && a.sx) {
+        const int Sd = a.Do - 2 * a.sfold, Sh = a.Ho - 2 * a.sfold, Sw = a.Wo - 2 * a.sfold;
+        const int cd = min(max(od0 + s - a.sfold, 0), Sd - 1), cw = min(max(ow0 + bw - a.sfold, 0), Sw - 1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int ch = min(max(oh0 + bh0 + 2 * i - a.sfold, 0), Sh - 1);
+          const float* xp = a.sx + ((((int64_t)nb * Sd + cd) * Sh + ch) * Sw + cw) * kC + 16 * lh;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sxv[i][q] = *reinterpret_cast<const float4*>(xp + 4 * q);
+        }
       }
       f32x16 acc[2] = {f32x16{}, f32x16{}};
 #pragma unroll
@@ -268,9 +293,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             if (a.act != kActNone)
               v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
             *reinterpret_cast<float4*>(yv + 4 * q) = v;
-            if (a.part) {
+            if (a.part && !a.sx) {
               ps[4 * q] += v.x; ps[4 * q + 1] += v.y; ps[4 * q + 2] += v.z; ps[4 * q + 3] += v.w;
               pq[4 * q] += v.x * v.x; pq[4 * q + 1] += v.y * v.y; pq[4 * q + 2] += v.z * v.z; pq[4 * q + 3] += v.w * v.w;
+            } else if (a.part) {
+              const float4 xv = sxv[i][q];
+              const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float xh = (xs[e] - smu[4 * q + e]) * srs[4 * q + e];
+                const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
+                                 : (a.sact == kActLrelu && !(xh > 0.f)) ? vs[e] * kLreluSlope : vs[e];
+                ps[4 * q + e] += gv;
+                pq[4 * q + e] += gv * xh;
+              }
             }
           }
         }
@@ -347,8 +383,13 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   pick_chunk(columns, t.Do, cu_count(), a.L, a.nch, grid);
   a.items = (int)(columns * a.nch);
   static const bool no_stats = getenv("MRAGAN_NO_THIN1_STATS") != nullptr;   // A/B switch
-  if (t.in_part && !no_stats && !t.trans && t.act == kActNone && !t.bias) {
-    a.part = t.in_part;                   // conv3d_in_stats: the stem InstanceNorm's partials
+  if (t.in_part && !no_stats && t.act == kActNone && !t.bias &&
+      (t.bs_x ? (t.trans && t.bs_fold >= 0 && t.Do > 2 * t.bs_fold && t.Ho > 2 * t.bs_fold && t.Wo > 2 * t.bs_fold)
+              : !t.trans)) {
+    // conv3d_in_stats: the stem InstanceNorm's partials; conv3d_dgrad_in_stats (the G head's data
+    // gradient): the backward statistics of the InstanceNorm in front of the head
+    a.part = t.in_part;
+    a.sx = t.bs_x; a.smean = t.bs_mean; a.srstd = t.bs_rstd; a.sact = t.bs_act; a.sfold = t.bs_fold;
     if (t.in_chunks) *t.in_chunks = a.nch * a.nbh * a.nbw;
   }
   const size_t lds = kFLds + kFRed;

@@ -77,6 +77,10 @@ struct ThinArgs {
   int rnd;             // operand rounding (op_round): the precision mode, set by the C ABI
   double* in_part = nullptr;   // optional (thin1_x3 forward only): the next InstanceNorm's Σy / Σy²
   int* in_chunks = nullptr;    // set to the items per instance when in_part was filled
+  // optional, with in_part on the transposed form (thin1_x3): backward statistics of the
+  // InstanceNorm(+act) of bs_x whose output, replication-padded by bs_fold, was the conv's input
+  const float* bs_x = nullptr; const float* bs_mean = nullptr; const float* bs_rstd = nullptr;
+  int bs_act = 0, bs_fold = 0;
 };
 int conv_thin(ThinArgs a, hipStream_t st);
 // bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -86,6 +86,11 @@ SIGNATURES = {
                                                 vp, sz, vp, vp]),
     "mragan_instnorm_bwd_partials_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32,
                                                 vp, sz, vp]),
+    # ABI 12: the G head's data gradient with the backward statistics of the IN in front of it
+    "mragan_conv3d_dgrad_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, sz, vp, vp, vp, i32, i32,
+                                           vp, sz, vp, vp]),
+    "mragan_instnorm_bwd_partials": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, vp, sz,
+                                           vp]),
 }
 
 _lock = threading.Lock()

@@ -28,6 +28,7 @@ from ._lib import call
 # A/B switch: MRAGAN_NO_IN_STATS=1 runs the ResnetBlock InstanceNorms with their own statistics
 # pass instead of the brick conv's epilogue partials
 _NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") or "0"))
+_NO_HEAD_STATS = __import__("os").environ.get("MRAGAN_NO_HEAD_STATS") is not None   # A/B: head dgrad without IN statistics
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -171,6 +172,21 @@ class ConvLayer:
         """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
         return ops.conv3d(dy, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial,
                           transposed=not self.transposed, wsplit=self.ws_bwd)
+
+    def dgrad_in_stats_ok(self):
+        """The G head (ngf → 1, k7 p0): its data gradient runs thin1_x3 in the MFMA modes, whose
+        epilogue can leave the backward statistics of the InstanceNorm in front of it (ABI 12)."""
+        return (not _NO_IN_STATS and not _NO_HEAD_STATS and ops.get_conv_precision() != "f32" and not self.transposed
+                and self.cout == 1
+                and self.k == 7 and self.s == 1 and self.p == 0)
+
+    def dgrad_in_stats(self, dy, in_spatial, norm_x, mean, rstd, act, fold_pad):
+        """dgrad() that also leaves the backward-statistics partials of the IN(+act) whose output,
+        replication-padded by fold_pad, was this conv's input.  Returns (dz, part, chunks)."""
+        part = ops.in_partials_buffer(dy.shape[0], in_spatial, self.cin, dy.device)
+        dz, chunks = ops.conv3d_dgrad_in_stats(dy, self.wp_bwd, self.cin, self.k, norm_x, mean, rstd, act, fold_pad,
+                                               part)
+        return dz, part, chunks
 
     def wgrad(self, x, dy, accumulate=True):
         g = self.m.weight.grad
@@ -343,6 +359,7 @@ class NetPlan:
         accumulated into the parameters' flat grad buffers.  Returns dL/dx (NDHWC) when
         need_input_grad (written to dx_out, plus dx_add if given)."""
         g, gpad, gadd = None, 0, None
+        bstats = None            # (part, chunks): backward statistics of the next IN, from the dgrad epilogue
         last = len(self.stages) - 1
         for i in range(last, -1, -1):
             st, sc = self.stages[i], ctx.stages[i]
@@ -388,7 +405,10 @@ class NetPlan:
                 continue
             conv = st.conv
             if st.norm is not None:
-                dh = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
+                if bstats is not None:
+                    dh = ops.instnorm_bwd_partials(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                else:
+                    dh = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
             else:
                 if i == last:
                     srcs = [t for t in dout if t is not None]
@@ -402,8 +422,19 @@ class NetPlan:
                 conv.wgrad(sc.inp, dh)
                 if st.use_bias and conv.m.bias is not None:
                     ops.channel_sum(dh, conv.m.bias.grad, accumulate=True)
+            bstats = None
             if want_dgrad:
-                g = conv.dgrad(dh, sc.inp.shape[1:4])
+                nxt = self.stages[i - 1] if i > 0 else None
+                if (nxt is not None and nxt.kind != "block" and nxt.norm is not None and st.prepad
+                        and conv.dgrad_in_stats_ok()):
+                    # the G head: its data gradient also accumulates the last up-conv IN's backward
+                    # statistics (the pad-3 statistics pass over dz and x goes)
+                    nsc = ctx.stages[i - 1]
+                    g, bpart, bchunks = conv.dgrad_in_stats(dh, sc.inp.shape[1:4], nsc.h, nsc.mean, nsc.rstd, nxt.act,
+                                                            st.prepad)
+                    bstats = (bpart, bchunks) if bchunks else None
+                else:
+                    g = conv.dgrad(dh, sc.inp.shape[1:4])
                 gpad, gadd = st.prepad, None
         if not need_input_grad:
             return None

@@ -514,6 +514,53 @@ def instnorm_bwd_partials_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.
     return dx16
 
 
+def conv3d_dgrad_in_stats(dy: torch.Tensor, wp: torch.Tensor, cout: int, k: int, x_in: torch.Tensor,
+                          mean: torch.Tensor, rstd: torch.Tensor, act, fold_pad: int, part: torch.Tensor):
+    """Data gradient (transposed form, stride 1, pad 0: output = input + k − 1 per dim) of a valid
+    conv whose input was ReplicationPad(fold_pad)(act(IN(x_in))), that also leaves that IN's
+    backward-statistics partials when its kernel has the epilogue (ABI 12: thin1_x3, the G head).
+    Returns (dz, chunks); chunks = 0: no partials (run instnorm_bwd)."""
+    _check(dy, "dgrad_in_stats.dy")
+    _check(x_in, "dgrad_in_stats.x_in")
+    N, Di, Hi, Wi, cin = dy.shape
+    osp = (Di + k - 1, Hi + k - 1, Wi + k - 1)
+    if tuple(x_in.shape) != (N,) + tuple(o - 2 * fold_pad for o in osp) + (cout,):
+        raise ValueError(f"dgrad_in_stats: x_in shape {tuple(x_in.shape)} does not match fold {fold_pad}")
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError("dgrad_in_stats: packed weight size mismatch")
+    if part.dtype != torch.float64 or not part.is_cuda:
+        raise ValueError("dgrad_in_stats: part must be a float64 device tensor")
+    out = torch.empty((N,) + osp + (cout,), device=dy.device, dtype=torch.float32)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, 1, 0, *osp, 1)
+    ws = WS.get(nbytes) if nbytes else None
+    chunks = _ct.c_int(0)
+    fn = lambda: call("mragan_conv3d_dgrad_in_stats", _ptr(dy), N, Di, Hi, Wi, cin, _ptr(wp), cout, k, _ptr(out),
+                      _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act], fold_pad, _ptr(part),
+                      part.numel() * 8, _ct.byref(chunks), _stream())
+    _timed(lambda: _conv_info(cin, cout, k, 1, 0, True, N, (Di, Hi, Wi), osp), fn)
+    return out, chunks.value
+
+
+def instnorm_bwd_partials(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int,
+                          dy_add: Optional[torch.Tensor], act, part: torch.Tensor, chunks: int,
+                          g_out: Optional[torch.Tensor] = None):
+    """instnorm_bwd (fp32 dx) from backward-statistics partials (conv3d_dgrad_in_stats)."""
+    _check(x, "instnorm_bwd.x")
+    N, D, H, W, C = x.shape
+    if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
+        raise ValueError(f"instnorm_bwd: dy shape {tuple(dy.shape)} does not match pad {dypad}")
+    dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+    nbytes = query("mragan_instnorm_workspace", N, D, H, W, C)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_instnorm_bwd_partials", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy),
+                      dypad, _ptr(dy_add), ACT[act], _ptr(dx), _ptr(g_out), _ptr(part), chunks, _ptr(ws), ws.numel(),
+                      _stream())
+    _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad} partials",
+                        bytes=4.0 * (2 * x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                     + (x.numel() if g_out is not None else 0))), fn)
+    return dx
+
+
 def conv3d_wgrad_op16(dense16: torch.Tensor, gathered16: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
                       accumulate: bool) -> torch.Tensor:
     """conv3d_wgrad on the operand planes of dense and gathered (the k3 s1 valid weight gradient)."""

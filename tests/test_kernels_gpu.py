@@ -565,6 +565,32 @@ def test_op16_dgrad_backward_statistics(op16, N, C, S, W, act):
     assert (got != plane).float().mean().item() < 1e-3
 
 
+@pytest.mark.parametrize("N,S,act", [(2, 16, "relu"), (1, 13, "lrelu")])
+def test_head_dgrad_backward_statistics(x3, N, S, act):
+    """ABI 12: the G head's data gradient (conv 32 → 1, k7 p0, transposed form on thin1_x3) leaves
+    the backward statistics of the InstanceNorm in front of the head (its output replication-
+    padded by 3): dz bit-identical to the plain data gradient, dx within fp32 summation-order
+    noise of the statistics-pass result."""
+    ops = x3
+    C, k, f = 32, 7, 3
+    g = torch.Generator().manual_seed(N * 17 + S)
+    x = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()                # up-conv output (pre-IN)
+    _, mean, rstd = ops.instnorm_fwd(x, act=act, ypad=f)
+    w = torch.randn(1, C, k, k, k, generator=g, dtype=torch.float64) * 0.02          # head Conv3d(32 → 1)
+    wp_b = pack(ops, w, False, True)
+    P = S + 2 * f
+    O = P - k + 1
+    dy = ndhwc(torch.randn(N, 1, O, O, O, generator=g).float()).cuda()
+    dz_ref = ops.conv3d(dy, wp_b, C, k, 1, 0, (P, P, P), transposed=True)
+    part = ops.in_partials_buffer(N, (P, P, P), C, "cuda")
+    dz, chunks = ops.conv3d_dgrad_in_stats(dy, wp_b, C, k, x, mean, rstd, act, f, part)
+    assert chunks > 0
+    assert torch.equal(dz, dz_ref)
+    ref = ops.instnorm_bwd(x, mean, rstd, dz, f, None, act=act)                      # statistics pass
+    got = ops.instnorm_bwd_partials(x, mean, rstd, dz, f, None, act, part, chunks)
+    assert rel(got, ref) < 1e-5
+
+
 def test_op16_rejected_outside_16bit_modes(ops):
     from mragan_hip import MraganError
     ops.set_conv_precision("bf16x3")
