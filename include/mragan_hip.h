@@ -211,6 +211,16 @@ int mragan_conv3d_dgrad_in_stats(const float* dy, int N, int Di, int Hi, int Wi,
 int mragan_instnorm_bwd_partials(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                                  const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out,
                                  const double* part, int chunks, void* ws, size_t ws_bytes, void* stream);
+/* The same without a fold, for the stride-2 layers (ABI 12): a conv (forward or transposed form,
+ * pre-split weights, no bias / act) whose output y is the data gradient of an InstanceNorm(+act)
+ * of x_in (same shape as y) — G down1 / up1 norms (networks3D.py:192-210) — leaving that norm's
+ * backward-statistics partials when the kernel that runs it has the epilogue (the 16-bit-MFMA
+ * implicit GEMM without a K split); otherwise the plain conv and *chunks = 0. */
+int mragan_conv3d_presplit_bwd_stats(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                                     const void* wsplit, int cout, int k, int stride, int pad, float* y, int Do, int Ho,
+                                     int Wo, int transposed, void* ws, size_t ws_bytes, const float* x_in,
+                                     const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                     int* chunks, void* stream);
 
 /* Running-stat update for a table of IN layers (device array of mragan_running_entry), each
  * entry listing the per-instance statistics of the reference's sequential calls in call order. */

@@ -219,6 +219,30 @@ int mragan_conv3d_dgrad_in_stats(const float* dy, int N, int Di, int Hi, int Wi,
   return conv_common(dy, N, Di, Hi, Wi, cin, w, nullptr, cout, k, 1, 0, kActNone, y, Do, Ho, Wo, 1, ws, ws_bytes, stream);
 }
 
+int mragan_conv3d_presplit_bwd_stats(const float* x, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                     const void* wsplit, int cout, int k, int stride, int pad, float* y, int Do, int Ho,
+                                     int Wo, int transposed, void* ws, size_t ws_bytes, const float* x_in,
+                                     const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                     int* chunks, void* stream) {
+  MRAGAN_CHECK_ARG(x && w && y && x_in && mean && rstd && part && chunks, "conv3d_presplit_bwd_stats: null pointer");
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_presplit_bwd_stats: transposed must be 0/1");
+  MRAGAN_CHECK_ARG(act == kActNone || act == kActRelu || act == kActLrelu, "conv3d_presplit_bwd_stats: act %d", act);
+  const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+  MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_presplit_bwd_stats: partials %zu < %zu bytes", part_bytes, bound);
+  *chunks = 0;
+  // the epilogue exists in the 16-bit-MFMA implicit GEMM (stride-2 layers); elsewhere the plain conv
+  if (stride < 2 || g_conv_precision == MRAGAN_PREC_F32)
+    return conv_common(x, N, Di, Hi, Wi, cin, w, nullptr, cout, k, stride, pad, kActNone, y, Do, Ho, Wo, transposed, ws,
+                       ws_bytes, stream, wsplit);
+  if (thin_side(cin, cout))
+    return conv_common(x, N, Di, Hi, Wi, cin, w, nullptr, cout, k, stride, pad, kActNone, y, Do, Ho, Wo, transposed, ws,
+                       ws_bytes, stream, wsplit);
+  IgemmArgs a{x, w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, kActNone, 1,
+              g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
+  a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act;
+  return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
 int mragan_instnorm_bwd_partials(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                                  const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out,
                                  const double* part, int chunks, void* ws, size_t ws_bytes, void* stream) {

@@ -360,7 +360,7 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
   if (blocks == 0) return kOk;
   static const bool no_stats = getenv("MRAGAN_NO_BRICKT_STATS") != nullptr;   // A/B switch
-  if (g.in_part && !no_stats) {           // conv3d_in_stats: the following InstanceNorm's partials
+  if (g.in_part && !no_stats && !g.bs_x) {   // conv3d_in_stats: the following InstanceNorm's partials
     a.part = g.in_part;
     if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
   }

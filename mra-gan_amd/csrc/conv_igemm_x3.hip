@@ -283,12 +283,16 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     return;
   }
   double ps[TN], pq[TN];                 // InstanceNorm statistics of the written values
+  // backward statistics instead (a.bs_x, ABI 12): y is the gradient of the InstanceNorm(+act) of
+  // bs_x (same shape, no fold): Σ g, Σ g·x̂ with g = y·act'(x̂)
+  const int snb = a.bs_x ? (int)(m0 / (Mc / a.N)) : 0;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     int col = n0 + wn0 + j * 32 + li;
     ps[j] = pq[j] = 0.0;
     if (col >= a.ny) continue;
     float bsum = a.bias ? a.bias[col] : 0.f;
+    const float smu = a.bs_x ? a.bs_mean[snb * a.ny + col] : 0.f, srs = a.bs_x ? a.bs_rstd[snb * a.ny + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -298,8 +302,16 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
         if (off >= 0) {
           const float v = act_fwd(acc[i][j][r] + bsum, a.act);
           a.y[(int64_t)off * a.ny + col] = v;
-          ps[j] += v;
-          pq[j] += (double)v * v;
+          if (a.bs_x) {
+            const float xh = (a.bs_x[(int64_t)off * a.ny + col] - smu) * srs;
+            const float gv = (a.bs_act == kActRelu && !(xh > 0.f)) ? 0.f
+                             : (a.bs_act == kActLrelu && !(xh > 0.f)) ? v * kLreluSlope : v;
+            ps[j] += gv;
+            pq[j] += (double)gv * xh;
+          } else {
+            ps[j] += v;
+            pq[j] += (double)v * v;
+          }
         }
       }
     }
@@ -460,7 +472,7 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
     const int bm = kX3Cfg[pl.cfg].bm;
     const int64_t per_cls = total_m / ((int64_t)a.N * a.nclass);
     const bool even = per_cls * a.N * a.nclass == total_m && per_cls == max_mc / a.N && max_mc % a.N == 0;
-    if (pl.splits == 1 && !a.shell && even && per_cls % bm == 0 && a.bias == nullptr) {
+    if (pl.splits == 1 && !a.shell && even && per_cls % bm == 0 && a.bias == nullptr && a.act == kActNone) {
       if (a.in_chunks) *a.in_chunks = (int)(a.nclass * (per_cls / bm));
     } else {
       a.in_part = nullptr;

@@ -91,6 +91,8 @@ SIGNATURES = {
                                            vp, sz, vp, vp]),
     "mragan_instnorm_bwd_partials": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, vp, sz,
                                            vp]),
+    "mragan_conv3d_presplit_bwd_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, i32,
+                                               i32, vp, sz, vp, vp, vp, i32, vp, sz, vp, vp]),
 }
 
 _lock = threading.Lock()

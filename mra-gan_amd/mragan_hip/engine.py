@@ -29,6 +29,7 @@ from ._lib import call
 # pass instead of the brick conv's epilogue partials
 _NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") or "0"))
 _NO_HEAD_STATS = __import__("os").environ.get("MRAGAN_NO_HEAD_STATS") is not None   # A/B: head dgrad without IN statistics
+_NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None       # A/B: stride-2 dgrads without them
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -186,6 +187,20 @@ class ConvLayer:
         part = ops.in_partials_buffer(dy.shape[0], in_spatial, self.cin, dy.device)
         dz, chunks = ops.conv3d_dgrad_in_stats(dy, self.wp_bwd, self.cin, self.k, norm_x, mean, rstd, act, fold_pad,
                                                part)
+        return dz, part, chunks
+
+    def dgrad_bwd_stats_ok(self):
+        """Stride-2 layers: their data gradient runs the 16-bit-MFMA implicit GEMM, whose epilogue
+        can leave the backward statistics of the (unpadded) InstanceNorm in front (ABI 12)."""
+        return (not _NO_IN_STATS and not _NO_S2_STATS and ops.get_conv_precision() != "f32" and self.s == 2
+                and min(self.cin, self.cout) >= 8)
+
+    def dgrad_bwd_stats(self, dy, in_spatial, norm_x, mean, rstd, act):
+        """dgrad() that also leaves the backward-statistics partials of the IN(+act) whose output
+        was this conv's input.  Returns (dz, part, chunks)."""
+        part = ops.in_partials_buffer(dy.shape[0], in_spatial, self.cin, dy.device)
+        dz, chunks = ops.conv3d_bwd_stats(dy, self.wp_bwd, self.cin, self.k, self.s, self.p, in_spatial, self.ws_bwd,
+                                          norm_x, mean, rstd, act, part, transposed=not self.transposed)
         return dz, part, chunks
 
     def wgrad(self, x, dy, accumulate=True):
@@ -432,6 +447,13 @@ class NetPlan:
                     nsc = ctx.stages[i - 1]
                     g, bpart, bchunks = conv.dgrad_in_stats(dh, sc.inp.shape[1:4], nsc.h, nsc.mean, nsc.rstd, nxt.act,
                                                             st.prepad)
+                    bstats = (bpart, bchunks) if bchunks else None
+                elif (nxt is not None and nxt.kind != "block" and nxt.norm is not None and not st.prepad
+                        and conv.dgrad_bwd_stats_ok()):
+                    # stride-2 layers: the data gradient's epilogue accumulates the next IN's
+                    # backward statistics (no fold: that IN's output is this conv's input)
+                    nsc = ctx.stages[i - 1]
+                    g, bpart, bchunks = conv.dgrad_bwd_stats(dh, sc.inp.shape[1:4], nsc.h, nsc.mean, nsc.rstd, nxt.act)
                     bstats = (bpart, bchunks) if bchunks else None
                 else:
                     g = conv.dgrad(dh, sc.inp.shape[1:4])

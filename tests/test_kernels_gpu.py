@@ -591,6 +591,38 @@ def test_head_dgrad_backward_statistics(x3, N, S, act):
     assert rel(got, ref) < 1e-5
 
 
+@pytest.mark.parametrize("N,cin,cout,S,k,tr,act,expect", [
+    (2, 128, 64, 16, 3, True, "relu", True),     # G down2's data gradient (convT form) → down1's IN
+    (2, 32, 64, 16, 3, True, "lrelu", True),     # convT form, 32 → 64 channels
+    (2, 32, 64, 32, 3, False, "relu", True),     # G up2's data gradient (forward form) → up1's IN
+    (1, 64, 32, 8, 3, True, "lrelu", False),     # 32 output channels: brickT, no epilogue → stats pass
+])
+def test_stride2_dgrad_backward_statistics(x3, N, cin, cout, S, k, tr, act, expect):
+    """ABI 12: the stride-2 data gradient's implicit-GEMM epilogue leaves the backward statistics of
+    the InstanceNorm whose output was the layer's input: output bit-identical to the plain conv, dx
+    within fp32 summation-order noise of the statistics-pass result.  (tr: the conv run here is
+    the transposed form, i.e. the data gradient of a forward stride-2 conv.)"""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 19 + cin + cout + S)
+    x = ndhwc(torch.randn(N, cin, S, S, S, generator=g).float()).cuda()
+    w = torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) * 0.05 if tr else \
+        torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.05
+    wp = pack(ops, w, tr, False)
+    o = ops.convT_out_size(S, k, 2, 1, 1) if tr else ops.conv_out_size(S, k, 2, 1)
+    osp = (o, o, o)
+    y_ref = ops.conv3d(x, wp, cout, k, 2, 1, osp, transposed=tr)
+    xin = ndhwc(torch.randn(N, cout, o, o, o, generator=g).float()).cuda()          # the IN's input
+    _, mean, rstd = ops.instnorm_fwd(xin, act=act)
+    part = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y, chunks = ops.conv3d_bwd_stats(x, wp, cout, k, 2, 1, osp, None, xin, mean, rstd, act, part, transposed=tr)
+    assert torch.equal(y, y_ref)
+    assert (chunks > 0) == expect
+    ref = ops.instnorm_bwd(xin, mean, rstd, y, 0, None, act=act)
+    if chunks:
+        got = ops.instnorm_bwd_partials(xin, mean, rstd, y, 0, None, act, part, chunks)
+        assert rel(got, ref) < 1e-5
+
+
 def test_op16_rejected_outside_16bit_modes(ops):
     from mragan_hip import MraganError
     ops.set_conv_precision("bf16x3")
