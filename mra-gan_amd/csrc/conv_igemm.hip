@@ -292,6 +292,7 @@ static int conv_igemm_x3_chunked(const IgemmArgs& a, int64_t max_mc, int64_t tot
   for (int n0 = 0; n0 < a.N; n0 += nb) {
     IgemmArgs c = a;
     c.in_part = nullptr;                 // instance ranges: no InstanceNorm partials (stats pass instead)
+    c.bs_x = nullptr;
     c.N = nb < a.N - n0 ? nb : a.N - n0;
     c.x = a.x + n0 * in_vol;
     c.y = a.y + n0 * out_vol;

@@ -478,6 +478,7 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
       a.in_part = nullptr;
     }
   }
+  if (!a.in_part) a.bs_x = nullptr;     // no partials: the epilogue skips the backward-statistics reads
   int rc = a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
                           : dispatch_x3<16>(a, max_mc, pl.cfg, pl.splits, st);
   if (rc || pl.splits == 1) return rc;
