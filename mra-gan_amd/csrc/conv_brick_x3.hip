@@ -419,6 +419,15 @@ static int launch_brick_x3(const BrickArgs& a, hipStream_t st) {
 // 117 KB LDS halo allows one block per CU, and two-per-SIMD (8-wave) variants spill at kPF = 9
 size_t conv_brick_x3_ws_bytes(int C, int ny) { return (size_t)kTaps * C * ny * sizeof(float); }
 
+// packed fp32 weights [27][ny][C] → the fragment-order copy in `out` (conv_brick_x3_ws_bytes)
+int brick_x3_pack(const float* w, int ny, int C, void* out, int mode, hipStream_t st) {
+  const int64_t groups = (int64_t)kTaps * ny * (C / 8);
+  const dim3 grid((unsigned)((groups + 255) / 256));
+  MRAGAN_PREC_DISPATCH(mode, hipLaunchKernelGGL(brick_x3_pack_kernel<PM>, grid, dim3(256), 0, st, w, ny, C,
+                                                static_cast<__bf16*>(out));
+                       return check_launch("brick_x3_pack"))
+}
+
 template <int PM>
 static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
   if (wsplit) {
@@ -429,10 +438,7 @@ static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_b
       set_error("conv_brick_x3: workspace %zu < %zu", ws_bytes, need);
       return kWorkspace;
     }
-    const int64_t groups = (int64_t)kTaps * a.ny * (a.C / 8);
-    hipLaunchKernelGGL(brick_x3_pack_kernel<PM>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a.w, a.ny,
-                       a.C, static_cast<__bf16*>(ws));
-    int rc = check_launch("brick_x3_pack");
+    const int rc = brick_x3_pack(a.w, a.ny, a.C, ws, PM, st);
     if (rc) return rc;
     a.wx3 = ws;
   }

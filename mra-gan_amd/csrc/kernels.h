@@ -62,6 +62,13 @@ bool full_dgrad_split_applicable(const IgemmArgs& a);
 int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, int mode,
                          hipStream_t st);
 size_t conv_brick_x3_ws_bytes(int C, int ny);
+int brick_x3_pack(const float* w, int ny, int C, void* out, int mode, hipStream_t st);
+// GEMM-row → brick-voxel permutation that makes the brick kernels' A reads bank-conflict free
+void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short* rowvox);
+// bf16 / fp16 k3 s1 brick with the contraction split over the block's 4 waves (conv_brick_ks.hip)
+bool conv_brick_ks_applicable(const IgemmArgs& a);
+int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* wsplit, int mode, int* in_chunks,
+                  hipStream_t st);
 bool conv_brick_x3_active(const IgemmArgs& a);
 // bf16x3 stride-2 transposed convolutions from an LDS halo (conv_brickT_x3.hip)
 bool brickT_x3_applicable(const IgemmArgs& a);
