@@ -461,7 +461,9 @@ int mragan_skip_count(int* flag, int* counter, void* stream) {
   return skip_count(flag, counter, static_cast<hipStream_t>(stream));
 }
 
-int mragan_debug_stamps(unsigned long long* host, int n) { return thin1_debug_stamps(host, n); }
+int mragan_debug_stamps(unsigned long long* host, int n) {
+  return n < 0 ? ks_debug_stamps(host, -n) : thin1_debug_stamps(host, n);
+}
 
 int mragan_fill(float* p, int64_t n, float value, void* stream) {
   MRAGAN_CHECK_ARG(p, "fill: null");

@@ -40,6 +40,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kTaps = 27;
@@ -56,6 +57,16 @@ constexpr size_t ks_region_bytes() {
 
 }  // namespace
 
+// diagnostic stamps (MRAGAN_STAMPS=1): s_memtime per wave at entry / tables ready / prologue done /
+// main loop done / reduction done / exit — 6 per wave, 4 waves per block (mragan_debug_stamps, n < 0)
+constexpr int kKsStampBlocks = 1024;
+__device__ unsigned long long g_ks_stamps[kKsStampBlocks * 24];
+#define KS_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (a.stamp && lane == 0 && blockIdx.x < kKsStampBlocks)                                          \
+      g_ks_stamps[blockIdx.x * 24 + wave * 6 + (i)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+
 template <int TN, int PM, int X16>
 __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   static_assert(!prec::has_lo<PM>(), "the K-split brick runs the one-plane modes");
@@ -67,12 +78,11 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   constexpr int LPS = X16 ? 1 : 2;                  // slices loaded per step
   constexpr int NLD = (NSL + LPS - 1) / LPS;        // steps that load
   constexpr int kHalf = kTaps;                      // steps per half-chunk (one tap each)
-  constexpr int kSteps = 2 * kHalf;                 // steps per 32-channel chunk
-  constexpr int kHD = 8;                            // a slice is stored kHD steps after its load
+  constexpr int kHD = X16 ? 8 : 2;                  // a slice is stored kHD steps after its load
   constexpr int kPF = 9;                            // weight prefetch distance (steps)
   constexpr int kAD = 2;                            // A-fragment read distance (steps)
   static_assert(NLD + kHD <= kHalf, "halo stream does not fit a half-chunk");
-  static_assert(kSteps % kPF == 0 && kSteps % (kAD + 1) == 0 && kHalf % (kHD + 1) == 0, "ring periods");
+  static_assert(kHalf % kPF == 0 && kHalf % (kAD + 1) == 0 && kHalf % (kHD + 1) == 0, "ring periods");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* out_off = reinterpret_cast<int*>(smem);      // [BM]
@@ -83,6 +93,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, lh = lane >> 5;
+  KS_STAMP(0);
 
   // tile → (instance, brick, n-block); XCD-aware order (n fastest, then bricks)
   int L = blockIdx.x, tile = L;
@@ -147,6 +158,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const char*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C * ES,
                                               (uint32_t)a.Di * a.Hi * a.Wi * a.C * (uint32_t)ES);
   __syncthreads();
+  KS_STAMP(1);
 
   // this lane's halo slices (the same positions for every half-chunk): element offset or −1
   int ho[NSL];
@@ -175,32 +187,49 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
       }
     }
   };
-  auto b_load = [&](int k, int s, bf16x8 (&dst)[TN]) __attribute__((always_inline)) {
-    const int t = s % kHalf, kk = s / kHalf;
-    const int tap = flip ? kTaps - 1 - t : t;
-    const int sb = __builtin_amdgcn_readfirstlane(((tap * nch + wave + 4 * k) * 2 + kk) * 2 * blkb);
+  // step (half-chunk g = 2k + h, tap t): weights of tap t (flipped for the transposed form), channels
+  // 16h … of chunk wave + 4k; the A fragments of tap t in half-slot h of the halo rows
+  // Per-step offsets are built from strides made opaque to the compiler once per step (an empty
+  // asm on SGPR copies): left alone, LICM hoists all 27 taps' offsets out of the half-chunk loop
+  // and the SGPR file overflows (spills to VGPR lanes and a scratch frame).
+  const int tstride = flip ? -nch * 4 * blkb : nch * 4 * blkb;     // weight bytes per tap
+  const int tbase = flip ? (kTaps - 1) * nch * 4 * blkb : 0;
+  const int wgb = wave * 4 * blkb;                                    // this wave's chunk, half 0
+  const int pstride = HH * HWd * kRowB, rstride = HWd * kRowB;       // halo bytes per d / h tap
+  auto b_load = [&](int g, int t, bf16x8 (&dst)[TN]) __attribute__((always_inline)) {
+    int ts = tstride, tb = tbase;
+    asm volatile("" : "+s"(ts), "+s"(tb));
+    const int sb = tb + t * ts + wgb + (g >> 1) * 16 * blkb + (g & 1) * 2 * blkb;
 #pragma unroll
     for (int j = 0; j < TN; ++j) dst[j] = __builtin_bit_cast(bf16x8, buf_load_16b(wr, boff[j], sb));
   };
-  auto a_read = [&](int s, bf16x8 (&dst)[TM]) __attribute__((always_inline)) {
-    const int t = s % kHalf, kk = s / kHalf;
-    const int tap_off = __builtin_amdgcn_readfirstlane((((t / 9) * HH + (t / 3) % 3) * HWd + t % 3) * kRowB + kk * 32);
+  auto a_read = [&](int g, int t, bf16x8 (&dst)[TM]) __attribute__((always_inline)) {
+    int ps = pstride, rs = rstride;
+    asm volatile("" : "+s"(ps), "+s"(rs));
+    const int tap_off = (t / 9) * ps + ((t / 3) % 3) * rs + (t % 3) * kRowB + (g & 1) * 32;
 #pragma unroll
     for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(Hw + abase[i] + tap_off);
   };
 
-  // prologue: half 0 of chunk 0 (all loads in flight before the first store), weights of the
-  // first kPF steps
-  {
-    float4 pv[NSL];
+  // prologue: half-chunk 0 (all loads in flight before the first store), weights of the first
+  // kPF steps, A fragments of the first kAD
+  constexpr int kPB = 13;                           // prologue slices in flight per batch
 #pragma unroll
-    for (int sl = 0; sl < NSL; ++sl) pv[sl] = halo_ld(0, 0, sl);
+  for (int s0 = 0; s0 < NSL; s0 += kPB) {
+    float4 pv[kPB];
 #pragma unroll
-    for (int sl = 0; sl < NSL; ++sl) halo_st(0, sl, pv[sl]);
+    for (int sl = 0; sl < kPB; ++sl)
+      if (s0 + sl < NSL) pv[sl] = halo_ld(0, 0, s0 + sl);
+#pragma unroll
+    for (int sl = 0; sl < kPB; ++sl)
+      if (s0 + sl < NSL) halo_st(0, s0 + sl, pv[sl]);
   }
   bf16x8 rb[kPF][TN];
 #pragma unroll
   for (int u = 0; u < kPF; ++u) b_load(0, u, rb[u]);
+  bf16x8 af[kAD + 1][TM];
+#pragma unroll
+  for (int v = 0; v < kAD; ++v) a_read(0, v, af[v]);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -208,49 +237,49 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
-  for (int k = 0; k < nck; ++k) {
-    const bool more = k + 1 < nck;
-    bf16x8 af[kAD + 1][TM];
-#pragma unroll
-    for (int v = 0; v < kAD; ++v) a_read(v, af[v]);
+  KS_STAMP(2);
+  // one loop iteration = one half-chunk (27 taps, unrolled: ring slots are compile-time because 9
+  // and 3 divide 27); the next half-chunk streams into the other half-slot meanwhile
+  const int nhalf = 2 * nck;
+  for (int g = 0; g < nhalf; ++g) {
+    const bool next = g + 1 < nhalf;
+    const int gn = next ? g + 1 : g;          // past the last half: harmless re-reads, no stores
     float4 rh[kHD + 1][LPS];
 #pragma unroll
-    for (int u = 0; u < kSteps; ++u) {
+    for (int t = 0; t < kHalf; ++t) {
       __builtin_amdgcn_sched_barrier(0);
-      const int h = u / kHalf, t = u % kHalf;
-      // the half-chunk streamed during this half: (k, 1) during half 0, (k + 1, 0) during half 1
-      const int sk = h == 0 ? k : k + 1, sh = h == 0 ? 1 : 0;
-      const bool stream = h == 0 || more;
-      if (t < NLD && stream) {
+      if (t < NLD && next) {
 #pragma unroll
         for (int l = 0; l < LPS; ++l)
-          if (t * LPS + l < NSL) rh[t % (kHD + 1)][l] = halo_ld(sk, sh, t * LPS + l);
+          if (t * LPS + l < NSL) rh[t % (kHD + 1)][l] = halo_ld(gn >> 1, gn & 1, t * LPS + l);
       }
-      if (t >= kHD && t - kHD < NLD && stream) {
+      if (t >= kHD && t - kHD < NLD && next) {
 #pragma unroll
         for (int l = 0; l < LPS; ++l)
-          if ((t - kHD) * LPS + l < NSL) halo_st(sh, (t - kHD) * LPS + l, rh[(t - kHD) % (kHD + 1)][l]);
+          if ((t - kHD) * LPS + l < NSL) halo_st(gn & 1, (t - kHD) * LPS + l, rh[(t - kHD) % (kHD + 1)][l]);
       }
-      // B fragments of this step (loaded kPF steps ago); refill the slot with step u + kPF
+      // B fragments of this step (loaded kPF steps ago); refill the slot with step + kPF
       bf16x8 bc[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bc[j] = rb[u % kPF][j];
-      if (u + kPF < kSteps) b_load(k, u + kPF, rb[u % kPF]);
-      else b_load(more ? k + 1 : k, u + kPF - kSteps, rb[u % kPF]);
-      // A fragments kAD steps ahead (the chunk's last steps read nothing ahead: the next chunk
-      // re-primes after its half-slot 0 was refilled during half 1)
-      if (u + kAD < kSteps) a_read(u + kAD, af[(u + kAD) % (kAD + 1)]);
+      for (int j = 0; j < TN; ++j) bc[j] = rb[t % kPF][j];
+      if (t + kPF < kHalf) b_load(g, t + kPF, rb[t % kPF]);
+      else b_load(gn, t + kPF - kHalf, rb[t % kPF]);
+      // A fragments kAD steps ahead (into the next half-chunk's slot near the end: stored at
+      // steps kHD … kHD + NLD − 1 of this half, before these reads)
+      if (t + kAD < kHalf) a_read(g, t + kAD, af[(t + kAD) % (kAD + 1)]);
+      else a_read(gn, t + kAD - kHalf, af[(t + kAD) % (kAD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const bf16x8& A = af[u % (kAD + 1)][i];
+          const bf16x8& A = af[t % (kAD + 1)][i];
           acc[i][j] = prec::mma<PM>(A, A, bc[j], bc[j], acc[i][j]);
         }
     }
   }
 
+  KS_STAMP(3);
   // K reduction: every wave leaves the partials of the three fragment rows it does not finish
   // (float4 quads, lane-contiguous: conflict-free 16-B stores / loads); wave w then sums rows
   // 32w … 32w + 31 over the waves in order 0, 1, 2, 3
@@ -262,9 +291,12 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
     if (i != wave) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          red[red_idx(i, wave, j, q)] = f32x4v{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+      {
+        red[red_idx(i, wave, j, 0)] = __builtin_shufflevector(acc[i][j], acc[i][j], 0, 1, 2, 3);
+        red[red_idx(i, wave, j, 1)] = __builtin_shufflevector(acc[i][j], acc[i][j], 4, 5, 6, 7);
+        red[red_idx(i, wave, j, 2)] = __builtin_shufflevector(acc[i][j], acc[i][j], 8, 9, 10, 11);
+        red[red_idx(i, wave, j, 3)] = __builtin_shufflevector(acc[i][j], acc[i][j], 12, 13, 14, 15);
+      }
     }
   }
   f32x16 own[TN];
@@ -284,18 +316,19 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   for (int src = 0; src < 4; ++src) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      f32x16 v = own[j];
-      if (src != wave) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4v r = red[red_idx(wave, src, j, q)];
-          v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
-        }
+      if (src == wave) {
+        fin[j] += own[j];
+      } else {
+        const f32x4v r0 = red[red_idx(wave, src, j, 0)], r1 = red[red_idx(wave, src, j, 1)],
+                     r2 = red[red_idx(wave, src, j, 2)], r3 = red[red_idx(wave, src, j, 3)];
+        const f32x8 r01 = __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const f32x8 r23 = __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7);
+        fin[j] += __builtin_shufflevector(r01, r23, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
       }
-      fin[j] += v;
     }
   }
 
+  KS_STAMP(4);
   // epilogue on rows 32w + …: bias / activation, output store, InstanceNorm partials
   const int wm0 = wave * 32;
   double ps[TN], pq[TN];
@@ -368,6 +401,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
       dst[1] = q2;
     }
   }
+  KS_STAMP(5);
 }
 
 template <int TN, int PM, int X16>
@@ -451,10 +485,17 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   const int64_t ntiles = (int64_t)a.N * a.nbd * a.nbh * a.nbw * a.gn;
   MRAGAN_CHECK_ARG(ntiles < ((int64_t)1 << 31), "conv_brick_ks: grid too large");
   a.ntiles = (int)ntiles;
+  static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
+  a.stamp = stamps;
   if (in_chunks && a.part) *in_chunks = a.nbd * a.nbh * a.nbw;
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, kKsBM, a.rowvox);
   MRAGAN_PREC_DISPATCH(mode, return brick_ks_launch_pm<PM>(a, best_tn, ws, ws_bytes, wsplit, st))
+}
+
+int ks_debug_stamps(unsigned long long* host, int n) {
+  if (n > kKsStampBlocks * 24) n = kKsStampBlocks * 24;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ks_stamps), (size_t)n * 8) == hipSuccess ? kOk : kLaunch;
 }
 
 }  // namespace mragan

@@ -53,6 +53,7 @@ struct BrickArgs {
   // ([N][Do−2][Ho−2][Wo−2][ny] fp32, statistics smean / srstd [N][ny]): part = Σ_p g, Σ_p g·x̂
   // with g = dz_p·act'(x̂) at the interior voxel p folds into (conv_brick_x3 only)
   const float* sx; const float* smean; const float* srstd; int sact;
+  int stamp;        // diagnostics: record s_memtime phase stamps (conv_brick_ks only)
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st, bool interior = false);
@@ -67,6 +68,7 @@ int brick_x3_pack(const float* w, int ny, int C, void* out, int mode, hipStream_
 void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short* rowvox);
 // bf16 / fp16 k3 s1 brick with the contraction split over the block's 4 waves (conv_brick_ks.hip)
 bool conv_brick_ks_applicable(const IgemmArgs& a);
+int ks_debug_stamps(unsigned long long* host, int n);
 int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* wsplit, int mode, int* in_chunks,
                   hipStream_t st);
 bool conv_brick_x3_active(const IgemmArgs& a);
