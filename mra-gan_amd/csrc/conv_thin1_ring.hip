@@ -226,10 +226,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
 
     // InstanceNorm partials of this item (a.part): lane (li, lh) holds channels 16·lh + q of its
-    // voxels; fp32 over the item's ≤ 2·L values per lane, fp64 across lanes and waves
-    float ps[16], pq[16], smu[16], srs[16];
+    // voxels; fp64 throughout, y² formed in fp64 as the other producers do (fp32 sums of y and y²
+    // lose var = E[y²] − E[y]² to cancellation by mean² / var — the stem reads a non-centred
+    // volume).  One wave per SIMD by design: the 32 extra registers cost no occupancy.
+    double ps[16], pq[16];
+    float smu[16], srs[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ps[q] = pq[q] = smu[q] = srs[q] = 0.f;
+    for (int q = 0; q < 16; ++q) {
+      ps[q] = pq[q] = 0.0;
+      smu[q] = srs[q] = 0.f;
+    }
     if (a.part && a.sx) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -295,7 +301,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             *reinterpret_cast<float4*>(yv + 4 * q) = v;
             if (a.part && !a.sx) {
               ps[4 * q] += v.x; ps[4 * q + 1] += v.y; ps[4 * q + 2] += v.z; ps[4 * q + 3] += v.w;
-              pq[4 * q] += v.x * v.x; pq[4 * q + 1] += v.y * v.y; pq[4 * q + 2] += v.z * v.z; pq[4 * q + 3] += v.w * v.w;
+              pq[4 * q] += (double)v.x * v.x; pq[4 * q + 1] += (double)v.y * v.y;
+              pq[4 * q + 2] += (double)v.z * v.z; pq[4 * q + 3] += (double)v.w * v.w;
             } else if (a.part) {
               const float4 xv = sxv[i][q];
               const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, vs[4] = {v.x, v.y, v.z, v.w};
@@ -305,7 +312,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
                 const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
                                  : (a.sact == kActLrelu && !(xh > 0.f)) ? vs[e] * kLreluSlope : vs[e];
                 ps[4 * q + e] += gv;
-                pq[4 * q + e] += gv * xh;
+                pq[4 * q + e] += (double)gv * xh;
               }
             }
           }

@@ -634,24 +634,25 @@ def test_op16_rejected_outside_16bit_modes(ops):
         ops.set_conv_precision("f32")
 
 
-@pytest.mark.parametrize("N,cin,cout,S,k,s,p,tr,expect", [
-    (2, 32, 64, 16, 3, 2, 1, False, True),      # G down1 (k3 s2 p1)
-    (2, 64, 128, 32, 3, 2, 1, False, True),     # G down2 (16³ outputs: no K split)
-    (2, 128, 64, 8, 3, 2, 1, True, True),       # G up1 (ConvTranspose3d k3 s2 p1 op1)
-    (2, 64, 32, 8, 3, 2, 1, True, True),        # G up2 (32 output channels: brickT epilogue partials)
-    (1, 64, 32, 6, 3, 2, 1, True, True),        # up2 form with partial 4×16×16 output bricks (12³)
-    (2, 1, 32, 22, 7, 1, 0, False, True),       # G stem (k7, 1 → 32: thin1 epilogue partials, 16³)
-    (1, 1, 32, 27, 7, 1, 0, False, True),       # stem form with partial 16×16 output columns (21³)
-    (2, 32, 64, 16, 4, 2, 1, False, False),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
-    (1, 128, 256, 8, 4, 1, 1, False, False),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
+@pytest.mark.parametrize("N,cin,cout,S,k,s,p,tr,expect,dc", [
+    (2, 32, 64, 16, 3, 2, 1, False, True, 0),      # G down1 (k3 s2 p1)
+    (2, 64, 128, 32, 3, 2, 1, False, True, 0),     # G down2 (16³ outputs: no K split)
+    (2, 128, 64, 8, 3, 2, 1, True, True, 0),       # G up1 (ConvTranspose3d k3 s2 p1 op1)
+    (2, 64, 32, 8, 3, 2, 1, True, True, 0),        # G up2 (32 output channels: brickT epilogue partials)
+    (1, 64, 32, 6, 3, 2, 1, True, True, 0),        # up2 form with partial 4×16×16 output bricks (12³)
+    (2, 1, 32, 22, 7, 1, 0, False, True, 0),       # G stem (k7, 1 → 32: thin1 epilogue partials, 16³)
+    (1, 1, 32, 27, 7, 1, 0, False, True, 0),       # stem form with partial 16×16 output columns (21³)
+    (2, 1, 32, 22, 7, 1, 0, False, True, 10.0),    # stem on a non-centred volume (x + 10): fp64 partials
+    (2, 32, 64, 16, 4, 2, 1, False, False, 0),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
+    (1, 128, 256, 8, 4, 1, 1, False, False, 0),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
 ])
-def test_igemm_in_stats_partials(x3, N, cin, cout, S, k, s, p, tr, expect):
+def test_igemm_in_stats_partials(x3, N, cin, cout, S, k, s, p, tr, expect, dc):
     """ABI 11: the 16-bit implicit GEMM's epilogue InstanceNorm partials (no K split, tiles inside
     one instance and class) and the brickT epilogue's (per output brick) feed mragan_instnorm_fwd_partials; output, mean / rstd and the
     normalised tensor match the statistics-pass path."""
     ops = x3
     g = torch.Generator().manual_seed(N * 7 + cin + cout + S + k)
-    x = torch.randn(N, cin, S, S, S, generator=g, dtype=torch.float64)
+    x = torch.randn(N, cin, S, S, S, generator=g, dtype=torch.float64) + dc
     shape_w = (cin, cout, k, k, k) if tr else (cout, cin, k, k, k)
     w = torch.randn(*shape_w, generator=g, dtype=torch.float64) * 0.05
     xg = ndhwc(x.float()).cuda()
