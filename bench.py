@@ -68,10 +68,13 @@ def parse():
     ap.add_argument("--alt-precisions", default="bf16x3,f32",
                     help="comma list of further precisions timed in the same run (same workload, same protocol) "
                          "and reported under alt_precisions; '' for none")
-    ap.add_argument("--legs", default="128:1",
-                    help="comma list of further workloads SIZE:BATCH timed in the same run (BASELINE configs[2]'s "
-                         "per-GPU unit 128^3 b1 by default), reported under legs; '' for none")
-    ap.add_argument("--leg-alt-precisions", default="bf16x3", help="alt precisions timed for each extra leg")
+    ap.add_argument("--legs", default="128:1,96:1:2:resnet_9blocks:fp16,64:1:1:unet_custom:bf16",
+                    help="comma list of further workloads SIZE:BATCH[:NC[:NETG[:PRECISION]]] timed in the same run, "
+                         "reported under legs; '' for none.  Default: BASELINE configs[2]'s per-GPU unit (128^3 b1), "
+                         "configs[4]'s (2ch->2ch 96^3 b1 fp16) and configs[3]'s generator family at 64^3 "
+                         "(unet_custom: the reference's unet_256 needs a >= 256^3 patch, networks3D.py:270-343)")
+    ap.add_argument("--leg-alt-precisions", default="bf16x3",
+                    help="alt precisions timed for each extra leg that runs the headline precision")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-launch-class timing (profiled runs: the trace then holds only the steps)")
     ap.add_argument("--cpu-warmup", type=int, default=2, help="CPU baseline: untimed oracle steps first")
@@ -219,12 +222,13 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
-def build_model(args, precision, batch=None):
+def build_model(args, precision, batch=None, nc=None, netG=None):
     from models import create_model
     from options.train_options import TrainOptions
+    nc, netG = nc or args.nc, netG or args.netG
     sys_argv = sys.argv
-    sys.argv = ["train.py", "--netG", args.netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
-                "--input_nc", str(args.nc), "--output_nc", str(args.nc),
+    sys.argv = ["train.py", "--netG", netG, "--ngf", str(args.ngf), "--ndf", str(args.ngf),
+                "--input_nc", str(nc), "--output_nc", str(nc),
                 "--checkpoints_dir", "/tmp/mragan_bench", "--batch_size", str(batch or args.batch),
                 "--conv_precision", precision] + (["--no_cuda_graph"] if args.no_graph else []) + \
         (["--single_stream"] if args.single_stream else [])
@@ -244,7 +248,8 @@ def build_model(args, precision, batch=None):
 def ew_bytes_per_patch(S, netG, elem_bytes=4):
     """SURVEY §8(d) secondary HBM term: the InstanceNorm/activation/pad/residual traffic of one
     patch's step, ≈ 8 passes × 118·S³ elements per G fwd+bwd × 6 G passes = 5664·S³ elements
-    (resnet generators; None for the UNet)."""
+    (resnet generators; None for the UNet).  Priced in the leg's activation dtype (2 B for the
+    bf16 / fp16 modes, BASELINE.md §4: 2.97 GB per 64³ patch; 4 B otherwise)."""
     if netG.startswith("unet"):
         return None
     return 5664.0 * S ** 3 * elem_bytes
@@ -319,13 +324,14 @@ def kernel_classes(model, inputs, reps=10):
     return ops.TIMER.classes(reps)
 
 
-def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_top=40):
+def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_top=40, nc=None, netG=None):
     """One workload: the timed step in `precision`, its launch classes and roofline, and the same
     protocol in each precision of `alts` (a fresh model each)."""
     from mragan_hip import ops
-    shape = (batch, args.nc, size, size, size)
+    nc, netG = nc or args.nc, netG or args.netG
+    shape = (batch, nc, size, size, size)
     inputs = make_inputs(shape, args.warmup + args.steps, rank)
-    model = build_model(args, precision, batch)
+    model = build_model(args, precision, batch, nc, netG)
     elapsed, median_ms = time_steps(model, inputs, args.warmup, args.steps, barrier, dist)
     graphed = getattr(model, "_graphs", None) is not None
     classes = kernel_classes(model, inputs) if not args.no_kernel_timing else None
@@ -334,7 +340,7 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
     torch.cuda.empty_cache()
     alt = {}
     for p in alts:
-        m = build_model(args, p, batch)
+        m = build_model(args, p, batch, nc, netG)
         e, med = time_steps(m, inputs, args.warmup, args.steps, barrier, dist)
         alt[p] = {"value": round(world * batch * args.steps / e, 3), "ms_per_step": round(1e3 * e / args.steps, 3),
                   "ms_per_step_median": round(med, 3), "dtype": DTYPE[p], "dtype_detail": DTYPE_DETAIL[p],
@@ -346,9 +352,12 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
     barrier()
     t_step = elapsed / args.steps
     mfma_peak = mfma_peak_of(precision)
-    step_tf = step_flops(size, batch, args.ngf, args.netG, nc=args.nc) / 1e12
-    ew = ew_bytes_per_patch(size, args.netG)
+    step_tf = step_flops(size, batch, args.ngf, netG, nc=nc) / 1e12
+    act_bytes = 2 if precision in ("bf16", "fp16") else 4
+    ew = ew_bytes_per_patch(size, netG, act_bytes)
+    ew32 = ew_bytes_per_patch(size, netG, 4)
     ideal_s = step_tf / mfma_peak + (batch * ew / (HBM_PEAK_GBS * 1e9) if ew else 0.0)
+    ideal32_s = step_tf / mfma_peak + (batch * ew32 / (HBM_PEAK_GBS * 1e9) if ew32 else 0.0)
     leg = {
         "value": round(world * batch * args.steps / elapsed, 3),
         "unit": "patches/s",
@@ -356,12 +365,16 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
         "ms_per_step_median": round(median_ms, 3),
         "dtype": DTYPE[precision],
         "dtype_detail": DTYPE_DETAIL[precision],
-        "workload": f"{args.netG} G + 3-layer PatchGAN D, {args.nc}ch->{args.nc}ch, {size}^3 patch, batch {batch}/GPU",
+        "workload": f"{netG} G + 3-layer PatchGAN D, {nc}ch->{nc}ch, {size}^3 patch, batch {batch}/GPU",
         "step_launch": "hip_graph" if graphed else "eager",
         "step_roofline": {"achieved": round(ideal_s / t_step, 4), "ideal_ms": round(1e3 * ideal_s, 3),
                           "formula": "(F/P_mfma + B_ew/BW_hbm) / T_step (SURVEY 8d)",
                           "F_tflop": round(step_tf, 4), "P_mfma_tflops": round(mfma_peak, 1),
-                          "B_ew_gb": round(batch * ew / 1e9, 3) if ew else None, "BW_hbm_gbs": HBM_PEAK_GBS},
+                          "B_ew_gb": round(batch * ew / 1e9, 3) if ew else None, "B_ew_elem_bytes": act_bytes,
+                          "BW_hbm_gbs": HBM_PEAK_GBS,
+                          "achieved_fp32_storage": round(ideal32_s / t_step, 4),
+                          "note": "B_ew priced in the activation dtype of the precision mode; achieved_fp32_storage "
+                                  "prices it at 4 B per element"},
         "step_tflop": round(step_tf, 4),
         "step_tflops_achieved": round(step_tf / t_step, 2),
     }
@@ -429,12 +442,18 @@ def main():
     head = run_leg(args, args.size, args.batch, args.precision, alts, barrier, dist, world, rank)
     legs = {}
     for spec in [s for s in args.legs.split(",") if s]:
-        S, bsz = (int(v) for v in spec.split(":"))
-        if (S, bsz) == (args.size, args.batch):
+        f = spec.split(":")
+        S, bsz = int(f[0]), int(f[1])
+        nc = int(f[2]) if len(f) > 2 and f[2] else args.nc
+        netG = f[3] if len(f) > 3 and f[3] else args.netG
+        prec = f[4] if len(f) > 4 and f[4] else args.precision
+        if (S, bsz, nc, netG, prec) == (args.size, args.batch, args.nc, args.netG, args.precision):
             continue
-        legs[f"{S}^3 b{bsz}"] = run_leg(args, S, bsz, args.precision,
-                                        [p for p in args.leg_alt_precisions.split(",") if p and p != args.precision],
-                                        barrier, dist, world, rank, n_top=12)
+        key = f"{S}^3 b{bsz}" + (f" nc{nc}" if nc != args.nc else "") + (f" {netG}" if netG != args.netG else "") + \
+            (f" {prec}" if prec != args.precision else "")
+        alt_l = [p for p in args.leg_alt_precisions.split(",") if p and p != prec] if prec == args.precision else []
+        legs[key] = run_leg(args, S, bsz, prec, alt_l, barrier, dist, world, rank, n_top=12, nc=nc, netG=netG)
+        legs[key]["config"] = {"patch": S, "batch": bsz, "nc": nc, "netG": netG, "conv_precision": prec}
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
         return

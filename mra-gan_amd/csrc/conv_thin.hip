@@ -537,7 +537,10 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     return check_launch("thin_k");
   }
   const int64_t total = (int64_t)a.N * a.Do * a.Ho * a.Wo;
-  if (a.ny <= 4 && s1 && a.cx % TN_CC == 0 && (a.k == 3 || a.k == 4 || a.k == 7) && total >= 4096) {
+  // the row-sweep kernel is the k7 head's (ngf ≤ 64 contraction channels); a wide contraction
+  // (the PatchGAN last layer, 8·ndf channels) goes to thin_dot at any output count — at 128³ the
+  // D-last forward (256 → 1, 5,488 outputs) took 535 µs on thin_n
+  if (a.ny <= 4 && s1 && a.cx % TN_CC == 0 && a.cx <= 64 && (a.k == 3 || a.k == 4 || a.k == 7) && total >= 4096) {
     int th = ceil_div(a.Ho, TN_TH), tw = ceil_div(a.Wo, TN_OW);
     size_t lds = ((size_t)(TN_TH + a.k - 1) * tn_row_stride(TN_OW + a.k - 1) + (size_t)a.k * a.k * a.ny * 2) *
                  sizeof(float4);

@@ -65,6 +65,7 @@ CONV_CASES = [
     (2, 256, 1, 7, 4, 1, 1),
     (1, 64, 1, 6, 4, 1, 1),
     (4, 512, 1, 7, 4, 1, 1),        # D last at 64³ (thin_dot)
+    (2, 256, 1, 15, 4, 1, 1),       # D last at 128³ (ndf 32: 5,488 outputs, thin_dot — was thin_n, 535 µs)
     (1, 64, 2, 6, 4, 1, 1),
     # ngf = 4 generators (thin_k with a cut weight slice: cin ≤ 4, k7, few output channels)
     (1, 4, 1, 12, 7, 1, 0),

@@ -8,7 +8,7 @@ mkdir -p "$O"
 cd "$R"
 export TMPDIR=/tmp
 source tools/gpu_step.sh
-step kt 300 python -u -m pytest tests/test_kernels_gpu.py -q -x --tb=short --timeout 300 --timeout-method thread -k "op16_brick or op16_dgrad or in_stats_partials" > "$O/kt.log" 2>&1
+step kt 300 python -u -m pytest tests/test_kernels_gpu.py -q -x --tb=short --timeout 300 --timeout-method thread -k "op16_brick or op16_dgrad or in_stats_partials or test_conv" > "$O/kt.log" 2>&1
 tail -1 "$O/kt.log"
 step stamps 200 python3 tools/diag_ks.py bf16 > "$O/stamps.txt" 2>&1
 cat "$O/stamps.txt"
