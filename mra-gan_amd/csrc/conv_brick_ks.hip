@@ -12,27 +12,45 @@
 // Here the 4 waves split the CONTRACTION instead: wave w owns the channels [32w, 32w + 32) (+128
 // per further chunk) of every tap, and the WHOLE 128 × BN output tile.  Per K-step (one tap × 16
 // channels) a wave issues 4 × TN MFMAs from 4 A fragments (LDS) and TN B fragments (L1/L2): each
-// weight byte is used by 128 output rows (4 MFMAs) and each halo byte by BN columns — at the MFMA
-// rate 32 B/clk/CU of weights from L1 (TN = 2) and 64 B/clk/CU of LDS reads (of 256).  The price
-// is a 4-way reduction of the fp32 tiles through LDS after the main loop (≈ 10 % of it).
+// weight byte is used by 128 output rows and each halo byte by BN columns.  The price is a 4-way
+// reduction of the fp32 tiles through LDS after the main loop.
 //
-// No block barrier inside the main loop: a wave's halo is its own (HMAX positions × [16 ch | 16
-// ch] bf16 + 16-B pad = 80 B rows, an odd count of 16-B slots so brick_row_perm's conflict-free
-// A-read assignment holds), and LDS executes one wave's instructions in order.  The halo streams
-// in half-chunks of 16 channels: while a wave's 27 taps run on one half-slot of every row, the
-// next half-chunk's 16 channels are loaded into the other half-slot (loads at steps 0…, stored
-// kHD steps later).  Weights are the pre-split fragment-order copy (brick_x3_pack / tr 2/3 packs:
-// [tap][chunk][16-ch half][hi|lo][n][8-ch group][8]), read through a buffer descriptor with
-// wave-uniform per-step offsets, kPF steps ahead.
+// No block barrier inside the main loop: a wave's halo is its own, and LDS executes one wave's
+// instructions in order.  Halo rows are an odd number of 16-B slots (brick_row_perm's conflict-free
+// A-read assignment).  The halo streams in half-chunks of 16 channels; the next half-chunk's
+// slices are loaded during the current half's taps:
+//   DB = 1: two half-slots per row (80-B rows, 128 KB per block, ONE block per CU): the slices are
+//           stored into the idle half-slot kHD steps after their load;
+//   DB = 0: one half-slot (48-B rows, 77 KB per block, TWO blocks per CU, ≤ 256 registers): the
+//           slices wait in registers and are stored right after the half's last A reads — the
+//           co-resident block's MFMAs cover this block's prologue, boundaries and epilogue
+//           (tools/diag_ks.py phase stamps, r04b: with one block per CU the table set-up,
+//           prologue, reduction and epilogue were 54 % of a wave's cycles).
+// Weights are the pre-split fragment-order copy (brick_x3_pack / tr 2/3 packs: [tap][chunk][16-ch
+// half][hi|lo][n][8-ch group][8]) through a buffer descriptor with wave-uniform per-step offsets,
+// kPF steps ahead.
 //
-// The result per output element is p0 + p1 + p2 + p3 over the waves' fp32 partials in that order
-// (deterministic); the same order serves the fp32-input and the operand-plane input (X16), so the
-// two stay bit-identical (tests/test_kernels_gpu.py::test_op16_brick_conv_and_wgrad).
+// Epilogue: wave w sums rows 32w … over the 4 waves' partials (order p0 + p1 + p2 + p3:
+// deterministic, and the same for the fp32-input and the operand-plane input X16, so the two stay
+// bit-identical — tests/test_kernels_gpu.py::test_op16_brick_conv_and_wgrad), then transposes each
+// 4×4 block of its accumulator within lane quads (DPP) so that a lane holds 4 consecutive channels
+// of one voxel: 16-B output stores (the 4-B column stores of the MFMA layout were store-issue bound:
+// 11.8 k cycles of a 48 k-cycle wave, r04b) and 16-B loads of the backward-statistics operand.
 #include "conv_geo.h"
 #include "kernels.h"
 #include "prec.h"
 
 #include <cstdlib>
+#include <type_traits>
+
+// build-time knobs of the two-blocks-per-CU variant (≤ 256 registers): weight prefetch distance and
+// A-fragment read distance, in steps (divisors of 27 and 27 / (kAD + 1) integral)
+#ifndef MRAGAN_KS_PF0
+#define MRAGAN_KS_PF0 3
+#endif
+#ifndef MRAGAN_KS_AD0
+#define MRAGAN_KS_AD0 2
+#endif
 
 namespace mragan {
 
@@ -40,19 +58,41 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kTaps = 27;
-constexpr int kRowB = 80;     // per-wave halo row: 2 half-slots of 16 channels × 2 B + 16-B pad
 constexpr int kKsBM = 128;    // GEMM rows per block (4 fragment rows of 32)
 constexpr int kKsHmax = 400;  // halo positions per wave
 
+template <int DB>
+constexpr int ks_row_bytes() { return DB ? 80 : 48; }
 constexpr size_t ks_tables_bytes() { return (size_t)(2 * kKsBM + kKsHmax) * sizeof(int); }
-template <int TN>
+template <int TN, int DB>
 constexpr size_t ks_region_bytes() {
-  // halos [4 waves][HMAX][80 B], later the reduction [4 tiles][4 waves][TN][4 quads][64 lanes] × 16 B
-  return (size_t)4 * kKsHmax * kRowB > (size_t)TN * 65536 ? (size_t)4 * kKsHmax * kRowB : (size_t)TN * 65536;
+  // halos [4 waves][HMAX][row], later the reduction [4 tiles][4 waves][TN][4 quads][64 lanes] × 16 B
+  return (size_t)4 * kKsHmax * ks_row_bytes<DB>() > (size_t)TN * 65536 ? (size_t)4 * kKsHmax * ks_row_bytes<DB>()
+                                                                          : (size_t)TN * 65536;
+}
+
+// 4×4 transpose inside each quad of lanes (lane 4m + k holds row k of the block as v[0..3] → it
+// ends up holding column k): two DPP bit-swap stages
+__device__ __forceinline__ f32x4v quad_transpose(f32x4v v, int k) {
+  const bool k0 = k & 1, k1 = k & 2;
+  // stage 1, lanes k ↔ k ^ 1: the components whose bit 0 differs from the lane's
+  {
+    const float s01 = k0 ? v[0] : v[1], s23 = k0 ? v[2] : v[3];
+    const float r01 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s01), 0xB1, 0xF, 0xF, false));
+    const float r23 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s23), 0xB1, 0xF, 0xF, false));
+    if (k0) { v[0] = r01; v[2] = r23; } else { v[1] = r01; v[3] = r23; }
+  }
+  // stage 2, lanes k ↔ k ^ 2: the components whose bit 1 differs from the lane's
+  {
+    const float s02 = k1 ? v[0] : v[2], s13 = k1 ? v[1] : v[3];
+    const float r02 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s02), 0x4E, 0xF, 0xF, false));
+    const float r13 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s13), 0x4E, 0xF, 0xF, false));
+    if (k1) { v[0] = r02; v[1] = r13; } else { v[2] = r02; v[3] = r13; }
+  }
+  return v;
 }
 
 }  // namespace
@@ -67,10 +107,12 @@ __device__ unsigned long long g_ks_stamps[kKsStampBlocks * 24];
       g_ks_stamps[blockIdx.x * 24 + wave * 6 + (i)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
 
-template <int TN, int PM, int X16>
-__global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
+template <int TN, int DB, int PM, int X16>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DB ? 1 : 2, DB ? 1 : 2)))
+conv_brick_ks_kernel(BrickArgs a) {
   static_assert(!prec::has_lo<PM>(), "the K-split brick runs the one-plane modes");
   constexpr int TM = 4, BM = kKsBM, BN = TN * 32, HMAX = kKsHmax;
+  constexpr int kRowB = ks_row_bytes<DB>();
   constexpr int ES = X16 ? 2 : 4;                   // bytes per input element
   constexpr int SPP = X16 ? 2 : 4;                  // 16-B global slices per position per half-chunk
   constexpr int CPS = 16 / SPP;                     // channels per slice
@@ -78,10 +120,12 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   constexpr int LPS = X16 ? 1 : 2;                  // slices loaded per step
   constexpr int NLD = (NSL + LPS - 1) / LPS;        // steps that load
   constexpr int kHalf = kTaps;                      // steps per half-chunk (one tap each)
-  constexpr int kHD = X16 ? 8 : 2;                  // a slice is stored kHD steps after its load
-  constexpr int kPF = 9;                            // weight prefetch distance (steps)
-  constexpr int kAD = 2;                            // A-fragment read distance (steps)
-  static_assert(NLD + kHD <= kHalf, "halo stream does not fit a half-chunk");
+  // a slice is stored (DB) or packed into its staging register (DB = 0) kHD steps after its load
+  constexpr int kHD = (X16 && DB) ? 8 : 2;
+  constexpr int kPF = DB ? 9 : MRAGAN_KS_PF0;       // weight prefetch distance (steps)
+  constexpr int kAD = DB ? 2 : MRAGAN_KS_AD0;       // A-fragment read distance (steps)
+  static_assert(!DB || NLD + kHD <= kHalf, "halo stream does not fit a half-chunk");
+  static_assert(DB || NLD + kHD <= kHalf - kAD, "halo stream does not fit a half-chunk");
   static_assert(kHalf % kPF == 0 && kHalf % (kAD + 1) == 0 && kHalf % (kHD + 1) == 0, "ring periods");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -167,28 +211,33 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
     const int e = sl * 64 + lane, pos = e / SPP;
     ho[sl] = pos < HP ? hoff[pos] : -1;
   }
-  // half-chunk (chunk k of this wave, half h): channels (wave + 4k)·32 + 16h …, LDS half-slot h
-  auto halo_ld = [&](int k, int h, int sl) __attribute__((always_inline)) -> float4 {
+  // half-chunk g = 2k + h (chunk k of this wave, half h): channels (wave + 4k)·32 + 16h …, LDS
+  // half-slot h (DB) or the only slot (DB = 0)
+  auto halo_ld = [&](int g, int sl) __attribute__((always_inline)) -> float4 {
     const int e = sl * 64 + lane;
     const int o = ho[sl];
-    const int cb = (wave + 4 * k) * 32 + 16 * h;
+    const int cb = (wave + 4 * (g >> 1)) * 32 + 16 * (g & 1);
     return buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + cb + CPS * (e % SPP)) * (uint32_t)ES);
   };
-  auto halo_st = [&](int h, int sl, const float4& v) __attribute__((always_inline)) {
-    const int e = sl * 64 + lane, pos = e / SPP;
-    if (pos < HP) {
-      char* row = Hw + pos * kRowB + 32 * h;
-      if constexpr (X16) {
-        *reinterpret_cast<f32x4v*>(row + 16 * (e % SPP)) = f32x4v{v.x, v.y, v.z, v.w};
-      } else {
-        uint2 hi, lo;
-        prec::split4<PM>(v, hi, lo);
-        *reinterpret_cast<uint2*>(row + 8 * (e % SPP)) = hi;
-      }
+  // a loaded slice in its LDS format: the 16 B of a plane as they are, or 4 fp32 → 4 16-bit words
+  typedef typename std::conditional<X16, f32x4v, uint2>::type Packed;
+  auto halo_pack = [&](const float4& v) __attribute__((always_inline)) -> Packed {
+    if constexpr (X16) {
+      return f32x4v{v.x, v.y, v.z, v.w};
+    } else {
+      uint2 hi, lo;
+      prec::split4<PM>(v, hi, lo);
+      return hi;
     }
   };
-  // step (half-chunk g = 2k + h, tap t): weights of tap t (flipped for the transposed form), channels
-  // 16h … of chunk wave + 4k; the A fragments of tap t in half-slot h of the halo rows
+  auto halo_put = [&](int g, int sl, const Packed& v) __attribute__((always_inline)) {
+    const int e = sl * 64 + lane, pos = e / SPP;
+    if (pos < HP) {
+      char* row = Hw + pos * kRowB + (DB ? 32 * (g & 1) : 0);
+      *reinterpret_cast<Packed*>(row + (X16 ? 16 : 8) * (e % SPP)) = v;
+    }
+  };
+  auto halo_st = [&](int g, int sl, const float4& v) __attribute__((always_inline)) { halo_put(g, sl, halo_pack(v)); };
   // Per-step offsets are built from strides made opaque to the compiler once per step (an empty
   // asm on SGPR copies): left alone, LICM hoists all 27 taps' offsets out of the half-chunk loop
   // and the SGPR file overflows (spills to VGPR lanes and a scratch frame).
@@ -206,20 +255,20 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   auto a_read = [&](int g, int t, bf16x8 (&dst)[TM]) __attribute__((always_inline)) {
     int ps = pstride, rs = rstride;
     asm volatile("" : "+s"(ps), "+s"(rs));
-    const int tap_off = (t / 9) * ps + ((t / 3) % 3) * rs + (t % 3) * kRowB + (g & 1) * 32;
+    const int tap_off = (t / 9) * ps + ((t / 3) % 3) * rs + (t % 3) * kRowB + (DB ? (g & 1) * 32 : 0);
 #pragma unroll
     for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(Hw + abase[i] + tap_off);
   };
 
-  // prologue: half-chunk 0 (all loads in flight before the first store), weights of the first
-  // kPF steps, A fragments of the first kAD
-  constexpr int kPB = 13;                           // prologue slices in flight per batch
+  // prologue: half-chunk 0 (13 slices in flight per batch), weights of the first kPF steps, A
+  // fragments of the first kAD
+  constexpr int kPB = 13;
 #pragma unroll
   for (int s0 = 0; s0 < NSL; s0 += kPB) {
     float4 pv[kPB];
 #pragma unroll
     for (int sl = 0; sl < kPB; ++sl)
-      if (s0 + sl < NSL) pv[sl] = halo_ld(0, 0, s0 + sl);
+      if (s0 + sl < NSL) pv[sl] = halo_ld(0, s0 + sl);
 #pragma unroll
     for (int sl = 0; sl < kPB; ++sl)
       if (s0 + sl < NSL) halo_st(0, s0 + sl, pv[sl]);
@@ -239,24 +288,39 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
 
   KS_STAMP(2);
   // one loop iteration = one half-chunk (27 taps, unrolled: ring slots are compile-time because 9
-  // and 3 divide 27); the next half-chunk streams into the other half-slot meanwhile
+  // and 3 divide 27); the next half-chunk streams in meanwhile
   const int nhalf = 2 * nck;
   for (int g = 0; g < nhalf; ++g) {
     const bool next = g + 1 < nhalf;
     const int gn = next ? g + 1 : g;          // past the last half: harmless re-reads, no stores
-    float4 rh[kHD + 1][LPS];
+    constexpr int kRing = kHD + 1;
+    float4 rh[kRing][LPS];
+    Packed stg[DB ? 1 : NSL];                 // DB = 0: the next half-chunk, packed, until its store
 #pragma unroll
     for (int t = 0; t < kHalf; ++t) {
       __builtin_amdgcn_sched_barrier(0);
       if (t < NLD && next) {
 #pragma unroll
         for (int l = 0; l < LPS; ++l)
-          if (t * LPS + l < NSL) rh[t % (kHD + 1)][l] = halo_ld(gn >> 1, gn & 1, t * LPS + l);
+          if (t * LPS + l < NSL) rh[t % kRing][l] = halo_ld(gn, t * LPS + l);
       }
       if (t >= kHD && t - kHD < NLD && next) {
 #pragma unroll
-        for (int l = 0; l < LPS; ++l)
-          if ((t - kHD) * LPS + l < NSL) halo_st(gn & 1, (t - kHD) * LPS + l, rh[(t - kHD) % (kHD + 1)][l]);
+        for (int l = 0; l < LPS; ++l) {
+          const int sl = (t - kHD) * LPS + l;
+          if (sl < NSL) {
+            if constexpr (DB) halo_st(gn, sl, rh[(t - kHD) % kRing][l]);
+            else stg[sl] = halo_pack(rh[(t - kHD) % kRing][l]);
+          }
+        }
+      }
+      if constexpr (!DB) {
+        // one slot: the next half-chunk overwrites it once this half's last A reads are issued
+        // (they were, kAD steps ago: LDS runs this wave's instructions in order)
+        if (t == kHalf - kAD && next) {
+#pragma unroll
+          for (int sl = 0; sl < NSL; ++sl) halo_put(gn, sl, stg[sl]);
+        }
       }
       // B fragments of this step (loaded kPF steps ago); refill the slot with step + kPF
       bf16x8 bc[TN];
@@ -264,8 +328,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
       for (int j = 0; j < TN; ++j) bc[j] = rb[t % kPF][j];
       if (t + kPF < kHalf) b_load(g, t + kPF, rb[t % kPF]);
       else b_load(gn, t + kPF - kHalf, rb[t % kPF]);
-      // A fragments kAD steps ahead (into the next half-chunk's slot near the end: stored at
-      // steps kHD … kHD + NLD − 1 of this half, before these reads)
+      // A fragments kAD steps ahead (into the next half-chunk near the end: stored by then)
       if (t + kAD < kHalf) a_read(g, t + kAD, af[(t + kAD) % (kAD + 1)]);
       else a_read(gn, t + kAD - kHalf, af[(t + kAD) % (kAD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
@@ -290,8 +353,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   for (int i = 0; i < TM; ++i) {
     if (i != wave) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-      {
+      for (int j = 0; j < TN; ++j) {
         red[red_idx(i, wave, j, 0)] = __builtin_shufflevector(acc[i][j], acc[i][j], 0, 1, 2, 3);
         red[red_idx(i, wave, j, 1)] = __builtin_shufflevector(acc[i][j], acc[i][j], 4, 5, 6, 7);
         red[red_idx(i, wave, j, 2)] = __builtin_shufflevector(acc[i][j], acc[i][j], 8, 9, 10, 11);
@@ -309,82 +371,104 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
       for (int j = 0; j < TN; ++j) own[j] = acc[i][j];
     }
   __syncthreads();
-  f32x16 fin[TN];
+  // fin[j][q]: quad q of column tile j — rows 8q + 4lh + {0..3}, column j·32 + li
+  f32x4v fin[TN][4];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) fin[j] = f32x16{};
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) fin[j][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int src = 0; src < 4; ++src) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if (src == wave) {
-        fin[j] += own[j];
+        fin[j][0] += __builtin_shufflevector(own[j], own[j], 0, 1, 2, 3);
+        fin[j][1] += __builtin_shufflevector(own[j], own[j], 4, 5, 6, 7);
+        fin[j][2] += __builtin_shufflevector(own[j], own[j], 8, 9, 10, 11);
+        fin[j][3] += __builtin_shufflevector(own[j], own[j], 12, 13, 14, 15);
       } else {
-        const f32x4v r0 = red[red_idx(wave, src, j, 0)], r1 = red[red_idx(wave, src, j, 1)],
-                     r2 = red[red_idx(wave, src, j, 2)], r3 = red[red_idx(wave, src, j, 3)];
-        const f32x8 r01 = __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7);
-        const f32x8 r23 = __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7);
-        fin[j] += __builtin_shufflevector(r01, r23, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fin[j][q] += red[red_idx(wave, src, j, q)];
       }
     }
   }
 
   KS_STAMP(4);
-  // epilogue on rows 32w + …: bias / activation, output store, InstanceNorm partials
-  const int wm0 = wave * 32;
-  double ps[TN], pq[TN];
-  if (!a.sx) {
+  // epilogue: transpose each quad's 4×4 block across lanes 4m … 4m + 3 → lane (li = 4m + k, lh)
+  // holds voxel row 32w + 8q + 4lh + k, channels n0 + 32j + 4m … 4m + 3
+  const int k4 = li & 3, m4 = li >> 2;
+  int orow[4], xrow[4];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + j * 32 + li;
-      const float bsum = a.bias ? a.bias[col] : 0.f;
-      ps[j] = 0.0;
-      pq[j] = 0.0;
+  for (int q = 0; q < 4; ++q) {
+    const int row = wave * 32 + 8 * q + 4 * lh + k4;
+    orow[q] = out_off[row];
+    xrow[q] = a.sx ? xoff[row] : 0;
+  }
+  // per-lane statistics over its 4 voxels, per channel (fp64)
+  double ps[TN][4], pq[TN][4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int off = out_off[row];
-        if (off >= 0) {
-          const float v = act_fwd(fin[j][r] + bsum, a.act);
-          a.y[(int64_t)off * a.ny + col] = v;
-          ps[j] += v;
-          pq[j] += (double)v * v;
-        }
-      }
+  for (int j = 0; j < TN; ++j) {
+    const int c0 = n0 + j * 32 + 4 * m4;
+    float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + c0);
+    float4 mu = bq, rs = bq;
+    if (a.sx) {
+      mu = *reinterpret_cast<const float4*>(a.smean + nb * a.ny + c0);
+      rs = *reinterpret_cast<const float4*>(a.srstd + nb * a.ny + c0);
     }
-  } else {
-    // backward statistics of the InstanceNorm in front of this conv (see conv_brick_x3.hip)
+    const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
+    const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + j * 32 + li;
-      const float mu = a.smean[nb * a.ny + col], rs = a.srstd[nb * a.ny + col];
-      ps[j] = 0.0;
-      pq[j] = 0.0;
+    for (int e = 0; e < 4; ++e) ps[j][e] = pq[j][e] = 0.0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int off = out_off[row];
-        if (off >= 0) {
-          const float v = fin[j][r];
-          a.y[(int64_t)off * a.ny + col] = v;
-          const float xh = (a.sx[(int64_t)xoff[row] * a.ny + col] - mu) * rs;
-          const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? v * kLreluSlope : v;
-          ps[j] += gv;
-          pq[j] += (double)gv * xh;
+    for (int q = 0; q < 4; ++q) {
+      const f32x4v t = quad_transpose(fin[j][q], k4);
+      if (orow[q] < 0) continue;
+      float v[4] = {t[0], t[1], t[2], t[3]};
+      if (!a.sx) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = act_fwd(v[e] + bv[e], a.act);
+          ps[j][e] += v[e];
+          pq[j][e] += (double)v[e] * v[e];
+        }
+      } else {
+        const float4 xs = *reinterpret_cast<const float4*>(a.sx + (int64_t)xrow[q] * a.ny + c0);
+        const float xv[4] = {xs.x, xs.y, xs.z, xs.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xv[e] - muv[e]) * rsv[e];
+          const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? v[e] * kLreluSlope : v[e];
+          ps[j][e] += gv;
+          pq[j][e] += (double)gv * xh;
         }
       }
+      *reinterpret_cast<f32x4v*>(a.y + (int64_t)orow[q] * a.ny + c0) = f32x4v{v[0], v[1], v[2], v[3]};
     }
   }
   if (a.part) {
-    __syncthreads();
-    double* red2 = reinterpret_cast<double*>(region);        // [4 waves][BN][2]
+    // lanes k = 0..3 of a quad hold the same channels: sum over k (xor 1, 2), then over the lane
+    // halves and the 4 waves through LDS, one double2 per channel
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const double s2 = ps[j] + __shfl_xor(ps[j], 32);
-      const double q2 = pq[j] + __shfl_xor(pq[j], 32);
-      if (lh == 0) {
-        red2[(wave * BN + j * 32 + li) * 2] = s2;
-        red2[(wave * BN + j * 32 + li) * 2 + 1] = q2;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ps[j][e] += __shfl_xor(ps[j][e], 1);
+        pq[j][e] += __shfl_xor(pq[j][e], 1);
+        ps[j][e] += __shfl_xor(ps[j][e], 2);
+        pq[j][e] += __shfl_xor(pq[j][e], 2);
       }
+    __syncthreads();
+    double* red2 = reinterpret_cast<double*>(region);        // [4 waves][2 halves][BN][2]
+    if (k4 == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = j * 32 + 4 * m4 + e;
+          red2[((wave * 2 + lh) * BN + c) * 2] = ps[j][e];
+          red2[((wave * 2 + lh) * BN + c) * 2 + 1] = pq[j][e];
+        }
     }
     __syncthreads();
     const int chunks = a.nbd * a.nbh * a.nbw;
@@ -392,7 +476,7 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
     for (int c = tid; c < BN; c += 256) {
       double s2 = 0.0, q2 = 0.0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < 8; ++w) {
         s2 += red2[(w * BN + c) * 2];
         q2 += red2[(w * BN + c) * 2 + 1];
       }
@@ -404,10 +488,10 @@ __global__ void __launch_bounds__(256) conv_brick_ks_kernel(BrickArgs a) {
   KS_STAMP(5);
 }
 
-template <int TN, int PM, int X16>
+template <int TN, int DB, int PM, int X16>
 static int launch_brick_ks_as(const BrickArgs& a, hipStream_t st) {
-  const size_t lds = ks_tables_bytes() + ks_region_bytes<TN>();
-  auto kern = conv_brick_ks_kernel<TN, PM, X16>;
+  const size_t lds = ks_tables_bytes() + ks_region_bytes<TN, DB>();
+  auto kern = conv_brick_ks_kernel<TN, DB, PM, X16>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -418,7 +502,7 @@ static int launch_brick_ks_as(const BrickArgs& a, hipStream_t st) {
 }
 
 template <int PM>
-static int brick_ks_launch_pm(BrickArgs a, int tn, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
+static int brick_ks_launch_pm(BrickArgs a, int tn, int db, void* ws, size_t ws_bytes, const void* wsplit, hipStream_t st) {
   if constexpr (prec::has_lo<PM>()) {
     set_error("conv_brick_ks: the K-split brick runs the bf16 / fp16 modes only");
     return kBadArg;
@@ -435,8 +519,11 @@ static int brick_ks_launch_pm(BrickArgs a, int tn, void* ws, size_t ws_bytes, co
       if (rc) return rc;
       a.wx3 = ws;
     }
-    if (tn == 2) return a.x16 ? launch_brick_ks_as<2, PM, 1>(a, st) : launch_brick_ks_as<2, PM, 0>(a, st);
-    return a.x16 ? launch_brick_ks_as<1, PM, 1>(a, st) : launch_brick_ks_as<1, PM, 0>(a, st);
+    if (tn == 2 && db) return a.x16 ? launch_brick_ks_as<2, 1, PM, 1>(a, st) : launch_brick_ks_as<2, 1, PM, 0>(a, st);
+    if (db) return a.x16 ? launch_brick_ks_as<1, 1, PM, 1>(a, st) : launch_brick_ks_as<1, 1, PM, 0>(a, st);
+    // the fp32-input form of the two-per-CU variant would not fit 256 registers: it runs one per CU
+    // (same per-element summation order — bit-identical results)
+    return a.x16 ? launch_brick_ks_as<1, 0, PM, 1>(a, st) : launch_brick_ks_as<1, 1, PM, 0>(a, st);
   }
 }
 
@@ -448,22 +535,35 @@ bool conv_brick_ks_applicable(const IgemmArgs& g) {
   return !off && (g.x3 == kPrecBf16 || g.x3 == kPrecF16) && g.cx % 128 == 0 && g.ny % 32 == 0;
 }
 
-// Brick shape and column tile: the fewest rounds of 256 blocks (one block per CU: 131 KB of LDS)
-// × the block's time (∝ TN), then the fewest GEMM rows computed, then the smallest halo.  Every
-// shape keeps bh ≥ 4 and bw ≥ 6 (the partials bound in capi.hip) and a halo ≤ 400 positions.
+// Brick shape and variant: the fewest rounds of the CU slots (DB = 1: one block per CU; DB = 0, TN
+// = 1: two) × the block's MFMA time (∝ TN), then the fewest GEMM rows computed, then the smallest
+// halo.  Every shape keeps bh ≥ 4 and bw ≥ 6 (the partials bound in capi.hip) and a halo ≤ 400
+// positions.  MRAGAN_BRICK_KS=1|2|3 forces the variant (1: TN 1 two per CU, 2: TN 1 one per CU,
+// 3: TN 2 one per CU) for A/B.
 int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* wsplit, int mode, int* in_chunks,
                   hipStream_t st) {
   static const int shapes[][3] = {{4, 4, 8}, {2, 8, 8}, {3, 6, 6}, {2, 6, 9}, {3, 4, 8}, {5, 4, 6}, {2, 6, 8}, {4, 4, 6}};
-  int best_tn = 0, best_s = -1;
+  static const int force = [] {
+    const char* e = getenv("MRAGAN_BRICK_KS");
+    return e ? atoi(e) : 0;
+  }();
+  struct Var { int tn, db, per_cu; };
+  static const Var vars[] = {{1, 0, 2}, {1, 1, 1}, {2, 1, 1}};
+  int best_v = -1, best_s = -1;
   double best[4] = {1e30, 1e30, 1e30, 1e30};
-  for (int tn = 2; tn >= 1; --tn) {
-    if (ny % (32 * tn)) continue;
+  for (int vi = 0; vi < 3; ++vi) {
+    const Var& V = vars[vi];
+    if (force >= 1 && force <= 3 && force - 1 != vi) continue;
+    if (ny % (32 * V.tn)) continue;
     for (int s = 0; s < (int)(sizeof(shapes) / sizeof(shapes[0])); ++s) {
       const int* b = shapes[s];
       const int64_t bricks = (int64_t)a.N * ceil_div(a.Do, b[0]) * ceil_div(a.Ho, b[1]) * ceil_div(a.Wo, b[2]);
-      const int64_t blocks = bricks * (ny / (32 * tn));
-      const double key[4] = {(double)((blocks + 255) / 256) * tn, (double)blocks * tn, (double)(b[0] + 2) * (b[1] + 2) * (b[2] + 2),
-                             (double)blocks};
+      const int64_t blocks = bricks * (ny / (32 * V.tn));
+      const int64_t slots = 256 * V.per_cu;
+      // a round of two co-resident TN-1 blocks takes the MFMA time of one TN-2 block
+      const double round_t = V.per_cu == 2 ? 2.0 : V.tn;
+      const double key[4] = {(double)((blocks + slots - 1) / slots) * round_t, (double)blocks * V.tn,
+                             (double)(b[0] + 2) * (b[1] + 2) * (b[2] + 2), (double)vi};
       bool better = false;
       for (int q = 0; q < 4; ++q) {
         if (key[q] < best[q]) { better = true; break; }
@@ -471,17 +571,18 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
       }
       if (better) {
         for (int q = 0; q < 4; ++q) best[q] = key[q];
-        best_tn = tn;
+        best_v = vi;
         best_s = s;
       }
     }
   }
   MRAGAN_CHECK_ARG(best_s >= 0, "conv_brick_ks: %d output channels are not a multiple of 32", ny);
   const int* b = shapes[best_s];
+  const Var& V = vars[best_v];
   a.BD = b[0]; a.BH = b[1]; a.BW = b[2];
   a.HD = b[0] + 2; a.HH = b[1] + 2; a.HW = b[2] + 2;
   a.nbd = ceil_div(a.Do, b[0]); a.nbh = ceil_div(a.Ho, b[1]); a.nbw = ceil_div(a.Wo, b[2]);
-  a.gn = ny / (32 * best_tn);
+  a.gn = ny / (32 * V.tn);
   const int64_t ntiles = (int64_t)a.N * a.nbd * a.nbh * a.nbw * a.gn;
   MRAGAN_CHECK_ARG(ntiles < ((int64_t)1 << 31), "conv_brick_ks: grid too large");
   a.ntiles = (int)ntiles;
@@ -490,7 +591,7 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   if (in_chunks && a.part) *in_chunks = a.nbd * a.nbh * a.nbw;
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, kKsBM, a.rowvox);
-  MRAGAN_PREC_DISPATCH(mode, return brick_ks_launch_pm<PM>(a, best_tn, ws, ws_bytes, wsplit, st))
+  MRAGAN_PREC_DISPATCH(mode, return brick_ks_launch_pm<PM>(a, V.tn, V.db, ws, ws_bytes, wsplit, st))
 }
 
 int ks_debug_stamps(unsigned long long* host, int n) {
