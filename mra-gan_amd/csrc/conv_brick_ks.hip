@@ -536,8 +536,8 @@ bool conv_brick_ks_applicable(const IgemmArgs& g) {
 }
 
 // Brick shape and variant: the fewest rounds of the CU slots (DB = 1: one block per CU; DB = 0, TN
-// = 1: two) × the block's MFMA time (∝ TN), then the fewest GEMM rows computed, then the smallest
-// halo.  Every shape keeps bh ≥ 4 and bw ≥ 6 (the partials bound in capi.hip) and a halo ≤ 400
+// = 1: two) × the block's MFMA time (∝ TN), then the fewest GEMM rows computed, then conflict-free
+// A reads, then the smallest halo.  Every shape keeps bh ≥ 4 and bw ≥ 6 (the partials bound in capi.hip) and a halo ≤ 400
 // positions.  MRAGAN_BRICK_KS=1|2|3 forces the variant (1: TN 1 two per CU, 2: TN 1 one per CU,
 // 3: TN 2 one per CU) for A/B.
 int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* wsplit, int mode, int* in_chunks,
@@ -550,7 +550,7 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   struct Var { int tn, db, per_cu; };
   static const Var vars[] = {{1, 0, 2}, {1, 1, 1}, {2, 1, 1}};
   int best_v = -1, best_s = -1;
-  double best[4] = {1e30, 1e30, 1e30, 1e30};
+  double best[5] = {1e30, 1e30, 1e30, 1e30, 1e30};
   for (int vi = 0; vi < 3; ++vi) {
     const Var& V = vars[vi];
     if (force >= 1 && force <= 3 && force - 1 != vi) continue;
@@ -562,15 +562,25 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
       const int64_t slots = 256 * V.per_cu;
       // a round of two co-resident TN-1 blocks takes the MFMA time of one TN-2 block
       const double round_t = V.per_cu == 2 ? 2.0 : V.tn;
-      const double key[4] = {(double)((blocks + slots - 1) / slots) * round_t, (double)blocks * V.tn,
+      // A-read bank conflicts: brick_row_perm deals each residue class (halo position mod 16) over
+      // the 8 lane groups of a 128-row tile — conflict-free iff no class has more than 8 voxels
+      // (3×6×6 in an 8×8 halo plane has 9 per class: 2-way on every read)
+      int cnt[16] = {0}, worst = 0;
+      for (int v = 0; v < b[0] * b[1] * b[2]; ++v) {
+        const int bd = v / (b[1] * b[2]), bh = (v / b[2]) % b[1], bw = v % b[2];
+        const int r = (((bd * (b[1] + 2) + bh) * (b[2] + 2) + bw) % 16);
+        worst = ++cnt[r] > worst ? cnt[r] : worst;
+      }
+      const double conflict = worst > kKsBM / 16 ? 1.0 : 0.0;
+      const double key[5] = {(double)((blocks + slots - 1) / slots) * round_t, (double)blocks * V.tn, conflict,
                              (double)(b[0] + 2) * (b[1] + 2) * (b[2] + 2), (double)vi};
       bool better = false;
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 5; ++q) {
         if (key[q] < best[q]) { better = true; break; }
         if (key[q] > best[q]) break;
       }
       if (better) {
-        for (int q = 0; q < 4; ++q) best[q] = key[q];
+        for (int q = 0; q < 5; ++q) best[q] = key[q];
         best_v = vi;
         best_s = s;
       }
