@@ -411,8 +411,10 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   }
   // bf16 / fp16 with a multiple of 128 contraction channels: the K-split brick (conv_brick_ks.hip)
   if (conv_brick_ks_applicable(g)) {
-    if (g.in_part) a.part = g.in_part;
-    return conv_brick_ks(a, g.ny, g.ws, g.ws_bytes, g.wx3, g.x3, g.in_chunks, st);
+    BrickArgs k = a;
+    if (g.in_part) k.part = g.in_part;
+    const int rc = conv_brick_ks(k, g.ny, g.ws, g.ws_bytes, g.wx3, g.x3, g.in_chunks, st);
+    if (rc != kUnsupported) return rc;   // kUnsupported: no K-split variant fits one round of CU slots
   }
   const bool x3 = g.x3 != 0;
   BrickChoice c = choose_brick(g.N, a.Do, a.Ho, a.Wo, g.ny, x3);

@@ -66,7 +66,7 @@ constexpr int kKsHmax = 400;  // halo positions per wave
 
 template <int DB>
 constexpr int ks_row_bytes() { return DB ? 80 : 48; }
-constexpr size_t ks_tables_bytes() { return (size_t)(2 * kKsBM + kKsHmax) * sizeof(int); }
+constexpr size_t ks_tables_bytes() { return (size_t)(2 * kKsBM) * sizeof(int); }
 template <int TN, int DB>
 constexpr size_t ks_region_bytes() {
   // halos [4 waves][HMAX][row], later the reduction [4 tiles][4 waves][TN][4 quads][64 lanes] × 16 B
@@ -93,6 +93,15 @@ __device__ __forceinline__ f32x4v quad_transpose(f32x4v v, int k) {
     if (k1) { v[0] = r02; v[1] = r13; } else { v[2] = r02; v[3] = r13; }
   }
   return v;
+}
+
+// a double from the lane given by the DPP quad permutation CTRL (two 32-bit moves)
+template <int CTRL>
+__device__ __forceinline__ double dpp_xor_d(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
 }  // namespace
@@ -131,13 +140,18 @@ conv_brick_ks_kernel(BrickArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* out_off = reinterpret_cast<int*>(smem);      // [BM]
   int* xoff = out_off + BM;                         // [BM] (backward statistics)
-  int* hoff = xoff + BM;                            // [HMAX]
   char* region = smem + ks_tables_bytes();          // halos, then the K reduction
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, lh = lane >> 5;
   KS_STAMP(0);
+
+  // Small non-negative quotients (< 2^22 / divisor) through an fp32 reciprocal: (n + ½)·(1/d) lies
+  // ≥ ½/d away from an integer and the product's relative error is ~2^-23, so the truncation is
+  // exact here (every index below is < 2^20).  Replaces ~30-instruction integer divisions: the
+  // block set-up (tables + prologue) took 9 k cycles of a 35 k-cycle wave (r04c phase stamps).
+  auto qdiv = [](int n, float rd) __attribute__((always_inline)) { return (int)(((float)n + 0.5f) * rd); };
 
   // tile → (instance, brick, n-block); XCD-aware order (n fastest, then bricks)
   int L = blockIdx.x, tile = L;
@@ -151,12 +165,48 @@ conv_brick_ks_kernel(BrickArgs a) {
   const int od0 = bd_i * a.BD, oh0 = bh_i * a.BH, ow0 = bw_i * a.BW;
   const int n0 = nbk * BN;
   const int HP = a.HD * a.HH * a.HW;
+  const float r_hw = 1.f / (float)a.HW, r_hplane = 1.f / (float)(a.HW * a.HH);
+  const float r_bw = 1.f / (float)a.BW, r_bplane = 1.f / (float)(a.BW * a.BH);
+
+  char* Hw = region + wave * (HMAX * kRowB);
+  const int nch = __builtin_amdgcn_readfirstlane(a.C / 32);
+  const int nck = __builtin_amdgcn_readfirstlane(a.C / 128);     // chunks of this wave: wave + 4k
+  const int flip = __builtin_amdgcn_readfirstlane(a.flip);
+  const int HH = __builtin_amdgcn_readfirstlane(a.HH), HWd = __builtin_amdgcn_readfirstlane(a.HW);
+  const int blkb = a.ny * 16 * 2;                   // bytes of one (hi|lo) fragment block
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const char*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C * ES,
+                                              (uint32_t)a.Di * a.Hi * a.Wi * a.C * (uint32_t)ES);
+  // this lane's halo slices (the same positions for every half-chunk): element offset or −1,
+  // computed per lane so that the first half-chunk's loads leave before anything else
+  int ho[NSL];
+#pragma unroll
+  for (int sl = 0; sl < NSL; ++sl) {
+    const int pos = (sl * 64 + lane) / SPP;
+    const int hd = qdiv(pos, r_hplane), rem = pos - hd * a.HW * a.HH;
+    const int hh = qdiv(rem, r_hw), hw = rem - hh * a.HW;
+    const int id = od0 - a.p + hd, ih = oh0 - a.p + hh, iw = ow0 - a.p + hw;
+    const bool ok = pos < HP && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+    ho[sl] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C : -1;
+  }
+  // half-chunk g = 2k + h (chunk k of this wave, half h): channels (wave + 4k)·32 + 16h …, LDS
+  // half-slot h (DB) or the only slot (DB = 0)
+  auto halo_ld = [&](int g, int sl) __attribute__((always_inline)) -> float4 {
+    const int e = sl * 64 + lane;
+    const int o = ho[sl];
+    const int cb = (wave + 4 * (g >> 1)) * 32 + 16 * (g & 1);
+    return buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + cb + CPS * (e % SPP)) * (uint32_t)ES);
+  };
+  // the first half-chunk's slices, in flight through the table set-up (one batch of ≤ kPB)
+  constexpr int kPB = NSL < 13 ? NSL : 13;
+  float4 pv0[kPB];
+#pragma unroll
+  for (int sl = 0; sl < kPB; ++sl) pv0[sl] = halo_ld(0, sl);
 
   for (int r = tid; r < BM; r += 256) {
     int off = -1;
     const int v = a.rowvox[r];
     if (v >= 0) {
-      const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
+      const int bd = qdiv(v, r_bplane), bh = qdiv(v - bd * a.BW * a.BH, r_bw), bw = v - (bd * a.BH + bh) * a.BW;
       const int od = od0 + bd, oh = oh0 + bh, ow = ow0 + bw;
       if (od < a.Do && oh < a.Ho && ow < a.Wo) {
         off = (int)((((int64_t)nb * a.Yd + od + a.ye) * a.Yh + oh + a.ye) * a.Yw + ow + a.ye);
@@ -169,24 +219,13 @@ conv_brick_ks_kernel(BrickArgs a) {
     }
     out_off[r] = off;
   }
-  for (int pos = tid; pos < HMAX; pos += 256) {
-    int o = -1;
-    if (pos < HP) {
-      const int hw = pos % a.HW, hh = (pos / a.HW) % a.HH, hd = pos / (a.HW * a.HH);
-      const int id = od0 - a.p + hd, ih = oh0 - a.p + hh, iw = ow0 - a.p + hw;
-      if ((unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
-        o = ((id * a.Hi + ih) * a.Wi + iw) * a.C;
-    }
-    hoff[pos] = o;
-  }
   // A: byte offset of each fragment row in this wave's halo (tap 0, this lane's 8-channel half)
-  char* Hw = region + wave * (HMAX * kRowB);
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     int v = a.rowvox[i * 32 + li];
     if (v < 0) v = -v - 1;
-    const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
+    const int bd = qdiv(v, r_bplane), bh = qdiv(v - bd * a.BW * a.BH, r_bw), bw = v - (bd * a.BH + bh) * a.BW;
     abase[i] = ((bd * a.HH + bh) * a.HW + bw) * kRowB + lh * 16;
   }
   // B: the pre-split weights through a descriptor (lane part fixed, step part wave-uniform)
@@ -194,31 +233,9 @@ conv_brick_ks_kernel(BrickArgs a) {
   int boff[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) boff[j] = ((n0 + j * 32 + li) * 16 + lh * 8) * 2;
-  const int nch = __builtin_amdgcn_readfirstlane(a.C / 32);
-  const int nck = __builtin_amdgcn_readfirstlane(a.C / 128);     // chunks of this wave: wave + 4k
-  const int flip = __builtin_amdgcn_readfirstlane(a.flip);
-  const int HH = __builtin_amdgcn_readfirstlane(a.HH), HWd = __builtin_amdgcn_readfirstlane(a.HW);
-  const int blkb = a.ny * 16 * 2;                   // bytes of one (hi|lo) fragment block
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const char*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C * ES,
-                                              (uint32_t)a.Di * a.Hi * a.Wi * a.C * (uint32_t)ES);
   __syncthreads();
   KS_STAMP(1);
 
-  // this lane's halo slices (the same positions for every half-chunk): element offset or −1
-  int ho[NSL];
-#pragma unroll
-  for (int sl = 0; sl < NSL; ++sl) {
-    const int e = sl * 64 + lane, pos = e / SPP;
-    ho[sl] = pos < HP ? hoff[pos] : -1;
-  }
-  // half-chunk g = 2k + h (chunk k of this wave, half h): channels (wave + 4k)·32 + 16h …, LDS
-  // half-slot h (DB) or the only slot (DB = 0)
-  auto halo_ld = [&](int g, int sl) __attribute__((always_inline)) -> float4 {
-    const int e = sl * 64 + lane;
-    const int o = ho[sl];
-    const int cb = (wave + 4 * (g >> 1)) * 32 + 16 * (g & 1);
-    return buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + cb + CPS * (e % SPP)) * (uint32_t)ES);
-  };
   // a loaded slice in its LDS format: the 16 B of a plane as they are, or 4 fp32 → 4 16-bit words
   typedef typename std::conditional<X16, f32x4v, uint2>::type Packed;
   auto halo_pack = [&](const float4& v) __attribute__((always_inline)) -> Packed {
@@ -260,11 +277,15 @@ conv_brick_ks_kernel(BrickArgs a) {
     for (int i = 0; i < TM; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(Hw + abase[i] + tap_off);
   };
 
-  // prologue: half-chunk 0 (13 slices in flight per batch), weights of the first kPF steps, A
-  // fragments of the first kAD
-  constexpr int kPB = 13;
+  // prologue: the weights of the first kPF steps, then half-chunk 0 (its first batch has been in
+  // flight since the kernel began), the A fragments of the first kAD steps
+  bf16x8 rb[kPF][TN];
 #pragma unroll
-  for (int s0 = 0; s0 < NSL; s0 += kPB) {
+  for (int u = 0; u < kPF; ++u) b_load(0, u, rb[u]);
+#pragma unroll
+  for (int sl = 0; sl < kPB; ++sl) halo_st(0, sl, pv0[sl]);
+#pragma unroll
+  for (int s0 = kPB; s0 < NSL; s0 += kPB) {
     float4 pv[kPB];
 #pragma unroll
     for (int sl = 0; sl < kPB; ++sl)
@@ -273,9 +294,6 @@ conv_brick_ks_kernel(BrickArgs a) {
     for (int sl = 0; sl < kPB; ++sl)
       if (s0 + sl < NSL) halo_st(0, s0 + sl, pv[sl]);
   }
-  bf16x8 rb[kPF][TN];
-#pragma unroll
-  for (int u = 0; u < kPF; ++u) b_load(0, u, rb[u]);
   bf16x8 af[kAD + 1][TM];
 #pragma unroll
   for (int v = 0; v < kAD; ++v) a_read(0, v, af[v]);
@@ -343,6 +361,31 @@ conv_brick_ks_kernel(BrickArgs a) {
   }
 
   KS_STAMP(3);
+  // The epilogue's operands are loaded before the reduction so that their latency hides under it.
+  // After the 4×4 quad transposes lane (li = 4m + k, lh) holds voxel row 32w + 8q + 4lh + k,
+  // channels n0 + 32j + 4m … 4m + 3 (q = 0 … 3).
+  const int k4 = li & 3, m4 = li >> 2;
+  int orow[4], xrow[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = wave * 32 + 8 * q + 4 * lh + k4;
+    orow[q] = out_off[row];
+    xrow[q] = a.sx ? xoff[row] : 0;
+  }
+  float4 bq[TN], mu[TN], rsd[TN], xs[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int c0 = n0 + j * 32 + 4 * m4;
+    bq[j] = a.bias ? *reinterpret_cast<const float4*>(a.bias + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.sx) {
+      mu[j] = *reinterpret_cast<const float4*>(a.smean + nb * a.ny + c0);
+      rsd[j] = *reinterpret_cast<const float4*>(a.srstd + nb * a.ny + c0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        xs[j][q] = orow[q] >= 0 ? *reinterpret_cast<const float4*>(a.sx + (int64_t)xrow[q] * a.ny + c0)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   // K reduction: every wave leaves the partials of the three fragment rows it does not finish
   // (float4 quads, lane-contiguous: conflict-free 16-B stores / loads); wave w then sums rows
   // 32w … 32w + 31 over the waves in order 0, 1, 2, 3
@@ -394,30 +437,14 @@ conv_brick_ks_kernel(BrickArgs a) {
   }
 
   KS_STAMP(4);
-  // epilogue: transpose each quad's 4×4 block across lanes 4m … 4m + 3 → lane (li = 4m + k, lh)
-  // holds voxel row 32w + 8q + 4lh + k, channels n0 + 32j + 4m … 4m + 3
-  const int k4 = li & 3, m4 = li >> 2;
-  int orow[4], xrow[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = wave * 32 + 8 * q + 4 * lh + k4;
-    orow[q] = out_off[row];
-    xrow[q] = a.sx ? xoff[row] : 0;
-  }
-  // per-lane statistics over its 4 voxels, per channel (fp64)
+  // epilogue: bias / activation or the backward-statistics operand, 16-B stores, per-lane fp64
+  // statistics over its 4 voxels per channel
   double ps[TN][4], pq[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int c0 = n0 + j * 32 + 4 * m4;
-    float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + c0);
-    float4 mu = bq, rs = bq;
-    if (a.sx) {
-      mu = *reinterpret_cast<const float4*>(a.smean + nb * a.ny + c0);
-      rs = *reinterpret_cast<const float4*>(a.srstd + nb * a.ny + c0);
-    }
-    const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
-    const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
+    const float muv[4] = {mu[j].x, mu[j].y, mu[j].z, mu[j].w}, rsv[4] = {rsd[j].x, rsd[j].y, rsd[j].z, rsd[j].w};
+    const float bv[4] = {bq[j].x, bq[j].y, bq[j].z, bq[j].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) ps[j][e] = pq[j][e] = 0.0;
 #pragma unroll
@@ -433,8 +460,7 @@ conv_brick_ks_kernel(BrickArgs a) {
           pq[j][e] += (double)v[e] * v[e];
         }
       } else {
-        const float4 xs = *reinterpret_cast<const float4*>(a.sx + (int64_t)xrow[q] * a.ny + c0);
-        const float xv[4] = {xs.x, xs.y, xs.z, xs.w};
+        const float xv[4] = {xs[j][q].x, xs[j][q].y, xs[j][q].z, xs[j][q].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float xh = (xv[e] - muv[e]) * rsv[e];
@@ -447,16 +473,17 @@ conv_brick_ks_kernel(BrickArgs a) {
     }
   }
   if (a.part) {
-    // lanes k = 0..3 of a quad hold the same channels: sum over k (xor 1, 2), then over the lane
-    // halves and the 4 waves through LDS, one double2 per channel
+    // lanes k = 0 … 3 of a quad hold the same channels: sum over k by DPP (xor 1, 2 — two 32-bit
+    // moves per double), then over the lane halves and the 4 waves through LDS, one double2 per
+    // channel
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        ps[j][e] += __shfl_xor(ps[j][e], 1);
-        pq[j][e] += __shfl_xor(pq[j][e], 1);
-        ps[j][e] += __shfl_xor(ps[j][e], 2);
-        pq[j][e] += __shfl_xor(pq[j][e], 2);
+        ps[j][e] += dpp_xor_d<0xB1>(ps[j][e]);
+        pq[j][e] += dpp_xor_d<0xB1>(pq[j][e]);
+        ps[j][e] += dpp_xor_d<0x4E>(ps[j][e]);
+        pq[j][e] += dpp_xor_d<0x4E>(pq[j][e]);
       }
     __syncthreads();
     double* red2 = reinterpret_cast<double*>(region);        // [4 waves][2 halves][BN][2]
@@ -560,8 +587,9 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
       const int64_t bricks = (int64_t)a.N * ceil_div(a.Do, b[0]) * ceil_div(a.Ho, b[1]) * ceil_div(a.Wo, b[2]);
       const int64_t blocks = bricks * (ny / (32 * V.tn));
       const int64_t slots = 256 * V.per_cu;
-      // a round of two co-resident TN-1 blocks takes the MFMA time of one TN-2 block
-      const double round_t = V.per_cu == 2 ? 2.0 : V.tn;
+      // a round costs about the same in every variant (r04c: fixed per-block costs dominate — one
+      // TN-1 block per CU took as long as two co-resident ones)
+      const double round_t = 2.0;
       // A-read bank conflicts: brick_row_perm deals each residue class (halo position mod 16) over
       // the 8 lane groups of a 128-row tile — conflict-free iff no class has more than 8 voxels
       // (3×6×6 in an 8×8 halo plane has 9 per class: 2-way on every read)
@@ -587,6 +615,9 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
     }
   }
   MRAGAN_CHECK_ARG(best_s >= 0, "conv_brick_ks: %d output channels are not a multiple of 32", ny);
+  // more than one round of CU slots (the 18³ data gradient at N = 4: 864 blocks): the r03 brick's
+  // 128×128 eight-wave tiles are faster there (30.0 vs 36.2 µs, r04c) — the caller falls back
+  if (!force && best[0] > 2.0) return kUnsupported;
   const int* b = shapes[best_s];
   const Var& V = vars[best_v];
   a.BD = b[0]; a.BH = b[1]; a.BW = b[2];
