@@ -309,7 +309,7 @@ const char* mragan_launch_log(int reset);
 
 /* diagnostics: copy the per-block phase timestamps (s_memtime) the 1-channel bf16x3 convolution
  * records when MRAGAN_STAMPS is set; n ≤ 40960 values, 5 per block.  n < 0: the K-split brick's
- * (conv_brick_ks.hip) −n values, 6 per wave, 24 per block, ≤ 1024 blocks. */
+ * (conv_brick_ks.hip) −n values, 8 per wave, 32 per block, ≤ 1024 blocks. */
 int mragan_debug_stamps(unsigned long long* host, int n);
 
 #ifdef __cplusplus

@@ -106,14 +106,15 @@ __device__ __forceinline__ double dpp_xor_d(double x) {
 
 }  // namespace
 
-// diagnostic stamps (MRAGAN_STAMPS=1): s_memtime per wave at entry / tables ready / prologue done /
-// main loop done / reduction done / exit — 6 per wave, 4 waves per block (mragan_debug_stamps, n < 0)
+// diagnostic stamps (MRAGAN_STAMPS=1): s_memtime per wave at entry / first half-chunk issued / tables
+// ready / prologue done / main loop done / reduction done / exit — 8 slots per wave, 4 waves per
+// block (mragan_debug_stamps, n < 0)
 constexpr int kKsStampBlocks = 1024;
-__device__ unsigned long long g_ks_stamps[kKsStampBlocks * 24];
+__device__ unsigned long long g_ks_stamps[kKsStampBlocks * 32];
 #define KS_STAMP(i)                                                                                   \
   do {                                                                                                \
     if (a.stamp && lane == 0 && blockIdx.x < kKsStampBlocks)                                          \
-      g_ks_stamps[blockIdx.x * 24 + wave * 6 + (i)] = __builtin_amdgcn_s_memtime();                   \
+      g_ks_stamps[blockIdx.x * 32 + wave * 8 + (i)] = __builtin_amdgcn_s_memtime();                   \
   } while (0)
 
 template <int TN, int DB, int PM, int X16>
@@ -201,6 +202,7 @@ conv_brick_ks_kernel(BrickArgs a) {
   float4 pv0[kPB];
 #pragma unroll
   for (int sl = 0; sl < kPB; ++sl) pv0[sl] = halo_ld(0, sl);
+  KS_STAMP(1);
 
   for (int r = tid; r < BM; r += 256) {
     int off = -1;
@@ -234,7 +236,7 @@ conv_brick_ks_kernel(BrickArgs a) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) boff[j] = ((n0 + j * 32 + li) * 16 + lh * 8) * 2;
   __syncthreads();
-  KS_STAMP(1);
+  KS_STAMP(2);
 
   // a loaded slice in its LDS format: the 16 B of a plane as they are, or 4 fp32 → 4 16-bit words
   typedef typename std::conditional<X16, f32x4v, uint2>::type Packed;
@@ -304,7 +306,7 @@ conv_brick_ks_kernel(BrickArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
-  KS_STAMP(2);
+  KS_STAMP(3);
   // one loop iteration = one half-chunk (27 taps, unrolled: ring slots are compile-time because 9
   // and 3 divide 27); the next half-chunk streams in meanwhile
   const int nhalf = 2 * nck;
@@ -360,7 +362,7 @@ conv_brick_ks_kernel(BrickArgs a) {
     }
   }
 
-  KS_STAMP(3);
+  KS_STAMP(4);
   // The epilogue's operands are loaded before the reduction so that their latency hides under it.
   // After the 4×4 quad transposes lane (li = 4m + k, lh) holds voxel row 32w + 8q + 4lh + k,
   // channels n0 + 32j + 4m … 4m + 3 (q = 0 … 3).
@@ -436,7 +438,7 @@ conv_brick_ks_kernel(BrickArgs a) {
     }
   }
 
-  KS_STAMP(4);
+  KS_STAMP(5);
   // epilogue: bias / activation or the backward-statistics operand, 16-B stores, per-lane fp64
   // statistics over its 4 voxels per channel
   double ps[TN][4], pq[TN][4];
@@ -512,7 +514,7 @@ conv_brick_ks_kernel(BrickArgs a) {
       dst[1] = q2;
     }
   }
-  KS_STAMP(5);
+  KS_STAMP(6);
 }
 
 template <int TN, int DB, int PM, int X16>
@@ -636,7 +638,7 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
 }
 
 int ks_debug_stamps(unsigned long long* host, int n) {
-  if (n > kKsStampBlocks * 24) n = kKsStampBlocks * 24;
+  if (n > kKsStampBlocks * 32) n = kKsStampBlocks * 32;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ks_stamps), (size_t)n * 8) == hipSuccess ? kOk : kLaunch;
 }
 

@@ -37,16 +37,17 @@ for N in (4, 2):
             fn()
         torch.cuda.synchronize()
         nb = 1024
-        buf = (C.c_ulonglong * (nb * 24))()
-        assert lib().mragan_debug_stamps(buf, -nb * 24) == 0
-        st = np.array(buf, dtype=np.float64).reshape(nb, 4, 6)
-        st = st[st[:, 0, 5] > st[:, 0, 0]]
-        d = np.diff(st, axis=2).reshape(-1, 5)
-        names = ["tables", "prologue", "main", "reduce", "epilogue"]
+        buf = (C.c_ulonglong * (nb * 32))()
+        assert lib().mragan_debug_stamps(buf, -nb * 32) == 0
+        st = np.array(buf, dtype=np.float64).reshape(nb, 4, 8)[:, :, :7]
+        st = st[st[:, 0, 6] > st[:, 0, 0]]
+        st = st[np.abs(st[:, 0, 0] - st[0, 0, 0]) < 20000]     # this launch's blocks only (stale slots of earlier, larger grids dropped)
+        d = np.diff(st, axis=2).reshape(-1, 6)
+        names = ["issue", "tables", "prologue", "main", "reduce", "epilogue"]
         med = "  ".join(f"{n} {np.median(d[:, i]):7.0f}" for i, n in enumerate(names))
-        tot = st[:, :, 5] - st[:, :, 0]
+        tot = st[:, :, 6] - st[:, :, 0]
         starts = st[:, 0, 0]
         print(f"N{N} {name:5s} blocks {len(st)}: median cycles {med}  | wave total {np.median(tot):.0f} "
-              f"(p90 {np.percentile(tot, 90):.0f}); span {st[:, :, 5].max() - starts.min():.0f}, "
-              f"start spread {starts.max() - starts.min():.0f}; main p10/p90 {np.percentile(d[:, 2], 10):.0f}/"
-              f"{np.percentile(d[:, 2], 90):.0f}")
+              f"(p90 {np.percentile(tot, 90):.0f}); span {st[:, :, 6].max() - starts.min():.0f}, "
+              f"start spread {starts.max() - starts.min():.0f}; main p10/p90 {np.percentile(d[:, 3], 10):.0f}/"
+              f"{np.percentile(d[:, 3], 90):.0f}")
