@@ -243,11 +243,50 @@ class RoundedConv:
     oracle's dtype (fp64: "emulated", no accumulation error; fp32: the calibration twin)."""
 
     def __init__(self, mode: str, loss_scale: float = 1.0):
-        if mode not in ("bf16", "fp16"):
-            raise ValueError(f"operand rounding must be 'bf16' or 'fp16', got {mode!r}")
+        if mode not in ("bf16", "fp16", "bf16x3"):
+            raise ValueError(f"operand rounding must be 'bf16', 'fp16' or 'bf16x3', got {mode!r}")
         self.mode = mode
-        self.dt = torch.bfloat16 if mode == "bf16" else torch.float16
+        self.dt = torch.float16 if mode == "fp16" else torch.bfloat16
         self.scale = float(loss_scale)
+
+    # ---- bf16x3 (the engine's fp32-grade split mode, csrc/prec.h kPrecBf16x3) -------------------
+    # Each fp32 operand v splits into hi = bf16(v), lo = bf16(v − hi) (RNE; v − hi is exact in
+    # fp32) and a product a·b is a_hi·b_hi + a_hi·b_lo + a_lo·b_hi — lo·lo dropped — accumulated in
+    # fp32 (three v_mfma_f32_32x32x16_bf16).  By linearity one bilinear op f (a convolution, its
+    # data or weight gradient) is then f(a_hi, b_hi + b_lo) + f(a_lo, b_hi): in fp64 both terms are
+    # exact sums of exact products.  Only the MFMA kernels split: the thin VALU kernels and the
+    # fp32 implicit-GEMM / weight-gradient fallbacks compute exact fp32 products in this mode
+    # (common.h op_round keeps the value), so each convolution takes the path the C ABI would
+    # dispatch it to (capi.hip conv_common / mragan_conv3d_wgrad, conv_igemm.hip, conv_wgrad.hip).
+    def split(self, t: torch.Tensor):
+        f = t.detach().float()
+        hi = f.to(torch.bfloat16)
+        lo = (f - hi.float()).to(torch.bfloat16)
+        return hi.to(t.dtype), lo.to(t.dtype)
+
+    def x3(self, f, a, b):
+        ah, al = self.split(a)
+        bh, bl = self.split(b)
+        return f(ah, bh + bl) + f(al, bh)
+
+    @staticmethod
+    def conv_splits(cx, ny, k, s):
+        """Does conv_common (a forward- or transposed-form launch: cx input channels, ny output
+        channels) run an MFMA (split) kernel?  thin_side → the 1-channel k7 MFMA kernels (thin1_x3,
+        thinn_x3) or the VALU thin kernels; else the implicit-GEMM family, whose MFMA paths (brick,
+        brickT, conv_igemm_x3) need cx % 16 == 0 and whose fp32 tiles take the rest."""
+        if cx <= 4 or ny <= 4 or cx % 8:
+            return k == 7 and s == 1 and ((cx == 1 and ny == 32) or (cx == 32 and ny == 1))
+        return cx % 16 == 0
+
+    @staticmethod
+    def wgrad_splits(cd, cg, k, s):
+        """Does mragan_conv3d_wgrad (dense cd channels, gathered cg) run an MFMA kernel?  thin side:
+        only thin1_wgrad_x3 (k7, 32 ↔ 1 channels); else wgrad3 / wgrad3s2 / conv_wgrad_x3, all of
+        which need multiples of 32 channels on both sides (the fp32 kernel takes the rest)."""
+        if cd < 8 or cg < 8:
+            return k == 7 and s == 1 and ((cd == 32 and cg == 1) or (cd == 1 and cg == 32))
+        return cd % 32 == 0 and cg % 32 == 0
 
     def op(self, t: torch.Tensor) -> torch.Tensor:
         return t.detach().float().to(self.dt).to(t.dtype)
@@ -267,6 +306,8 @@ class RoundedConv:
 class _RoundedConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, rnd, transposed, stride, padding, output_padding):
+        if rnd.mode == "bf16x3":
+            return _X3ConvFn.forward(ctx, x, w, b, rnd, transposed, stride, padding, output_padding)
         xr, wr = rnd.op(x), rnd.op(w)
         ctx.save_for_backward(xr, wr)
         ctx.cfg = (rnd, transposed, stride, padding, output_padding, b is not None)
@@ -275,6 +316,8 @@ class _RoundedConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        if ctx.cfg[0].mode == "bf16x3":
+            return _X3ConvFn.backward(ctx, gy)
         xr, wr = ctx.saved_tensors
         rnd, transposed, stride, padding, output_padding, has_b = ctx.cfg
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -288,6 +331,52 @@ class _RoundedConvFn(torch.autograd.Function):
                 got = list(torch.autograd.grad(y, want, rnd.grad(gy)))
             gx = got.pop(0) if need_x else None
             gw = got.pop(0) if need_w else None
+        if has_b and ctx.needs_input_grad[2]:
+            gb = gy.sum(dim=(0, 2, 3, 4))
+        return gx, gw, gb, None, None, None, None, None
+
+
+class _X3ConvFn:
+    """The bf16x3 mode's convolution (RoundedConv.x3): forward, data gradient and weight gradient
+    each split or exact as the engine dispatches it.  Shapes seen by the kernels: a Conv3d layer
+    (w [cout][cin]) runs its forward as conv_common(cx = cin, ny = cout), its data gradient in the
+    transposed form with (cx = cout, ny = cin) and its weight gradient with dense = dY (cout),
+    gathered = X (cin); a ConvTranspose3d layer (w [cin][cout]) the mirror image, with dense = X
+    (cin), gathered = dY (cout) (mragan_hip/engine.py Conv.dgrad / Conv.wgrad)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, rnd, transposed, stride, padding, output_padding):
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (rnd, transposed, stride, padding, output_padding, b is not None)
+        k = w.shape[-1]
+        cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
+        f = lambda a, c: _conv_any(a, c, transposed, stride, padding, output_padding)   # noqa: E731
+        y = rnd.x3(f, x, w) if rnd.conv_splits(cin, cout, k, stride) else f(x, w)
+        return y + b.view(1, -1, 1, 1, 1) if b is not None else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        rnd, transposed, stride, padding, output_padding, has_b = ctx.cfg
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        k = w.shape[-1]
+        cin, cout = (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
+
+        def vjp(xa, wa, ga, wrt):
+            with torch.enable_grad():
+                xl = xa.detach().requires_grad_(wrt == "x")
+                wl = wa.detach().requires_grad_(wrt == "w")
+                y = _conv_any(xl, wl, transposed, stride, padding, output_padding)
+                return torch.autograd.grad(y, xl if wrt == "x" else wl, ga)[0]
+
+        gx = gw = gb = None
+        if need_x:
+            dgrad = lambda g, c: vjp(x, c, g, "x")                                       # noqa: E731
+            gx = rnd.x3(dgrad, gy, w) if rnd.conv_splits(cout, cin, k, stride) else dgrad(gy, w)
+        if need_w:
+            wgrad = lambda a, g: vjp(a, w, g, "w")                                       # noqa: E731
+            dense, gathered = (cin, cout) if transposed else (cout, cin)
+            gw = rnd.x3(wgrad, x, gy) if rnd.wgrad_splits(dense, gathered, k, stride) else wgrad(x, gy)
         if has_b and ctx.needs_input_grad[2]:
             gb = gy.sum(dim=(0, 2, 3, 4))
         return gx, gw, gb, None, None, None, None, None
@@ -497,7 +586,8 @@ class CycleGANOracle:
                  operand_rounding: str = None, loss_scale: float = 1.0):
         """operand_rounding: None (the reference's arithmetic) or 'bf16' / 'fp16' — every
         convolution operand rounded as the engine's 16-bit contraction modes round it
-        (RoundedConv), fp16 gradients under the static `loss_scale`."""
+        (RoundedConv), fp16 gradients under the static `loss_scale` — or 'bf16x3', the split-bf16
+        products of the engine's fp32-grade MFMA mode where its MFMA kernels run (RoundedConv.x3)."""
         self.dtype = dtype
         self.conv = EXACT if operand_rounding is None else RoundedConv(operand_rounding, loss_scale)
         self.use_lsgan = use_lsgan

@@ -11,6 +11,14 @@ fp32-grade modes (f32, bf16x3) — gates calibrated on the reference's own fp32-
   * later steps: losses within max(1e-3, k × the reference's own fp32-vs-fp64 divergence at that
     step) — fp32 noise amplified by Adam, as for the reference (k = 4 exact f32, 10 bf16x3).
 
+bf16x3 against its own emulation: the oracle's operand_rounding="bf16x3" (RoundedConv.x3: the
+split products exactly where the engine's MFMA kernels split them, exact fp32 products where its
+VALU / fp32 kernels run) in fp64 ("emu64") and fp32 ("emu32", "emu32p1/p2"), tests/golden/prec_*.npz.
+The GPU's distance to emu64 is then fp32 accumulation order only: step-0 losses, volumes and
+running statistics within max(1e-4, 4 × the fp32 realisations' gap), gradients as the reduced
+modes below, later-step losses within max(1e-3, 10 × the gap at that step) — every gate value from
+the oracle, none from a GPU run.
+
 Reduced modes (bf16, fp16: every conv operand rounded) — against the oracle's rounded-operand
 step (tests/golden/prec_<case>.npz, tools/gen_precision_fixtures.py): "emu64" is the step with
 the engine's operand rounding evaluated in fp64, "emu32" the same in fp32 (and "emu32p1/p2" at
@@ -57,12 +65,20 @@ def build_model(meta, ckdir, precision="f32"):
 # every case in every contraction precision of the MFMA convolutions (include/mragan_hip.h)
 PRECISIONS = ("f32", "bf16x3", "bf16", "fp16")
 PARAMS = [(c, p) for p in PRECISIONS for c in CASES]
-# bf16 / fp16 round every MFMA operand once (one MFMA per product): their gates are the envelopes
-# measured against the reference's fp64 fixtures (tools/precision_envelope.py) with
-# ≈2× margin; a CPU restatement of the same operand rounding (fp64 oracle with bf16- / fp16-
-# rounded conv operands) reproduces the measured volume errors, so they are the arithmetic's,
-# not the kernels'.
+# bf16 / fp16 round every MFMA operand once (one MFMA per product): gated against the oracle's
+# rounded-operand step (below)
 REDUCED = ("bf16", "fp16")
+# per-tensor gradient outlier budget (all gradient gates): at most this fraction of the parameter
+# tensors (and at least 2) may exceed their envelope, none by more than OUTLIER_X×
+OUTLIER_FRAC, OUTLIER_X = 0.1, 5.0
+
+
+def check_outliers(label, bad, n_params):
+    worst = max(bad, key=lambda b: b[2] / b[3]) if bad else None
+    print(f"{label}: {len(bad)}/{n_params} parameter tensors over their envelope"
+          + (f"; worst {worst[0]}.{worst[1]} at {worst[2] / worst[3]:.2f}x" if worst else ""))
+    assert len(bad) <= max(2, int(OUTLIER_FRAC * n_params)), bad
+    assert all(r <= OUTLIER_X * env for _, _, r, env in bad), bad
 
 
 @pytest.fixture(scope="module", params=PARAMS, ids=[f"{c}-{p}" for c, p in PARAMS])
@@ -125,7 +141,7 @@ RS_TOL = {"f32": 1e-4, "bf16x3": 1e-3}
 # trajectory departs further: on the 6-step pool-1 case (r03a) 1.8e-4, 7.0e-4, 8.6e-4, 1.05e-3 at
 # steps 1-4, against the reference fp32's 5e-8 … 3.3e-5
 LATER_STEP_FACTOR = {"f32": 4.0, "bf16x3": 10.0}
-LATER_MIN = {"f32": 1e-3, "bf16x3": 3e-3}
+LATER_MIN = {"f32": 1e-3, "bf16x3": 1e-3}
 
 
 # ---- reduced precisions: against the rounded-operand oracle ----------------------------------
@@ -157,20 +173,49 @@ def _pgap(p, mode, key, got):
 
 
 REDUCED_MIN = 1e-3        # the north star's gate; the calibrated term can only widen it
+X3_MIN = 1e-4             # bf16x3 vs its emulation: the exact-f32 mode's gate vs the fp64 reference
+
+
+def _has_x3(name):
+    p = prec_fixture(name)
+    return p is not None and "bf16x3/emu64/steps" in p.files and "bf16x3/emu32/steps" in p.files
+
+
+def test_x3_against_emulation(stepped):
+    """bf16x3, step 0: losses, generated volumes and running statistics against the oracle's
+    bf16x3 emulation in fp64, within max(1e-4, 4 × the fp32 realisations' gap)."""
+    if stepped[2]["precision"] != "bf16x3":
+        pytest.skip("bf16x3 only")
+    name, mode, p, history, snap = _reduced(stepped)
+    w64 = p[f"{mode}/emu64/step0/losses"]
+    gap = max(rel_err(p[f"{mode}/{r}/step0/losses"], w64) for r in _cal_runs(p, mode))
+    err = rel_err(history[0], w64)
+    print(f"{name} bf16x3 step 0: loss rel err vs emulation {err:.2e} (fp32 gap {gap:.2e})")
+    assert err < max(X3_MIN, 4 * gap), (history[0], w64)
+    for vis, t in snap["vis"].items():
+        err, gap, *_ = _pgap(p, mode, f"step0/{vis}", t)
+        print(f"{name} bf16x3 {vis}: rel err vs emulation {err:.2e} (fp32 gap {gap:.2e})")
+        assert err < max(X3_MIN, 4 * gap), vis
+    for net, bufs in snap["bufs"].items():
+        for k, b in bufs.items():
+            err, gap, *_ = _pgap(p, mode, f"step0/buf/{net}/{k}", b)
+            assert err < max(X3_MIN, 4 * gap), (net, k, err, gap)
 
 
 def _reduced(stepped):
     name, z, meta, _, history, snap = stepped
     p = prec_fixture(name)
     mode = meta["precision"]
+    if mode == "bf16x3" and not _has_x3(name):
+        pytest.skip(f"no bf16x3 emulation fixture for {name} (tools/gen_precision_fixtures.py)")
     if p is None or f"{mode}/emu64/steps" not in p.files or f"{mode}/emu32/steps" not in p.files:
         pytest.skip(f"no rounded-operand fixture for {name} {mode} (tools/gen_precision_fixtures.py)")
     return name, mode, p, history, snap
 
 
 def test_reduced_losses(stepped):
-    if stepped[2]["precision"] not in REDUCED:
-        pytest.skip("fp32-grade mode")
+    if stepped[2]["precision"] not in REDUCED + ("bf16x3",):
+        pytest.skip("exact f32")
     name, mode, p, history, _ = _reduced(stepped)
     for step in range(int(p[f"{mode}/emu64/steps"])):
         w64 = p[f"{mode}/emu64/step{step}/losses"]
@@ -198,8 +243,8 @@ def test_reduced_volumes_and_running_stats(stepped):
 
 
 def test_reduced_gradients(stepped):
-    if stepped[2]["precision"] not in REDUCED:
-        pytest.skip("fp32-grade mode")
+    if stepped[2]["precision"] not in REDUCED + ("bf16x3",):
+        pytest.skip("exact f32")
     name, mode, p, _, snap = _reduced(stepped)
     bad, n_params = [], 0
     ours, r32, r64 = [], [], []
@@ -217,9 +262,7 @@ def test_reduced_gradients(stepped):
             ours.append(g * scale)
             r64.append(w64 * scale)
             r32.append(w32 * scale)
-    print(f"{name} {mode}: {len(bad)}/{n_params} parameters over their envelope: {bad}")
-    assert len(bad) <= max(2, int(0.2 * n_params)), bad
-    assert all(r <= 20 * env for _, _, r, env in bad), bad
+    check_outliers(f"{name} {mode}", bad, n_params)
     whole = rel_err(np.concatenate(ours), np.concatenate(r64))
     whole_ref = rel_err(np.concatenate(r32), np.concatenate(r64))
     print(f"{name} {mode}: whole-net grad rel err {whole:.2e} (emu32 gap {whole_ref:.2e})")
@@ -229,8 +272,8 @@ def test_reduced_gradients(stepped):
 def test_reduced_params_after_adam(stepped):
     """Adam's first step is ≈ ±lr·sign(g): count the sampled weights that stepped differently from
     emu64, against twice the emu32 run's count (and at least 2 %)."""
-    if stepped[2]["precision"] not in REDUCED:
-        pytest.skip("fp32-grade mode")
+    if stepped[2]["precision"] not in REDUCED + ("bf16x3",):
+        pytest.skip("exact f32")
     name, mode, p, _, snap = _reduced(stepped)
     total = bad = bad32 = 0
     for net, params in snap["params"].items():
@@ -255,6 +298,8 @@ def test_losses(stepped):
     got = history[0]
     want = z["fp64/step0/losses"]
     assert rel_err(got, want) < LOSS_TOL[meta["precision"]], (got, want)
+    if meta["precision"] == "bf16x3" and _has_x3(name):
+        return          # later steps: against the bf16x3 emulation's trajectory (test_reduced_losses)
     for step in range(1, meta["steps"]):
         # after an Adam step the reference's own fp32 run has left its fp64 run (elements with a
         # round-off-sized gradient step by ±lr either way): gate on that measured divergence
@@ -288,8 +333,8 @@ def conditioning(stepped):
     makes the step's gradients 1e-3…1e-2-conditioned (tools/diag_d.py traces it)."""
     from oracle.cyclegan_oracle import CycleGANOracle
     name, z, meta, _, _, _ = stepped
-    if meta["precision"] in REDUCED:
-        return None                 # reduced precisions: test_reduced_gradients
+    if meta["precision"] in REDUCED or (meta["precision"] == "bf16x3" and _has_x3(name)):
+        return None                 # reduced precisions / emulated bf16x3: test_reduced_gradients
     eps = PERTURB[meta["precision"]]
     pre = {4e-6: "fp64p4e-6", 4e-5: "fp64p4e-5"}[eps]
     if any(k.startswith(pre + "/") for k in z.files):
@@ -311,12 +356,16 @@ def conditioning(stepped):
 
 def test_gradients(stepped, conditioning):
     """Per parameter: ‖g − g64‖ ≤ max(1e-3, 2·‖g_ref32 − g64‖, 2·‖g64(perturbed) − g64‖)·‖g64‖
-    (SURVEY §8c calibrated protocol, plus the measured conditioning of this step) for all but 20 %
-    of the parameter tensors, and every tensor within 20× its envelope.  Pre-IN conv biases:
-    exactly 0.  Whole network: the same rule on all sampled elements together, no exceptions."""
+    (SURVEY §8c calibrated protocol, plus the measured conditioning of this step) for all but
+    OUTLIER_FRAC of the parameter tensors, and every tensor within OUTLIER_X× its envelope.
+    Pre-IN conv biases: exactly 0.  Whole network: the same rule on all sampled elements together,
+    no exceptions.  bf16x3 with an emulation fixture: test_reduced_gradients against it instead
+    (the split products move the gradients of this ill-conditioned step by more than fp32 does)."""
     name, z, meta, _, _, snap = stepped
     if meta["precision"] in REDUCED:
         pytest.skip("reduced precision: test_reduced_gradients")
+    if meta["precision"] == "bf16x3" and _has_x3(name):
+        pytest.skip("bf16x3: test_reduced_gradients against the bf16x3 emulation")
     bad = []
     n_params = 0
     ours, ref32, ref64, pert = [], [], [], [[] for _ in conditioning]
@@ -344,9 +393,7 @@ def test_gradients(stepped, conditioning):
     # outlier budget: one realization of the perturbation envelope is a noisy estimate and
     # under-states some kink-dominated tensors (measured at 64³: up to 6 of 36 UNet tensors at
     # ≤ 2.3×, 3 of 64 ResNet tensors at ≤ 13×); a kernel bug moves errors to O(1) in many tensors
-    print(f"{name} {meta['precision']}: {len(bad)}/{n_params} parameters over their envelope: {bad}")
-    assert len(bad) <= max(2, int(0.2 * n_params)), bad
-    assert all(r <= 20 * env for _, _, r, env in bad), bad
+    check_outliers(f"{name} {meta['precision']}", bad, n_params)
     cat = np.concatenate
     whole = rel_err(cat(ours), cat(ref64))
     whole_ref = rel_err(cat(ref32), cat(ref64))

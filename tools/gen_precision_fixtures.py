@@ -17,6 +17,7 @@ sampling losses, generated volumes, gradients, post-Adam parameters and running 
 the same indices in both, into tests/golden/prec_<case>.npz.  Data only.
 
 Usage:  python tools/gen_precision_fixtures.py [case ...]       (default: every case below)
+        PREC_MODES=bf16x3 python tools/gen_precision_fixtures.py ...   (a subset of the modes)
 """
 import os
 import random
@@ -34,9 +35,11 @@ from golden_util import CASE_KW, inputs, load  # noqa: E402
 from oracle.cyclegan_oracle import CycleGANOracle  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden")
-MODES = {"bf16": 1.0, "fp16": 1024.0}        # mode → the engine's loss scale (CycleGANModel default)
+# mode → the engine's loss scale (CycleGANModel default).  bf16x3: the fp32-grade split mode's
+# products (oracle RoundedConv.x3), the target of its multi-step gates (tests/test_step_gpu.py)
+MODES = {"bf16": 1.0, "fp16": 1024.0, "bf16x3": 1.0}
 SMALL = ["step_r9_s32_b1", "step_r6_s24_b2_nc2_lsgan", "step_unet_s32_b2_ngf8", "step_r6_s24_b1_noidt",
-         "step_r6_s24_b1_pool1"]
+         "step_r6_s24_b1_pool1", "step_r9_s32_b2_ngf16"]
 BIG = ["step_r9_s64_b2", "step_unet_s64_b1_ngf32", "step_r9_s96_b1_nc2", "step_r9_s128_b1",
        "step_unet256_s256_b1_ngf4"]
 # emu32p1 / emu32p2: the fp32 twin at inputs perturbed by ~2 fp32 ulps (relative 1e-7 N(0,1) noise):
@@ -100,7 +103,8 @@ def main():
     for case in cases:
         path = os.path.join(OUT, f"prec_{case}.npz")
         out = dict(np.load(path, allow_pickle=False)) if os.path.exists(path) else {}
-        for mode in MODES:
+        modes = os.environ.get("PREC_MODES", ",".join(MODES)).split(",")
+        for mode in modes:
             for r in RUNS:
                 if f"{mode}/{r}/steps" in out:
                     continue
