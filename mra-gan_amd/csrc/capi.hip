@@ -227,6 +227,10 @@ int mragan_conv3d_presplit_bwd_stats(const float* x, int N, int Di, int Hi, int 
   MRAGAN_CHECK_ARG(x && w && y && x_in && mean && rstd && part && chunks, "conv3d_presplit_bwd_stats: null pointer");
   MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_presplit_bwd_stats: transposed must be 0/1");
   MRAGAN_CHECK_ARG(act == kActNone || act == kActRelu || act == kActLrelu, "conv3d_presplit_bwd_stats: act %d", act);
+  // the shape checks conv_common makes, before the partials bound is computed from these ints
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv3d_presplit_bwd_stats: bad input shape");
+  MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv3d_presplit_bwd_stats: bad output shape");
+  MRAGAN_CHECK_ARG(k >= 1 && stride >= 1 && pad >= 0, "conv3d_presplit_bwd_stats: bad k/stride/pad");
   const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
   MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_presplit_bwd_stats: partials %zu < %zu bytes", part_bytes, bound);
   *chunks = 0;

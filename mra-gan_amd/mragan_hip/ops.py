@@ -556,6 +556,8 @@ def conv3d_bwd_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: in
         raise ValueError(f"bwd_stats: x_in shape {tuple(x_in.shape)} != {(N, Do, Ho, Wo, cout)}")
     if wp.numel() != k ** 3 * cin * cout:
         raise ValueError("bwd_stats: packed weight size mismatch")
+    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("bwd_stats: wsplit size does not match the packed weight")
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("bwd_stats: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
