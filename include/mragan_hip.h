@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 12
+#define MRAGAN_ABI_VERSION 13
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -282,6 +282,12 @@ int mragan_nonfinite_flag(const float* g, int64_t n, int* flag, void* stream);
 int mragan_adam_dev_checked(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* flag,
                             void* stream);
 int mragan_skip_count(int* flag, int* counter, void* stream);
+/* The step count net of skipped updates (torch's GradScaler does not advance the optimizer on a
+ * skipped step): writes into hyper[6] the mragan_adam_hyper scalars for step base[4] − *skipped,
+ * base = {lr, beta1, beta2, eps, step, grad_scale} in DEVICE memory (host-refreshed before each
+ * replay, like hyper), *skipped the DEVICE counter of mragan_skip_count.  Run it before the step's
+ * mragan_adam_dev_checked calls.  (ABI 13)                                                        */
+int mragan_adam_rebias(const float* base, const int* skipped, float* hyper, void* stream);
 int mragan_fill(float* p, int64_t n, float value, void* stream);
 /* ---- sliding-window inference (test.py:38-207 + TestModel, models/test_model.py) -------------
  * The normalised volume vol[X][Y][Z] (fp32, resident) is cut into the reference's patches and the

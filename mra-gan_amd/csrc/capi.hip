@@ -455,6 +455,11 @@ int mragan_adam_dev_checked(float* p, const float* g, float* m, float* v, int64_
   return adam_dev(p, g, m, v, n, hyper, flag, static_cast<hipStream_t>(stream));
 }
 
+int mragan_adam_rebias(const float* base, const int* skipped, float* hyper, void* stream) {
+  MRAGAN_CHECK_ARG(base && skipped && hyper && base != hyper, "adam_rebias: bad args");
+  return adam_rebias(base, skipped, hyper, static_cast<hipStream_t>(stream));
+}
+
 int mragan_nonfinite_flag(const float* g, int64_t n, int* flag, void* stream) {
   MRAGAN_CHECK_ARG(g && flag && n >= 0, "nonfinite_flag: bad args");
   return nonfinite_flag(g, n, flag, static_cast<hipStream_t>(stream));

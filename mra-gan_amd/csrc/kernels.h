@@ -184,6 +184,7 @@ int adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, floa
 void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float grad_scale, float* out);
 int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* skip,
              hipStream_t st);
+int adam_rebias(const float* base, const int* skipped, float* hyper, hipStream_t st);
 int nonfinite_flag(const float* g, int64_t n, int* flag, hipStream_t st);
 int skip_count(int* flag, int* counter, hipStream_t st);
 int pack_weight(const float* src, int A, int B, int T, int tr, float* dst, hipStream_t st);

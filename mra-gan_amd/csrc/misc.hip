@@ -498,6 +498,26 @@ void adam_hyper(float lr, float beta1, float beta2, float eps, int step, float g
   out[4] = (float)sqrt(bc2);
   out[5] = grad_scale;
 }
+// loss-scaled training: the six scalars of adam_hyper for t = base[4] − *skipped (the step count
+// net of the updates skipped for a non-finite gradient, as GradScaler leaves the optimizer's step
+// alone): base = {lr, beta1, beta2, eps, step, grad_scale}, written by the host; same formulas
+__global__ void adam_rebias_kernel(const float* __restrict__ base, const int* __restrict__ skipped,
+                                   float* __restrict__ hyper) {
+  if (threadIdx.x != 0) return;
+  const double t = (double)base[4] - (double)*skipped;
+  const double bc1 = 1.0 - pow((double)base[1], t);
+  const double bc2 = 1.0 - pow((double)base[2], t);
+  hyper[0] = (float)((double)base[0] / bc1);
+  hyper[1] = base[1];
+  hyper[2] = base[2];
+  hyper[3] = base[3];
+  hyper[4] = (float)sqrt(bc2);
+  hyper[5] = base[5];
+}
+int adam_rebias(const float* base, const int* skipped, float* hyper, hipStream_t st) {
+  hipLaunchKernelGGL(adam_rebias_kernel, dim3(1), dim3(64), 0, st, base, skipped, hyper);
+  return check_launch("adam_rebias");
+}
 int adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, const int* skip,
              hipStream_t st) {
   hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_cap(n)), dim3(256), 0, st, p, g, m, v, n, hyper, skip);

@@ -224,10 +224,16 @@ class FusedAdam(torch.optim.Optimizer):
             ops.fill(n._flat_grad, 0.0)
 
     def advance(self):
-        """Host half of a step: bump the step count and return the kernel's six scalars."""
+        """Host half of a step: bump the step count and return the six values step_dev reads — the
+        kernel's scalars, or with check_finite the base {lr, beta1, beta2, eps, step, grad_scale}
+        that step_dev turns into them on the device net of the skipped steps (mragan_adam_rebias:
+        like GradScaler, a skipped update does not advance the bias corrections)."""
         self.step_count += 1
         g = self.param_groups[0]
         beta1, beta2 = g['betas']
+        if self.check_finite:
+            return [float(g['lr']), float(beta1), float(beta2), float(g['eps']), float(self.step_count),
+                    float(self.grad_scale)]
         return ops_mod().adam_hyper(g['lr'], beta1, beta2, g['eps'], self.step_count, self.grad_scale)
 
     def _state(self, n):
@@ -247,6 +253,9 @@ class FusedAdam(torch.optim.Optimizer):
                 dev = self.nets[0]._flat_grad.device
                 self._flag = torch.zeros(1, dtype=torch.int32, device=dev)
                 self._skipped = torch.zeros(1, dtype=torch.int32, device=dev)
+                self._hyper = torch.empty(6, dtype=torch.float32, device=dev)
+            ops.adam_rebias(hyper, self._skipped, self._hyper)     # `hyper` holds advance()'s base
+            hyper = self._hyper
             for n in self.nets:
                 networks3D.ensure_flat(n)
                 ops.nonfinite_flag(n._flat_grad, self._flag)

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -67,6 +67,7 @@ SIGNATURES = {
     "mragan_adam_dev_checked": (i32, [vp, vp, vp, vp, i64, vp, vp, vp]),
     "mragan_nonfinite_flag": (i32, [vp, i64, vp, vp]),
     "mragan_skip_count": (i32, [vp, vp, vp]),
+    "mragan_adam_rebias": (i32, [vp, vp, vp, vp]),
     "mragan_fill": (i32, [vp, i64, f32, vp]),
     "mragan_debug_stamps": (i32, [vp, i32]),
     "mragan_launch_log": (C.c_char_p, [i32]),

@@ -722,6 +722,16 @@ def adam_dev_checked(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch
     call("mragan_adam_dev_checked", _ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(hyper), _ptr(flag), _stream())
 
 
+def adam_rebias(base: torch.Tensor, skipped: torch.Tensor, hyper: torch.Tensor):
+    """hyper (device, 6 fp32) ← adam_hyper(lr, beta1, beta2, eps, step − skipped, grad_scale) from
+    base = device {lr, beta1, beta2, eps, step, grad_scale} and the device skip counter."""
+    if base.dtype != torch.float32 or base.numel() < 6 or hyper.dtype != torch.float32 or hyper.numel() < 6:
+        raise ValueError("adam_rebias: base and hyper must be float32 tensors of 6 values")
+    if skipped.dtype != torch.int32 or not (base.is_cuda and hyper.is_cuda and skipped.is_cuda):
+        raise ValueError("adam_rebias: device tensors (skipped int32) expected")
+    call("mragan_adam_rebias", _ptr(base), _ptr(skipped), _ptr(hyper), _stream())
+
+
 def nonfinite_flag(g: torch.Tensor, flag: torch.Tensor):
     """flag |= 1 (device int32) when g holds an inf / NaN."""
     call("mragan_nonfinite_flag", _ptr(g), g.numel(), _ptr(flag), _stream())

@@ -1044,3 +1044,17 @@ def test_fp16_found_inf_skips_adam(ops):
     torch.cuda.synchronize()
     assert int(count) == 1 and int(flag) == 0
     assert all(torch.equal(a, b) for a, b in zip(p + m + v, snap))
+
+
+def test_adam_rebias_skipped_steps(ops):
+    """ABI 13: the device scalars for host step t with k skipped updates equal adam_hyper at t − k
+    (bit for bit), so a skipped step does not advance the bias corrections (GradScaler semantics)."""
+    lr, b1, b2, eps, scale = 2e-4, 0.5, 0.999, 1e-8, 1.0 / 1024
+    hyper = torch.empty(6, device="cuda")
+    for t, k in ((1, 0), (5, 0), (5, 2), (37, 11)):
+        base = torch.tensor([lr, b1, b2, eps, float(t), scale], device="cuda")
+        skipped = torch.tensor([k], dtype=torch.int32, device="cuda")
+        ops.adam_rebias(base, skipped, hyper)
+        torch.cuda.synchronize()
+        want = torch.tensor(ops.adam_hyper(lr, b1, b2, eps, t - k, scale))
+        assert torch.equal(hyper.cpu(), want), (t, k, hyper.cpu(), want)
