@@ -56,12 +56,12 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act, g_conv_precision};
-    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride)) {
+    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride, g_conv_precision)) {
       a.in_part = in_part;
       a.in_chunks = in_chunks;
       return conv_thin1_x3(a, g_conv_precision, ws, ws_bytes, st);
     }
-    if (g_conv_precision != MRAGAN_PREC_F32 && thinn_x3_applicable(cin, cout, k, stride))
+    if (g_conv_precision != MRAGAN_PREC_F32 && thinn_x3_applicable(cin, cout, k, stride, g_conv_precision))
       return conv_thinn_x3(a, g_conv_precision, ws, ws_bytes, st);
     return conv_thin(a, st);
   }
@@ -209,7 +209,7 @@ int mragan_conv3d_dgrad_in_stats(const float* dy, int N, int Di, int Hi, int Wi,
   const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
   MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_dgrad_in_stats: partials %zu < %zu bytes", part_bytes, bound);
   *chunks = 0;
-  if (g_conv_precision != MRAGAN_PREC_F32 && thin_side(cin, cout) && thin1_x3_applicable(cin, cout, k, 1)) {
+  if (g_conv_precision != MRAGAN_PREC_F32 && thin_side(cin, cout) && thin1_x3_applicable(cin, cout, k, 1, g_conv_precision)) {
     ThinArgs a{dy, N, Di, Hi, Wi, cin, w, nullptr, y, Do, Ho, Wo, cout, k, 1, 0, 1, kActNone, g_conv_precision};
     a.in_part = part; a.in_chunks = chunks;
     a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act; a.bs_fold = fold_pad;
@@ -299,8 +299,8 @@ size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout,
                                int Ho, int Wo, int transposed) {
   if (thin_side(cin, cout)) {
     if (g_conv_precision == MRAGAN_PREC_F32) return 0;
-    if (thin1_x3_applicable(cin, cout, k, stride)) return thin1_x3_ws_bytes(cout);
-    if (thinn_x3_applicable(cin, cout, k, stride)) return thinn_x3_ws_bytes();
+    if (thin1_x3_applicable(cin, cout, k, stride, g_conv_precision)) return thin1_x3_ws_bytes(cout);
+    if (thinn_x3_applicable(cin, cout, k, stride, g_conv_precision)) return thinn_x3_ws_bytes(cout);
     return 0;
   }
   IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad, transposed, 0, 1,
@@ -310,7 +310,7 @@ size_t mragan_conv3d_workspace(int N, int Di, int Hi, int Wi, int cin, int cout,
 
 size_t mragan_conv3d_wgrad_workspace(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k, int stride) {
   if (thin_wgrad_side(Cd, Cg)) {
-    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+    if (g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride, g_conv_precision))
       return thin1_wgrad_x3_ws_bytes();
     return conv_thin_wgrad_ws_bytes(N, Dd, Hd, Wd, Cd, Cg, k, stride);
   }
@@ -323,7 +323,7 @@ int mragan_conv3d_wgrad(const float* dense, int N, int Dd, int Hd, int Wd, int C
   MRAGAN_CHECK_ARG(dense && gathered && dw && ws, "wgrad: null pointer");
   MRAGAN_CHECK_ARG(Cd > 0 && Cg > 0 && k >= 1 && stride >= 1 && pad >= 0, "wgrad: bad args");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (thin_wgrad_side(Cd, Cg) && g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride))
+  if (thin_wgrad_side(Cd, Cg) && g_conv_precision != MRAGAN_PREC_F32 && thin1_wgrad_x3_applicable(Cd, Cg, k, stride, g_conv_precision))
     return conv_thin1_wgrad_x3(dense, N, Dd, Hd, Wd, Cd, gathered, Dg, Hg, Wg, Cg, pad, dw, accumulate, g_conv_precision,
                                ws, ws_bytes, st);
   if (thin_wgrad_side(Cd, Cg)) {

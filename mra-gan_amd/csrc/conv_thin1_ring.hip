@@ -62,23 +62,48 @@ __device__ __forceinline__ int x8_entry(int row, int pos, int slot) {
 }
 
 // eight consecutive w of one Q row (zero outside Q) through the volume's range-checked
-// descriptor: out-of-range elements get an offset past the end and read 0
+// descriptor: out-of-range elements get an offset past the end and read 0.  Q is channels-last
+// with C channels; this reads channel c.
 __device__ __forceinline__ void load_row8(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0,
-                                          float (&v)[8]) {
+                                          float (&v)[8], int C = 1, int c = 0) {
   const bool okdh = (unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H;
-  const uint32_t rowb = (uint32_t)(((int64_t)d * H + h) * W) * 4u;
+  const uint32_t rowb = ((uint32_t)(((int64_t)d * H + h) * W) * C + c) * 4u;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int w = w0 + j;
     const bool ok = okdh && (unsigned)w < (unsigned)W;
-    v[j] = buf_load_f32(q, ok ? rowb + 4u * (uint32_t)w : kOobOffset);
+    v[j] = buf_load_f32(q, ok ? rowb + 4u * C * (uint32_t)w : kOobOffset);
   }
 }
 
+// both channels of a two-channel Q row (one 8-B load per voxel): channel 0 → v, channel 1 → u
+__device__ __forceinline__ void load_row8x2(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0,
+                                            float (&v)[8], float (&u)[8]) {
+  const bool okdh = (unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H;
+  const uint32_t rowb = (uint32_t)(((int64_t)d * H + h) * W) * 8u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int w = w0 + j;
+    const bool ok = okdh && (unsigned)w < (unsigned)W;
+    const uint2 p = buf_load_8b(q, (int)(ok ? rowb + 8u * (uint32_t)w : kOobOffset), 0);
+    v[j] = __uint_as_float(p.x);
+    u[j] = __uint_as_float(p.y);
+  }
+}
+
+// load_row8 / load_row8x2 by channel count (C2: channel 1 → u)
+template <int C2>
+__device__ __forceinline__ void load_rows(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0,
+                                          float (&v)[8], float (&u)[8]) {
+  if constexpr (C2) load_row8x2(q, D, H, W, d, h, w0, v, u);
+  else load_row8(q, D, H, W, d, h, w0, v);
+}
+
 // X8 entry e of a plane (rows of kBW entries) from its 8 raw values, split hi / lo
-__device__ __forceinline__ f32x8 load_row8v(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0) {
+__device__ __forceinline__ f32x8 load_row8v(__amdgpu_buffer_rsrc_t q, int D, int H, int W, int d, int h, int w0,
+                                            int C = 1, int c = 0) {
   float v[8];
-  load_row8(q, D, H, W, d, h, w0, v);
+  load_row8(q, D, H, W, d, h, w0, v, C, c);
   return f32x8{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
 }
 
@@ -100,6 +125,26 @@ __device__ __forceinline__ void store_x8(bf16x8* ringH, bf16x8* ringL, int plane
   const int idx = slot * plane_e + x8_entry<SW>(e / kBW, e % kBW, slot);
   ringH[idx] = hi;
   if constexpr (prec::has_lo<PM>()) ringL[idx] = lo;
+}
+
+// X8 entry of a two-channel Q in a one-plane mode: channel 0 → the hi ring, channel 1 → the
+// ring the lo planes of bf16x3 occupy (one-plane modes leave it free)
+template <int PM, int C2>
+__device__ __forceinline__ void store_x8c(bf16x8* ringH, bf16x8* ringL, int plane_e, int slot, int e,
+                                          const float (&v)[8], const float (&u)[8]) {
+  if constexpr (C2) {
+    static_assert(!prec::has_lo<PM>(), "two-channel X8 rings use the lo ring: one-plane modes only");
+    const f32x8 fv = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+    const f32x8 fu = {u[0], u[1], u[2], u[3], u[4], u[5], u[6], u[7]};
+    bf16x8 h0, l0, h1, l1;
+    prec::split8v<PM>(fv, h0, l0);
+    prec::split8v<PM>(fu, h1, l1);
+    const int idx = slot * plane_e + x8_entry<0>(e / kBW, e % kBW, slot);
+    ringH[idx] = h0;
+    ringL[idx] = h1;
+  } else {
+    store_x8<PM, 0>(ringH, ringL, plane_e, slot, e, v);
+  }
 }
 
 // the depth-chunk length: items = columns × ⌈D / L⌉ spread over ≤ ncu blocks; cost ≈ rounds ×
@@ -129,24 +174,32 @@ int cu_count() {
   return ncu;
 }
 
-// wp: packed [343][ny] (cin = 1) → out[(g·2 + hl)·ny + co][8] bf16, e = kw (e = 7 and g = 49: 0)
+// wp: packed [343][ny][cx] (cx = 1, or 2 in the one-plane modes) → out[(g·2 + hl)·ny + co][8]
+// bf16, e = kw (e = 7 and g = 49: 0); hl = 1 holds the lo split (bf16x3) or channel 1 (cx = 2)
 template <int PM>
-__global__ void thin1_pack_kernel(const float* __restrict__ wp, int ny, int flip, __bf16* __restrict__ out) {
+__global__ void thin1_pack_kernel(const float* __restrict__ wp, int ny, int cx, int flip, __bf16* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= kGroups * ny) return;
   const int co = i % ny, g = i / ny;
-  f32x8 v;
+  f32x8 v, u;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    float w = 0.f;
+    float w = 0.f, w1 = 0.f;
     if (g < kK * kK && e < kK) {
       const int t = g * kK + e;
-      w = wp[(int64_t)(flip ? kT - 1 - t : t) * ny + co];
+      const int64_t o = ((int64_t)(flip ? kT - 1 - t : t) * ny + co) * cx;
+      w = wp[o];
+      if (cx == 2) w1 = wp[o + 1];
     }
     v[e] = w;
+    u[e] = w1;
   }
   bf16x8 hi, lo;
   prec::split8v<PM>(v, hi, lo);
+  if (cx == 2) {
+    bf16x8 l1;
+    prec::split8v<PM>(u, lo, l1);
+  }
   *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 0) * ny + co) * 8) = hi;
   *reinterpret_cast<bf16x8*>(out + ((int64_t)(g * 2 + 1) * ny + co) * 8) = lo;
 }
@@ -178,7 +231,9 @@ constexpr int kFPlaneE = kFRH * kBW;    // 352 entries per plane (hi or lo)
 constexpr int kFLds = 2 * kRing * kFPlaneE * 16 + kGroups * 2 * kC * 16;   // ring + weights: 141 312 B
 constexpr int kFRed = 4 * kC * 2 * 8;   // + [4 waves][32 channels][Σ, Σ²] doubles (a.part)
 
-template <int PM>
+// C2: a two-channel input (one-plane modes): channel 1's X8 planes and weights sit where the lo
+// splits of bf16x3 do, and each K-step issues one MFMA per channel
+template <int PM, int C2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_fwd_kernel(Thin1RArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);       // [kRing][kFPlaneE]
@@ -206,7 +261,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     const int od0 = chunk * a.L, oh0 = chh * kFH, ow0 = cw * kBW;
     const int nsteps = min(a.L, a.Do - od0);
     const int nplanes = nsteps + kK - 1;
-    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi, (uint32_t)a.Di * a.Hi * a.Wi * 4u);
+    constexpr int CX = C2 ? 2 : 1;
+    const __amdgpu_buffer_rsrc_t xr =
+        make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * CX, (uint32_t)a.Di * a.Hi * a.Wi * (4u * CX));
     const int d0 = od0 - a.pe, h0 = oh0 - a.pe, w0 = ow0 - a.pe;
     // this thread's X8 entries of a plane: tid and tid + 256 (< 352)
     const bool e1 = tid + 256 < kFPlaneE;
@@ -216,11 +273,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     // prologue: planes 0..6 → slots 0..6
 #pragma unroll
     for (int rp = 0; rp < kK; ++rp) {
-      float v0[8], v1[8];
-      load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er0, w0 + ep, v0);
-      if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er1, w0 + ep, v1);
-      store_x8<PM, 0>(ringH, ringL, kFPlaneE, rp, tid, v0);
-      if (e1) store_x8<PM, 0>(ringH, ringL, kFPlaneE, rp, tid + 256, v1);
+      float v0[8], v1[8], u0[8], u1[8];
+      load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er0, w0 + ep, v0, u0);
+      if (e1) load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er1, w0 + ep, v1, u1);
+      store_x8c<PM, C2>(ringH, ringL, kFPlaneE, rp, tid, v0, u0);
+      if (e1) store_x8c<PM, C2>(ringH, ringL, kFPlaneE, rp, tid + 256, v1, u1);
     }
     __syncthreads();
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
@@ -245,10 +302,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     for (int s = 0; s < nsteps; ++s) {
       const bool more = s + kK < nplanes;
-      float n0[8], n1[8];
+      float n0[8], n1[8], m0[8], m1[8];
       if (more) {
-        load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er0, w0 + ep, n0);
-        if (e1) load_row8(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er1, w0 + ep, n1);
+        load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er0, w0 + ep, n0, m0);
+        if (e1) load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er1, w0 + ep, n1, m1);
       }
       // backward statistics: this step's x̂ operands, loaded before the MFMAs so their latency hides
       // under them (loaded in the epilogue they stalled every depth step: +0.17 ms per step)
@@ -272,18 +329,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int g0 = 2 * ks, g1 = 2 * ks + 1 < kK * kK ? 2 * ks + 1 : kK * kK - 1;
         const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
         const bf16x8 ah = wsm[(g * 2 + 0) * kC + co];
-        const bf16x8 al = prec::has_lo<PM>() ? wsm[(g * 2 + 1) * kC + co] : ah;
+        const bf16x8 al = (prec::has_lo<PM>() || C2) ? wsm[(g * 2 + 1) * kC + co] : ah;
         const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<0>(bh0 + kh, bw, 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const bf16x8 xh = ringH[base + 2 * i * kBW];
-          const bf16x8 xl = prec::has_lo<PM>() ? ringL[base + 2 * i * kBW] : xh;
-          acc[i] = prec::mma<PM>(ah, al, xh, xl, acc[i]);
+          const bf16x8 xl = (prec::has_lo<PM>() || C2) ? ringL[base + 2 * i * kBW] : xh;
+          if constexpr (C2) {
+            acc[i] = prec::mma<PM>(ah, ah, xh, xh, acc[i]);
+            acc[i] = prec::mma<PM>(al, al, xl, xl, acc[i]);
+          } else {
+            acc[i] = prec::mma<PM>(ah, al, xh, xl, acc[i]);
+          }
         }
       }
       if (more) {
-        store_x8<PM, 0>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0);
-        if (e1) store_x8<PM, 0>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid + 256, n1);
+        store_x8c<PM, C2>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0, m0);
+        if (e1) store_x8c<PM, C2>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid + 256, n1, m1);
       }
 
       const int od = od0 + s, ow = ow0 + bw;
@@ -359,9 +421,25 @@ int thin1_debug_stamps(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_thin1_stamps), (size_t)n * 8) == hipSuccess ? kOk : kLaunch;
 }
 
-bool thin1_x3_applicable(int cx, int ny, int k, int s) { return cx == 1 && k == kK && s == 1 && ny == kC; }
+// cx = 2 (nc = 2 volumes, BASELINE configs[4]) in the one-plane modes: the second channel takes
+// the lo ring / weight rows bf16x3 would use
+bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode) {
+  const bool one_plane = mode == kPrecBf16 || mode == kPrecF16;
+  return (cx == 1 || (cx == 2 && one_plane)) && k == kK && s == 1 && ny == kC;
+}
 
 size_t thin1_x3_ws_bytes(int ny) { return (size_t)kGroups * 2 * ny * 8 * sizeof(__bf16); }
+
+template <int PM, int C2>
+static void launch_thin1_fwd(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM, C2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((thin1r_fwd_kernel<PM, C2>), dim3(grid), dim3(256), lds, st, a);
+}
 
 template <int PM>
 static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -370,7 +448,12 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
     set_error("thin1_x3: workspace %zu < %zu", ws_bytes, need);
     return kWorkspace;
   }
-  hipLaunchKernelGGL(thin1_pack_kernel<PM>, dim3(ceil_div(kGroups * t.ny, 256)), dim3(256), 0, st, t.w, t.ny,
+  const bool c2 = t.cx == 2;
+  if (!(t.cx == 1 || (c2 && !prec::has_lo<PM>()))) {
+    set_error("thin1_x3: %d input channels in precision mode %d", t.cx, PM);
+    return kBadArg;
+  }
+  hipLaunchKernelGGL(thin1_pack_kernel<PM>, dim3(ceil_div(kGroups * t.ny, 256)), dim3(256), 0, st, t.w, t.ny, t.cx,
                      t.trans ? 1 : 0, static_cast<__bf16*>(ws));
   int rc = check_launch("thin1_x3_pack");
   if (rc) return rc;
@@ -385,7 +468,7 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   a.nbh = ceil_div(t.Ho, kFH); a.nbw = ceil_div(t.Wo, kBW);
   const int64_t columns = (int64_t)t.N * a.nbh * a.nbw;
   if (columns == 0 || t.Do == 0) return kOk;
-  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * 4 < (int64_t)kOobOffset, "thin1_x3: input volume too large");
+  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * t.cx * 4 < (int64_t)kOobOffset, "thin1_x3: input volume too large");
   int grid = 1;
   pick_chunk(columns, t.Do, cu_count(), a.L, a.nch, grid);
   a.items = (int)(columns * a.nch);
@@ -400,13 +483,12 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
     if (t.in_chunks) *t.in_chunks = a.nch * a.nbh * a.nbw;
   }
   const size_t lds = kFLds + kFRed;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+  if constexpr (!prec::has_lo<PM>()) {
+    if (c2) launch_thin1_fwd<PM, 1>(a, grid, lds, st);
+    else launch_thin1_fwd<PM, 0>(a, grid, lds, st);
+  } else {
+    launch_thin1_fwd<PM, 0>(a, grid, lds, st);
   }
-  hipLaunchKernelGGL(thin1r_fwd_kernel<PM>, dim3(grid), dim3(256), lds, st, a);
   return check_launch("thin1_x3");
 }
 
@@ -420,7 +502,8 @@ int conv_thin1_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStr
 struct Thin1RWArgs {
   int stamp;
   const float* P; int N, Dp, Hp, Wp;          // [N][Dp][Hp][Wp][32]
-  const float* Q; int Dq, Hq, Wq;             // [N][Dq][Hq][Wq]
+  const float* Q; int Dq, Hq, Wq;             // [N][Dq][Hq][Wq][qC], channel qc
+  int qC, qc;
   int pe;
   int nbh, nbw, L, nch, items;
   float* slab;                                // [gridDim.x][343][32]
@@ -487,7 +570,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int vd0 = chunk * a.L, vh0 = chh * kBH, vw0 = cw * kBW;
     const int nsteps = min(a.L, a.Dp - vd0);
     const int nplanes = nsteps + kK - 1;
-    const __amdgpu_buffer_rsrc_t qr = make_rsrc(a.Q + (int64_t)nb * a.Dq * a.Hq * a.Wq, (uint32_t)a.Dq * a.Hq * a.Wq * 4u);
+    const __amdgpu_buffer_rsrc_t qr =
+        make_rsrc(a.Q + (int64_t)nb * a.Dq * a.Hq * a.Wq * a.qC, (uint32_t)a.Dq * a.Hq * a.Wq * a.qC * 4u);
     const __amdgpu_buffer_rsrc_t pr =
         make_rsrc(a.P + (int64_t)nb * a.Dp * a.Hp * a.Wp * kC, (uint32_t)a.Dp * a.Hp * a.Wp * kC * 4u);
     const int d0 = vd0 - a.pe, h0 = vh0 - a.pe, w0 = vw0 - a.pe;
@@ -501,7 +585,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       if (tid < kPlaneE) {
         float v[7][8];
 #pragma unroll
-        for (int rp = 0; rp < kK; ++rp) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + rp, h0 + erow, w0 + epos, v[rp]);
+        for (int rp = 0; rp < kK; ++rp) load_row8(qr, a.Dq, a.Hq, a.Wq, d0 + rp, h0 + erow, w0 + epos, v[rp], a.qC, a.qc);
 #pragma unroll
         for (int rp = 0; rp < kK; ++rp) store_x8<PM, 1>(ringH, ringL, kPlaneE, rp, tid, v[rp]);
       }
@@ -515,7 +599,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       const bool more_q = s + kK < nplanes && tid < kPlaneE, more_p = s + 1 < nsteps;
       float4 v0 = {}, v1 = {};
       f32x8 q = {};
-      if (more_q) q = load_row8v(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos);
+      if (more_q) q = load_row8v(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos, a.qC, a.qc);
       if (more_p) p_load(pr, vd0 + s + 1, vh0, vw0, v0, v1);
 
       const __bf16* ph = pt + (size_t)(s & 1) * 2 * kC * kPS;
@@ -575,12 +659,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 }
 
-// out[c][t] (=|+=) Σ_blocks slab[z][τ(t)][c]   (τ = tap mirror for the head form)
+// out[c·ocs + ooff + t] (=|+=) Σ_blocks slab[z][τ(t)][c]   (τ = tap mirror for the head form; ocs,
+// ooff place the 32-channel side and the Q channel in dW[dn][gn][343])
 // One block per tap: 8 groups of 32 lanes (lane = channel: 128 contiguous bytes per slab row),
 // group g sums slabs z ≡ g (mod 8) in increasing z, then the 8 partials are added in g order —
 // fixed order, deterministic.
 __global__ void __launch_bounds__(256) thin1_wgrad_reduce_kernel(const float* __restrict__ slab, int nz, int flip,
-                                                                 float* __restrict__ out, int accumulate) {
+                                                                 float* __restrict__ out, int ocs, int ooff,
+                                                                 int accumulate) {
   __shared__ float part[8][kC];
   const int t = blockIdx.x, c = threadIdx.x % kC, g = threadIdx.x / kC;
   const int ts = flip ? kT - 1 - t : t;
@@ -593,13 +679,16 @@ __global__ void __launch_bounds__(256) thin1_wgrad_reduce_kernel(const float* __
     float r = part[0][c];
 #pragma unroll
     for (int k = 1; k < 8; ++k) r += part[k][c];
-    const int e = c * kT + t;
+    const int64_t e = (int64_t)c * ocs + ooff + t;
     out[e] = accumulate ? out[e] + r : r;
   }
 }
 
-bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s) {
-  return k == kK && s == 1 && ((Cd == kC && Cg == 1) || (Cd == 1 && Cg == kC));
+// 2-channel single side (nc = 2) in the one-plane modes: one pass per channel of that side
+bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s, int mode) {
+  const bool one_plane = mode == kPrecBf16 || mode == kPrecF16;
+  auto thin = [&](int c) { return c == 1 || (c == 2 && one_plane); };
+  return k == kK && s == 1 && ((Cd == kC && thin(Cg)) || (thin(Cd) && Cg == kC));
 }
 
 size_t thin1_wgrad_x3_ws_bytes() { return (size_t)cu_count() * kT * kC * sizeof(float); }
@@ -610,18 +699,24 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
   Thin1RWArgs a{};
   static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
   a.stamp = stamps;
-  int flip;
-  if (Cg == 1) {          // stem: P = D (32 ch), Q = G
+  int flip, nq, ocs, qstride;
+  if (Cd == kC) {         // stem: P = D (32 ch), Q = G (Cg channels): dW[c][q][t]
     a.P = D; a.Dp = Dd; a.Hp = Hd; a.Wp = Wd;
     a.Q = G; a.Dq = Dg; a.Hq = Hg; a.Wq = Wg;
     a.pe = p; flip = 0;
-  } else {                // head: P = G (32 ch), Q = D, u = m − p + t
+    nq = Cg; ocs = Cg * kT; qstride = kT;
+  } else {                // head: P = G (32 ch), Q = D (Cd channels), u = m − p + t: dW[q][c][t]
     a.P = G; a.Dp = Dg; a.Hp = Hg; a.Wp = Wg;
     a.Q = D; a.Dq = Dd; a.Hq = Hd; a.Wq = Wd;
     a.pe = kK - 1 - p; flip = 1;
+    nq = Cd; ocs = kT; qstride = kC * kT;
   }
+  MRAGAN_CHECK_ARG(nq == 1 || (nq == 2 && (mode == kPrecBf16 || mode == kPrecF16)),
+                   "thin1_wgrad_x3: %d single-side channels in precision mode %d", nq, mode);
   a.N = N;
-  MRAGAN_CHECK_ARG((int64_t)a.Dp * a.Hp * a.Wp * kC * 4 < (int64_t)kOobOffset && (int64_t)a.Dq * a.Hq * a.Wq * 4 < (int64_t)kOobOffset,
+  a.qC = nq;
+  MRAGAN_CHECK_ARG((int64_t)a.Dp * a.Hp * a.Wp * kC * 4 < (int64_t)kOobOffset &&
+                       (int64_t)a.Dq * a.Hq * a.Wq * nq * 4 < (int64_t)kOobOffset,
                    "thin1_wgrad_x3: volume too large");
   a.nbh = ceil_div(a.Hp, kBH); a.nbw = ceil_div(a.Wp, kBW);
   const int64_t columns = (int64_t)N * a.nbh * a.nbw;
@@ -637,22 +732,30 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
   a.slab = static_cast<float*>(ws);
   const size_t lds = (size_t)2 * kRing * kPlaneE * 16 + (size_t)2 * 2 * kC * kPS * sizeof(__bf16);
   static_assert(kMT * 32 * kC * 4 <= 2 * kRing * kPlaneE * 16, "the wave reduction fits the ring");
-  int rc = kOk;
-  MRAGAN_PREC_DISPATCH(mode, {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_wgrad_kernel<PM>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(512), lds, st, a);
-    rc = check_launch("thin1_wgrad_x3");
-    break;
-  })
-  if (rc) return rc;
   static_assert(kC * 8 == 256, "reduce block = 8 groups of kC lanes");
-  hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, flip, out, accumulate);
-  return check_launch("thin1_wgrad_reduce");
+  // one pass per channel of the single side (nc = 2: the 32-channel operand is read twice; the
+  // slabs are reused, stream-ordered)
+  for (int qc = 0; qc < nq; ++qc) {
+    a.qc = qc;
+    int rc = kOk;
+    MRAGAN_PREC_DISPATCH(mode, {
+      static bool attr_set = false;
+      if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_wgrad_kernel<PM>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+      }
+      hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(512), lds, st, a);
+      rc = check_launch("thin1_wgrad_x3");
+      break;
+    })
+    if (rc) return rc;
+    hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, flip, out, ocs,
+                       qc * qstride, accumulate);
+    rc = check_launch("thin1_wgrad_reduce");
+    if (rc) return rc;
+  }
+  return kOk;
 }
 
 }  // namespace mragan

@@ -52,11 +52,15 @@ constexpr int kThreads = 512;            // 8 waves, one output row each (2 per 
 constexpr int kF4PT = (kNF4 + kThreads - 1) / kThreads;
 
 // weight fragment table: [kd' 8][half 2][step 4][hi|lo][lane 64][8 bf16]
+constexpr int kPackElems = 8 * 2 * 4 * 2 * 64 * 8;
 //   lane = 16g + n: column n = 8j + kw, k-group g → kh = 2·step + (g >> 1), channels
 //   16·half + 8(g & 1) … +7; zero where kd = kd' − j ∉ [0, 7), kh = 7 or kw = 7
+// (ny = 2, one-plane modes: one table per output channel co = blockIdx.y, weights packed
+// [343][ny][32])
 template <int PM>
-__global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, __bf16* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, int ny, __bf16* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, co = blockIdx.y;
+  out += (int64_t)co * kPackElems;
   if (i >= 8 * 2 * 4 * 64) return;
   const int lane = i & 63, s = (i >> 6) & 3, half = (i >> 8) & 1, kdp = i >> 9;
   const int n = lane & 15, g = lane >> 4;
@@ -67,7 +71,7 @@ __global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, __b
   const int t = ok ? (kd * kK + kh) * kK + kw : 0;
   const int tt = flip ? kK * kK * kK - 1 - t : t;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = ok ? wp[tt * kC + c0 + e] : 0.f;
+  for (int e = 0; e < 8; ++e) v[e] = ok ? wp[((int64_t)tt * ny + co) * kC + c0 + e] : 0.f;
   bf16x8 hi, lo;
   prec::split8v<PM>(v, hi, lo);
   const int64_t base = ((int64_t)((kdp * 2 + half) * 4 + s) * 2) * 64 * 8;
@@ -81,7 +85,7 @@ struct ThinnArgs {
   const float* x; int N, Di, Hi, Wi;      // [N][Di][Hi][Wi][32]
   const __bf16* wx;
   const float* bias;
-  float* y; int Do, Ho, Wo;               // [N][Do][Ho][Wo]
+  float* y; int Do, Ho, Wo, ny;           // [N][Do][Ho][Wo][ny]
   int pe, act;
   int P, nseg, nr, nw;                    // pairs per segment, segments, row blocks, column blocks
   int total, per;                         // blocks, blocks per XCD range
@@ -107,7 +111,8 @@ thinn_x3_kernel(ThinnArgs a) {
   const int cw = blk % a.nw; blk /= a.nw;
   const int r = blk % a.nr; blk /= a.nr;
   const int seg = blk % a.nseg;
-  const int nb = blk / a.nseg;
+  const int nbco = blk / a.nseg;          // (output channel, instance)
+  const int nb = nbco % a.N, co = nbco / a.N;
   const int od0 = 2 * a.P * seg, oh0 = r * kBH, ow0 = cw * kOW;
   const int npairs = min(a.P, (a.Do - od0 + 1) / 2);
   const int nunits = 2 * (2 * npairs + kK - 1);
@@ -159,9 +164,9 @@ thinn_x3_kernel(ThinnArgs a) {
   const int a_hi = 16 * ((g & 1) ^ thinn_rot(n16)), a_lo = 16 * ((2 + (g & 1)) ^ thinn_rot(n16));
   // weight fragments through a buffer descriptor: lane part fixed (VGPR), (plane, half, step)
   // part wave-uniform (SGPR soffset) — no 64-bit address arithmetic per fragment
-  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.wx, 8 * 2 * 4 * 2 * 64 * 8 * 2);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.wx + (int64_t)co * kPackElems, kPackElems * 2);
   const int wlane = lane * 16;
-  const float bias = a.bias ? a.bias[0] : 0.f;
+  const float bias = a.bias ? a.bias[co] : 0.f;
   const int oh = oh0 + wave;
 
   // pair j's sums → z[od0 + 2j + jj][oh][ow] = Σ_kw P[ow − ow0 + kw][8jj + kw] through the wave's
@@ -182,7 +187,7 @@ thinn_x3_kernel(ThinnArgs a) {
       for (int kw = 0; kw < kK; ++kw) sum += Pw[(owl + kw) * 17 + 8 * jj + kw];
       const int od = od0 + 2 * j + jj, ow = ow0 + owl;
       if (od < a.Do && oh < a.Ho && ow < a.Wo)
-        a.y[(((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow] = act_fwd(sum + bias, a.act);
+        a.y[((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * a.ny + co] = act_fwd(sum + bias, a.act);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
   };
@@ -246,31 +251,39 @@ thinn_x3_kernel(ThinnArgs a) {
   }
 }
 
-bool thinn_x3_applicable(int cx, int ny, int k, int s) { return cx == kC && ny == 1 && k == kK && s == 1; }
+// ny = 2 (nc = 2 volumes, BASELINE configs[4]) in the one-plane modes
+bool thinn_x3_applicable(int cx, int ny, int k, int s, int mode) {
+  const bool one_plane = mode == kPrecBf16 || mode == kPrecF16;
+  return cx == kC && (ny == 1 || (ny == 2 && one_plane)) && k == kK && s == 1;
+}
 
-size_t thinn_x3_ws_bytes() { return (size_t)8 * 2 * 4 * 2 * 64 * 8 * sizeof(__bf16); }
+size_t thinn_x3_ws_bytes(int ny) { return (size_t)ny * kPackElems * sizeof(__bf16); }
 
 template <int PM>
 static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!ws || ws_bytes < thinn_x3_ws_bytes()) {
-    set_error("thinn_x3: workspace %zu < %zu", ws_bytes, thinn_x3_ws_bytes());
+  if (!(t.ny == 1 || (t.ny == 2 && !prec::has_lo<PM>()))) {
+    set_error("thinn_x3: %d output channels in precision mode %d", t.ny, PM);
+    return kBadArg;
+  }
+  if (!ws || ws_bytes < thinn_x3_ws_bytes(t.ny)) {
+    set_error("thinn_x3: workspace %zu < %zu", ws_bytes, thinn_x3_ws_bytes(t.ny));
     return kWorkspace;
   }
-  hipLaunchKernelGGL(thinn_x3_pack_kernel<PM>, dim3(16), dim3(256), 0, st, t.w, t.trans ? 1 : 0,
+  hipLaunchKernelGGL(thinn_x3_pack_kernel<PM>, dim3(16, t.ny), dim3(256), 0, st, t.w, t.trans ? 1 : 0, t.ny,
                      static_cast<__bf16*>(ws));
   int rc = check_launch("thinn_x3_pack");
   if (rc) return rc;
   ThinnArgs a{};
   a.x = t.x; a.N = t.N; a.Di = t.Di; a.Hi = t.Hi; a.Wi = t.Wi;
   a.wx = static_cast<const __bf16*>(ws);
-  a.bias = t.bias; a.y = t.y; a.Do = t.Do; a.Ho = t.Ho; a.Wo = t.Wo;
+  a.bias = t.bias; a.y = t.y; a.Do = t.Do; a.Ho = t.Ho; a.Wo = t.Wo; a.ny = t.ny;
   a.pe = t.trans ? kK - 1 - t.p : t.p;
   a.act = t.act;
   a.nr = ceil_div(t.Ho, kBH); a.nw = ceil_div(t.Wo, kOW);
   // pairs per depth segment: rounds of resident blocks (one per CU) × the segment's units
   // (2P + 6 planes)
   const int nq = ceil_div(t.Do, 2);
-  const int64_t cols = (int64_t)a.N * a.nr * a.nw;
+  const int64_t cols = (int64_t)a.N * a.ny * a.nr * a.nw;
   if (cols == 0 || nq == 0) return kOk;
   static int ncu = 0;
   if (!ncu) {

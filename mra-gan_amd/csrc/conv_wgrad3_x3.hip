@@ -47,8 +47,12 @@ constexpr int kLdsW = 128 * kDRow + 64 * kGRow;     // 105 472 B (8-wave 128 × 
 // groups of a 32-lane half hit 16 distinct 16-B slots (conflict-free transposed reads; the
 // ds_write_b64 of 16 contiguous lanes stays one 128-B run): chunk c of row k sits at
 // c ^ tr_swz(k).  The kw-shifted X rows (k + 8kw) keep k's swizzle.
-constexpr int kTrRowsD = kSegW * kR;                 // 128 K rows of dY per stage
-constexpr int kTrRowsG = (kSegW + 2) * kR;           // 144 K rows of X (two extra w for kw = 1, 2)
+// (SW: voxels per row segment of the 16-bit paths — 16, or 24 for 24-wide volumes such as the
+// 96³ configuration's ResnetBlocks, BASELINE configs[4]; the operand-plane path only)
+template <int SW> constexpr int tr_rows_d() { return SW * kR; }          // 128 K rows of dY per stage (SW 16)
+template <int SW> constexpr int tr_rows_g() { return (SW + 2) * kR; }    // 144 K rows of X (two extra w for kw = 1, 2)
+constexpr int kTrRowsD = tr_rows_d<kSegW>();
+constexpr int kTrRowsG = tr_rows_g<kSegW>();
 template <int RB>
 __device__ __forceinline__ int tr_swz(int row) {
   return RB == 256 ? (row & 3) << 2 : ((row >> 1) & 1) << 2;
@@ -59,6 +63,8 @@ constexpr int kTrStage = kTrRowsD * 64 * 2 + kTrRowsG * 64 * 2;    // 34 816 B
 constexpr int kTrStageW = kTrRowsD * 128 * 2 + kTrRowsG * 64 * 2;  // 51 200 B
 constexpr int kLdsTr = 2 * kTrStage;
 constexpr int kLdsTrW = 2 * kTrStageW;
+template <int SW, int TC>
+constexpr int lds_tr() { return 2 * (tr_rows_d<SW>() * TC * 2 + tr_rows_g<SW>() * 64 * 2); }
 typedef short tr_v4s __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ tr_v4s tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tr_v4s*)(p));
@@ -94,7 +100,7 @@ struct Wgrad3Args {
 // 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
 // the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
 // kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
-template <int TC, int TI, int PM, int X16, int AL>
+template <int TC, int TI, int PM, int X16, int AL, int SW>
 __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
   constexpr int WC = TC / 32;             // waves along co
@@ -106,6 +112,9 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   using RegT = std::conditional_t<X16 != 0, uint2, float4>;
   constexpr int RBD = TC * 2, RBG = TI * 2;         // tr image row bytes (dY, X)
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(SW == kSegW || (X16 && AL), "24-voxel segments: the aligned operand-plane path only");
+  constexpr int kSegW = SW;               // voxels per row segment (shadows the file constant)
+  constexpr int kTrRowsD = tr_rows_d<SW>(), kTrRowsG = tr_rows_g<SW>();
   constexpr int kStage = kTrRowsD * RBD + kTrRowsG * RBG;            // tr: bytes of one stage buffer
   char* Ds = smem;
   char* Gs = smem + (kTr ? kTrRowsD * RBD : TC * kDRow);
@@ -135,7 +144,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   // contiguous bytes (a w-fastest order, conflict-free for the LDS writes below, measured 35 %
   // slower overall).  dY: TC/4 quads × 16 w = one unit per thread.  X: TI/4 quads × 18 w'.
   constexpr int DQ = TC / 4, GQ = TI / 4;
-  static_assert(NT == 16 * DQ, "one dY unit per thread");
+  static_assert(SW != 16 || NT == 16 * DQ, "one dY unit per thread");
   const int cq = tid % DQ, uw = tid / DQ;          // dY unit
   const int gcq = tid % GQ, gw = tid / GQ;         // X unit: w' = gw
   // TC == TI: threads own w' 0..15 and threads < 2·GQ also w' 16, 17 (rg2).  TC = 2·TI: threads
@@ -198,8 +207,8 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   constexpr bool kW16 = X16 && AL;
   constexpr int NW = NT / 64, SPW = kR / NW;                   // waves, segments per wave
   constexpr int DO8 = TC / 8, GO8 = TI / 8;                    // 16-B octets per voxel
-  constexpr int DL = 16 * DO8 / 64, GU = 18 * GO8, GL = (GU + 63) / 64;
-  static_assert(kR % NW == 0 && (16 * DO8) % 64 == 0, "wave-per-segment staging");
+  constexpr int DL = kSegW * DO8 / 64, GU = (kSegW + 2) * GO8, GL = (GU + 63) / 64;
+  static_assert(kR % NW == 0 && (kSegW * DO8) % 64 == 0, "wave-per-segment staging");
   uint4 d16[kW16 ? SPW : 1][kW16 ? DL : 1], g16[kW16 ? SPW : 1][kW16 ? GL : 1];
   int dlo[kW16 ? DL : 1], glo[kW16 ? GL : 1], rdo[kW16 ? SPW : 1], rgo[kW16 ? SPW : 1];
   if constexpr (kW16) {
@@ -442,8 +451,18 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
 
 static bool w3_wide(const WgradArgs& a) { return a.Cd % 128 == 0 && a.Cg % 64 == 0; }
 
+// segment width: 16, or 24 on the aligned operand-plane path (whole w-runs per 8-segment stage)
+static int w3_segw(const WgradArgs& a) {
+  if (a.Wd % kSegW == 0) return kSegW;
+  if (a.in16 && a.Wd % 24 == 0) {
+    const int nsw = a.Wd / 24;
+    if (kR % nsw == 0 && a.Hd % (kR / nsw) == 0) return 24;
+  }
+  return 0;
+}
+
 bool wgrad3_x3_applicable(const WgradArgs& a) {
-  return a.x3 && a.k == 3 && a.s == 1 && a.p == 0 && a.Wd % kSegW == 0 && a.Dg == a.Dd + 2 && a.Hg == a.Hd + 2 &&
+  return a.x3 && a.k == 3 && a.s == 1 && a.p == 0 && w3_segw(a) != 0 && a.Dg == a.Dd + 2 && a.Hg == a.Hd + 2 &&
          a.Wg == a.Wd + 2 && a.Cd % kTile == 0 && a.Cg % kTile == 0 &&
          (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg * 4 < ((int64_t)1 << 31) &&     // byte offsets are 32-bit
          (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd * 4 < ((int64_t)1 << 31);
@@ -452,7 +471,7 @@ bool wgrad3_x3_applicable(const WgradArgs& a) {
 // splits: at most 2 blocks per CU in total (one round: a 513th block doubles the time),
 // ≥ 4 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
 int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
-  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
+  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / w3_segw(a));
   const bool wide = w3_wide(a);
   const int tiles = (a.Cd / (wide ? 128 : kTile)) * (a.Cg / kTile) * 9;
   static const int budget = [] {                              // A/B switch: MRAGAN_W3_BLOCKS
@@ -471,21 +490,22 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TC, int TI, int PM, int X16, int AL>
+template <int TC, int TI, int PM, int X16, int AL, int SW = kSegW>
 static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
-  if constexpr (X16 && prec::has_lo<PM>()) {
+  if constexpr ((X16 && prec::has_lo<PM>()) || (SW != kSegW && !(X16 && AL))) {
     return;                                     // rejected by the caller
   } else {
     constexpr bool tr = !prec::has_lo<PM>();
     constexpr bool wide = TC == 128;
-    const int lds = wide ? (tr ? kLdsTrW : kLdsW) : (tr ? kLdsTr : kLds);
+    const int lds = SW != kSegW ? lds_tr<SW, TC>() : wide ? (tr ? kLdsTrW : kLdsW) : (tr ? kLdsTr : kLds);
+    static_assert(SW == kSegW || lds_tr<SW, TC>() <= 160 * 1024, "LDS");
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
+    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
   }
 }
 
@@ -494,7 +514,12 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
   a.dy = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
   a.x = g.G; a.Cg = g.Cg;
   a.ws = g.ws;
-  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / kSegW);
+  const int segw = w3_segw(g);
+  if (!segw) {
+    set_error("wgrad3_x3: width %d is not a multiple of 16 (or of 24 on the operand-plane path)", g.Wd);
+    return -kBadArg;
+  }
+  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / segw);
   int per = (a.nseg + splits - 1) / splits;
   per = (per + kR - 1) / kR * kR;
   a.seg_per_split = per;
@@ -506,10 +531,19 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     return -kBadArg;
   }
   // aligned stages: whole w-runs of rows of one plane per stage, every stage full
-  const int nsw = g.Wd / kSegW;
+  const int nsw = g.Wd / segw;
   static const bool no_al = getenv("MRAGAN_W3_NO_AL") != nullptr;   // A/B switch
   const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
+  if (segw != kSegW && !(al && g.in16)) {
+    set_error("wgrad3_x3: 24-voxel segments need aligned stages on operand planes");
+    return -kBadArg;
+  }
   MRAGAN_PREC_DISPATCH(g.x3, {
+    if (segw != kSegW) {
+      if (wide) launch_wgrad3<128, 64, PM, 1, 1, 24>(a, blocks, st);
+      else launch_wgrad3<64, 64, PM, 1, 1, 24>(a, blocks, st);
+      return nsplit;
+    }
     if (wide) {
       if (g.in16) { if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st); }
       else { if (al) launch_wgrad3<128, 64, PM, 0, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 0, 0>(a, blocks, st); }

@@ -92,17 +92,18 @@ struct ThinArgs {
   int bs_act = 0, bs_fold = 0;
 };
 int conv_thin(ThinArgs a, hipStream_t st);
-// bf16x3 MFMA path for 1 → 32/64-channel k7 s1 convolutions (conv_thin1_x3.hip)
-bool thin1_x3_applicable(int cx, int ny, int k, int s);
+// MFMA path for 1 → 32-channel k7 s1 convolutions (conv_thin1_ring.hip); 2 → 32 in the one-plane
+// modes (mode = the precision code)
+bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode);
 size_t thin1_x3_ws_bytes(int ny);
 int conv_thin1_x3(const ThinArgs& a, int mode, void* ws, size_t ws_bytes, hipStream_t st);
 int thin1_debug_stamps(unsigned long long* host, int n);
 // bf16x3 MFMA path for 32 → 1-channel k7 s1 convolutions (conv_thinn_x3.hip)
-bool thinn_x3_applicable(int cx, int ny, int k, int s);
-size_t thinn_x3_ws_bytes();
+bool thinn_x3_applicable(int cx, int ny, int k, int s, int mode);
+size_t thinn_x3_ws_bytes(int ny);
 int conv_thinn_x3(const ThinArgs& a, int mode, void* ws, size_t ws_bytes, hipStream_t st);
 // bf16x3 MFMA weight gradient of the 1-channel k7 s1 convolutions (conv_thin1_wgrad_x3.hip)
-bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s);
+bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s, int mode);
 size_t thin1_wgrad_x3_ws_bytes();
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
                         int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st);

@@ -124,7 +124,9 @@ class ConvLayer:
         kernel (k3 s1), the implicit GEMM (no K split), brickT (32-channel ConvTranspose3d) and the
         stem's thin1 kernel (k7, 1 → 32) also leave the IN statistics partials.
         Returns (y, part, chunks); chunks = 0 when no partials were produced."""
-        thin1 = self.cin == 1 and self.k == 7 and self.s == 1 and not self.transposed   # G stem (thin1_x3)
+        # G stem (thin1 ring kernel): one input channel, or two in the one-plane modes (nc = 2)
+        thin1 = ((self.cin == 1 or (self.cin == 2 and ops.get_conv_precision() in ("bf16", "fp16")))
+                 and self.k == 7 and self.s == 1 and not self.transposed)
         if _NO_IN_STATS or ops.get_conv_precision() == "f32" or (min(self.cin, self.cout) < 8 and not thin1):
             return self.forward(x), None, 0
         N, D, H, W, _ = x.shape
@@ -164,10 +166,12 @@ class ConvLayer:
         """wgrad of a forward-form conv from the operand planes of X and dY (wgrad3, 16-bit modes)."""
         ops.conv3d_wgrad_op16(dy16, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
 
-    def op16_ok(self, W):
-        """Can this k3 s1 conv run on operand planes (brick both ways, wgrad3) at output width W?"""
+    def op16_ok(self, W, H=None):
+        """Can this k3 s1 conv run on operand planes (brick both ways, wgrad3) at output width W?
+        (wgrad3's row segments: 16 voxels, or 24 with whole rows per 8-segment stage — H % 8 == 0)"""
+        seg_ok = W % 16 == 0 or (W == 24 and (H is None or H % 8 == 0))
         return (not self.transposed and self.k == 3 and self.s == 1 and self.ws_fwd is not None
-                and self.ws_bwd is not None and self.cin % 64 == 0 and self.cout % 64 == 0 and W % 16 == 0)
+                and self.ws_bwd is not None and self.cin % 64 == 0 and self.cout % 64 == 0 and seg_ok)
 
     def dgrad(self, dy, in_spatial):
         """Gradient w.r.t. this layer's input (shape = input spatial dims, Cin channels)."""
@@ -175,10 +179,12 @@ class ConvLayer:
                           transposed=not self.transposed, wsplit=self.ws_bwd)
 
     def dgrad_in_stats_ok(self):
-        """The G head (ngf → 1, k7 p0): its data gradient runs thin1_x3 in the MFMA modes, whose
-        epilogue can leave the backward statistics of the InstanceNorm in front of it (ABI 12)."""
-        return (not _NO_IN_STATS and not _NO_HEAD_STATS and ops.get_conv_precision() != "f32" and not self.transposed
-                and self.cout == 1
+        """The G head (ngf → 1, k7 p0; ngf → 2 in the one-plane modes): its data gradient runs the
+        thin1 ring kernel in the MFMA modes, whose epilogue can leave the backward statistics of the
+        InstanceNorm in front of it (ABI 12)."""
+        prec = ops.get_conv_precision()
+        return (not _NO_IN_STATS and not _NO_HEAD_STATS and prec != "f32" and not self.transposed
+                and (self.cout == 1 or (self.cout == 2 and prec in ("bf16", "fp16")))
                 and self.k == 7 and self.s == 1 and self.p == 0)
 
     def dgrad_in_stats(self, dy, in_spatial, norm_x, mean, rstd, act, fold_pad):
@@ -343,7 +349,7 @@ class NetPlan:
                 if st.norm is not None:
                     # the conv's epilogue leaves the norm's statistics partials where it can
                     sc.h, part, chunks = st.conv.forward_in_stats(cur)
-                    if want16 and self._op16_blocks_ok(sc.h.shape[3]):
+                    if want16 and self._op16_blocks_ok(sc.h.shape[3], sc.h.shape[2]):
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad,
                                                                                 part=part, chunks=chunks,
                                                                                 want_f32=True)
@@ -362,9 +368,9 @@ class NetPlan:
         """16-bit operand planes for the ResnetBlock section: bf16 / fp16 mode, not switched off."""
         return not _NO_OP16 and ops.op16_dtype() is not None
 
-    def _op16_blocks_ok(self, W):
-        """Every ResnetBlock conv can run on operand planes at block width W."""
-        return all(st.conv1.op16_ok(W) and st.conv2.op16_ok(W) for st in self.stages if st.kind == "block")
+    def _op16_blocks_ok(self, W, H=None):
+        """Every ResnetBlock conv can run on operand planes at block width W (height H)."""
+        return all(st.conv1.op16_ok(W, H) and st.conv2.op16_ok(W, H) for st in self.stages if st.kind == "block")
 
     # ---- backward ----------------------------------------------------------------------
     def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,

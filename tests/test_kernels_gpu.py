@@ -76,6 +76,10 @@ CONV_CASES = [
     (1, 16, 2, 21, 7, 1, 0),
     (1, 8, 1, 20, 4, 1, 1),
     (2, 2, 32, 20, 7, 1, 0),
+    # nc = 2 stem / head at sizes past one 16×16 tile (thin1 ring with two channels, thinn with two
+    # output channels in the one-plane modes)
+    (2, 2, 32, 23, 7, 1, 0),
+    (1, 32, 2, 23, 7, 1, 0),
     # UnetGenerator downconvs (k4 s2 p1): stem nc→ngf, down to a 1³ innermost output
     (2, 1, 8, 16, 4, 2, 1),
     (1, 64, 64, 2, 4, 2, 1),
@@ -502,7 +506,7 @@ def test_op16_instnorm_bwd_plane(op16, C, dypad, act, with_g):
         assert torch.equal(G, G_ref)
 
 
-@pytest.mark.parametrize("N,C,S,W", [(2, 128, 16, 16), (1, 64, 9, 16), (1, 128, 5, 32)])
+@pytest.mark.parametrize("N,C,S,W", [(2, 128, 16, 16), (1, 64, 9, 16), (1, 128, 5, 32), (1, 128, 8, 24), (2, 64, 8, 24)])
 def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     """ABI 11: the brick forward (with its InstanceNorm partials), the whole-grid data gradient and
     the k3 s1 weight gradient on operand planes equal the same kernels on the fp32 tensors in the
@@ -531,7 +535,10 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     ops.conv3d_wgrad(dy, x, 3, 1, 0, gw_ref, False)
     gw = torch.full_like(gw_ref, float("nan"))
     ops.conv3d_wgrad_op16(dy.to(dt), x.to(dt), 3, 1, 0, gw, False)
-    assert torch.equal(gw, gw_ref)
+    if W % 16 == 0:
+        assert torch.equal(gw, gw_ref)
+    else:   # 24-wide rows: wgrad3's 24-voxel segments (planes only) vs the generic kernel on fp32
+        assert rel(gw, gw_ref) < 2e-5
     # and against fp64 on the rounded operands (the mode's definition)
     gw64 = F.conv3d(ncdhw(x.to(dt).double().cpu()).transpose(0, 1), ncdhw(dy.to(dt).double().cpu()).transpose(0, 1))
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
@@ -566,22 +573,25 @@ def test_op16_dgrad_backward_statistics(op16, N, C, S, W, act):
     assert (got != plane).float().mean().item() < 1e-3
 
 
-@pytest.mark.parametrize("N,S,act", [(2, 16, "relu"), (1, 13, "lrelu")])
-def test_head_dgrad_backward_statistics(x3, N, S, act):
-    """ABI 12: the G head's data gradient (conv 32 → 1, k7 p0, transposed form on thin1_x3) leaves
-    the backward statistics of the InstanceNorm in front of the head (its output replication-
-    padded by 3): dz bit-identical to the plain data gradient, dx within fp32 summation-order
-    noise of the statistics-pass result."""
+@pytest.mark.parametrize("N,S,act,nc", [(2, 16, "relu", 1), (1, 13, "lrelu", 1), (2, 16, "relu", 2),
+                                        (1, 13, "lrelu", 2)])
+def test_head_dgrad_backward_statistics(x3, N, S, act, nc):
+    """ABI 12: the G head's data gradient (conv 32 → nc, k7 p0, transposed form on the thin1 ring
+    kernel; nc = 2 in the one-plane modes) leaves the backward statistics of the InstanceNorm in
+    front of the head (its output replication-padded by 3): dz bit-identical to the plain data
+    gradient, dx within fp32 summation-order noise of the statistics-pass result."""
     ops = x3
+    if nc == 2 and ops.get_conv_precision() == "bf16x3":
+        pytest.skip("two-channel thin1 runs in the one-plane modes only")
     C, k, f = 32, 7, 3
     g = torch.Generator().manual_seed(N * 17 + S)
     x = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()                # up-conv output (pre-IN)
     _, mean, rstd = ops.instnorm_fwd(x, act=act, ypad=f)
-    w = torch.randn(1, C, k, k, k, generator=g, dtype=torch.float64) * 0.02          # head Conv3d(32 → 1)
+    w = torch.randn(nc, C, k, k, k, generator=g, dtype=torch.float64) * 0.02         # head Conv3d(32 → nc)
     wp_b = pack(ops, w, False, True)
     P = S + 2 * f
     O = P - k + 1
-    dy = ndhwc(torch.randn(N, 1, O, O, O, generator=g).float()).cuda()
+    dy = ndhwc(torch.randn(N, nc, O, O, O, generator=g).float()).cuda()
     dz_ref = ops.conv3d(dy, wp_b, C, k, 1, 0, (P, P, P), transposed=True)
     part = ops.in_partials_buffer(N, (P, P, P), C, "cuda")
     dz, chunks = ops.conv3d_dgrad_in_stats(dy, wp_b, C, k, x, mean, rstd, act, f, part)
@@ -652,6 +662,8 @@ def test_op16_rejected_outside_16bit_modes(ops):
     (2, 1, 32, 22, 7, 1, 0, False, True, 0),       # G stem (k7, 1 → 32: thin1 epilogue partials, 16³)
     (1, 1, 32, 27, 7, 1, 0, False, True, 0),       # stem form with partial 16×16 output columns (21³)
     (2, 1, 32, 22, 7, 1, 0, False, True, 10.0),    # stem on a non-centred volume (x + 10): fp64 partials
+    (2, 2, 32, 22, 7, 1, 0, False, "1p", 0),       # nc = 2 stem: thin1 with two channels (one-plane modes)
+    (1, 2, 32, 27, 7, 1, 0, False, "1p", 0),       # … with partial output columns
     (2, 32, 64, 16, 4, 2, 1, False, False, 0),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
     (1, 128, 256, 8, 4, 1, 1, False, False, 0),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
 ])
@@ -660,6 +672,8 @@ def test_igemm_in_stats_partials(x3, N, cin, cout, S, k, s, p, tr, expect, dc):
     one instance and class) and the brickT epilogue's (per output brick) feed mragan_instnorm_fwd_partials; output, mean / rstd and the
     normalised tensor match the statistics-pass path."""
     ops = x3
+    if expect == "1p":
+        expect = ops.get_conv_precision() in ("bf16", "fp16")
     g = torch.Generator().manual_seed(N * 7 + cin + cout + S + k)
     x = torch.randn(N, cin, S, S, S, generator=g, dtype=torch.float64) + dc
     shape_w = (cin, cout, k, k, k) if tr else (cout, cin, k, k, k)
