@@ -6,6 +6,7 @@ CycleGANModel.optimize_parameters() (tools/gen_fixtures.py).  The oracle must
 (2) match its fp64 step to ~1e-9 (same math, same precision), and
 (3) match its fp32 step within the fp32 envelope calibrated in SURVEY §8(c).
 """
+import os
 import random
 
 import numpy as np
@@ -18,6 +19,16 @@ from oracle.cyclegan_oracle import CycleGANOracle
 # the CPU oracle replays the small fixtures (the BASELINE-size ones compare the HIP engine with
 # the reference directly, tests/test_step_gpu.py; an fp64 CPU step at 128³ takes minutes)
 CASES = [c for c in available_cases() if load(c)[1]["S"] <= 32]
+# the two 9-block 32³ fp64 replays take 3–4 minutes each on the container's 8 CPUs; the 6-block
+# 24³ and UNet 32³ replays pin the same oracle code paths (every layer kind, ImagePool, both
+# losses) in seconds, so the full-size ones run on request (MRAGAN_SLOW_ORACLE=1)
+SLOW = {"step_r9_s32_b1", "step_r9_s32_b2_ngf16"}
+_RUN_SLOW = os.environ.get("MRAGAN_SLOW_ORACLE") == "1"
+
+
+def _gate(name):
+    if name in SLOW and not _RUN_SLOW:
+        pytest.skip(f"{name}: fp64 CPU replay of a 9-block 32³ step (minutes); set MRAGAN_SLOW_ORACLE=1")
 
 
 def _build(name, dtype):
@@ -45,6 +56,7 @@ def test_init_bit_exact(name):
 
 @pytest.mark.parametrize("name", CASES)
 def test_step_fp64_matches_reference(name):
+    _gate(name)
     z, meta, orc = _build(name, torch.float64)
     for step in range(meta["steps"]):
         A, B = inputs(meta, step)
@@ -87,6 +99,7 @@ def test_step_fp32_within_envelope(name):
     (all sampled elements, each parameter normalised) within 3× the reference's own
     fp32-vs-fp64 error or 1e-3 — an fp32 run is one sample of ReLU-kink-flip noise
     (tests/test_step_gpu.py::conditioning).  The fp64 path is pinned at 1e-9 above."""
+    _gate(name)
     z, meta, orc = _build(name, torch.float32)
     A, B = inputs(meta, 0)
     losses = orc.optimize_parameters(A, B)
