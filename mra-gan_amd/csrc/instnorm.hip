@@ -17,11 +17,20 @@ namespace mragan {
 constexpr float kInEps = 1e-5f;
 
 
-// row chunks per instance: ≈2048 blocks per launch, but ≥ 4 float4 loads per thread
+// partial bytes per instance the fused finalize + apply kernels reduce in every block (beyond it:
+// a separate finalize launch); MRAGAN_IN_UNFUSED: the separate launches always (A/B switch)
+constexpr int kFuseMaxBytes = 64 * 1024;
+static const bool g_in_unfused = getenv("MRAGAN_IN_UNFUSED") != nullptr;
+static bool in_fusable(int chunks, int C) { return (int64_t)chunks * C * 16 <= kFuseMaxBytes; }
+
+// row chunks per instance: ≈2048 blocks per launch, but ≥ 4 float4 loads per thread, and few
+// enough that the apply kernel can reduce them in-block (in_fusable)
 static int in_chunks(const InShape& s) {
   const int rows = s.D * s.H;
   const int64_t rowq = (int64_t)s.W * (s.C / 4);
   int64_t want = (2048 + s.N - 1) / s.N;
+  const int64_t fuse_cap = kFuseMaxBytes / ((int64_t)s.C * 16);
+  if (!g_in_unfused && want > fuse_cap) want = fuse_cap;
   int64_t min_rows = (4 * 256 + rowq - 1) / rowq;            // rows per block for ≥ 4 loads/thread
   int64_t cap = (rows + min_rows - 1) / min_rows;
   if (want > cap) want = cap;
@@ -339,6 +348,193 @@ __global__ void __launch_bounds__(256) in_bwd_apply_kernel(InBwdArgs a, InShape 
   }
 }
 
+// ---- fused finalize + apply ------------------------------------------------------------------
+// The separate finalize launches (one per InstanceNorm and direction, ~5 µs each plus the
+// dependency gap: 234 launches per 64³ b2 step, r04i trace) fold into the apply: every block of
+// instance n reduces the instance's partials [chunks][C][2] (≤ kFuseMaxBytes, L2-resident) in the
+// same fixed order — identical statistics in every block, deterministic — then applies them to its
+// rows.  Grid (Bi, N): block (bi, n) owns rows [bi·per, (bi+1)·per) of instance n.
+// mode 0: μ / rstd into sa / sb; mode 1: the backward coefficients mean(g), mean(g·x̂).
+__device__ void in_stats_block(const double* __restrict__ part, const InShape& s, int chunks, int n, int mode,
+                               float* sa, float* sb) {
+  __shared__ double fr[2][256];
+  const int tid = threadIdx.x;
+  int tpc = 1;                                   // threads per channel (power of two)
+  while (tpc * 2 * s.C <= 256) tpc *= 2;
+  const int cpp = 256 / tpc;                     // channels per pass
+  const double S = (double)s.S();
+  for (int c0 = 0; c0 < s.C; c0 += cpp) {
+    const int c = c0 + tid / tpc, j = tid % tpc;
+    double a = 0, b = 0;
+    if (c < s.C) {
+#pragma unroll 4
+      for (int k = j; k < chunks; k += tpc) {
+        const double2 p = *reinterpret_cast<const double2*>(part + (((int64_t)n * chunks + k) * s.C + c) * 2);
+        a += p.x; b += p.y;
+      }
+    }
+    fr[0][tid] = a; fr[1][tid] = b;
+    __syncthreads();
+    if (j == 0 && c < s.C) {
+      double A = 0, B = 0;
+      for (int r = 0; r < tpc; ++r) { A += fr[0][tid + r]; B += fr[1][tid + r]; }
+      if (mode == 0) {
+        const double mu = A / S;
+        double var = B / S - mu * mu;
+        if (var < 0) var = 0;
+        sa[c] = (float)mu;
+        sb[c] = (float)(1.0 / sqrt(var + (double)kInEps));
+      } else {
+        sa[c] = (float)(A / S);
+        sb[c] = (float)(B / S);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) in_apply_fused_kernel(const float* __restrict__ x, InShape s,
+                                                             const double* __restrict__ part, int chunks,
+                                                             float* __restrict__ mean, float* __restrict__ rstd,
+                                                             int act, const float* __restrict__ resid, int rpad,
+                                                             float* __restrict__ y, int ypad, uint2* __restrict__ y16,
+                                                             int mode, int per) {
+  __shared__ __attribute__((aligned(16))) float smu[1024], srs[1024];
+  const int n = blockIdx.y, bi = blockIdx.x, tid = threadIdx.x;
+  in_stats_block(part, s, chunks, n, 0, smu, srs);
+  if (bi == 0)
+    for (int c = tid; c < s.C; c += 256) { mean[n * s.C + c] = smu[c]; rstd[n * s.C + c] = srs[c]; }
+  const int CQ = s.C / 4, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
+  const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad;
+  const int Dr = s.D + 2 * rpad, Hr = s.H + 2 * rpad, Wr = s.W + 2 * rpad;
+  const int rowq = Wp * CQ;
+  const float4 mu = reinterpret_cast<const float4*>(smu)[q];
+  const float4 rs = reinterpret_cast<const float4*>(srs)[q];
+  const float4* xv = reinterpret_cast<const float4*>(x);
+  const float4* rv = reinterpret_cast<const float4*>(resid);
+  float4* yv = reinterpret_cast<float4*>(y);
+  const int r1 = min(Dp * Hp, (bi + 1) * per);
+  for (int rr = bi * per; rr < r1; ++rr) {
+    const int hp = rr % Hp, dp = rr / Hp;
+    const int row = n * Dp * Hp + rr;
+    const int sd = min(max(dp - ypad, 0), s.D - 1), sh = min(max(hp - ypad, 0), s.H - 1);
+    const float4* xrow = xv + (size_t)((n * s.D + sd) * s.H + sh) * s.W * CQ;
+    const float4* rrow = resid ? rv + ((size_t)((n * Dr + sd + rpad) * Hr + sh + rpad) * Wr + rpad) * CQ : nullptr;
+    float4* yrow = yv + (size_t)row * rowq + q;
+    uint2* y16row = y16 + (size_t)row * rowq + q;
+    for (int wp = wt; wp < Wp; wp += WS) {
+      const int sw = min(max(wp - ypad, 0), s.W - 1);
+      float4 v = xrow[sw * CQ + q];
+      v = make_float4((v.x - mu.x) * rs.x, (v.y - mu.y) * rs.y, (v.z - mu.z) * rs.z, (v.w - mu.w) * rs.w);
+      v = f4_act(v, act);
+      if (resid) {
+        const float4 r = rrow[sw * CQ + q];
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      }
+      if (y) yrow[wp * CQ] = v;
+      if (y16) y16row[wp * CQ] = f4_op16(v, mode);
+    }
+  }
+}
+
+template <int P>
+__global__ void __launch_bounds__(256) in_bwd_apply_fused_kernel(InBwdArgs a, InShape s, const double* __restrict__ part,
+                                                                 int chunks, int per) {
+  __shared__ __attribute__((aligned(16))) float sg[1024], sgx[1024];
+  const int n = blockIdx.y, bi = blockIdx.x, tid = threadIdx.x;
+  in_stats_block(part, s, chunks, n, 1, sg, sgx);
+  const int CQ = s.C / 4, q = tid % CQ, WS = 256 / CQ;
+  const int wt = tid / CQ < WS ? tid / CQ : (1 << 30);   // C/4 not dividing 256: spare threads idle
+  const float4 mg = reinterpret_cast<const float4*>(sg)[q], mgx = reinterpret_cast<const float4*>(sgx)[q];
+  float4* dx = reinterpret_cast<float4*>(a.dx);
+  const int r1 = min(s.D * s.H, (bi + 1) * per);
+  for (int r = bi * per; r < r1; ++r) {
+    const int h = r % s.H, d = r / s.H;
+    const int rr = n * s.D * s.H + r;
+    const InRow row = in_bwd_row(a, s, n, d, h, q);
+    float4* out = dx + (size_t)rr * s.W * CQ + q;
+    uint2* out16 = reinterpret_cast<uint2*>(a.dx16) + (size_t)rr * s.W * CQ + q;
+    float4* gout = a.g_out ? reinterpret_cast<float4*>(a.g_out) + (size_t)rr * s.W * CQ + q : nullptr;
+    for (int w = wt; w < s.W; w += WS) {
+      float4 g, xh, graw;
+      in_bwd_voxel<P>(a, s, row, w, g, xh, &graw);
+      if (gout) gout[w * CQ] = graw;
+      float4 o;
+      o.x = row.rs.x * (g.x - mg.x - xh.x * mgx.x);
+      o.y = row.rs.y * (g.y - mg.y - xh.y * mgx.y);
+      o.z = row.rs.z * (g.z - mg.z - xh.z * mgx.z);
+      o.w = row.rs.w * (g.w - mg.w - xh.w * mgx.w);
+      if (dx) out[w * CQ] = o;
+      if (a.dx16) out16[w * CQ] = f4_op16(o, a.mode16);
+    }
+  }
+}
+
+// fused grid: whole rows, never straddling instances; at least one block per CU in total, and
+// about 256 KB of traffic per block for the large (64³-class) norms, whose blocks then stay few
+// against their rows (each block re-reads the instance's partials once: ≤ 64 KB)
+static void fused_grid(int N, int rows, int64_t bytes_per_row, int& bi, int& per) {
+  int64_t want = (256 + N - 1) / N;
+  const int64_t by_bytes = (rows * bytes_per_row + (256 << 10) - 1) / (256 << 10);
+  if (want < by_bytes) want = by_bytes;
+  if (want > rows) want = rows;
+  if (want < 1) want = 1;
+  per = (rows + want - 1) / want;
+  bi = (rows + per - 1) / per;
+}
+
+static int launch_in_apply(const float* x, const InShape& s, const double* part, int chunks, float* mean, float* rstd,
+                           int act, const float* resid, int rpad, float* y, int ypad, void* y16, int mode16,
+                           hipStream_t st) {
+  if (in_fusable(chunks, s.C) && !g_in_unfused) {
+    int bi, per;
+    // per padded row: the source row read, the fp32 / 16-bit output rows written
+    const int64_t bpr = (int64_t)s.C * ((int64_t)s.W * 4 * (resid ? 2 : 1) + (int64_t)(s.W + 2 * ypad) * ((y ? 4 : 0) + (y16 ? 2 : 0)));
+    fused_grid(s.N, (s.D + 2 * ypad) * (s.H + 2 * ypad), bpr, bi, per);
+    hipLaunchKernelGGL(in_apply_fused_kernel, dim3(bi, s.N), dim3(256), 0, st, x, s, part, chunks, mean, rstd, act,
+                       resid, rpad, y, ypad, static_cast<uint2*>(y16), mode16, per);
+    return check_launch(y16 ? "in_apply_fused(op16)" : "in_apply_fused");
+  }
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
+  int rc = check_launch("in_finalize");
+  if (rc) return rc;
+  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
+  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
+                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
+  return check_launch(y16 ? "in_apply(op16)" : "in_apply");
+}
+
+static int launch_in_bwd_apply(const InBwdArgs& a, const InShape& s, const double* part, int chunks, float* coef,
+                               hipStream_t st) {
+  if (in_fusable(chunks, s.C) && !g_in_unfused) {
+    int bi, per;
+    // per row: dy (padded rows folded in: ≈ the row), x, dx / dx16, g_out
+    const int64_t bpr = (int64_t)s.C * s.W * (4 + 4 + (a.dx ? 4 : 0) + (a.dx16 ? 2 : 0) + (a.g_out ? 4 : 0) + (a.dy_add ? 4 : 0));
+    fused_grid(s.N, s.D * s.H, bpr, bi, per);
+    const dim3 g(bi, s.N);
+    switch (a.dypad) {
+      case 0: hipLaunchKernelGGL(in_bwd_apply_fused_kernel<0>, g, dim3(256), 0, st, a, s, part, chunks, per); break;
+      case 1: hipLaunchKernelGGL(in_bwd_apply_fused_kernel<1>, g, dim3(256), 0, st, a, s, part, chunks, per); break;
+      case 3: hipLaunchKernelGGL(in_bwd_apply_fused_kernel<3>, g, dim3(256), 0, st, a, s, part, chunks, per); break;
+      default: hipLaunchKernelGGL(in_bwd_apply_fused_kernel<-1>, g, dim3(256), 0, st, a, s, part, chunks, per); break;
+    }
+    return check_launch(a.dx16 ? "in_bwd_apply_fused(op16)" : "in_bwd_apply_fused");
+  }
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
+  int rc = check_launch("in_bwd_finalize");
+  if (rc) return rc;
+  const int rows = s.N * s.D * s.H;
+  const dim3 ga(rows < 16384 ? rows : 16384);
+  switch (a.dypad) {
+    case 0: hipLaunchKernelGGL(in_bwd_apply_kernel<0>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 1: hipLaunchKernelGGL(in_bwd_apply_kernel<1>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
+    default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
+  }
+  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
+}
+
 // ---- running statistics (composite of the reference's sequential calls) ------------------
 // One entry per IN layer: the segments (one per reference call, in call order) of per-instance
 // mean/rstd.  r ← (1−m)·r + m·avg_call(μ_n + bias), rv ← (1−m)·rv + m·avg_call(σ²_n · S/(S−1)).
@@ -396,12 +592,7 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, x, s, chunks, part);
   int rc = check_launch("in_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
-  if ((rc = check_launch("in_finalize"))) return rc;
-  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
-  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
-                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
-  return check_launch("in_apply");
+  return launch_in_apply(x, s, part, chunks, mean, rstd, act, resid, rpad, y, ypad, y16, mode16, st);
 }
 
 // Forward from statistics partials a producer conv already accumulated (conv_brick_x3 epilogue:
@@ -417,13 +608,7 @@ int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act
               s.H, s.W);
     return kBadArg;
   }
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
-  int rc = check_launch("in_finalize");
-  if (rc) return rc;
-  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
-  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
-                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
-  return check_launch(y16 ? "in_apply(op16)" : "in_apply");
+  return launch_in_apply(x, s, part, chunks, mean, rstd, act, resid, rpad, y, ypad, y16, mode16, st);
 }
 
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -445,15 +630,7 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   }
   int rc = check_launch("in_bwd_stats");
   if (rc) return rc;
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
-  if ((rc = check_launch("in_bwd_finalize"))) return rc;
-  switch (a.dypad) {
-    case 0: hipLaunchKernelGGL(in_bwd_apply_kernel<0>, ga, dim3(256), 0, st, a, s, coef); break;
-    case 1: hipLaunchKernelGGL(in_bwd_apply_kernel<1>, ga, dim3(256), 0, st, a, s, coef); break;
-    case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
-    default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
-  }
-  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
+  return launch_in_bwd_apply(a, s, part, chunks, coef, st);
 }
 
 // Backward from statistics partials the producer of dy already accumulated (conv_brick_x3's
@@ -466,18 +643,7 @@ int instnorm_bwd_partials(const InBwdArgs& a, InShape s, const double* part, int
   const size_t need = (size_t)s.N * s.C * 2 * sizeof(float);
   if (need > ws_bytes) { set_error("instnorm_bwd_partials: workspace too small"); return kWorkspace; }
   float* coef = static_cast<float*>(ws);
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
-  int rc = check_launch("in_bwd_finalize");
-  if (rc) return rc;
-  const int rows = s.N * s.D * s.H;
-  const dim3 ga(rows < 16384 ? rows : 16384);
-  switch (a.dypad) {
-    case 0: hipLaunchKernelGGL(in_bwd_apply_kernel<0>, ga, dim3(256), 0, st, a, s, coef); break;
-    case 1: hipLaunchKernelGGL(in_bwd_apply_kernel<1>, ga, dim3(256), 0, st, a, s, coef); break;
-    case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
-    default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
-  }
-  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
+  return launch_in_bwd_apply(a, s, part, chunks, coef, st);
 }
 
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st) {
