@@ -18,9 +18,13 @@ constexpr float kInEps = 1e-5f;
 
 
 // partial bytes per instance the fused finalize + apply kernels reduce in every block (beyond it:
-// a separate finalize launch); MRAGAN_IN_UNFUSED: the separate launches always (A/B switch)
+// a separate finalize launch).  Opt-in A/B switch MRAGAN_IN_FUSED=1, off by default: measured
+// slower on MI355X (64³ b2 bf16 step 12.95 vs 12.32 ms, same box, r04j) — every apply block
+// re-reads its instance's partials (up to 64 KB; 100 MB per launch for the 64³ norms), and the
+// capped statistics chunks halve the parallelism of the statistics pass (C128 4×16³ backward
+// 43.9 vs 23.1 µs)
 constexpr int kFuseMaxBytes = 64 * 1024;
-static const bool g_in_unfused = getenv("MRAGAN_IN_UNFUSED") != nullptr;
+static const bool g_in_unfused = getenv("MRAGAN_IN_FUSED") == nullptr;
 static bool in_fusable(int chunks, int C) { return (int64_t)chunks * C * 16 <= kFuseMaxBytes; }
 
 // row chunks per instance: ≈2048 blocks per launch, but ≥ 4 float4 loads per thread, and few
