@@ -23,14 +23,8 @@ constexpr float kInEps = 1e-5f;
 // re-reads its instance's partials (up to 64 KB; 100 MB per launch for the 64³ norms), and the
 // capped statistics chunks halve the parallelism of the statistics pass (C128 4×16³ backward
 // 43.9 vs 23.1 µs)
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
+constexpr int kFuseMaxBytes = 64 * 1024;
 static const bool g_in_unfused = getenv("MRAGAN_IN_FUSED") == nullptr;
-static const int kFuseMaxBytes = env_int("MRAGAN_IN_FUSED_CAP", 64 * 1024);
-static const bool g_in_cap_stats = env_int("MRAGAN_IN_FUSED_CAPSTATS", 1) != 0;
-static const int64_t g_in_fused_max = (int64_t)env_int("MRAGAN_IN_FUSED_MAXMB", 1 << 20) << 20;   // bytes per instance
 static bool in_fusable(int chunks, int C) { return (int64_t)chunks * C * 16 <= kFuseMaxBytes; }
 
 // row chunks per instance: ≈2048 blocks per launch, but ≥ 4 float4 loads per thread, and few
@@ -40,7 +34,7 @@ static int in_chunks(const InShape& s) {
   const int64_t rowq = (int64_t)s.W * (s.C / 4);
   int64_t want = (2048 + s.N - 1) / s.N;
   const int64_t fuse_cap = kFuseMaxBytes / ((int64_t)s.C * 16);
-  if (!g_in_unfused && g_in_cap_stats && want > fuse_cap) want = fuse_cap;
+  if (!g_in_unfused && want > fuse_cap) want = fuse_cap;
   int64_t min_rows = (4 * 256 + rowq - 1) / rowq;            // rows per block for ≥ 4 loads/thread
   int64_t cap = (rows + min_rows - 1) / min_rows;
   if (want > cap) want = cap;
@@ -497,8 +491,7 @@ static void fused_grid(int N, int rows, int64_t bytes_per_row, int& bi, int& per
 static int launch_in_apply(const float* x, const InShape& s, const double* part, int chunks, float* mean, float* rstd,
                            int act, const float* resid, int rpad, float* y, int ypad, void* y16, int mode16,
                            hipStream_t st) {
-  if (in_fusable(chunks, s.C) && !g_in_unfused &&
-      (int64_t)s.D * s.H * s.W * s.C * 4 <= g_in_fused_max) {
+  if (in_fusable(chunks, s.C) && !g_in_unfused) {
     int bi, per;
     // per padded row: the source row read, the fp32 / 16-bit output rows written
     const int64_t bpr = (int64_t)s.C * ((int64_t)s.W * 4 * (resid ? 2 : 1) + (int64_t)(s.W + 2 * ypad) * ((y ? 4 : 0) + (y16 ? 2 : 0)));
@@ -518,8 +511,7 @@ static int launch_in_apply(const float* x, const InShape& s, const double* part,
 
 static int launch_in_bwd_apply(const InBwdArgs& a, const InShape& s, const double* part, int chunks, float* coef,
                                hipStream_t st) {
-  if (in_fusable(chunks, s.C) && !g_in_unfused &&
-      (int64_t)s.D * s.H * s.W * s.C * 4 <= g_in_fused_max) {
+  if (in_fusable(chunks, s.C) && !g_in_unfused) {
     int bi, per;
     // per row: dy (padded rows folded in: ≈ the row), x, dx / dx16, g_out
     const int64_t bpr = (int64_t)s.C * s.W * (4 + 4 + (a.dx ? 4 : 0) + (a.dx16 ? 2 : 0) + (a.g_out ? 4 : 0) + (a.dy_add ? 4 : 0));

@@ -18,7 +18,6 @@ phase (which only needs pre-update G outputs and D weights), then both optimizer
 Reordering "G step, then D phase" → "D phase, then G step" is exact for the same reason.
 """
 import itertools
-import os
 import random
 from collections import OrderedDict
 
@@ -146,25 +145,16 @@ class _Lanes:
     lane 1 an auxiliary stream forked from it (under capture: two branches of the HIP graph).
     `on(i)` issues on lane i with lane i's workspace; `mark` / `wait` order one lane after a
     point of the other; `join` ends the fork.  With `parallel=False` both lanes are the current
-    stream (the --single_stream order, also what bench.py times kernels under).
-    With weight-gradient streams (`wg`), each lane's weight gradients go to a stream of their
-    own (engine.WgradSink, workspace lanes 2 and 3): `wg_mark(i)` / `wg_wait(i, ev)` order the
-    two gradient streams where they accumulate into the same buffers; `join` waits for them."""
+    stream (the --single_stream order, also what bench.py times kernels under)."""
 
-    def __init__(self, aux, parallel=True, wg=None):
-        from mragan_hip import ops, engine
+    def __init__(self, aux, parallel=True):
+        from mragan_hip import ops
         self._ops = ops
-        self._engine = engine
         cur = torch.cuda.current_stream()
         self.s = [cur, aux if parallel else cur]
         self.parallel = parallel
         if parallel:
             aux.wait_stream(cur)
-        self.sinks = [None, None]
-        if parallel and wg is not None:
-            for i in range(2):
-                wg[i].wait_stream(cur)
-                self.sinks[i] = engine.WgradSink(wg[i], 2 + i)
 
     def on(self, i):
         lanes = self
@@ -173,24 +163,14 @@ class _Lanes:
             def __enter__(self_):
                 self_.st = torch.cuda.stream(lanes.s[i])
                 self_.ln = lanes._ops.lane(i)
-                self_.wg = lanes._engine.wgrad_sink(lanes.sinks[i])
                 self_.st.__enter__()
                 self_.ln.__enter__()
-                self_.wg.__enter__()
 
             def __exit__(self_, *exc):
-                self_.wg.__exit__(*exc)
                 self_.ln.__exit__(*exc)
                 self_.st.__exit__(*exc)
                 return False
         return _On()
-
-    def wg_mark(self, i):
-        return self.sinks[i].mark() if self.sinks[i] is not None else None
-
-    def wg_wait(self, i, ev):
-        if self.sinks[i] is not None and ev is not None:
-            self.sinks[i].wait(ev)
 
     def mark(self, i):
         ev = torch.cuda.Event()
@@ -204,10 +184,6 @@ class _Lanes:
     def join(self):
         if self.parallel:
             self.s[0].wait_stream(self.s[1])
-            for k in self.sinks:
-                if k is not None:
-                    self.s[0].wait_stream(k.stream)
-                    k.keep.clear()       # after the join: frees are ordered behind the gradients
 
 
 def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
@@ -381,9 +357,6 @@ class CycleGANModel(BaseModel):
         self._use_graph = self.isTrain and not getattr(opt, 'no_cuda_graph', False) and self.device.type == 'cuda'
         self.parallel_lanes = not getattr(opt, 'single_stream', False)
         self._aux_stream = None
-        # weight gradients on streams of their own (MRAGAN_WGRAD_INLINE=1: in the lanes, A/B)
-        self.wgrad_streams = os.environ.get("MRAGAN_WGRAD_INLINE") is None
-        self._wg_streams = None
         self._graphs = None          # (G-phase graph, D-phase graph) of the step being replayed
         self._rs_tables = None       # running-stat update tables of that capture
         self._graph_key = None
@@ -513,30 +486,23 @@ class CycleGANModel(BaseModel):
         with ln.on(0):
             self._cDA1 = head(pDA, self._fake_B, 1, self._cGB2.out, A, lA, d_recA, self._cGA1, dGA1, B, lB * li, 3, 2)
             pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b])
-            rec_done_0, wg_done_0 = ln.mark(0), ln.wg_mark(0)
+            rec_done_0 = ln.mark(0)
         with ln.on(1):
             self._cDB1 = head(pDB, self._fake_A, 5, self._cGA2.out, B, lB, d_recB, self._cGB1, dGB1, A, lA * li, 7, 6)
             pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b])
-            rec_done_1, wg_done_1 = ln.mark(1), ln.wg_mark(1)
+            rec_done_1 = ln.mark(1)
         with ln.on(0):
             ln.wait(0, rec_done_1)
-            ln.wg_wait(0, wg_done_1)      # G_A's gradients: lane 1's cycle pass wrote them first
             pGA.backward(self._cGA1, [dGA1])
         with ln.on(1):
             ln.wait(1, rec_done_0)
-            ln.wg_wait(1, wg_done_0)      # G_B's likewise
             pGB.backward(self._cGB1, [dGB1])
         ln.join()
 
     def _lanes(self):
         if self.parallel_lanes and self._aux_stream is None:
             self._aux_stream = torch.cuda.Stream(device=self.device)
-        wg = None
-        if self.parallel_lanes and self.wgrad_streams:
-            if self._wg_streams is None:
-                self._wg_streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
-            wg = self._wg_streams
-        return _Lanes(self._aux_stream, self.parallel_lanes, wg)
+        return _Lanes(self._aux_stream, self.parallel_lanes)
 
     def backward_D_basic(self, netD, real, pool, fakes, ret_idx, store_idx, loss_slot):
         """cycle_gan_model.py:138-149 with real and (pooled, detached) fake batched."""

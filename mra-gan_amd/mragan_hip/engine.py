@@ -33,65 +33,6 @@ _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None   
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
-
-
-class WgradSink:
-    """Weight gradients off the data-gradient chain.  A backward pass's data gradients are a
-    serial chain of latency-bound launches (16³-class convolutions and their InstanceNorms fill a
-    fraction of the 256 CUs); its weight gradients feed nothing but the optimizer.  With a sink
-    active, every weight-gradient call is issued on the sink's stream (its own workspace lane)
-    after an event on the issuing stream, so it overlaps the rest of the chain.  The tensors it
-    reads are kept referenced until the owner joins the stream (the caching allocator must not
-    hand their memory to the chain meanwhile).  Calls into one gradient buffer from two sinks are
-    ordered by the owner with mark() / wait() (the accumulation order stays fixed)."""
-
-    def __init__(self, stream, lane_idx):
-        self.stream = stream
-        self.lane = lane_idx
-        self.keep = []
-
-    def submit(self, fn, *tensors):
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
-        self.stream.wait_event(ev)
-        with torch.cuda.stream(self.stream), ops.lane(self.lane):
-            fn()
-        self.keep.extend(t for t in tensors if t is not None)
-
-    def mark(self):
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        return ev
-
-    def wait(self, ev):
-        self.stream.wait_event(ev)
-
-
-_SINK = [None]
-
-
-class wgrad_sink:
-    """`with engine.wgrad_sink(sink):` — weight-gradient calls inside go to `sink` (None: inline)."""
-
-    def __init__(self, sink):
-        self.sink = sink
-
-    def __enter__(self):
-        self.prev = _SINK[0]
-        _SINK[0] = self.sink
-        return self
-
-    def __exit__(self, *exc):
-        _SINK[0] = self.prev
-        return False
-
-
-def _wgrad(fn, *tensors):
-    sink = _SINK[0]
-    if sink is None:
-        fn()
-    else:
-        sink.submit(fn, *tensors)
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
 _FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") or "0"))
                # the library's A/B switches that send those convs to the fp32-pack kernels
@@ -453,7 +394,7 @@ class NetPlan:
                     G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                     dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
-                    _wgrad(lambda: st.conv2.wgrad_op16(sc.z1, dh2), sc.z1, dh2)
+                    st.conv2.wgrad_op16(sc.z1, dh2)
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
                 dz1, part, chunks = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
                 if chunks:
@@ -461,7 +402,7 @@ class NetPlan:
                 else:
                     dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
-                    _wgrad(lambda: st.conv1.wgrad_op16(sc.inp16, dh1), sc.inp16, dh1)
+                    st.conv1.wgrad_op16(sc.inp16, dh1)
                 g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue
@@ -475,11 +416,11 @@ class NetPlan:
                     G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                     dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
-                    _wgrad(lambda: st.conv2.wgrad(sc.z1, dh2), sc.z1, dh2)
+                    st.conv2.wgrad(sc.z1, dh2)
                 dz1 = st.conv2.dgrad(dh2, sc.z1.shape[1:4])
                 dh1 = ops.instnorm_bwd(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
-                    _wgrad(lambda: st.conv1.wgrad(sc.inp, dh1), sc.inp, dh1)
+                    st.conv1.wgrad(sc.inp, dh1)
                 g = st.conv1.dgrad(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue
@@ -499,11 +440,9 @@ class NetPlan:
                 dh = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                 ops.act_bwd(sc.h, srcs, st.act, dh)
             if need_wgrad:
-                def _wg(conv=conv, st=st, inp=sc.inp, dh=dh):
-                    conv.wgrad(inp, dh)
-                    if st.use_bias and conv.m.bias is not None:
-                        ops.channel_sum(dh, conv.m.bias.grad, accumulate=True)
-                _wgrad(_wg, sc.inp, dh)
+                conv.wgrad(sc.inp, dh)
+                if st.use_bias and conv.m.bias is not None:
+                    ops.channel_sum(dh, conv.m.bias.grad, accumulate=True)
             bstats = None
             if want_dgrad:
                 nxt = self.stages[i - 1] if i > 0 else None
@@ -819,11 +758,11 @@ class UnetPlan:
                 dg = torch.empty_like(lc.g)
                 ops.act_bwd(lc.g, srcs, "tanh", dg)
                 if need_wgrad and lv.up.m.bias is not None:
-                    _wgrad(lambda: ops.channel_sum(dg, lv.up.m.bias.grad, accumulate=True), dg)
+                    ops.channel_sum(dg, lv.up.m.bias.grad, accumulate=True)
             else:
                 dg = ops.instnorm_bwd(lc.g, lc.umean, lc.urstd, du[i], 0, None, act="relu")
             if need_wgrad:
-                _wgrad(lambda: lv.up.wgrad(lc.r, dg), lc.r, dg)
+                lv.up.wgrad(lc.r, dg)
             dr = lv.up.dgrad(dg, lc.r.shape[1:4])
             if lv.kind == "inner":
                 dh = torch.empty_like(lc.h)
@@ -843,7 +782,7 @@ class UnetPlan:
                 dh = torch.empty_like(lc.nxt)
                 ops.act_bwd(lc.nxt, [g_in, skip[i + 1]], "lrelu", dh)
             if need_wgrad:
-                _wgrad(lambda: lv.down.wgrad(lc.inp, dh), lc.inp, dh)
+                lv.down.wgrad(lc.inp, dh)
             if i > 0 or need_input_grad:
                 g_in = lv.down.dgrad(dh, lc.inp.shape[1:4])
         if not need_input_grad:
