@@ -85,10 +85,16 @@ def main():
         ops.pack_weight(w_res, c4, c4, 27, base, ws_res_f)
         ops.pack_weight(w_res, c4, c4, 27, base + 1, ws_res_b)
         part_res = ops.in_partials_buffer(N, (s4, s4, s4), c4, dev)
+        h1_res = rnd(N, s4, s4, s4, c4)
+        _, m_res, r_res = ops.instnorm_fwd(h1_res, act="relu", ypad=1)
+        part_bs = ops.in_partials_buffer(N, (s4 + 2,) * 3, c4, dev)
     table = {
         "res_fwd16": lambda: ops.conv3d_op16(x_res16, w_res, c4, 3, 1, 0, (s4, s4, s4), ws_res_f, part_res),
         "res_dgrad16": lambda: ops.conv3d_op16(dy_res16, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, ws_res_b, transposed=True),
         "res_wgrad16": lambda: ops.conv3d_wgrad_op16(dy_res16, x_res16, 3, 1, 0, gw_res, False),
+        # the step's form of the res dgrad: with the backward statistics of the IN in front (ABI 11)
+        "res_dgrad16s": lambda: ops.conv3d_op16_dgrad_in_stats(dy_res16, w_res, c4, ws_res_b, h1_res, m_res, r_res,
+                                                               "relu", part_bs),
         "pack_g": lambda: pack_tab.run(pk),
         "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
