@@ -36,7 +36,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;                    // channels per chunk
-constexpr int kRow = 144;                  // LDS row: hi 64 B, lo 64 B, 16 B pad
+constexpr int kRow = 144;                  // LDS row: hi 64 B, lo 64 B, 16 B pad (also the epilogue's fp32 voxel row)
+// halo row of the one-plane modes (bf16 / fp16): hi 64 B + 16 B pad — the halo buffers take 64 KB
+// instead of 115 KB, so two blocks share a CU and one block's epilogue stores overlap the other's
+// MFMAs (the store stream bounded the one-block-per-CU kernel: 132 µs with stores, 60 without)
+template <int PM>
+constexpr int halo_row() { return prec::has_lo<PM>() ? 144 : 80; }
 constexpr int kOD = 4, kOH = 16, kOW = 16; // output brick
 constexpr int kHD = 4, kHH = 10, kHW = 10; // input halo (k ≤ 4, p = 1)
 constexpr int kHP = kHD * kHH * kHW;       // 400 positions
@@ -102,8 +107,9 @@ struct BrickTArgs {
 };
 
 template <int K, int PM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(prec::has_lo<PM>() ? 1 : 2, prec::has_lo<PM>() ? 1 : 2)))
 brickT_x3_kernel(BrickTArgs a) {
+  constexpr int kHRow = halo_row<PM>();
   constexpr TSteps<K> ts{};
   constexpr int NS = 2 * TSteps<K>::N;          // (class tap, 16-channel half) steps per chunk
   // weight prefetch distance in steps (divides NS: a ring slot is compile-time in every chunk)
@@ -113,9 +119,9 @@ brickT_x3_kernel(BrickTArgs a) {
   // their latency once per chunk; streaming them in slices instead exposes it once per slice.
   constexpr int kHD = D + 1;
   static_assert(NS % D == 0, "prefetch ring");
-  static_assert(kHD < NS, "halo store step");
-  extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 × [kHP][kRow] + [kHP] offsets
-  int* hoff = reinterpret_cast<int*>(smem + 2 * kHP * kRow);
+  static_assert(kHD < NS / 2, "halo store step");
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 × [kHP][kHRow] + [kHP] offsets
+  int* hoff = reinterpret_cast<int*>(smem + 2 * kHP * kHRow);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   int blk = blockIdx.x;
@@ -156,8 +162,8 @@ brickT_x3_kernel(BrickTArgs a) {
     if (pos < kHP) {
       uint2 h, lo;
       prec::split4<PM>(v, h, lo);
-      *reinterpret_cast<uint2*>(buf + pos * kRow + 8 * q) = h;
-      if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + pos * kRow + 64 + 8 * q) = lo;
+      *reinterpret_cast<uint2*>(buf + pos * kHRow + 8 * q) = h;
+      if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + pos * kHRow + 64 + 8 * q) = lo;
     }
   };
   auto bload = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) __attribute__((always_inline)) {
@@ -199,30 +205,38 @@ brickT_x3_kernel(BrickTArgs a) {
   __syncthreads();
 
   for (int chunk = 0; chunk < nch; ++chunk) {
-    const char* H = smem + (chunk & 1) * kHP * kRow + lh * 16 + lane_row * kRow;
-    char* Hn = smem + ((chunk + 1) & 1) * kHP * kRow;
+    const char* H = smem + (chunk & 1) * kHP * kHRow + lh * 16 + lane_row * kHRow;
+    char* Hn = smem + ((chunk + 1) & 1) * kHP * kHRow;
     const int cn = chunk + 1 < nch ? chunk + 1 : chunk;
     auto a_read = [&](int i, bf16x8 (&dst)[2]) __attribute__((always_inline)) {
       const TStep st = ts.s[i >> 1];
-      const char* arow = H + ((st.od * kHH + st.oh) * kHW + st.ow) * kRow + (i & 1) * 32;
+      const char* arow = H + ((st.od * kHH + st.oh) * kHW + st.ow) * kHRow + (i & 1) * 32;
       dst[0] = *reinterpret_cast<const bf16x8*>(arow);
       if constexpr (prec::has_lo<PM>()) dst[1] = *reinterpret_cast<const bf16x8*>(arow + 64);
       else dst[1] = dst[0];
     };
-    float4 pv[kSL];
+    // the next chunk's halo in NB batches (one-plane modes: two, so the 256-register budget of
+    // two blocks per CU holds half of it at a time)
+    constexpr int NB = prec::has_lo<PM>() ? 1 : 2, BS = (kSL + NB - 1) / NB;
+    float4 pv[BS];
     bf16x8 af[2][2];
     a_read(0, af[0]);
 #pragma clang loop unroll(full)
     for (int i = 0; i < NS; ++i) {
       // (unconditional: on the last chunk this re-reads chunk cn = chunk into the idle buffer —
       // a branch here makes the compiler unswitch the loop and serialize the copy without it)
-      if (i == 0) {
 #pragma unroll
-        for (int sl = 0; sl < kSL; ++sl) pv[sl] = xload(halo_off(sl), __builtin_amdgcn_readfirstlane(cn * kBK * 4));
-      }
-      if (i == kHD) {
+      for (int b = 0; b < NB; ++b) {
+        if (i == b * (NS / NB)) {
 #pragma unroll
-        for (int sl = 0; sl < kSL; ++sl) halo_store(Hn, sl, pv[sl]);
+          for (int sl = 0; sl < BS; ++sl)
+            if (b * BS + sl < kSL) pv[sl] = xload(halo_off(b * BS + sl), __builtin_amdgcn_readfirstlane(cn * kBK * 4));
+        }
+        if (i == b * (NS / NB) + kHD) {
+#pragma unroll
+          for (int sl = 0; sl < BS; ++sl)
+            if (b * BS + sl < kSL) halo_store(Hn, b * BS + sl, pv[sl]);
+        }
       }
       const int c = ts.s[i >> 1].c;
       const bf16x8 bh = rb[i % D][0], bl = rb[i % D][1];
@@ -242,28 +256,39 @@ brickT_x3_kernel(BrickTArgs a) {
   // epilogue through LDS (the halo buffers are free after the last chunk's barrier): in the MFMA
   // layout a store instruction writes 32 B into each of 32 voxel lines; transposed, each lane
   // stores 16 B and 8 lanes a whole 128-B voxel, 64 lanes 8 w-consecutive voxels (1 KB).
-  // Two halves (output depth parity cd), 128 voxels × 144-B rows per wave each.
-  char* ew = smem + wave * (128 * kRow);
+  // NP passes of 8 / NP classes: two halves (output depth parity cd, 128 voxels × 144-B rows per
+  // wave each) in the bf16x3 mode; four quarters (cd, ch; 64 voxels per wave) in the one-plane
+  // modes, whose LDS is the 64 KB of the halo buffers
+  constexpr int NP = prec::has_lo<PM>() ? 2 : 4, CPP = 8 / NP, VPW = 32 * CPP;
+  char* ew = smem + wave * (VPW * kRow);
   const int q = lane & 7;                                   // read-back: channel quad 4q … 4q+3
   float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + 4 * q);
   double ps[4] = {0.0, 0.0, 0.0, 0.0}, pq[4] = {0.0, 0.0, 0.0, 0.0};   // InstanceNorm partials (a.part)
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int pass = 0; pass < NP; ++pass) {
+    // pass classes c = pass·CPP …: cd = c >> 2 (and, in quarters, ch = (c >> 1) & 1) fixed
 #pragma unroll
-    for (int c = half * 4; c < half * 4 + 4; ++c) {
-      const int v = (qd * 4 + 2 * qh + ((c >> 1) & 1)) * 16 + 2 * qw + (c & 1);
+    for (int c = pass * CPP; c < pass * CPP + CPP; ++c) {
+      // voxel of the pass's (VPW) rows: (dq, h, w) with h over the pass's h parities
+      const int v = NP == 2 ? (qd * 4 + 2 * qh + ((c >> 1) & 1)) * 16 + 2 * qw + (c & 1)
+                            : (qd * 2 + qh) * 16 + 2 * qw + (c & 1);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(ew + v * kRow + (8 * g + 4 * lh) * 4) =
             f32x4{acc[c][4 * g], acc[c][4 * g + 1], acc[c][4 * g + 2], acc[c][4 * g + 3]};
     }
     __syncthreads();
+    const int pcd = NP == 2 ? pass : pass >> 1, pch = NP == 2 ? 0 : pass & 1;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < VPW / 8; ++j) {
       const int v = j * 8 + (lane >> 3);
-      const int dq = v >> 6, hh = (v >> 4) & 3, ww = v & 15;
-      const int od = o0d + 2 * dq + half, oh = o0h + 4 * wave + hh, ow = o0w + ww;
+      // halves: v = (dq·4 + hh)·16 + ww (hh over 4 rows); quarters: v = (dq·2 + hq)·16 + ww,
+      // output row hh = 2·hq + ch
+      const int dq = NP == 2 ? v >> 6 : v >> 5;
+      const int hh = NP == 2 ? (v >> 4) & 3 : 2 * ((v >> 4) & 1) + pch;
+      const int ww = v & 15;
+      const int od = o0d + 2 * dq + pcd, oh = o0h + 4 * wave + hh, ow = o0w + ww;
       const f32x4 t = *reinterpret_cast<const f32x4*>(ew + v * kRow + 16 * q);
       if (od < a.Do && oh < a.Ho && ow < a.Wo) {
         const float4 r = make_float4(act_fwd(t[0] + bq.x, a.act), act_fwd(t[1] + bq.y, a.act),
@@ -278,7 +303,7 @@ brickT_x3_kernel(BrickTArgs a) {
         }
       }
     }
-    if (half == 0) __syncthreads();
+    if (pass + 1 < NP) __syncthreads();
   }
   // the consumer InstanceNorm's per-(instance, channel) Σy / Σy² of this brick (its separate
   // statistics pass over the 64³ output disappears): the 8 lanes of a channel quad add by
@@ -292,7 +317,7 @@ brickT_x3_kernel(BrickTArgs a) {
         pq[k] += __shfl_xor(pq[k], m);
       }
     }
-    double* red = reinterpret_cast<double*>(smem + 4 * 128 * kRow);   // [4 waves][32 channels][2]
+    double* red = reinterpret_cast<double*>(smem + 4 * VPW * kRow);   // [4 waves][32 channels][2]
     if (lane < 8) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -326,7 +351,12 @@ bool brickT_x3_applicable(const IgemmArgs& g) {
 // one static per kernel instantiation (the LDS opt-in is per function)
 template <int K, int PM>
 static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
-  const size_t lds = (size_t)2 * kHP * kRow + kHP * sizeof(int);
+  // halos + offsets; the epilogue rows (4 waves × 32·(8/NP) voxels × kRow) and the statistics
+  // reduction after them reuse the same bytes
+  constexpr int NP = prec::has_lo<PM>() ? 2 : 4;
+  const size_t halo = (size_t)2 * kHP * halo_row<PM>() + kHP * sizeof(int);
+  const size_t epi = (size_t)4 * 32 * (8 / NP) * kRow + 4 * 32 * 2 * sizeof(double);
+  const size_t lds = halo > epi ? halo : epi;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM>),
