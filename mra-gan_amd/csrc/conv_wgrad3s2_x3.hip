@@ -20,6 +20,8 @@
 // (the 32-channel side at full resolution): 4 waves as 2 sub-tiles × 2 K halves (even / odd
 // K-steps), the halves added in LDS before the slab store.  Split-K partial tiles go to slabs
 // ws[z][t][dn][gn], reduced in fixed order by wgrad_reduce_kernel (deterministic).
+#include <type_traits>
+
 #include "kernels.h"
 #include "prec.h"
 
@@ -41,6 +43,27 @@ constexpr int kGHalf = kGPos * 16;
 
 // fine position q (0 … 32) of a segment → its slot: odd positions (q even) are the O phase
 __device__ __forceinline__ int gslot(int q) { return (q & 1) ? (q - 1) >> 1 : 16 + (q >> 1); }
+
+// One-plane modes (bf16 / fp16), as conv_wgrad3_x3.hip's: the tiles are staged in natural
+// [K row][channel] order — row = slot·8 + r (slot: the coarse w of D, the phase slot of G), each
+// thread converts its float4 (4 channels of one voxel) and stores 8 B — and the MFMA operands come
+// out of LDS through ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, channels
+// 4p … 4p+3).  Rows of ≥ 128 B XOR their 16-B chunks by the row so the transposed reads are
+// conflict-free; the 64-B rows of a 32-channel G tile put a group's 4 rows on disjoint banks as
+// they are.  No fp32 → bf16 hi/lo transposition in VALU (the split staging was 29 VALU + 38 SALU
+// per MFMA, PMC r03v).
+constexpr int kTrRowsD = kSegW * kR;        // 128
+constexpr int kTrRowsG = kGPos * kR;        // 264
+template <int RB>
+__device__ __forceinline__ int tr_swz(int row) {
+  return RB == 256 ? (row & 3) << 2 : RB == 128 ? ((row >> 1) & 1) << 2 : 0;
+}
+typedef short tr_v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ tr_v4s tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tr_v4s*)(p));
+}
+template <int TG>
+constexpr int tr_stage() { return kTrRowsD * kTD * 2 + kTrRowsG * TG * 2; }
 
 // one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half
 template <int PM>
@@ -67,8 +90,10 @@ struct Wgrad3s2Args {
 template <int TG, int PM>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool kTr = !prec::has_lo<PM>();
+  constexpr int RBD = kTD * 2, RBG = TG * 2;        // tr: row bytes of the D / G images
   char* Ds = smem;
-  char* Gs = smem + kTD * kDRow;
+  char* Gs = smem + (kTr ? kTrRowsD * RBD : kTD * kDRow);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   // TG = 64: wave → (dn half, gn half); TG = 32: wave → (dn half, K half)
@@ -161,50 +186,126 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
     split8_store<PM>(p + ((2 + rot) & 3) * row_bytes, half, u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z);
     split8_store<PM>(p + ((3 + rot) & 3) * row_bytes, half, u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w);
   };
+  // tr: unit (slot, channel quad c) → rows slot·8 + r, 8 B at chunk c/2 (swizzled), half c&1
+  auto put16 = [&](char* base, auto rb_c, int slot, int c, const float4 (&v)[kR]) __attribute__((always_inline)) {
+    constexpr int RB = decltype(rb_c)::value;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int row = slot * kR + r;
+      uint2 h, l;
+      prec::split4<PM>(v[r], h, l);
+      *reinterpret_cast<uint2*>(base + row * RB + 16 * ((c >> 1) ^ tr_swz<RB>(row)) + 8 * (c & 1)) = h;
+    }
+  };
   auto store = [&]() __attribute__((always_inline)) {
+    if constexpr (kTr) {
+      put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+#pragma unroll
+      for (int pass = 0; pass < GPASS; ++pass)
+        put16(Gs, std::integral_constant<int, RBG>{}, gslot(pass * GP + gq), gcq, rg[pass]);
+      if (gx) put16(Gs, std::integral_constant<int, RBG>{}, gslot(gqx), gcq, rgx);
+      return;
+    }
     put(Ds, kDRow, kDHalf, uw, cq, rd);
 #pragma unroll
     for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot(pass * GP + gq), gcq, rg[pass]);
     if (gx) put(Gs, kGRow, kGHalf, gslot(gqx), gcq, rgx);
+  };
+  // tr read offsets: lane 4q+p of its 16-lane group g (lane bit 4) reads row 8h + q (+ the read's
+  // K offset) and channels (sub-tile base + 16g + 4p … +3)
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tgi = (lane >> 4) & 1;
+  const int trA = (8 * lh + tq) * RBD + 16 * (((wm0 + 16 * tgi) / 8 + (tp >> 1)) ^ tr_swz<RBD>(tq)) + 8 * (tp & 1);
+  const int trB = (8 * lh + tq) * RBG + 16 * (((wn0 + 16 * tgi) / 8 + (tp >> 1)) ^ tr_swz<RBG>(tq)) + 8 * (tp & 1);
+  auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
+    Ds = smem + b * tr_stage<TG>();
+    Gs = Ds + kTrRowsD * RBD;
   };
 
   f32x16 acc[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
 
-  if (nstage > 0) load(0);
-  for (int st = 0; st < nstage; ++st) {
-    store();
-    __syncthreads();
-    if (st + 1 < nstage) {                          // lands during this stage's MFMAs
+  auto advance = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
-      load(st + 1);
+    for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
+  };
+  if constexpr (kTr) {
+    // two stage buffers: the stage after next is loaded while this one's MFMAs run and stored
+    // right after them, so a load has a whole stage to land
+    if (nstage > 0) {
+      use_buf(0);
+      load(0);
+      store();
     }
-    const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
-    const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+    if (nstage > 1) {
+      advance();
+      load(1);
+    }
+  } else if (nstage > 0) {
+    load(0);
+  }
+  for (int st = 0; st < nstage; ++st) {
+    if constexpr (kTr) {
+      use_buf(st & 1);
+      __syncthreads();              // stage st staged by every wave; the other buffer read by nobody now
+    } else {
+      store();
+      __syncthreads();
+      if (st + 1 < nstage) {                        // lands during this stage's MFMAs
+        advance();
+        load(st + 1);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < kSegW / 2; ++ks) {
       if (TG == 32 && (ks & 1) != kpar) continue;   // K half of this wave
-      // K-step ks: coarse w = 2ks + lh (folded into arow / brow) × 8 segments
+      // K-step ks: coarse w = 2ks + lh × 8 segments
       bf16x8 fa[2], fb[3][2];
-      fa[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
-      fa[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : fa[0];
       // tap kw: kw = 1 → E[w] (slot w), kw = 0 → O[w − 1] (slot 16 + w), kw = 2 → O[w] (slot 17 + w)
-      constexpr int koff[3] = {16 * 16, 0, 17 * 16};
+      if constexpr (kTr) {
+        // rows 16ks … 16ks+15 (slots 2ks, 2ks+1 × 8 segments): two 4-row reads per operand
+        const char* ar = Ds + trA + (16 * ks) * RBD;
+        const tr_v4s a0 = tr_read(ar), a1 = tr_read(ar + 4 * RBD);
+        fa[0] = fa[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+        constexpr int kslot[3] = {16, 0, 17};
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        fb[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw]);
-        fb[kw][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw] + kGHalf) : fb[kw][0];
+        for (int kw = 0; kw < 3; ++kw) {
+          const char* br = Gs + trB + (16 * ks + kR * kslot[kw]) * RBG;
+          const tr_v4s b0 = tr_read(br), b1 = tr_read(br + 4 * RBG);
+          fb[kw][0] = fb[kw][1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      } else {
+        const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
+        const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+        fa[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
+        fa[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : fa[0];
+        constexpr int koff[3] = {16 * 16, 0, 17 * 16};
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          fb[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw]);
+          fb[kw][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(brow + ks * 32 + koff[kw] + kGHalf) : fb[kw][0];
+        }
       }
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) acc[kw] = prec::mma<PM>(fa[0], fa[1], fb[kw][0], fb[kw][1], acc[kw]);
     }
-    __syncthreads();
+    if constexpr (kTr) {
+      if (st + 1 < nstage) {
+        use_buf((st + 1) & 1);
+        store();                    // stage st+1 (loaded one stage ago) into the other buffer
+        if (st + 2 < nstage) {
+          advance();
+          load(st + 2);
+        }
+      }
+    } else {
+      __syncthreads();
+    }
   }
 
   // TG = 32: the odd-K waves' partial sums join the even-K waves' through LDS (fixed order)
   if constexpr (TG == 32) {
+    if constexpr (kTr) __syncthreads();             // every wave is past its last stage's reads
     float* red = reinterpret_cast<float*>(smem);    // [2 dn halves][3 taps][16][64 lanes]
     if (kpar == 1) {
 #pragma unroll
@@ -243,7 +344,10 @@ bool wgrad3s2_x3_applicable(const WgradArgs& a) {
 
 static int s2_tg(const WgradArgs& a) { return a.Cg % 64 == 0 ? 64 : 32; }
 
-static size_t s2_lds(int tg) { return (size_t)kTD * kDRow + (size_t)tg * kGRow; }
+static size_t s2_lds(int tg, bool tr) {
+  if (tr) return (size_t)2 * (tg == 64 ? tr_stage<64>() : tr_stage<32>());
+  return (size_t)kTD * kDRow + (size_t)tg * kGRow;
+}
 
 // splits: one round of resident blocks (1 per CU at TG 64, 2 at TG 32), ≥ 4 stages per block;
 // never more than the generic plan's (its workspace query sizes the slabs)
@@ -275,8 +379,9 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const int nsplit = (a.nseg + per - 1) / per;
   const int tg = s2_tg(g);
   const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
-  const size_t lds = s2_lds(tg);
+  const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16);
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
+  static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
       static bool attr64 = false;

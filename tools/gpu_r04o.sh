@@ -10,7 +10,7 @@ cd "$R"
 export TMPDIR=/tmp
 source tools/gpu_step.sh
 step kern 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py \
-  -k "brickT or transpose or in_stats_partials or all_paths_rounding or stride2" > "$O/kern.log" 2>&1
+  -k "brickT or transpose or in_stats_partials or all_paths_rounding or stride2 or three_tap or wgrad" > "$O/kern.log" 2>&1
 tail -2 "$O/kern.log"
 step stepp 900 python3 -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_step_gpu.py \
   -k "r9_s64_b2 or r6_s24_b1_pool1 or unet_s64" > "$O/step.log" 2>&1
