@@ -87,7 +87,7 @@ struct Wgrad3s2Args {
   int nseg, seg_per_split;
 };
 
-template <int TG, int PM>
+template <int TG, int PM, int AL>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kTr = !prec::has_lo<PM>();
@@ -141,7 +141,52 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
     if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
   };
+  // AL (aligned stages, the host checks): a stage's kR segments are whole coarse rows (kR / nsw of
+  // them) of one (n, d) plane and every stage is full, so segment r's G row is the stage's first
+  // fine row + 2·(r / nsw) and its w run starts 32·(r % nsw) fine voxels in — wave-uniform
+  // constants; the only out-of-range G reads left are the fine row −1 (d or h = 0 with kd or kh =
+  // 0) and the fine voxel −1 (lane q = 0 of a row's first segment).  The per-segment carries and
+  // range checks were ~35 SALU per MFMA (PMC r04p).
+  const int gplane_b = Wg * a.Cg * 4;                               // G bytes per fine row
+  const int glane_al = ((gq - 1) * a.Cg + gn0 + 4 * gcq) * 4;      // fine voxel q − 1 of a run
+  const int glane_alx = (((gx ? gqx : gq) - 1) * a.Cg + gn0 + 4 * gcq) * 4;
+  auto load_al = [&](int st) __attribute__((always_inline)) {
+    // stage base: (sn, sd, sh) is its first row (sw = 0)
+    const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
+    const int gd = 2 * sd - 1 + kd;
+    const bool dok = (unsigned)gd < (unsigned)Dg;
+    const int gh0 = 2 * sh - 1 + kh;                                 // fine row of segment 0
+    const int gbase = __builtin_amdgcn_readfirstlane(((sn * Dg + (dok ? gd : 0)) * Hg + (gh0 < 0 ? 0 : gh0)) * gplane_b);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const buf_f32x4 dv = buf_load_16b(dr, dlane, dso0 + r * dseg);
+      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      const int rr = r / nsw, wr = r - rr * nsw;                     // coarse row / run of the segment
+      const bool rok = dok && (gh0 >= 0 || rr > 0);
+      // gh0 < 0 only for segment rows rr = 0 (then invalid): rows rr > 0 start at fine row gh0 + 2rr.
+      // The soffset carries the row only; the run's w start goes into the (non-negative) voffset:
+      // the range check must see the lane's real offset
+      const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
+      const int wrun = 32 * wr * a.Cg * 4;
+      const bool w_edge = wr == 0;                                   // fine voxel −1 is outside
+#pragma unroll
+      for (int pass = 0; pass < GPASS; ++pass) {
+        const int q = pass * GP + gq;
+        const bool ok = rok && !(w_edge && q == 0);
+        const buf_f32x4 v = buf_load_16b(gr, ok ? glane_al + wrun + pass * GP * a.Cg * 4 : (int)kOobOffset, gso);
+        rg[pass][r] = make_float4(v.x, v.y, v.z, v.w);
+      }
+      const int qx = gx ? gqx : gq;
+      const bool okx = rok && !(w_edge && qx == 0);
+      const buf_f32x4 v = buf_load_16b(gr, okx ? glane_alx + wrun : (int)kOobOffset, gso);
+      rgx[r] = make_float4(v.x, v.y, v.z, v.w);
+    }
+  };
   auto load = [&](int st) __attribute__((always_inline)) {
+    if constexpr (AL) {
+      load_al(st);
+      return;
+    }
     int cw = sw, chh = sh, cdd = sd, cn = sn;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
@@ -226,6 +271,11 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
 
   auto advance = [&]() __attribute__((always_inline)) {
+    if constexpr (AL) {           // whole rows: one carry chain per stage
+      sh += kR / nsw;
+      if (sh == a.H) { sh = 0; if (++sd == a.D) { sd = 0; ++sn; } }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < kR; ++r) bump(sw, sh, sd, sn);
   };
@@ -367,6 +417,17 @@ int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
+template <int TG, int PM, int AL>
+static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL>), dim3(blocks), dim3(256), lds, st, a);
+}
+
 int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   Wgrad3s2Args a{};
   a.d = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
@@ -380,25 +441,19 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const int tg = s2_tg(g);
   const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
   const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16);
+  // aligned stages: whole coarse rows of one plane per stage, every stage full
+  const int nsw = g.Wd / kSegW;
+  static const bool no_al = getenv("MRAGAN_W3S2_NO_AL") != nullptr;   // A/B switch
+  const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
   static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
-      static bool attr64 = false;
-      if (!attr64) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<64, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr64 = true;
-      }
-      hipLaunchKernelGGL((wgrad3s2_x3_kernel<64, PM>), dim3(blocks), dim3(256), lds, st, a);
+      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, st);
+      else launch_w3s2<64, PM, 0>(a, blocks, lds, st);
     } else {
-      static bool attr32 = false;
-      if (!attr32) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<32, PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr32 = true;
-      }
-      hipLaunchKernelGGL((wgrad3s2_x3_kernel<32, PM>), dim3(blocks), dim3(256), lds, st, a);
+      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, st);
+      else launch_w3s2<32, PM, 0>(a, blocks, lds, st);
     }
     return nsplit;
   })

@@ -274,7 +274,10 @@ def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
 
 
 @pytest.mark.parametrize("N,cin,cout,dims", [(1, 32, 64, (8, 10, 32)), (2, 64, 128, (6, 4, 64)), (1, 32, 128, (4, 2, 32)),
-                                             (3, 64, 64, (2, 6, 32))])
+                                             (3, 64, 64, (2, 6, 32)),
+                                             # aligned stages (whole coarse rows per 8-segment stage)
+                                             (1, 32, 64, (4, 16, 32)), (2, 64, 128, (4, 8, 64)),
+                                             (1, 32, 64, (6, 16, 64))])
 def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
     """Weight gradients of the k3 s2 p1 down convs (networks3D.py:192-197) and of the transposed
     up convs (op 1, networks3D.py:203-210) on the 3-kw-tap even/odd-phase kernel
