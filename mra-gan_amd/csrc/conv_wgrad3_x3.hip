@@ -100,10 +100,14 @@ struct Wgrad3Args {
 // 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
 // the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
 // kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
-template <int TC, int TI, int PM, int X16, int AL, int SW>
-__global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
-  constexpr int NT = TC * TI / 16;        // 32 × 32 sub-tile per wave
-  constexpr int WC = TC / 32;             // waves along co
+// WM = 2 (128 × 64 on operand planes, aligned stages): 4 waves of 64 × 32 instead of 8 of 32 × 32.
+// Per K-step a wave then reads 2 A + 3 B fragments for 6 MFMAs instead of 1 + 3 for 3: the
+// transposing LDS reads (1.37 KB per MFMA per wave, ≈ 170 B/clk per CU at the MFMA rate against
+// the LDS's 128) drop to 0.85 KB per MFMA.
+template <int TC, int TI, int PM, int X16, int AL, int SW, int WM>
+__global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
+  constexpr int NT = TC * TI / (16 * WM); // 32·WM × 32 sub-tile per wave
+  constexpr int WC = TC / (32 * WM);      // waves along co
   constexpr bool kTr = !prec::has_lo<PM>();        // 16-bit modes: natural-order tiles + transposing reads
   // X16: dY and X are the producers' 16-bit operand planes (bf16 / fp16 words, rounded as the
   // staging below would round them): 8-B loads stored as they are, no conversion
@@ -120,7 +124,7 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   char* Gs = smem + (kTr ? kTrRowsD * RBD : TC * kDRow);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  const int wm0 = (wave % WC) * 32, wn0 = (wave / WC) * 32;
+  const int wm0 = (wave % WC) * 32 * WM, wn0 = (wave / WC) * 32;
 
   // logical block: (co tile, ci tile) fastest, then (kd, kh), then split; XCD-aware remap so an
   // XCD's blocks share a contiguous range of splits (their dY / X rows stay in its L2)
@@ -144,7 +148,8 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   // contiguous bytes (a w-fastest order, conflict-free for the LDS writes below, measured 35 %
   // slower overall).  dY: TC/4 quads × 16 w = one unit per thread.  X: TI/4 quads × 18 w'.
   constexpr int DQ = TC / 4, GQ = TI / 4;
-  static_assert(SW != 16 || NT == 16 * DQ, "one dY unit per thread");
+  static_assert((X16 && AL) || SW != 16 || NT == 16 * DQ, "one dY unit per thread");
+  static_assert(WM == 1 || (X16 && AL), "64-row waves: the aligned operand-plane path only");
   const int cq = tid % DQ, uw = tid / DQ;          // dY unit
   const int gcq = tid % GQ, gw = tid / GQ;         // X unit: w' = gw
   // TC == TI: threads own w' 0..15 and threads < 2·GQ also w' 16, 17 (rg2).  TC = 2·TI: threads
@@ -349,12 +354,17 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
   // transposed-read lane offsets: lane 4q+p of its 16-lane group g (g = lane bit 4) addresses row
   // 8h + q (+ the read's K offset) and channels (sub-tile base + 16g + 4p … +3)
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
-  const int trA = (8 * lh + tq) * RBD + 16 * (((wm0 + 16 * tg) / 8 + (tp >> 1)) ^ tr_swz<RBD>(tq)) + 8 * (tp & 1);
+  int trA[WM];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+    trA[i] = (8 * lh + tq) * RBD + 16 * (((wm0 + 32 * i + 16 * tg) / 8 + (tp >> 1)) ^ tr_swz<RBD>(tq)) + 8 * (tp & 1);
   const int trB = (8 * lh + tq) * RBG + 16 * (((wn0 + 16 * tg) / 8 + (tp >> 1)) ^ tr_swz<RBG>(tq)) + 8 * (tp & 1);
 
-  f32x16 acc[3];
+  f32x16 acc[3][WM];
 #pragma unroll
-  for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < WM; ++i) acc[t][i] = f32x16{};
 
   auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
     Ds = smem + b * kStage;
@@ -385,16 +395,20 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
         load(st + 1);
       }
     }
-    const char* arow = kTr ? Ds + trA : Ds + (wm0 + li) * kDRow + lh * 16;
+    const char* arow = kTr ? Ds + trA[0] : Ds + (wm0 + li) * kDRow + lh * 16;
     const char* brow = kTr ? Gs + trB : Gs + (wn0 + li) * kGRow + lh * 16;
     // fragments of K-step ks: A hi/lo (dY) and B hi/lo for the three kw taps (X shifted by kw
     // slots); software-pipelined one K-step ahead so the LDS latency hides under the MFMAs
-    bf16x8 fa[2][2], fb[2][3][2];
-    auto frag = [&](int ks, bf16x8 (&A)[2], bf16x8 (&Bf)[3][2]) __attribute__((always_inline)) {
+    bf16x8 fa[2][WM][2], fb[2][3][2];
+    auto frag = [&](int ks, bf16x8 (&A)[WM][2], bf16x8 (&Bf)[3][2]) __attribute__((always_inline)) {
       if constexpr (kTr) {
         // K-step ks covers rows 16ks … 16ks+15: two 4-row reads per operand for this lane's 8 K
-        const tr_v4s a0 = tr_read(arow + (16 * ks) * RBD), a1 = tr_read(arow + (16 * ks + 4) * RBD);
-        A[0] = A[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+          const char* ar = Ds + trA[i];
+          const tr_v4s a0 = tr_read(ar + (16 * ks) * RBD), a1 = tr_read(ar + (16 * ks + 4) * RBD);
+          A[i][0] = A[i][1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const tr_v4s b0 = tr_read(brow + (16 * ks + 8 * kw) * RBG), b1 = tr_read(brow + (16 * ks + 8 * kw + 4) * RBG);
@@ -402,8 +416,8 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
         }
         return;
       }
-      A[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
-      A[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : A[0];
+      A[0][0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
+      A[0][1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : A[0][0];
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         Bf[kw][0] = *reinterpret_cast<const bf16x8*>(brow + ks * 32 + kw * 16);
@@ -416,9 +430,10 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
       const int c = ks & 1;
       if (ks + 1 < kSegW / 2) frag(ks + 1, fa[c ^ 1], fb[c ^ 1]);
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        acc[kw] = prec::mma<PM>(fa[c][0], fa[c][1], fb[c][kw][0], fb[c][kw][1], acc[kw]);
-      }
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+          acc[kw][i] = prec::mma<PM>(fa[c][i][0], fa[c][i][1], fb[c][kw][0], fb[c][kw][1], acc[kw][i]);
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (kTr) {
@@ -442,10 +457,12 @@ __global__ void __launch_bounds__(TC * TI / 16, TC == 64 ? 2 : 1) wgrad3_x3_kern
     float* slab = a.ws + ((int64_t)z * 27 + t) * a.Cd * a.Cg;
     const int col = ci0 + wn0 + li;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = co0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      slab[(int64_t)row * a.Cg + col] = acc[kw][r];
-    }
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = co0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        slab[(int64_t)row * a.Cg + col] = acc[kw][i][r];
+      }
   }
 }
 
@@ -490,9 +507,9 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TC, int TI, int PM, int X16, int AL, int SW = kSegW>
+template <int TC, int TI, int PM, int X16, int AL, int SW = kSegW, int WM = 1>
 static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
-  if constexpr ((X16 && prec::has_lo<PM>()) || (SW != kSegW && !(X16 && AL))) {
+  if constexpr ((X16 && prec::has_lo<PM>()) || ((SW != kSegW || WM != 1) && !(X16 && AL))) {
     return;                                     // rejected by the caller
   } else {
     constexpr bool tr = !prec::has_lo<PM>();
@@ -501,11 +518,11 @@ static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
     static_assert(SW == kSegW || lds_tr<SW, TC>() <= 160 * 1024, "LDS");
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW>), dim3(blocks), dim3(TC * TI / 16), lds, st, a);
+    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM>), dim3(blocks), dim3(TC * TI / (16 * WM)), lds, st, a);
   }
 }
 
@@ -539,13 +556,20 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     return -kBadArg;
   }
   MRAGAN_PREC_DISPATCH(g.x3, {
+    // 64-row waves on the wide aligned operand-plane tiles (MRAGAN_W3_WM=1: 32-row waves, A/B)
+    static const bool wm2 = [] { const char* e = getenv("MRAGAN_W3_WM"); return !(e && atoi(e) == 1); }();
     if (segw != kSegW) {
-      if (wide) launch_wgrad3<128, 64, PM, 1, 1, 24>(a, blocks, st);
-      else launch_wgrad3<64, 64, PM, 1, 1, 24>(a, blocks, st);
+      if (wide) {
+        if (wm2) launch_wgrad3<128, 64, PM, 1, 1, 24, 2>(a, blocks, st);
+        else launch_wgrad3<128, 64, PM, 1, 1, 24>(a, blocks, st);
+      } else {
+        launch_wgrad3<64, 64, PM, 1, 1, 24>(a, blocks, st);
+      }
       return nsplit;
     }
     if (wide) {
-      if (g.in16) { if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st); }
+      if (g.in16 && al && wm2) launch_wgrad3<128, 64, PM, 1, 1, kSegW, 2>(a, blocks, st);
+      else if (g.in16) { if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st); }
       else { if (al) launch_wgrad3<128, 64, PM, 0, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 0, 0>(a, blocks, st); }
     } else {
       if (g.in16) { if (al) launch_wgrad3<64, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<64, 64, PM, 1, 0>(a, blocks, st); }
