@@ -100,10 +100,9 @@ struct Wgrad3Args {
 // 128-channel ResnetBlock convs): 8 waves (4 × 2), one block per CU — per staged element twice
 // the MFMAs of the 64 × 64 tile; the split-to-bf16 staging, not the matrix pipe, bounds this
 // kernel (PMC: VALU instructions ≈ 9× the MFMAs, ACTIVE 39 % vs MFMA busy 33 %).
-// WM = 2 (128 × 64 on operand planes, aligned stages): 4 waves of 64 × 32 instead of 8 of 32 × 32.
-// Per K-step a wave then reads 2 A + 3 B fragments for 6 MFMAs instead of 1 + 3 for 3: the
-// transposing LDS reads (1.37 KB per MFMA per wave, ≈ 170 B/clk per CU at the MFMA rate against
-// the LDS's 128) drop to 0.85 KB per MFMA.
+// WM = 2 (128 × 64 on operand planes, aligned stages; opt-in, measured slower — see the launch):
+// 4 waves of 64 × 32 instead of 8 of 32 × 32.  Per K-step a wave then reads 2 A + 3 B fragments
+// for 6 MFMAs instead of 1 + 3 for 3 (0.85 instead of 1.37 KB of transposing LDS reads per MFMA).
 template <int TC, int TI, int PM, int X16, int AL, int SW, int WM>
 __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / (16 * WM); // 32·WM × 32 sub-tile per wave
@@ -556,8 +555,10 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     return -kBadArg;
   }
   MRAGAN_PREC_DISPATCH(g.x3, {
-    // 64-row waves on the wide aligned operand-plane tiles (MRAGAN_W3_WM=1: 32-row waves, A/B)
-    static const bool wm2 = [] { const char* e = getenv("MRAGAN_W3_WM"); return !(e && atoi(e) == 1); }();
+    // 64-row waves on the wide aligned operand-plane tiles: opt-in A/B (MRAGAN_W3_WM=2), measured
+    // slower than the 8-wave tiles (res wgrad [4×16³] 34.2 vs 32.2 µs, [2×32³] 90.3 vs 81.9 µs,
+    // r04r): the LDS reads were not the limiter, the two waves per SIMD are worth more
+    static const bool wm2 = [] { const char* e = getenv("MRAGAN_W3_WM"); return e && atoi(e) == 2; }();
     if (segw != kSegW) {
       if (wide) {
         if (wm2) launch_wgrad3<128, 64, PM, 1, 1, 24, 2>(a, blocks, st);
