@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 13
+#define MRAGAN_ABI_VERSION 14
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -161,7 +161,9 @@ int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, 
  *   instnorm_bwd_op16: mragan_instnorm_bwd_g writing dx only as its plane dx16 (g_out nullable);
  *   conv3d_op16: mragan_conv3d_presplit_in_stats (no bias, no activation) on the plane x16 of
  *       the input — the k3 s1 brick kernel (ResnetBlock convs and their whole-grid data
- *       gradients); part / chunks nullable (no InstanceNorm partials);
+ *       gradients), and (ABI 14) the implicit GEMM for the other forward-form convs with a multiple
+ *       of 32 input channels (G down1 / down2 on the stem / down1 InstanceNorm planes);
+ *       wsplit nullable (the brick then splits per call); part / chunks nullable (no partials);
  *   conv3d_wgrad_op16: mragan_conv3d_wgrad on the planes of dense and gathered — the k3 s1 valid
  *       weight gradient of the ResnetBlock convs (wgrad3_x3).                                   */
 int mragan_instnorm_fwd_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
@@ -179,6 +181,13 @@ int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, 
 int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
                              int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
                              size_t ws_bytes, void* stream);
+/* ABI 14: mragan_conv3d_wgrad with only the gathered (fine-grid) operand as its 16-bit plane — the
+ * k3 s2 p1 weight gradients of G down1 / down2 (networks3D.py:192-197; the reference's
+ * Conv3d.weight.grad via ATen's convolution_backward), whose gathered operand is the stem / down1
+ * InstanceNorm output that exists only as a plane in the bf16 / fp16 modes; dense stays fp32. */
+int mragan_conv3d_wgrad_g16(const float* dense, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
+                            int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                            size_t ws_bytes, void* stream);
 /* InstanceNorm backward statistics in the data-gradient epilogue (ABI 11).  In a
  * ResnetBlock (networks3D.py:241-257) conv2's input is z1 = relu(IN(h1)) padded by 1, so the IN
  * backward of h1 reads g = fold(dz1)·relu'(x̂) with dz1 = conv2's padded data gradient.  Its two

@@ -147,7 +147,7 @@ int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, 
                        int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
                        size_t ws_bytes, double* part, size_t part_bytes, int* chunks, void* stream) {
   if (int rc = op16_mode_ok()) return rc;
-  MRAGAN_CHECK_ARG(x16 && w && wsplit && y, "conv3d_op16: null pointer");
+  MRAGAN_CHECK_ARG(x16 && w && y, "conv3d_op16: null pointer");   // wsplit: optional (the brick packs per call)
   MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_op16: transposed must be 0/1");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && Do > 0 && Ho > 0 && Wo > 0,
                    "conv3d_op16: bad shape");
@@ -264,6 +264,19 @@ int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd,
   MRAGAN_CHECK_ARG(!thin_wgrad_side(Cd, Cg) && k >= 1 && stride >= 1 && pad >= 0, "wgrad_op16: bad args");
   WgradArgs a{static_cast<const float*>(dense16), N, Dd, Hd, Wd, Cd, static_cast<const float*>(gathered16), Dg, Hg, Wg,
               Cg, k, stride, pad, static_cast<float*>(ws), 0, 0, g_conv_precision, 1};
+  return conv_wgrad(a, dw, accumulate, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mragan_conv3d_wgrad_g16(const float* dense, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
+                            int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                            size_t ws_bytes, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(dense && gathered16 && dw && ws, "wgrad_g16: null pointer");
+  MRAGAN_CHECK_ARG(!thin_wgrad_side(Cd, Cg) && k == 3 && stride == 2 && pad == 1, "wgrad_g16: the k3 s2 p1 weight "
+                   "gradients only");
+  WgradArgs a{dense, N, Dd, Hd, Wd, Cd, static_cast<const float*>(gathered16), Dg, Hg, Wg, Cg, k, stride, pad,
+              static_cast<float*>(ws), 0, 0, g_conv_precision, 0};
+  a.in16g = 1;
   return conv_wgrad(a, dw, accumulate, ws_bytes, static_cast<hipStream_t>(stream));
 }
 

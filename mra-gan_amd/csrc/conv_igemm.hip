@@ -289,12 +289,13 @@ static int conv_igemm_x3_chunked(const IgemmArgs& a, int64_t max_mc, int64_t tot
   MRAGAN_CHECK_ARG(nb > 0, "conv (16-bit MFMA modes): one %d×%d×%d×%d instance exceeds 2 GiB", a.Di, a.Hi, a.Wi, a.cx);
   if (nb >= a.N) return conv_igemm_x3(a, max_mc, total_m, st);
   const int64_t in_vol = (int64_t)a.Di * a.Hi * a.Wi * a.cx, out_vol = (int64_t)a.Do * a.Ho * a.Wo * a.ny;
+  const int64_t in_bytes = in_vol * (a.x16 ? 2 : 4);
   for (int n0 = 0; n0 < a.N; n0 += nb) {
     IgemmArgs c = a;
     c.in_part = nullptr;                 // instance ranges: no InstanceNorm partials (stats pass instead)
     c.bs_x = nullptr;
     c.N = nb < a.N - n0 ? nb : a.N - n0;
-    c.x = a.x + n0 * in_vol;
+    c.x = reinterpret_cast<const float*>(reinterpret_cast<const char*>(a.x) + n0 * in_bytes);
     c.y = a.y + n0 * out_vol;
     int64_t mc, tm;
     igemm_geometry(c, mc, tm);
@@ -311,10 +312,12 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   igemm_geometry(a, max_mc, total_m);
   if (max_mc == 0 || a.ny == 0) return kOk;
   if (a.x16) {
-    // 16-bit operand planes: the ResnetBlock convs (forward and whole-grid data gradient) only
-    MRAGAN_CHECK_ARG(!g_brick_off && conv_brick_applicable(a), "conv: a 16-bit operand plane input is supported by the "
-                     "k3 s1 brick kernel only");
-    return conv_brick(a, st);
+    // 16-bit operand planes: the ResnetBlock convs (forward and whole-grid data gradient) on the
+    // brick; the others (the 64³-level stride-2 forward-form convs) on the implicit GEMM
+    if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+    MRAGAN_CHECK_ARG(a.x3 && a.cx % 32 == 0, "conv: a 16-bit operand plane input needs the bf16 / fp16 implicit GEMM "
+                     "(multiples of 32 input channels)");
+    return conv_igemm_x3_chunked(a, max_mc, total_m, st);
   }
   if (full_dgrad_split_applicable(a)) {
     // the 16-bit brick kernel on the interior (no padded rows, no all-zero taps) + the shell pass

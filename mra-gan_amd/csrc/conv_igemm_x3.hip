@@ -22,6 +22,8 @@
 //
 // Precision modes (prec.h): the same kernel is instantiated for bf16x3 (three MFMAs, hi + lo
 // planes), bf16 and fp16 (one MFMA per block product, hi planes only).
+#include <type_traits>
+
 #include "conv_geo.h"
 #include "kernels.h"
 #include "prec.h"
@@ -33,16 +35,22 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH>
+// X16: the input is the producer's 16-bit operand plane (bf16 / fp16 words, rounded as the
+// staging would round them; the one-plane modes): an A row's BK channels are BK / 8 16-B loads
+// stored to LDS as they are — half the bytes of the fp32 input and no conversion.
+template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH, int X16>
 __global__ void __launch_bounds__(256)
 conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
+  static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int LDK = BK + 8;               // bf16 per padded row
   constexpr int LPR = BK / 4;               // float4 per row (global side)
-  constexpr int A_LOADS = (BM * LPR + 255) / 256;
+  constexpr int LPRA = X16 ? BK / 8 : LPR;  // A loads per row (16 B each)
+  constexpr int A_LOADS = (BM * LPRA + 255) / 256;
   constexpr int B_LOADS = (BN * LPR + 255) / 256;
   constexpr int ROWS_PER_PASS = 256 / LPR;
+  constexpr int ROWS_PER_PASS_A = 256 / LPRA;
   constexpr int PLANE_A = BM * LDK, PLANE_B = BN * LDK;   // bf16 elements per plane
   // hi (+ lo in bf16x3) planes of A and B.  The one-plane modes drop the lo planes of the 2-tile
   // waves' blocks: 128×64 at 31 instead of 62 KB, two more blocks per CU (G down1 [4×64³]: 64.6
@@ -100,10 +108,11 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   }
 
   const int q = tid % LPR;
+  const int qa = tid % LPRA;                // A: this thread's 16-B slice of a row
   int a_nb[A_LOADS], a_bd[A_LOADS], a_bh[A_LOADS], a_bw[A_LOADS];
 #pragma unroll
   for (int i = 0; i < A_LOADS; ++i) {
-    int r = tid / LPR + i * ROWS_PER_PASS;
+    int r = tid / LPRA + i * ROWS_PER_PASS_A;
     int64_t m = m0 + r;
     if (r < BM && m < Mc) {
       int qw = (int)(m % gw.Q); int64_t t = m / gw.Q;
@@ -125,7 +134,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int nK = min(nK_all, ks0 + kper) - ks0;       // steps of this slice: ks0 … ks0+nK−1
   // DEPTH 2 (A/B only, measured slower): two register stages, the tiles of step ks + 2 loaded
   // while step ks runs and stored to LDS at the end of step ks + 1; DEPTH 1 (default): one stage
-  float4 ra[2][A_LOADS], rb[2][B_LOADS];
+  using RegA = std::conditional_t<X16 != 0, uint4, float4>;   // X16: eight 16-bit words, else four fp32
+  RegA ra[2][A_LOADS];
+  float4 rb[2][B_LOADS];
 
   // Operands through buffer descriptors (byte offsets are 32-bit: the host checks the sizes).
   // A: per thread and row a fixed base offset of its (nb, bd, bh, bw) voxel + channel quad; a
@@ -133,12 +144,13 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   // zeros through an out-of-range voffset.  B: the lane part is fixed, the step part is the
   // SGPR soffset.  K-steps advance (channel chunk, kw, kh, kd) with carries: no per-step
   // divisions, no 64-bit address arithmetic.
-  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * 4));
+  constexpr int ESA = X16 ? 2 : 4;          // bytes per input element
+  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * ESA));
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4));
   int a_base[A_LOADS];
 #pragma unroll
   for (int i = 0; i < A_LOADS; ++i)
-    a_base[i] = ((((a_nb[i] < 0 ? 0 : a_nb[i]) * a.Di + a_bd[i]) * a.Hi + a_bh[i]) * a.Wi + a_bw[i]) * a.cx * 4 + 16 * q;
+    a_base[i] = ((((a_nb[i] < 0 ? 0 : a_nb[i]) * a.Di + a_bd[i]) * a.Hi + a_bh[i]) * a.Wi + a_bw[i]) * a.cx * ESA + 16 * qa;
   int b_voff[B_LOADS];
 #pragma unroll
   for (int i = 0; i < B_LOADS; ++i) {
@@ -154,19 +166,20 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
   };
 
-  auto load_tiles = [&](float4 (&ra_)[A_LOADS], float4 (&rb_)[B_LOADS]) __attribute__((always_inline)) {
+  auto load_tiles = [&](RegA (&ra_)[A_LOADS], float4 (&rb_)[B_LOADS]) __attribute__((always_inline)) {
     const int c0 = kc * BK;
     const int td = gd.t0 + gd.tstep * kjd, th = gh.t0 + gh.tstep * kjh, tw = gw.t0 + gw.tstep * kjw;
     const int wt = (td * a.k + th) * a.k + tw;
     const int dd = gd.sign * kjd, dh = gh.sign * kjh, dw = gw.sign * kjw;
-    const int toff = __builtin_amdgcn_readfirstlane((((dd * a.Hi + dh) * a.Wi + dw) * a.cx + c0) * 4);
+    const int toff = __builtin_amdgcn_readfirstlane((((dd * a.Hi + dh) * a.Wi + dw) * a.cx + c0) * ESA);
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
       const int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
       const bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
                       (unsigned)iw < (unsigned)a.Wi;
       const buf_f32x4 v = buf_load_16b(xrs, ok ? a_base[i] + toff : (int)kOobOffset, 0);
-      ra_[i] = make_float4(v.x, v.y, v.z, v.w);
+      if constexpr (X16) ra_[i] = __builtin_bit_cast(uint4, v);
+      else ra_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
     const int wso = __builtin_amdgcn_readfirstlane((wt * a.ny * a.cx + c0) * 4);
 #pragma unroll
@@ -176,16 +189,20 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
     advance();
   };
-  auto store_tiles = [&](int buf, const float4 (&ra_)[A_LOADS], const float4 (&rb_)[B_LOADS]) {
+  auto store_tiles = [&](int buf, const RegA (&ra_)[A_LOADS], const float4 (&rb_)[B_LOADS]) {
     __bf16* st = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
-      int r = tid / LPR + i * ROWS_PER_PASS;
+      int r = tid / LPRA + i * ROWS_PER_PASS_A;
       if (r < BM) {
-        uint2 hi, lo;
-        prec::split4<PM>(ra_[i], hi, lo);
-        *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
-        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
+        if constexpr (X16) {
+          *reinterpret_cast<uint4*>(st + r * LDK + 8 * qa) = ra_[i];
+        } else {
+          uint2 hi, lo;
+          prec::split4<PM>(ra_[i], hi, lo);
+          *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
+          if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
+        }
       }
     }
 #pragma unroll
@@ -408,6 +425,21 @@ size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_
   return pl.splits > 1 ? (size_t)pl.splits * total_m * a.ny * sizeof(float) : 0;
 }
 
+template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH>
+static void launch_x3_pm(const IgemmArgs& a, dim3 grid, int gm, int gn, int ntiles, int splits, hipStream_t st) {
+  if constexpr (prec::has_lo<PM>()) {
+    hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0>), grid, dim3(256), 0, st, a, gm, gn,
+                       ntiles, splits);
+  } else {
+    if (a.x16)
+      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 1>), grid, dim3(256), 0, st, a, gm, gn,
+                         ntiles, splits);
+    else
+      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0>), grid, dim3(256), 0, st, a, gm, gn,
+                         ntiles, splits);
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int BK>
 static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -418,13 +450,9 @@ static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t
   // 87.6 vs 72.8, D layer 2 28.8 vs 25.2 at N = 4) — the extra 24–32 VGPRs cost occupancy
   static const bool depth1 = getenv("MRAGAN_IG_DEPTH2") == nullptr;
   MRAGAN_PREC_DISPATCH(a.x3, {
-    if (depth1)
-      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, 1>), dim3(ntiles * splits), dim3(256), 0, st, a,
-                         gm, gn, ntiles, splits);
-    else
-      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, 2>), dim3(ntiles * splits), dim3(256), 0, st, a,
-                         gm, gn, ntiles, splits);
-    return check_launch("conv_igemm_x3");
+    if (depth1) launch_x3_pm<WM, WN, TM, TN, BK, PM, 1>(a, dim3(ntiles * splits), gm, gn, ntiles, splits, st);
+    else launch_x3_pm<WM, WN, TM, TN, BK, PM, 2>(a, dim3(ntiles * splits), gm, gn, ntiles, splits, st);
+    return check_launch(a.x16 ? "conv_igemm_x3(op16)" : "conv_igemm_x3");
   })
 }
 
@@ -452,6 +480,8 @@ int conv_igemm_x3_shell(IgemmArgs a, hipStream_t st) {
 }
 
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  MRAGAN_CHECK_ARG(!a.x16 || ((a.x3 == kPrecBf16 || a.x3 == kPrecF16) && a.cx % 32 == 0),
+                   "conv (16-bit operand plane): the one-plane modes and multiples of 32 input channels only");
   // operand byte offsets are 32-bit (buffer descriptors)
   MRAGAN_CHECK_ARG((int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx * 4 < ((int64_t)1 << 31) &&
                        (int64_t)a.k * a.k * a.k * a.ny * a.cx * 4 < ((int64_t)1 << 31),

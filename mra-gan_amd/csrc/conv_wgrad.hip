@@ -416,6 +416,8 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   const bool w3 = !no_w3 && wgrad3_x3_applicable(a), w3s2 = !no_w3 && !w3 && wgrad3s2_x3_applicable(a);
   MRAGAN_CHECK_ARG(!a.in16 || w3, "conv_wgrad: 16-bit operand planes are supported by the k3 s1 valid weight "
                    "gradient (wgrad3_x3) only");
+  MRAGAN_CHECK_ARG(!a.in16g || w3s2, "conv_wgrad: a 16-bit gathered-operand plane is supported by the k3 s2 weight "
+                   "gradient (wgrad3s2_x3) only");
   if (w3 || w3s2) {
     const int used = w3 ? conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st)
                         : conv_wgrad3s2_x3(a, wgrad3s2_x3_splits(a, a.splits), st);

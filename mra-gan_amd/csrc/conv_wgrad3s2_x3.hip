@@ -82,15 +82,19 @@ __device__ __forceinline__ void split8_store(char* p, int half, float v0, float 
 
 struct Wgrad3s2Args {
   const float* d; int N, D, H, W, Cd;     // D [N][D][H][W][Cd] (coarse)
-  const float* g; int Cg;                 // G [N][2D][2H][2W][Cg] (fine)
+  const float* g; int Cg;                 // G [N][2D][2H][2W][Cg] (fine; X16G: its 16-bit operand plane)
   float* ws;                              // slabs [splits][27][Cd][Cg]
   int nseg, seg_per_split;
 };
 
-template <int TG, int PM, int AL>
+// X16G: G is the producer's 16-bit operand plane (bf16 / fp16 words): its staging units are
+// (fine position, 8-channel octet), one 16-B load each, stored as they are (one-plane modes)
+template <int TG, int PM, int AL, int X16G>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kTr = !prec::has_lo<PM>();
+  static_assert(!X16G || kTr, "16-bit operand planes exist in the one-plane modes only");
+  constexpr int ESG = X16G ? 2 : 4;       // bytes per G element
   constexpr int RBD = kTD * 2, RBG = TG * 2;        // tr: row bytes of the D / G images
   char* Ds = smem;
   char* Gs = smem + (kTr ? kTrRowsD * RBD : kTD * kDRow);
@@ -128,13 +132,18 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int gcq = tid % GQ, gq = tid / GQ;
   const int gqx = GPASS * GP + gq;                 // the remainder pass (q = 32 …)
   const bool gx = gqx < kGPos;
+  // X16G units: (q8 = tid / GO, octet go = tid % GO): one pass covers the 33 positions (TG ≤ 64)
+  constexpr int GO = TG / 8;
+  const int go = tid % GO, q8 = tid / GO;
+  const bool g8 = q8 < kGPos;
 
   float4 rd[kR], rg[2][kR], rgx[kR];
+  uint4 rg8[X16G ? kR : 1];
   // D / G rows through buffer descriptors: segment / row parts of the offsets are wave-uniform
   // (SGPR soffset); out-of-range rows and positions read zeros through an out-of-range voffset
   // (no select on the loaded values, no 64-bit address arithmetic)
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.d, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * 4));
-  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.g, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * 4));
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.g, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * ESG));
   const int dlane = (uw * a.Cd + dn0 + 4 * cq) * 4;
   const int dseg = kSegW * a.Cd * 4;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
@@ -147,9 +156,10 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   // constants; the only out-of-range G reads left are the fine row −1 (d or h = 0 with kd or kh =
   // 0) and the fine voxel −1 (lane q = 0 of a row's first segment).  The per-segment carries and
   // range checks were ~35 SALU per MFMA (PMC r04p).
-  const int gplane_b = Wg * a.Cg * 4;                               // G bytes per fine row
+  const int gplane_b = Wg * a.Cg * ESG;                             // G bytes per fine row
   const int glane_al = ((gq - 1) * a.Cg + gn0 + 4 * gcq) * 4;      // fine voxel q − 1 of a run
   const int glane_alx = (((gx ? gqx : gq) - 1) * a.Cg + gn0 + 4 * gcq) * 4;
+  const int glane_al8 = ((q8 - 1) * a.Cg + gn0 + 8 * go) * 2;      // X16G: octet go of fine voxel q8 − 1
   auto load_al = [&](int st) __attribute__((always_inline)) {
     // stage base: (sn, sd, sh) is its first row (sw = 0)
     const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
@@ -167,8 +177,13 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       // The soffset carries the row only; the run's w start goes into the (non-negative) voffset:
       // the range check must see the lane's real offset
       const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
-      const int wrun = 32 * wr * a.Cg * 4;
+      const int wrun = 32 * wr * a.Cg * ESG;
       const bool w_edge = wr == 0;                                   // fine voxel −1 is outside
+      if constexpr (X16G) {
+        const bool ok8 = rok && g8 && !(w_edge && q8 == 0);
+        rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, ok8 ? glane_al8 + wrun : (int)kOobOffset, gso));
+        continue;
+      }
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass) {
         const int q = pass * GP + gq;
@@ -201,7 +216,13 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
       const int gd = 2 * d - 1 + kd, gh = 2 * h - 1 + kh;
       const bool rok = ok && (unsigned)gd < (unsigned)Dg && (unsigned)gh < (unsigned)Hg;
-      const int gso = __builtin_amdgcn_readfirstlane(rok ? ((n * Dg + gd) * Hg + gh) * Wg * a.Cg * 4 : 0);
+      const int gso = __builtin_amdgcn_readfirstlane(rok ? ((n * Dg + gd) * Hg + gh) * Wg * a.Cg * ESG : 0);
+      if constexpr (X16G) {
+        const int p = 2 * w0 - 1 + q8;
+        const bool pok = rok && g8 && (unsigned)p < (unsigned)Wg;
+        rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, pok ? (p * a.Cg + gn0 + 8 * go) * 2 : (int)kOobOffset, gso));
+        continue;
+      }
       auto gload = [&](int q) __attribute__((always_inline)) {
         const int p = 2 * w0 - 1 + q;
         const bool pok = rok && (unsigned)p < (unsigned)Wg;
@@ -242,9 +263,23 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       *reinterpret_cast<uint2*>(base + row * RB + 16 * ((c >> 1) ^ tr_swz<RB>(row)) + 8 * (c & 1)) = h;
     }
   };
+  // X16G: unit (slot, octet o) → rows slot·8 + r, the 16 B at chunk o (swizzled)
+  auto put8 = [&](char* base, int slot, int o, const uint4 (&v)[X16G ? kR : 1]) __attribute__((always_inline)) {
+    if constexpr (X16G) {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int row = slot * kR + r;
+        *reinterpret_cast<uint4*>(base + row * RBG + 16 * (o ^ tr_swz<RBG>(row))) = v[r];
+      }
+    }
+  };
   auto store = [&]() __attribute__((always_inline)) {
     if constexpr (kTr) {
       put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+      if constexpr (X16G) {
+        if (g8) put8(Gs, gslot(q8), go, rg8);
+        return;
+      }
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass)
         put16(Gs, std::integral_constant<int, RBG>{}, gslot(pass * GP + gq), gcq, rg[pass]);
@@ -417,15 +452,25 @@ int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TG, int PM, int AL>
-static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, hipStream_t st) {
+template <int TG, int PM, int AL, int X16G>
+static void launch_w3s2_as(const Wgrad3s2Args& a, int blocks, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL, X16G>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL>), dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL, X16G>), dim3(blocks), dim3(256), lds, st, a);
+}
+
+template <int TG, int PM, int AL>
+static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, bool g16, hipStream_t st) {
+  if constexpr (prec::has_lo<PM>()) {
+    launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);      // (g16 rejected by the caller)
+  } else {
+    if (g16) launch_w3s2_as<TG, PM, AL, 1>(a, blocks, lds, st);
+    else launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);
+  }
 }
 
 int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
@@ -447,13 +492,17 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
   static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
+  if (g.in16g && g.x3 != kPrecBf16 && g.x3 != kPrecF16) {
+    set_error("wgrad3s2_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
+    return -kBadArg;
+  }
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
-      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, st);
-      else launch_w3s2<64, PM, 0>(a, blocks, lds, st);
+      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, g.in16g != 0, st);
+      else launch_w3s2<64, PM, 0>(a, blocks, lds, g.in16g != 0, st);
     } else {
-      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, st);
-      else launch_w3s2<32, PM, 0>(a, blocks, lds, st);
+      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, g.in16g != 0, st);
+      else launch_w3s2<32, PM, 0>(a, blocks, lds, g.in16g != 0, st);
     }
     return nsplit;
   })

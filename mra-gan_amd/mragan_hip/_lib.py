@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -83,6 +83,9 @@ SIGNATURES = {
                                  vp, sz, vp, vp]),
     "mragan_conv3d_wgrad_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
                                        sz, vp]),
+    # ABI 14: stride-2 weight gradient with a 16-bit gathered operand
+    "mragan_conv3d_wgrad_g16": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp,
+                                      sz, vp]),
     "mragan_conv3d_op16_dgrad_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, sz, vp, vp, vp, i32,
                                                 vp, sz, vp, vp]),
     "mragan_instnorm_bwd_partials_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32,

@@ -33,6 +33,8 @@ _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None   
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
+# A/B switch: MRAGAN_NO_S2_PLANES keeps the stem / down1 InstanceNorm outputs in fp32 (no ABI 14 planes)
+_NO_S2_PLANES = __import__("os").environ.get("MRAGAN_NO_S2_PLANES") is not None
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
 _FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") or "0"))
                # the library's A/B switches that send those convs to the fp32-pack kernels
@@ -209,6 +211,17 @@ class ConvLayer:
                                           norm_x, mean, rstd, act, part, transposed=not self.transposed)
         return dz, part, chunks
 
+    def wgrad_g16(self, x16, dy, accumulate=True):
+        """wgrad of a forward-form k3 s2 conv whose input exists only as its operand plane (ABI 14)."""
+        ops.conv3d_wgrad_g16(dy, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
+
+    def s2_plane_ok(self, W_in):
+        """A forward-form k3 s2 p1 conv (G down1 / down2) that can read its input of width W_in as
+        an operand plane: the implicit GEMM (Cin % 32) forward and wgrad3s2 (Cout % 64, coarse row
+        segments of 16 voxels) weight gradient."""
+        return (not self.transposed and self.k == 3 and self.s == 2 and self.p == 1 and self.cin % 32 == 0
+                and self.cout % 64 == 0 and W_in % 32 == 0)
+
     def wgrad(self, x, dy, accumulate=True):
         g = self.m.weight.grad
         if not self.transposed:
@@ -348,8 +361,19 @@ class NetPlan:
                 bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
                 if st.norm is not None:
                     # the conv's epilogue leaves the norm's statistics partials where it can
-                    sc.h, part, chunks = st.conv.forward_in_stats(cur)
-                    if want16 and self._op16_blocks_ok(sc.h.shape[3], sc.h.shape[2]):
+                    if cur is None:                  # the input exists only as its plane (only16 below)
+                        sc.h, part, chunks = st.conv.forward_in_stats_op16(cur16)
+                    else:
+                        sc.h, part, chunks = st.conv.forward_in_stats(cur)
+                    # a stride-2 forward conv next (G down1 / down2): this norm's output only as its
+                    # plane — that conv and its weight gradient are its only readers (ABI 14)
+                    nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
+                    only16 = (op16 and not _NO_S2_PLANES and ypad == 0 and nxt is not None and nxt.kind != "block"
+                              and nxt.norm is not None and not nxt.prepad and nxt.conv.s2_plane_ok(sc.h.shape[3]))
+                    if only16:
+                        _, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=0, part=part,
+                                                                           chunks=chunks)
+                    elif want16 and self._op16_blocks_ok(sc.h.shape[3], sc.h.shape[2]):
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad,
                                                                                 part=part, chunks=chunks,
                                                                                 want_f32=True)
@@ -439,8 +463,12 @@ class NetPlan:
                     srcs = [g, gadd]
                 dh = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                 ops.act_bwd(sc.h, srcs, st.act, dh)
+            in_spatial = (sc.inp if sc.inp is not None else sc.inp16).shape[1:4]
             if need_wgrad:
-                conv.wgrad(sc.inp, dh)
+                if sc.inp is None:
+                    conv.wgrad_g16(sc.inp16, dh)        # the input exists only as its plane
+                else:
+                    conv.wgrad(sc.inp, dh)
                 if st.use_bias and conv.m.bias is not None:
                     ops.channel_sum(dh, conv.m.bias.grad, accumulate=True)
             bstats = None
@@ -451,7 +479,7 @@ class NetPlan:
                     # the G head: its data gradient also accumulates the last up-conv IN's backward
                     # statistics (the pad-3 statistics pass over dz and x goes)
                     nsc = ctx.stages[i - 1]
-                    g, bpart, bchunks = conv.dgrad_in_stats(dh, sc.inp.shape[1:4], nsc.h, nsc.mean, nsc.rstd, nxt.act,
+                    g, bpart, bchunks = conv.dgrad_in_stats(dh, in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act,
                                                             st.prepad)
                     bstats = (bpart, bchunks) if bchunks else None
                 elif (nxt is not None and nxt.kind != "block" and nxt.norm is not None and not st.prepad
@@ -459,10 +487,10 @@ class NetPlan:
                     # stride-2 layers: the data gradient's epilogue accumulates the next IN's
                     # backward statistics (no fold: that IN's output is this conv's input)
                     nsc = ctx.stages[i - 1]
-                    g, bpart, bchunks = conv.dgrad_bwd_stats(dh, sc.inp.shape[1:4], nsc.h, nsc.mean, nsc.rstd, nxt.act)
+                    g, bpart, bchunks = conv.dgrad_bwd_stats(dh, in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act)
                     bstats = (bpart, bchunks) if bchunks else None
                 else:
-                    g = conv.dgrad(dh, sc.inp.shape[1:4])
+                    g = conv.dgrad(dh, in_spatial)
                 gpad, gadd = st.prepad, None
         if not need_input_grad:
             return None

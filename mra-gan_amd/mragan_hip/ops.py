@@ -441,15 +441,16 @@ def instnorm_bwd_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, d
 
 def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
                 wsplit: torch.Tensor, part: Optional[torch.Tensor] = None, transposed: bool = False):
-    """conv3d (pre-split weights, no bias / act) on the operand plane x16 of its input (the k3 s1
-    brick kernel); with `part` also the InstanceNorm statistics partials.  Returns (out, chunks)."""
+    """conv3d (pre-split weights if any, no bias / act) on the operand plane x16 of its input (the
+    k3 s1 brick kernel; the implicit GEMM for other forward-form convs, ABI 14); with `part` also the
+    InstanceNorm statistics partials.  Returns (out, chunks)."""
     _check16(x16, "conv3d_op16.x16")
     N, Di, Hi, Wi, cin = x16.shape
     Do, Ho, Wo = out_spatial
     if wp.numel() != k ** 3 * cin * cout:
         raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
-    if wsplit is None or wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-        raise ValueError("conv3d_op16: wsplit missing or its size does not match the packed weight")
+    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("conv3d_op16: wsplit size does not match the packed weight")
     if part is not None and (part.dtype != torch.float64 or not part.is_cuda):
         raise ValueError("conv3d_op16: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
@@ -605,6 +606,26 @@ def conv3d_wgrad_op16(dense16: torch.Tensor, gathered16: torch.Tensor, k: int, s
     nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
     ws = WS.get(nbytes)
     fn = lambda: call("mragan_conv3d_wgrad_op16", _ptr(dense16), N, Dd, Hd, Wd, Cd, _ptr(gathered16), Dg, Hg, Wg, Cg,
+                      k, s, p, _ptr(dw), int(accumulate), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
+                        flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)
+    return dw
+
+
+def conv3d_wgrad_g16(dense: torch.Tensor, gathered16: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
+                     accumulate: bool) -> torch.Tensor:
+    """conv3d_wgrad (k3 s2 p1) with the gathered operand as its 16-bit plane, dense fp32 (ABI 14)."""
+    _check(dense, "wgrad_g16.dense")
+    _check16(gathered16, "wgrad_g16.gathered")
+    N, Dd, Hd, Wd, Cd = dense.shape
+    Ng, Dg, Hg, Wg, Cg = gathered16.shape
+    if Ng != N:
+        raise ValueError("wgrad: batch mismatch")
+    if dw.numel() != Cd * Cg * k ** 3 or not dw.is_contiguous():
+        raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
+    nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_conv3d_wgrad_g16", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered16), Dg, Hg, Wg, Cg,
                       k, s, p, _ptr(dw), int(accumulate), _ptr(ws), ws.numel(), _stream())
     _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}]",
                         flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)

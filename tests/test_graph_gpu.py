@@ -12,7 +12,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(tmp_path, graph, steps, precision, batches=None, extra=()):
+def _run(tmp_path, graph, steps, precision, batches=None, extra=(), size=24):
     from models import create_model
     from options.train_options import TrainOptions
     argv = sys.argv
@@ -34,8 +34,8 @@ def _run(tmp_path, graph, steps, precision, batches=None, extra=()):
     losses = []
     for step in range(steps):
         b = batches[step] if batches else 2
-        A = torch.randn(b, 1, 24, 24, 24, generator=g)
-        B = torch.randn(b, 1, 24, 24, 24, generator=g)
+        A = torch.randn(b, 1, size, size, size, generator=g)
+        B = torch.randn(b, 1, size, size, size, generator=g)
         model.set_input([A, B])
         model.optimize_parameters()
         losses.append(torch.stack([getattr(model, "loss_" + n).detach().clone() for n in model.loss_names]))
@@ -86,3 +86,30 @@ def test_graph_step_changing_batch_and_no_identity(tmp_path):
         assert torch.equal(se[k], sg[k]), k
     for k in ve:
         assert torch.equal(ve[k], vg[k]), k
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
+    """ABI 14: in the one-plane modes the stem's InstanceNorm output (G down1's input) exists only as
+    its 16-bit operand plane; down1's forward and weight gradient read the plane.  The step must
+    agree bit for bit with the step that keeps that tensor in fp32 (the kernels round it to the very
+    same words) — and the plane path must actually have run."""
+    from mragan_hip import engine, ops
+    calls = []
+    wg = engine.ConvLayer.wgrad_g16
+    monkeypatch.setattr(engine.ConvLayer, "wgrad_g16", lambda self, *a, **k: (calls.append(1), wg(self, *a, **k)))
+    extra = ["--ngf", "32"]
+    try:
+        monkeypatch.setattr(engine, "_NO_S2_PLANES", True)
+        lr, sr, vr, _ = _run(tmp_path / "r", False, 3, precision, extra=extra, size=32)
+        assert not calls
+        monkeypatch.setattr(engine, "_NO_S2_PLANES", False)
+        lp, sp, vp, _ = _run(tmp_path / "p", False, 3, precision, extra=extra, size=32)
+    finally:
+        ops.set_conv_precision("f32")
+    assert calls, "the stride-2 plane path did not run"
+    assert torch.equal(lr, lp), (lr - lp).abs().max()
+    for k in sr:
+        assert torch.equal(sr[k], sp[k]), k
+    for k in vr:
+        assert torch.equal(vr[k], vp[k]), k

@@ -547,6 +547,55 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
+@pytest.mark.parametrize("N,cin,cout,dims", [(2, 32, 64, (32, 32, 32)), (1, 64, 128, (16, 16, 32)),
+                                              (1, 32, 64, (8, 12, 64))])
+def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
+    """ABI 14: G down1 / down2 (Conv3d k3 s2 p1) on the operand plane of their input — the implicit
+    GEMM's 16-bit A tiles (forward, with its InstanceNorm partials) and wgrad3s2's 16-bit gathered
+    operand — equal the same kernels on the fp32 tensor in the same mode bit for bit."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 7 + cin + cout + dims[2])
+    D, H, W = dims
+    x16 = ndhwc(torch.randn(N, cin, D, H, W, generator=g).float()).cuda().to(dt)
+    x = x16.float()
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_f = pack(ops, w, False, False)
+    osp = (D // 2, H // 2, W // 2)
+    part_ref = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y_ref, ch_ref = ops.conv3d_in_stats(x, wp_f, cout, 3, 2, 1, osp, None, part_ref)
+    part = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y, ch = ops.conv3d_op16(x16, wp_f, cout, 3, 2, 1, osp, None, part)
+    assert ch == ch_ref
+    assert torch.equal(y, y_ref)
+    n = N * ch * cout * 2
+    assert torch.equal(part[:n], part_ref[:n])
+    dy = ndhwc(torch.randn(N, cout, *osp, generator=g).float()).cuda()
+    gw_ref = torch.empty(cout * cin * 27, device="cuda")
+    ops.conv3d_wgrad(dy, x, 3, 2, 1, gw_ref, False)
+    gw = torch.full_like(gw_ref, float("nan"))
+    ops.conv3d_wgrad_g16(dy, x16, 3, 2, 1, gw, False)
+    assert torch.equal(gw, gw_ref)
+    # and against fp64 on the rounded operands (the mode's definition)
+    gw64 = torch.nn.grad.conv3d_weight(ncdhw(x.double().cpu()), (cout, cin, 3, 3, 3),
+                                       ncdhw(dy.to(dt).double().cpu()), stride=2, padding=1)
+    assert rel(gw.view(cout, cin, 3, 3, 3), gw64) < 2e-5
+
+
+def test_op16_stride2_plane_rejected_outside_one_plane_modes(ops):
+    """ABI 14: the 16-bit gathered operand of wgrad3s2 exists only in the bf16 / fp16 modes."""
+    from mragan_hip import MraganError
+    ops.set_conv_precision("bf16x3")
+    try:
+        x16 = torch.zeros(1, 16, 16, 32, 32, device="cuda", dtype=torch.bfloat16)
+        dy = torch.zeros(1, 8, 8, 16, 64, device="cuda")
+        gw = torch.empty(64 * 32 * 27, device="cuda")
+        with pytest.raises((MraganError, ValueError)):
+            ops.conv3d_wgrad_g16(dy, x16, 3, 2, 1, gw, False)
+    finally:
+        ops.set_conv_precision("f32")
+
+
 @pytest.mark.parametrize("N,C,S,W,act", [(2, 128, 16, 16, "relu"), (1, 64, 9, 16, "relu"), (1, 128, 5, 32, "lrelu"),
                                           (2, 64, 6, 16, None)])
 def test_op16_dgrad_backward_statistics(op16, N, C, S, W, act):
