@@ -132,13 +132,18 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int gcq = tid % GQ, gq = tid / GQ;
   const int gqx = GPASS * GP + gq;                 // the remainder pass (q = 32 …)
   const bool gx = gqx < kGPos;
-  // X16G units: (q8 = tid / GO, octet go = tid % GO): one pass covers the 33 positions (TG ≤ 64)
+  // X16G units: (q8 = tid / GO, octet go = tid % GO); TG 32: one pass covers the 33 positions,
+  // TG 64: 32 of them, the last one (q8x = 32) on the first GO threads (wave 0 only: the other
+  // waves branch round it)
   constexpr int GO = TG / 8;
   const int go = tid % GO, q8 = tid / GO;
   const bool g8 = q8 < kGPos;
+  constexpr bool kG8X = X16G && 256 / GO < kGPos;
+  const int q8x = 256 / GO + q8;
+  const bool g8x = kG8X && q8x < kGPos;
 
   float4 rd[kR], rg[2][kR], rgx[kR];
-  uint4 rg8[X16G ? kR : 1];
+  uint4 rg8[X16G ? kR : 1], rg8x[kG8X ? kR : 1];
   // D / G rows through buffer descriptors: segment / row parts of the offsets are wave-uniform
   // (SGPR soffset); out-of-range rows and positions read zeros through an out-of-range voffset
   // (no select on the loaded values, no 64-bit address arithmetic)
@@ -160,6 +165,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int glane_al = ((gq - 1) * a.Cg + gn0 + 4 * gcq) * 4;      // fine voxel q − 1 of a run
   const int glane_alx = (((gx ? gqx : gq) - 1) * a.Cg + gn0 + 4 * gcq) * 4;
   const int glane_al8 = ((q8 - 1) * a.Cg + gn0 + 8 * go) * 2;      // X16G: octet go of fine voxel q8 − 1
+  const int glane_al8x = ((q8x - 1) * a.Cg + gn0 + 8 * go) * 2;
   auto load_al = [&](int st) __attribute__((always_inline)) {
     // stage base: (sn, sd, sh) is its first row (sw = 0)
     const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
@@ -182,6 +188,8 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       if constexpr (X16G) {
         const bool ok8 = rok && g8 && !(w_edge && q8 == 0);
         rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, ok8 ? glane_al8 + wrun : (int)kOobOffset, gso));
+        if constexpr (kG8X)
+          if (g8x) rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, rok ? glane_al8x + wrun : (int)kOobOffset, gso));
         continue;
       }
 #pragma unroll
@@ -221,6 +229,13 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         const int p = 2 * w0 - 1 + q8;
         const bool pok = rok && g8 && (unsigned)p < (unsigned)Wg;
         rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, pok ? (p * a.Cg + gn0 + 8 * go) * 2 : (int)kOobOffset, gso));
+        if constexpr (kG8X) {
+          if (g8x) {
+            const int px = 2 * w0 - 1 + q8x;
+            const bool pokx = rok && (unsigned)px < (unsigned)Wg;
+            rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, pokx ? (px * a.Cg + gn0 + 8 * go) * 2 : (int)kOobOffset, gso));
+          }
+        }
         continue;
       }
       auto gload = [&](int q) __attribute__((always_inline)) {
@@ -264,7 +279,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
     }
   };
   // X16G: unit (slot, octet o) → rows slot·8 + r, the 16 B at chunk o (swizzled)
-  auto put8 = [&](char* base, int slot, int o, const uint4 (&v)[X16G ? kR : 1]) __attribute__((always_inline)) {
+  auto put8 = [&](char* base, int slot, int o, const uint4 (&v)[kR]) __attribute__((always_inline)) {
     if constexpr (X16G) {
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
@@ -278,6 +293,8 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
       if constexpr (X16G) {
         if (g8) put8(Gs, gslot(q8), go, rg8);
+        if constexpr (kG8X)
+          if (g8x) put8(Gs, gslot(q8x), go, rg8x);
         return;
       }
 #pragma unroll

@@ -90,24 +90,25 @@ def test_graph_step_changing_batch_and_no_identity(tmp_path):
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
 def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
-    """ABI 14: in the one-plane modes the stem's InstanceNorm output (G down1's input) exists only as
-    its 16-bit operand plane; down1's forward and weight gradient read the plane.  The step must
+    """ABI 14: in the one-plane modes the stem's and down1's InstanceNorm outputs (G down1's and
+    down2's inputs; 64³: 32- and 64-channel planes, both wgrad3s2 tile widths) exist only as 16-bit
+    operand planes; the stride-2 convs' forwards and weight gradients read the planes.  The step must
     agree bit for bit with the step that keeps that tensor in fp32 (the kernels round it to the very
     same words) — and the plane path must actually have run."""
     from mragan_hip import engine, ops
     calls = []
     wg = engine.ConvLayer.wgrad_g16
-    monkeypatch.setattr(engine.ConvLayer, "wgrad_g16", lambda self, *a, **k: (calls.append(1), wg(self, *a, **k)))
+    monkeypatch.setattr(engine.ConvLayer, "wgrad_g16", lambda self, *a, **k: (calls.append(self.cin), wg(self, *a, **k)))
     extra = ["--ngf", "32"]
     try:
         monkeypatch.setattr(engine, "_NO_S2_PLANES", True)
-        lr, sr, vr, _ = _run(tmp_path / "r", False, 3, precision, extra=extra, size=32)
+        lr, sr, vr, _ = _run(tmp_path / "r", False, 3, precision, extra=extra, size=64)
         assert not calls
         monkeypatch.setattr(engine, "_NO_S2_PLANES", False)
-        lp, sp, vp, _ = _run(tmp_path / "p", False, 3, precision, extra=extra, size=32)
+        lp, sp, vp, _ = _run(tmp_path / "p", False, 3, precision, extra=extra, size=64)
     finally:
         ops.set_conv_precision("f32")
-    assert calls, "the stride-2 plane path did not run"
+    assert set(calls) == {32, 64}, f"the stride-2 plane path did not run for both layers: {set(calls)}"
     assert torch.equal(lr, lp), (lr - lp).abs().max()
     for k in sr:
         assert torch.equal(sr[k], sp[k]), k

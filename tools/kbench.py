@@ -88,7 +88,13 @@ def main():
         h1_res = rnd(N, s4, s4, s4, c4)
         _, m_res, r_res = ops.instnorm_fwd(h1_res, act="relu", ypad=1)
         part_bs = ops.in_partials_buffer(N, (s4 + 2,) * 3, c4, dev)
+        # G down1 / down2 on the planes of their inputs (ABI 14)
+        x_dn1_16, x_dn2_16 = x_dn1.to(dt16), x_dn2.to(dt16)
     table = {
+        "down1_fwd16": lambda: ops.conv3d_op16(x_dn1_16, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2), None),
+        "down2_fwd16": lambda: ops.conv3d_op16(x_dn2_16, w_dn2, c4, 3, 2, 1, (s4, s4, s4), None),
+        "down1_wgrad16": lambda: ops.conv3d_wgrad_g16(dy_dn1, x_dn1_16, 3, 2, 1, gw_dn1, False),
+        "down2_wgrad16": lambda: ops.conv3d_wgrad_g16(dy_dn2, x_dn2_16, 3, 2, 1, gw_dn2, False),
         "res_fwd16": lambda: ops.conv3d_op16(x_res16, w_res, c4, 3, 1, 0, (s4, s4, s4), ws_res_f, part_res),
         "res_dgrad16": lambda: ops.conv3d_op16(dy_res16, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, ws_res_b, transposed=True),
         "res_wgrad16": lambda: ops.conv3d_wgrad_op16(dy_res16, x_res16, 3, 1, 0, gw_res, False),
