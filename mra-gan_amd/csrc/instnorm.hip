@@ -55,39 +55,41 @@ size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
 }
 
 // Σ over chunks of partials[n][chunk][C][2] in fixed order (deterministic).  Block = 4
-// channels × 64 chunk rows; grid (ceil(C/4), N): each thread sums ≤ chunks/64 partials with its
-// loads in flight together (16 rows × 32 sequential partials took ~5 µs of dependent latency).
+// channels × 64 chunk rows, one wave per channel; grid (ceil(C/4), N): each lane sums ≤ chunks/64
+// partials with its loads in flight together, then a fixed xor butterfly over the wave's 64 lanes
+// (lane 0's result: the same association every launch).  The 64 row sums were combined by one
+// thread per channel through LDS before: 64 dependent LDS round trips, most of a 4.8 µs launch
+// (r04i trace, ≈ 250 of these per 64³ b2 step).
 // mode 0: mean / rstd (out0, out1); mode 1: backward coefficients (out0 = coef[2C]).
 __device__ void in_finalize_group(const double* __restrict__ part, const InShape& s, int chunks, int n, int cgroup,
                                   int mode, float* __restrict__ out0, float* __restrict__ out1) {
-  __shared__ double fr[2][256];
   constexpr int CW = 4, ROWS = 64;
-  const int tid = threadIdx.x, cl = tid % CW, row = tid / CW;
+  const int tid = threadIdx.x, cl = tid / ROWS, row = tid % ROWS;
   const int c = cgroup * CW + cl;
+  if (c >= s.C) return;                          // wave-uniform: the wave's channel
   double sa = 0, sb = 0;
-  if (c < s.C) {
 #pragma unroll 8
-    for (int k = row; k < chunks; k += ROWS) {
-      const double2 p = *reinterpret_cast<const double2*>(part + (((int64_t)n * chunks + k) * s.C + c) * 2);
-      sa += p.x; sb += p.y;
-    }
+  for (int k = row; k < chunks; k += ROWS) {
+    const double2 p = *reinterpret_cast<const double2*>(part + (((int64_t)n * chunks + k) * s.C + c) * 2);
+    sa += p.x; sb += p.y;
   }
-  fr[0][tid] = sa; fr[1][tid] = sb;
-  __syncthreads();
-  if (row == 0 && c < s.C) {
-    double a = 0, b = 0;
-    for (int r = 0; r < ROWS; ++r) { a += fr[0][r * CW + cl]; b += fr[1][r * CW + cl]; }
+#pragma unroll
+  for (int off = ROWS / 2; off >= 1; off >>= 1) {
+    sa += __shfl_xor(sa, off);
+    sb += __shfl_xor(sb, off);
+  }
+  if (row == 0) {
     const double S = (double)s.S();
     const int i = n * s.C + c;
     if (mode == 0) {
-      const double mu = a / S;
-      double var = b / S - mu * mu;
+      const double mu = sa / S;
+      double var = sb / S - mu * mu;
       if (var < 0) var = 0;
       out0[i] = (float)mu;
       out1[i] = (float)(1.0 / sqrt(var + (double)kInEps));
     } else {
-      out0[2 * i] = (float)(a / S);
-      out0[2 * i + 1] = (float)(b / S);
+      out0[2 * i] = (float)(sa / S);
+      out0[2 * i + 1] = (float)(sb / S);
     }
   }
 }
