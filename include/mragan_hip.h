@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 14
+#define MRAGAN_ABI_VERSION 15
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -205,6 +205,32 @@ int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const f
                                       int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
                                       float* g_out, const double* part, int chunks, void* ws, size_t ws_bytes,
                                       void* stream);
+/* ABI 15: InstanceNorm statistics finalized inside the producing conv ("last block done"; VERDICT
+ * r03 item 5).  The _fin forms take, besides the partials, `tickets` — N·cout/32 uint32 counters,
+ * zero on entry, that no kernel which may run at the same time uses (the launch leaves them zero:
+ * hand them out round-robin from one zeroed pool) — and the statistics outputs.  When the kernel
+ * that runs the conv finalizes in-launch (the K-split brick, bf16 / fp16, a multiple of 128
+ * contraction channels, one round of CU slots), *finalized = 1 and mean / rstd ([N][cout]) — or,
+ * for the data gradient, coef ([N][cout][2] = mean(g), mean(g·x̂), the IN backward's two
+ * coefficients) — are written; then the apply-only entries below replace
+ * mragan_instnorm_fwd_partials_op16 / mragan_instnorm_bwd_partials_op16 (no finalize launch).
+ * Otherwise *finalized = 0 and the partials are left as by the non-_fin form.  The in-launch sums
+ * run in a different fixed order than the finalize kernel's: deterministic, equal to ~1e-16
+ * relative. */
+int mragan_conv3d_op16_fin(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, const void* wsplit,
+                           int cout, int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed,
+                           void* ws, size_t ws_bytes, double* part, size_t part_bytes, int* chunks, unsigned* tickets,
+                           float* mean, float* rstd, int* finalized, void* stream);
+int mragan_conv3d_op16_dgrad_in_stats_fin(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                                          const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes,
+                                          const float* x_in, const float* mean, const float* rstd, int act, double* part,
+                                          size_t part_bytes, int* chunks, unsigned* tickets, float* coef, int* finalized,
+                                          void* stream);
+int mragan_instnorm_apply_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
+                               const float* resid, int rpad, const float* mean, const float* rstd, void* stream);
+int mragan_instnorm_bwd_apply_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,
+                                   int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
+                                   float* g_out, const float* coef, void* stream);
 /* The same for the G head (ABI 12; networks3D.py:211-213): the head conv (ngf → 1, k7 p0) reads
  * ReplicationPad3d(3)(relu(IN(x))) of the last up-conv's output x.  mragan_conv3d_dgrad_in_stats
  * is its data gradient — the transposed form (stride 1, pad 0) of the packed weight, output

@@ -143,10 +143,33 @@ static int op16_mode_ok() {
   return kOk;
 }
 
+static int conv3d_op16_impl(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit,
+                            int cout, int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed,
+                            void* ws, size_t ws_bytes, double* part, size_t part_bytes, int* chunks, unsigned* tickets,
+                            float* mean, float* rstd, int* finalized, void* stream);
+
 int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit, int cout,
                        int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
                        size_t ws_bytes, double* part, size_t part_bytes, int* chunks, void* stream) {
+  return conv3d_op16_impl(x16, N, Di, Hi, Wi, cin, w, wsplit, cout, k, stride, pad, y, Do, Ho, Wo, transposed, ws,
+                          ws_bytes, part, part_bytes, chunks, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int mragan_conv3d_op16_fin(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit,
+                           int cout, int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed,
+                           void* ws, size_t ws_bytes, double* part, size_t part_bytes, int* chunks, unsigned* tickets,
+                           float* mean, float* rstd, int* finalized, void* stream) {
+  MRAGAN_CHECK_ARG(part && chunks && tickets && mean && rstd && finalized, "conv3d_op16_fin: null pointer");
+  return conv3d_op16_impl(x16, N, Di, Hi, Wi, cin, w, wsplit, cout, k, stride, pad, y, Do, Ho, Wo, transposed, ws,
+                          ws_bytes, part, part_bytes, chunks, tickets, mean, rstd, finalized, stream);
+}
+
+static int conv3d_op16_impl(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const void* wsplit,
+                            int cout, int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed,
+                            void* ws, size_t ws_bytes, double* part, size_t part_bytes, int* chunks, unsigned* tickets,
+                            float* mean, float* rstd, int* finalized, void* stream) {
   if (int rc = op16_mode_ok()) return rc;
+  if (finalized) *finalized = 0;
   MRAGAN_CHECK_ARG(x16 && w && y, "conv3d_op16: null pointer");   // wsplit: optional (the brick packs per call)
   MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_op16: transposed must be 0/1");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && Do > 0 && Ho > 0 && Wo > 0,
@@ -161,14 +184,39 @@ int mragan_conv3d_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, 
   IgemmArgs a{static_cast<const float*>(x16), w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad,
               transposed, kActNone, 1, g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
   a.x16 = 1;
+  if (part && tickets) { a.in_tick = tickets; a.in_fin0 = mean; a.in_fin1 = rstd; a.in_finalized = finalized; }
   return conv_igemm(a, static_cast<hipStream_t>(stream));
 }
+
+static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                    const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
+                                    const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream);
 
 int mragan_conv3d_op16_dgrad_in_stats(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
                                       const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
                                       const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
                                       int* chunks, void* stream) {
+  return op16_dgrad_in_stats_impl(dy16, N, Di, Hi, Wi, cin, w, wsplit, cout, y, ws, ws_bytes, x_in, mean, rstd, act,
+                                  part, part_bytes, chunks, nullptr, nullptr, nullptr, stream);
+}
+
+int mragan_conv3d_op16_dgrad_in_stats_fin(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                          const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes,
+                                          const float* x_in, const float* mean, const float* rstd, int act, double* part,
+                                          size_t part_bytes, int* chunks, unsigned* tickets, float* coef, int* finalized,
+                                          void* stream) {
+  MRAGAN_CHECK_ARG(tickets && coef && finalized, "conv3d_op16_dgrad_in_stats_fin: null pointer");
+  return op16_dgrad_in_stats_impl(dy16, N, Di, Hi, Wi, cin, w, wsplit, cout, y, ws, ws_bytes, x_in, mean, rstd, act,
+                                  part, part_bytes, chunks, tickets, coef, finalized, stream);
+}
+
+static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                    const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
+                                    const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
+                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream) {
   if (int rc = op16_mode_ok()) return rc;
+  if (finalized) *finalized = 0;
   MRAGAN_CHECK_ARG(dy16 && w && wsplit && y && x_in && mean && rstd && part && chunks,
                    "conv3d_op16_dgrad_in_stats: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && !thin_side(cin, cout),
@@ -182,7 +230,26 @@ int mragan_conv3d_op16_dgrad_in_stats(const void* dy16, int N, int Di, int Hi, i
               1, g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
   a.x16 = 1;
   a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act;
+  if (tickets) { a.in_tick = tickets; a.in_fin0 = coef; a.in_fin1 = nullptr; a.in_finalized = finalized; }
   return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
+int mragan_instnorm_apply_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
+                               const float* resid, int rpad, const float* mean, const float* rstd, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && (y || y16) && mean && rstd, "instnorm_apply_op16: null pointer");
+  return instnorm_apply(x, InShape{N, D, H, W, C}, y, ypad, act, resid, rpad, mean, rstd,
+                        static_cast<hipStream_t>(stream), y16, g_conv_precision);
+}
+
+int mragan_instnorm_bwd_apply_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,
+                                   int C, const float* dy, int dypad, const float* dy_add, int act, void* dx16,
+                                   float* g_out, const float* coef, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x && mean && rstd && dy && dx16 && coef, "instnorm_bwd_apply_op16: null pointer");
+  MRAGAN_CHECK_ARG(!g_out || (g_out != dy && g_out != dy_add), "instnorm_bwd_apply_op16: g_out aliases an operand");
+  InBwdArgs a{x, mean, rstd, dy, dypad, dy_add, act, nullptr, g_out, dx16, g_conv_precision};
+  return instnorm_bwd_apply(a, InShape{N, D, H, W, C}, coef, static_cast<hipStream_t>(stream));
 }
 
 int mragan_instnorm_bwd_partials_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,

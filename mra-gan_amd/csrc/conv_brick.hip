@@ -413,6 +413,13 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
   if (conv_brick_ks_applicable(g)) {
     BrickArgs k = a;
     if (g.in_part) k.part = g.in_part;
+    if (g.in_part && g.in_tick) {
+      // finalize in the launch (ABI 15): forward statistics of the output, or the backward
+      // coefficients of the InstanceNorm in front (its tensor: the input grid, output − 2)
+      k.tick = g.in_tick; k.fin0 = g.in_fin0; k.fin1 = g.in_fin1; k.finalized = g.in_finalized;
+      k.fin_mode = g.bs_x ? 1 : 0;
+      k.fin_S = g.bs_x ? (double)g.Di * g.Hi * g.Wi : (double)g.Do * g.Ho * g.Wo;
+    }
     const int rc = conv_brick_ks(k, g.ny, g.ws, g.ws_bytes, g.wx3, g.x3, g.in_chunks, st);
     if (rc != kUnsupported) return rc;   // kUnsupported: no K-split variant fits one round of CU slots
   }

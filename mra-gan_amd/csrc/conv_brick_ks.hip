@@ -37,6 +37,7 @@
 // of one voxel: 16-B output stores (the 4-B column stores of the MFMA layout were store-issue bound:
 // 11.8 k cycles of a 48 k-cycle wave, r04b) and 16-B loads of the backward-statistics operand.
 #include "conv_geo.h"
+#include "in_ticket.h"
 #include "kernels.h"
 #include "prec.h"
 
@@ -510,9 +511,17 @@ conv_brick_ks_kernel(BrickArgs a) {
         q2 += red2[(w * BN + c) * 2 + 1];
       }
       double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + n0 + c) * 2;
-      dst[0] = s2;
-      dst[1] = q2;
+      if (a.tick) {                     // write-through: the tile's reducer reads them (in_ticket.h)
+        st_sc1(dst, s2);
+        st_sc1(dst + 1, q2);
+      } else {
+        dst[0] = s2;
+        dst[1] = q2;
+      }
     }
+    // ABI 15: the last block of this (instance, column tile) finalizes the tile's statistics
+    if (a.tick && in_ticket_draw(a.tick + nb * a.gn + nbk, chunks, reinterpret_cast<int*>(region)))
+      in_ticket_reduce<BN>(a.part, chunks, a.ny, nb, n0, a.fin_mode, a.fin_S, a.fin0, a.fin1);
   }
   KS_STAMP(6);
 }
@@ -632,6 +641,8 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
   a.stamp = stamps;
   if (in_chunks && a.part) *in_chunks = a.nbd * a.nbh * a.nbw;
+  if (a.tick && !a.part) a.tick = nullptr;
+  if (a.tick && a.finalized) *a.finalized = 1;   // the launch below finalizes (in_ticket.h)
   if (a.ntiles == 0) return kOk;
   brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, kKsBM, a.rowvox);
   MRAGAN_PREC_DISPATCH(mode, return brick_ks_launch_pm<PM>(a, V.tn, V.db, ws, ws_bytes, wsplit, st))

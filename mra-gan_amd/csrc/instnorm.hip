@@ -61,6 +61,41 @@ size_t instnorm_ws_bytes(int N, int D, int H, int W, int C) {
 // thread per channel through LDS before: 64 dependent LDS round trips, most of a 4.8 µs launch
 // (r04i trace, ≈ 250 of these per 64³ b2 step).
 // mode 0: mean / rstd (out0, out1); mode 1: backward coefficients (out0 = coef[2C]).
+__device__ void in_finalize_group_lds(const double* __restrict__ part, const InShape& s, int chunks, int n, int cgroup,
+                                      int mode, float* __restrict__ out0, float* __restrict__ out1) {
+  // A/B (MRAGAN_IN_FIN_LDS): the r04 form — channel fastest, 64 row sums combined by one thread
+  __shared__ double fr[2][256];
+  constexpr int CW = 4, ROWS = 64;
+  const int tid = threadIdx.x, cl = tid % CW, row = tid / CW;
+  const int c = cgroup * CW + cl;
+  double sa = 0, sb = 0;
+  if (c < s.C) {
+#pragma unroll 8
+    for (int k = row; k < chunks; k += ROWS) {
+      const double2 p = *reinterpret_cast<const double2*>(part + (((int64_t)n * chunks + k) * s.C + c) * 2);
+      sa += p.x; sb += p.y;
+    }
+  }
+  fr[0][tid] = sa; fr[1][tid] = sb;
+  __syncthreads();
+  if (row == 0 && c < s.C) {
+    double a = 0, b = 0;
+    for (int r = 0; r < ROWS; ++r) { a += fr[0][r * CW + cl]; b += fr[1][r * CW + cl]; }
+    const double S = (double)s.S();
+    const int i = n * s.C + c;
+    if (mode == 0) {
+      const double mu = a / S;
+      double var = b / S - mu * mu;
+      if (var < 0) var = 0;
+      out0[i] = (float)mu;
+      out1[i] = (float)(1.0 / sqrt(var + (double)kInEps));
+    } else {
+      out0[2 * i] = (float)(a / S);
+      out0[2 * i + 1] = (float)(b / S);
+    }
+  }
+}
+
 __device__ void in_finalize_group(const double* __restrict__ part, const InShape& s, int chunks, int n, int cgroup,
                                   int mode, float* __restrict__ out0, float* __restrict__ out1) {
   constexpr int CW = 4, ROWS = 64;
@@ -162,9 +197,11 @@ __global__ void __launch_bounds__(256) in_stats_kernel(const float* __restrict__
 // one block per instance (kernel boundary = coherence point for the partials of all XCDs; an
 // in-kernel last-block reduction needs agent-scope release fences, i.e. L2 write-backs, per block)
 __global__ void __launch_bounds__(256) in_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
-                                                          float* __restrict__ mean, float* __restrict__ rstd) {
-  in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 0, mean, rstd);
+                                                          float* __restrict__ mean, float* __restrict__ rstd, int lds) {
+  if (lds) in_finalize_group_lds(part, s, chunks, blockIdx.y, blockIdx.x, 0, mean, rstd);
+  else in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 0, mean, rstd);
 }
+static const int g_in_fin_lds = getenv("MRAGAN_IN_FIN_LDS") ? 1 : 0;
 
 // ---- forward apply: y (padded by ypad) = act((x − μ)·rstd) + resid(interior of rpad-padded) --
 // One output row (n, dp, hp) of the padded y per block iteration; source row and the residual
@@ -321,8 +358,9 @@ __global__ void __launch_bounds__(256) in_bwd_stats_kernel(InBwdArgs a, InShape 
 }
 
 __global__ void __launch_bounds__(256) in_bwd_finalize_kernel(const double* __restrict__ part, InShape s, int chunks,
-                                                              float* __restrict__ coef) {
-  in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 1, coef, nullptr);
+                                                              float* __restrict__ coef, int lds) {
+  if (lds) in_finalize_group_lds(part, s, chunks, blockIdx.y, blockIdx.x, 1, coef, nullptr);
+  else in_finalize_group(part, s, chunks, blockIdx.y, blockIdx.x, 1, coef, nullptr);
 }
 
 template <int P>
@@ -502,7 +540,7 @@ static int launch_in_apply(const float* x, const InShape& s, const double* part,
                        resid, rpad, y, ypad, static_cast<uint2*>(y16), mode16, per);
     return check_launch(y16 ? "in_apply_fused(op16)" : "in_apply_fused");
   }
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd);
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, mean, rstd, g_in_fin_lds);
   int rc = check_launch("in_finalize");
   if (rc) return rc;
   const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
@@ -527,7 +565,7 @@ static int launch_in_bwd_apply(const InBwdArgs& a, const InShape& s, const doubl
     }
     return check_launch(a.dx16 ? "in_bwd_apply_fused(op16)" : "in_bwd_apply_fused");
   }
-  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef);
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(ceil_div(s.C, 4), s.N), dim3(256), 0, st, part, s, chunks, coef, g_in_fin_lds);
   int rc = check_launch("in_bwd_finalize");
   if (rc) return rc;
   const int rows = s.N * s.D * s.H;
@@ -615,6 +653,31 @@ int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act
     return kBadArg;
   }
   return launch_in_apply(x, s, part, chunks, mean, rstd, act, resid, rpad, y, ypad, y16, mode16, st);
+}
+
+// ABI 15: the apply passes alone, the statistics already finalized by the producing conv
+int instnorm_apply(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
+                   const float* mean, const float* rstd, hipStream_t st, void* y16, int mode16) {
+  MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm: C=%d must be a multiple of 4 (≤1024)", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, ypad > rpad ? ypad : rpad), "instnorm: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
+  const int rows = s.N * (s.D + 2 * ypad) * (s.H + 2 * ypad);
+  hipLaunchKernelGGL(in_apply_kernel, dim3(rows < 16384 ? rows : 16384), dim3(256), 0, st, x, s, mean, rstd, act, resid,
+                     rpad, y, ypad, static_cast<uint2*>(y16), mode16);
+  return check_launch(y16 ? "in_apply(op16)" : "in_apply");
+}
+
+int instnorm_bwd_apply(const InBwdArgs& a, InShape s, const float* coef, hipStream_t st) {
+  MRAGAN_CHECK_ARG(s.C % 4 == 0 && s.C <= 1024, "instnorm_bwd: C=%d must be a multiple of 4", s.C);
+  MRAGAN_CHECK_ARG(in_fits(s, a.dypad), "instnorm_bwd: tensor of %d×%d×%d×%d×%d too large", s.N, s.D, s.H, s.W, s.C);
+  const int rows = s.N * s.D * s.H;
+  const dim3 ga(rows < 16384 ? rows : 16384);
+  switch (a.dypad) {
+    case 0: hipLaunchKernelGGL(in_bwd_apply_kernel<0>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 1: hipLaunchKernelGGL(in_bwd_apply_kernel<1>, ga, dim3(256), 0, st, a, s, coef); break;
+    case 3: hipLaunchKernelGGL(in_bwd_apply_kernel<3>, ga, dim3(256), 0, st, a, s, coef); break;
+    default: hipLaunchKernelGGL(in_bwd_apply_kernel<-1>, ga, dim3(256), 0, st, a, s, coef); break;
+  }
+  return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
 }
 
 int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipStream_t st) {

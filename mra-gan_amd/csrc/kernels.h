@@ -25,6 +25,9 @@ struct IgemmArgs {
   int x16;          // x is a 16-bit operand plane (bf16 / fp16 words of the precision mode), not fp32
   // with in_part, backward statistics instead (BrickArgs::sx): the producing IN's x, μ, rstd, act
   const float* bs_x; const float* bs_mean; const float* bs_rstd; int bs_act;
+  // optional with in_part (ABI 15): finalize the statistics in the launch where the kernel can
+  // (BrickArgs::tick …); *in_finalized = 1 when it did, else left 0 (the caller finalizes)
+  unsigned* in_tick = nullptr; float* in_fin0 = nullptr; float* in_fin1 = nullptr; int* in_finalized = nullptr;
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
@@ -54,6 +57,11 @@ struct BrickArgs {
   // with g = dz_p·act'(x̂) at the interior voxel p folds into (conv_brick_x3 only)
   const float* sx; const float* smean; const float* srstd; int sact;
   int stamp;        // diagnostics: record s_memtime phase stamps (conv_brick_ks only)
+  // optional with part (ABI 15, conv_brick_ks only): finalize in the launch (in_ticket.h) —
+  // tick: N·gn zeroed counters; fin_mode 0: μ → fin0, rstd → fin1 ([N][ny]); 1: the backward
+  // coefficients → fin0 ([N][ny][2]); fin_S: voxels per instance of the normalised tensor;
+  // finalized (host side): set to 1 when the launch does it
+  unsigned* tick; float* fin0; float* fin1; int fin_mode; double fin_S; int* finalized;
 };
 bool conv_brick_applicable(const IgemmArgs& a);
 int conv_brick(const IgemmArgs& a, hipStream_t st, bool interior = false);
@@ -165,6 +173,10 @@ int instnorm_fwd_partials(const float* x, InShape s, float* y, int ypad, int act
                           int mode16 = 0);
 int instnorm_bwd_partials(const InBwdArgs& a, InShape s, const double* part, int chunks, void* ws, size_t ws_bytes,
                           hipStream_t st);
+// ABI 15: the apply passes alone (statistics finalized by the producing conv, in_ticket.h)
+int instnorm_apply(const float* x, InShape s, float* y, int ypad, int act, const float* resid, int rpad,
+                   const float* mean, const float* rstd, hipStream_t st, void* y16, int mode16);
+int instnorm_bwd_apply(const InBwdArgs& a, InShape s, const float* coef, hipStream_t st);
 size_t instnorm_ws_bytes(int N, int D, int H, int W, int C);
 int instnorm_running(const void* table, int nentries, float momentum, hipStream_t st);
 size_t instnorm_running_entry_bytes();

@@ -35,6 +35,8 @@ _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None   
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
 # A/B switch: MRAGAN_NO_S2_PLANES keeps the stem / down1 InstanceNorm outputs in fp32 (no ABI 14 planes)
 _NO_S2_PLANES = __import__("os").environ.get("MRAGAN_NO_S2_PLANES") is not None
+# ABI 15: InstanceNorm statistics finalized in the producing brick's launch (MRAGAN_NO_IN_TICKETS: off)
+_IN_FIN = ops.in_tickets_enabled()
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
 _FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") or "0"))
                # the library's A/B switches that send those convs to the fp32-pack kernels
@@ -138,11 +140,20 @@ class ConvLayer:
                                         transposed=self.transposed)
         return y, part, chunks
 
-    def forward_in_stats_op16(self, x16):
-        """forward_in_stats on the operand plane of the input (brick kernel, 16-bit modes)."""
+    def forward_in_stats_op16(self, x16, fin=False):
+        """forward_in_stats on the operand plane of the input (brick kernel, 16-bit modes).  With fin
+        (ABI 15) returns (y, part, chunks, stats): stats = (mean, rstd) when the conv's launch
+        finalized them (instnorm_fwd_op16(stats=…)), else None."""
         N, D, H, W, _ = x16.shape
         osp = self.out_spatial(D, H, W)
         part = None if _NO_IN_STATS else ops.in_partials_buffer(N, osp, self.cout, x16.device)
+        if fin:
+            if part is None:
+                y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd)
+                return y, None, chunks, None
+            y, chunks, stats = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd,
+                                               part, fin=True)
+            return y, part, chunks, stats
         y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
         return y, part, chunks
 
@@ -154,15 +165,20 @@ class ConvLayer:
     def dgrad_op16_in_stats(self, dy16, norm_x, mean, rstd, act):
         """dgrad_op16 (whole-grid, k3 s1 p0) that also leaves the backward-statistics partials of
         the InstanceNorm(+act) that produced this conv's input (norm_x its pre-norm input).
-        Returns (dz, part, chunks); chunks = 0: no partials."""
+        Returns (dz, part, chunks, coef); chunks = 0: no partials; coef: that IN backward's
+        coefficients when the launch finalized them (ABI 15), else None."""
         if _NO_IN_STATS:
             N, D, H, W, _ = dy16.shape
-            return self.dgrad_op16(dy16, (D + 2, H + 2, W + 2)), None, 0
+            return self.dgrad_op16(dy16, (D + 2, H + 2, W + 2)), None, 0, None
         N, D, H, W, _ = dy16.shape
         part = ops.in_partials_buffer(N, (D + 2, H + 2, W + 2), self.cin, dy16.device)
+        if _IN_FIN:
+            dz, chunks, coef = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean,
+                                                              rstd, act, part, fin=True)
+            return dz, part, chunks, coef
         dz, chunks = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean, rstd, act,
                                                     part)
-        return dz, part, chunks
+        return dz, part, chunks, None
 
     def wgrad_op16(self, x16, dy16, accumulate=True):
         """wgrad of a forward-form conv from the operand planes of X and dY (wgrad3, 16-bit modes)."""
@@ -339,15 +355,17 @@ class NetPlan:
                 if cur16 is not None:
                     # 16-bit operand planes (ABI 11): conv1 reads the block input's plane, IN1 writes
                     # only the plane of relu(IN(h1)) (conv2's operand), IN2 both copies of the output
-                    sc.h1, part, chunks = st.conv1.forward_in_stats_op16(cur16)
+                    # ABI 15: where the brick's launch finalizes the statistics, the IN is its apply pass alone
+                    sc.h1, part, chunks, stats = st.conv1.forward_in_stats_op16(cur16, fin=_IN_FIN)
                     _, sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd_op16(sc.h1, act="relu", ypad=1, part=part,
-                                                                          chunks=chunks)
-                    sc.h, part, chunks = st.conv2.forward_in_stats_op16(sc.z1)
+                                                                          chunks=chunks, stats=stats)
                     if want16:
+                        sc.h, part, chunks, stats = st.conv2.forward_in_stats_op16(sc.z1, fin=_IN_FIN)
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=None, ypad=ypad, resid=cur,
                                                                                 rpad=1, part=part, chunks=chunks,
-                                                                                want_f32=True)
+                                                                                want_f32=True, stats=stats)
                     else:
+                        sc.h, part, chunks = st.conv2.forward_in_stats_op16(sc.z1)
                         sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=None, ypad=ypad, resid=cur, rpad=1,
                                                                     part=part, chunks=chunks)
                 else:
@@ -420,9 +438,10 @@ class NetPlan:
                 if need_wgrad:
                     st.conv2.wgrad_op16(sc.z1, dh2)
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
-                dz1, part, chunks = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
+                dz1, part, chunks, coef = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
                 if chunks:
-                    dh1 = ops.instnorm_bwd_partials_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, "relu", part, chunks)
+                    dh1 = ops.instnorm_bwd_partials_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, "relu", part, chunks,
+                                                         coef=coef)
                 else:
                     dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:

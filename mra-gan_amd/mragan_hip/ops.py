@@ -211,6 +211,37 @@ def _conv_info(cin, cout, k, s, p, transposed, N, in_sp, out_sp):
                 flops=2.0 * N * vox * cin * cout * k ** 3)
 
 
+# ---- ABI 15: in-launch InstanceNorm finalize ---------------------------------------------------
+# One zeroed pool of uint32 ticket counters per device; each call takes the next N·cout/32 slots
+# round-robin (the launch leaves them zero).  A graph capture holds ≪ 2^16 slots' worth of calls,
+# so no two kernels that can run at the same time share a slot.  MRAGAN_NO_IN_TICKETS: off (A/B).
+_TICKET_SLOTS = 1 << 16
+_tickets = {}
+_ticket_next = [0]
+_NO_IN_TICKETS = __import__("os").environ.get("MRAGAN_NO_IN_TICKETS") is not None
+
+
+def in_tickets_enabled() -> bool:
+    return not _NO_IN_TICKETS
+
+
+def _ticket_ptr(n: int, device) -> int:
+    dev = torch.device(device)
+    pool = _tickets.get(dev)
+    if pool is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("in-launch InstanceNorm finalize: the ticket pool must be allocated before a graph "
+                               "capture (run one eager step first)")
+        pool = _tickets[dev] = torch.zeros(_TICKET_SLOTS, device=dev, dtype=torch.int32)
+    if n > _TICKET_SLOTS:
+        raise ValueError(f"in-launch finalize: {n} ticket slots > the pool's {_TICKET_SLOTS}")
+    if _ticket_next[0] + n > _TICKET_SLOTS:
+        _ticket_next[0] = 0
+    off = _ticket_next[0]
+    _ticket_next[0] += n
+    return pool.data_ptr() + 4 * off
+
+
 def in_partials_buffer(N: int, out_spatial: Sequence[int], cout: int, device) -> torch.Tensor:
     """fp64 buffer for conv3d_in_stats' InstanceNorm statistics partials (the header's bound)."""
     Do, Ho, Wo = out_spatial
@@ -383,9 +414,12 @@ def _check16(t: torch.Tensor, name: str):
 
 
 def instnorm_fwd_op16(x: torch.Tensor, act=None, ypad: int = 0, resid: Optional[torch.Tensor] = None, rpad: int = 0,
-                      part: Optional[torch.Tensor] = None, chunks: int = 0, want_f32: bool = False):
+                      part: Optional[torch.Tensor] = None, chunks: int = 0, want_f32: bool = False, stats=None):
     """instnorm_fwd writing the output's operand plane (and the fp32 output too when want_f32).
+    stats = (mean, rstd) finalized by the producing conv (ABI 15): the apply pass alone.
     Returns (out or None, out16, mean, rstd)."""
+    if stats is not None:
+        return _instnorm_apply_op16(x, act, ypad, resid, rpad, want_f32, stats)
     _check(x, "instnorm.x")
     dt = op16_dtype()
     if dt is None:
@@ -439,11 +473,38 @@ def instnorm_bwd_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, d
     return dx16
 
 
+def _instnorm_apply_op16(x, act, ypad, resid, rpad, want_f32, stats):
+    _check(x, "instnorm.x")
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError("instnorm_apply_op16: 16-bit operand planes need the bf16 or fp16 precision mode")
+    mean, rstd = stats
+    N, D, H, W, C = x.shape
+    if tuple(mean.shape) != (N, C) or tuple(rstd.shape) != (N, C):
+        raise ValueError("instnorm_apply_op16: statistics shape mismatch")
+    shp = (N, D + 2 * ypad, H + 2 * ypad, W + 2 * ypad, C)
+    out = torch.empty(shp, device=x.device, dtype=torch.float32) if want_f32 else None
+    out16 = torch.empty(shp, device=x.device, dtype=dt)
+    if resid is not None:
+        _check(resid, "instnorm.resid")
+        if tuple(resid.shape) != (N, D + 2 * rpad, H + 2 * rpad, W + 2 * rpad, C):
+            raise ValueError("instnorm: residual shape mismatch")
+    fn = lambda: call("mragan_instnorm_apply_op16", _ptr(x), N, D, H, W, C, _ptr(out), _ptr(out16), ypad, ACT[act],
+                      _ptr(resid), rpad, _ptr(mean), _ptr(rstd), _stream())
+    _timed(lambda: dict(op="in_fwd", cls=f"instnorm_fwd C{C} [{N}x{D}x{H}x{W}] pad{ypad} op16 fin",
+                        bytes=4.0 * x.numel() * (2 if resid is not None else 1) + out16.numel() * (6 if want_f32 else 2)),
+           fn)
+    return out, out16, mean, rstd
+
+
 def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
-                wsplit: torch.Tensor, part: Optional[torch.Tensor] = None, transposed: bool = False):
+                wsplit: torch.Tensor, part: Optional[torch.Tensor] = None, transposed: bool = False, fin: bool = False):
     """conv3d (pre-split weights if any, no bias / act) on the operand plane x16 of its input (the
     k3 s1 brick kernel; the implicit GEMM for other forward-form convs, ABI 14); with `part` also the
-    InstanceNorm statistics partials.  Returns (out, chunks)."""
+    InstanceNorm statistics partials.  Returns (out, chunks); with fin (ABI 15) (out, chunks, stats):
+    stats = (mean, rstd) when the launch finalized them (then instnorm_fwd_op16(stats=…)), else None."""
+    if fin and part is not None:
+        return _conv3d_op16_fin(x16, wp, cout, k, s, p, out_spatial, wsplit, part, transposed)
     _check16(x16, "conv3d_op16.x16")
     N, Di, Hi, Wi, cin = x16.shape
     Do, Ho, Wo = out_spatial
@@ -464,12 +525,39 @@ def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, 
     return out, chunks.value
 
 
+def _conv3d_op16_fin(x16, wp, cout, k, s, p, out_spatial, wsplit, part, transposed):
+    _check16(x16, "conv3d_op16.x16")
+    N, Di, Hi, Wi, cin = x16.shape
+    Do, Ho, Wo = out_spatial
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
+        raise ValueError("conv3d_op16: wsplit size does not match the packed weight")
+    if part.dtype != torch.float64 or not part.is_cuda:
+        raise ValueError("conv3d_op16: part must be a float64 device tensor")
+    out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
+    mean = torch.empty((N, cout), device=x16.device, dtype=torch.float32)
+    rstd = torch.empty((N, cout), device=x16.device, dtype=torch.float32)
+    tick = _ticket_ptr(N * max(1, cout // 32), x16.device)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
+    chunks, done = _ct.c_int(0), _ct.c_int(0)
+    fn = lambda: call("mragan_conv3d_op16_fin", _ptr(x16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), cout, k, s, p,
+                      _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(part), part.numel() * 8,
+                      _ct.byref(chunks), tick, _ptr(mean), _ptr(rstd), _ct.byref(done), _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
+    return out, chunks.value, ((mean, rstd) if done.value else None)
+
+
 def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, wsplit: torch.Tensor,
-                               x_in: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, act, part: torch.Tensor):
+                               x_in: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, act, part: torch.Tensor,
+                               fin: bool = False):
     """Whole-grid data gradient (k3 s1 p0 transposed form, output = input + 2 per dim) from the
     plane dy16 that also leaves, in `part`, the backward-statistics partials of the InstanceNorm
     (+act) whose output was this conv's input: x_in (pre-norm, [N, D, H, W, cout]), mean, rstd.
-    Returns (dz, chunks); chunks = 0: no partials (run instnorm_bwd_op16)."""
+    Returns (dz, chunks); chunks = 0: no partials (run instnorm_bwd_op16).  With fin (ABI 15):
+    (dz, chunks, coef) — coef [N, cout, 2] when the launch finalized the IN backward's coefficients
+    (then instnorm_bwd_partials_op16(coef=…)), else None."""
     _check16(dy16, "dgrad_in_stats.dy16")
     _check(x_in, "dgrad_in_stats.x_in")
     N, Di, Hi, Wi, cin = dy16.shape
@@ -484,6 +572,15 @@ def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, 
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, 3, 1, 0, *osp, 1)
     ws = WS.get(nbytes) if nbytes else None
     chunks = _ct.c_int(0)
+    if fin:
+        coef = torch.empty((N, cout, 2), device=dy16.device, dtype=torch.float32)
+        tick = _ticket_ptr(N * max(1, cout // 32), dy16.device)
+        done = _ct.c_int(0)
+        fn = lambda: call("mragan_conv3d_op16_dgrad_in_stats_fin", _ptr(dy16), N, Di, Hi, Wi, cin, _ptr(wp),
+                          _ptr(wsplit), cout, _ptr(out), _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act],
+                          _ptr(part), part.numel() * 8, _ct.byref(chunks), tick, _ptr(coef), _ct.byref(done), _stream())
+        _timed(lambda: _conv_info(cin, cout, 3, 1, 0, True, N, (Di, Hi, Wi), osp), fn)
+        return out, chunks.value, (coef if done.value else None)
     fn = lambda: call("mragan_conv3d_op16_dgrad_in_stats", _ptr(dy16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), cout,
                       _ptr(out), _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act], _ptr(part),
                       part.numel() * 8, _ct.byref(chunks), _stream())
@@ -493,9 +590,12 @@ def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, 
 
 def instnorm_bwd_partials_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int,
                                dy_add: Optional[torch.Tensor], act, part: torch.Tensor, chunks: int,
-                               g_out: Optional[torch.Tensor] = None):
+                               g_out: Optional[torch.Tensor] = None, coef: Optional[torch.Tensor] = None):
     """instnorm_bwd_op16 from backward-statistics partials (conv3d_op16_dgrad_in_stats): no
-    statistics pass.  Returns the dx plane."""
+    statistics pass; with coef (ABI 15, finalized in that launch) the apply pass alone.  Returns
+    the dx plane."""
+    if coef is not None:
+        return _instnorm_bwd_apply_op16(x, mean, rstd, dy, dypad, dy_add, act, g_out, coef)
     _check(x, "instnorm_bwd.x")
     dt = op16_dtype()
     if dt is None:
@@ -510,6 +610,25 @@ def instnorm_bwd_partials_op16(x: torch.Tensor, mean: torch.Tensor, rstd: torch.
                       dypad, _ptr(dy_add), ACT[act], _ptr(dx16), _ptr(g_out), _ptr(part), chunks, _ptr(ws), ws.numel(),
                       _stream())
     _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad} op16 partials",
+                        bytes=4.0 * (x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
+                                     + (x.numel() if g_out is not None else 0)) + 2.0 * x.numel()), fn)
+    return dx16
+
+
+def _instnorm_bwd_apply_op16(x, mean, rstd, dy, dypad, dy_add, act, g_out, coef):
+    _check(x, "instnorm_bwd.x")
+    dt = op16_dtype()
+    if dt is None:
+        raise ValueError("instnorm_bwd_apply_op16: 16-bit operand planes need the bf16 or fp16 precision mode")
+    N, D, H, W, C = x.shape
+    if tuple(dy.shape) != (N, D + 2 * dypad, H + 2 * dypad, W + 2 * dypad, C):
+        raise ValueError(f"instnorm_bwd: dy shape {tuple(dy.shape)} does not match pad {dypad}")
+    if tuple(coef.shape) != (N, C, 2) or coef.dtype != torch.float32:
+        raise ValueError("instnorm_bwd_apply_op16: coef must be float32 [N, C, 2]")
+    dx16 = torch.empty(x.shape, device=x.device, dtype=dt)
+    fn = lambda: call("mragan_instnorm_bwd_apply_op16", _ptr(x), _ptr(mean), _ptr(rstd), N, D, H, W, C, _ptr(dy), dypad,
+                      _ptr(dy_add), ACT[act], _ptr(dx16), _ptr(g_out), _ptr(coef), _stream())
+    _timed(lambda: dict(op="in_bwd", cls=f"instnorm_bwd C{C} [{N}x{D}x{H}x{W}] pad{dypad} op16 fin",
                         bytes=4.0 * (x.numel() + dy.numel() + (x.numel() if dy_add is not None else 0)
                                      + (x.numel() if g_out is not None else 0)) + 2.0 * x.numel()), fn)
     return dx16

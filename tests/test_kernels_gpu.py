@@ -547,6 +547,55 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
+@pytest.mark.parametrize("N,S", [(2, 16), (4, 16), (1, 12)])
+def test_in_launch_finalize(op16, N, S):
+    """ABI 15: the K-split brick's last block per (instance, column tile) finalizes the InstanceNorm
+    statistics (ticket counters, write-through partials): the conv output and partials are
+    bit-identical to the non-finalizing launch, μ / rstd and the backward coefficients agree with the
+    finalize kernel to fp64 summation-order noise, and repeated launches (tickets reset by the last
+    block) give bit-identical results."""
+    ops = op16
+    dt = ops.op16_dtype()
+    C = 128
+    g = torch.Generator().manual_seed(N * 5 + S)
+    x16 = ndhwc(torch.randn(N, C, S + 2, S + 2, S + 2, generator=g).float()).cuda().to(dt)
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_f, wp_b = pack(ops, w, False, False), pack(ops, w, False, True)
+    ws_f, ws_b = _presplit(ops, w, C, C, False), _presplit(ops, w, C, C, True)
+    osp = (S, S, S)
+    part_ref = ops.in_partials_buffer(N, osp, C, "cuda")
+    y_ref, ch_ref = ops.conv3d_op16(x16, wp_f, C, 3, 1, 0, osp, ws_f, part_ref)
+    _, z_ref, m_ref, r_ref = ops.instnorm_fwd_op16(y_ref, act="relu", ypad=1, part=part_ref, chunks=ch_ref)
+    runs = []
+    for _ in range(3):
+        part = ops.in_partials_buffer(N, osp, C, "cuda")
+        y, ch, stats = ops.conv3d_op16(x16, wp_f, C, 3, 1, 0, osp, ws_f, part, fin=True)
+        runs.append((y, ch, stats))
+    y, ch, stats = runs[0]
+    assert ch == ch_ref > 0 and stats is not None, "the K-split brick did not finalize in-launch"
+    assert torch.equal(y, y_ref)
+    n = N * ch * C * 2
+    assert torch.equal(part[:n], part_ref[:n])
+    m, r = stats
+    assert rel(m, m_ref) < 1e-6 and rel(r, r_ref) < 1e-6
+    for yy, cc, ss in runs[1:]:
+        assert torch.equal(yy, y) and torch.equal(ss[0], m) and torch.equal(ss[1], r)
+    _, z, _, _ = ops.instnorm_fwd_op16(y, act="relu", ypad=1, stats=stats)
+    assert (z != z_ref).float().mean().item() < 1e-3          # only round-half cases of ~1e-7 shifts
+    # the data gradient with the backward coefficients of IN1 (the step's conv2 data gradient)
+    dh2 = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda().to(dt)
+    pb_ref = ops.in_partials_buffer(N, (S + 2,) * 3, C, "cuda")
+    dz_ref, cb_ref = ops.conv3d_op16_dgrad_in_stats(dh2, wp_b, C, ws_b, y, m, r, "relu", pb_ref)
+    pb = ops.in_partials_buffer(N, (S + 2,) * 3, C, "cuda")
+    dz, cb, coef = ops.conv3d_op16_dgrad_in_stats(dh2, wp_b, C, ws_b, y, m, r, "relu", pb, fin=True)
+    assert torch.equal(dz, dz_ref) and cb == cb_ref > 0
+    ref = ops.instnorm_bwd_partials_op16(y, m, r, dz_ref, 1, None, "relu", pb_ref, cb_ref)
+    if coef is None:
+        pytest.skip("this data-gradient shape runs the 8-wave brick (no in-launch finalize)")
+    got = ops.instnorm_bwd_partials_op16(y, m, r, dz, 1, None, "relu", pb, cb, coef=coef)
+    assert (got != ref).float().mean().item() < 1e-3
+
+
 @pytest.mark.parametrize("N,cin,cout,dims", [(2, 32, 64, (32, 32, 32)), (1, 64, 128, (16, 16, 32)),
                                               (1, 32, 64, (8, 12, 64))])
 def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
