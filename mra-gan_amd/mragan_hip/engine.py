@@ -140,22 +140,25 @@ class ConvLayer:
                                         transposed=self.transposed)
         return y, part, chunks
 
-    def forward_in_stats_op16(self, x16, fin=False):
-        """forward_in_stats on the operand plane of the input (brick kernel, 16-bit modes).  With fin
-        (ABI 15) returns (y, part, chunks, stats): stats = (mean, rstd) when the conv's launch
-        finalized them (instnorm_fwd_op16(stats=…)), else None."""
+    def forward_in_stats_op16(self, x16):
+        """forward_in_stats on the operand plane of the input (brick kernel, 16-bit modes)."""
         N, D, H, W, _ = x16.shape
         osp = self.out_spatial(D, H, W)
         part = None if _NO_IN_STATS else ops.in_partials_buffer(N, osp, self.cout, x16.device)
-        if fin:
-            if part is None:
-                y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd)
-                return y, None, chunks, None
-            y, chunks, stats = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd,
-                                               part, fin=True)
-            return y, part, chunks, stats
         y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
         return y, part, chunks
+
+    def forward_in_stats_op16_fin(self, x16):
+        """forward_in_stats_op16 → (y, part, chunks, stats): stats = (mean, rstd) when the conv's
+        launch finalized them (ABI 15; then instnorm_fwd_op16(stats=…)), else None."""
+        if not _IN_FIN or _NO_IN_STATS:
+            return self.forward_in_stats_op16(x16) + (None,)
+        N, D, H, W, _ = x16.shape
+        osp = self.out_spatial(D, H, W)
+        part = ops.in_partials_buffer(N, osp, self.cout, x16.device)
+        y, chunks, stats = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part,
+                                           fin=True)
+        return y, part, chunks, stats
 
     def dgrad_op16(self, dy16, in_spatial):
         """dgrad from the operand plane of dy (brick kernel, 16-bit modes)."""
@@ -356,11 +359,11 @@ class NetPlan:
                     # 16-bit operand planes (ABI 11): conv1 reads the block input's plane, IN1 writes
                     # only the plane of relu(IN(h1)) (conv2's operand), IN2 both copies of the output
                     # ABI 15: where the brick's launch finalizes the statistics, the IN is its apply pass alone
-                    sc.h1, part, chunks, stats = st.conv1.forward_in_stats_op16(cur16, fin=_IN_FIN)
+                    sc.h1, part, chunks, stats = st.conv1.forward_in_stats_op16_fin(cur16)
                     _, sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd_op16(sc.h1, act="relu", ypad=1, part=part,
                                                                           chunks=chunks, stats=stats)
                     if want16:
-                        sc.h, part, chunks, stats = st.conv2.forward_in_stats_op16(sc.z1, fin=_IN_FIN)
+                        sc.h, part, chunks, stats = st.conv2.forward_in_stats_op16_fin(sc.z1)
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=None, ypad=ypad, resid=cur,
                                                                                 rpad=1, part=part, chunks=chunks,
                                                                                 want_f32=True, stats=stats)

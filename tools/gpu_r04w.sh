@@ -11,7 +11,7 @@ cd "$R"
 export TMPDIR=/tmp
 source tools/gpu_step.sh
 step kern 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py \
-  -k "finalize or op16 or instnorm or statistics" > "$O/kern.log" 2>&1
+  -k "finalize or op16 or instnorm or statistics" -rs > "$O/kern.log" 2>&1
 tail -2 "$O/kern.log"
 step graph 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_graph_gpu.py \
   > "$O/graph.log" 2>&1
