@@ -108,6 +108,7 @@ def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
         lp, sp, vp, _ = _run(tmp_path / "p", False, 3, precision, extra=extra, size=64)
     finally:
         ops.set_conv_precision("f32")
+        ops.set_loss_scale(1.0)
     assert set(calls) == {32, 64}, f"the stride-2 plane path did not run for both layers: {set(calls)}"
     assert torch.equal(lr, lp), (lr - lp).abs().max()
     for k in sr:

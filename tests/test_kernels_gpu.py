@@ -30,6 +30,9 @@ def ops():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from mragan_hip import ops as _ops
+    # a model built in another test file (fp16: loss scale 1024) leaves the process-wide state set
+    _ops.set_conv_precision("f32")
+    _ops.set_loss_scale(1.0)
     return _ops
 
 
