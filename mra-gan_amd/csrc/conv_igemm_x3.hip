@@ -428,8 +428,10 @@ size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_
 template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH>
 static void launch_x3_pm(const IgemmArgs& a, dim3 grid, int gm, int gn, int ntiles, int splits, hipStream_t st) {
   if constexpr (prec::has_lo<PM>()) {
-    hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0>), grid, dim3(256), 0, st, a, gm, gn,
-                       ntiles, splits);
+    // BK 64 runs the one-plane modes only (the host's use64): two planes would not fit the LDS
+    if constexpr (BK != 64)
+      hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0>), grid, dim3(256), 0, st, a, gm, gn,
+                         ntiles, splits);
   } else {
     if (a.x16)
       hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 1>), grid, dim3(256), 0, st, a, gm, gn,
@@ -509,8 +511,13 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
     }
   }
   if (!a.in_part) a.bs_x = nullptr;     // no partials: the epilogue skips the backward-statistics reads
-  int rc = a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
-                          : dispatch_x3<16>(a, max_mc, pl.cfg, pl.splits, st);
+  // BK 64 (one-plane modes, a multiple of 64 input channels): 8 MFMAs per wave between barriers
+  // instead of 4 — A/B switch MRAGAN_IG_BK64
+  static const bool bk64 = getenv("MRAGAN_IG_BK64") != nullptr;
+  const bool use64 = bk64 && a.cx % 64 == 0 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16);
+  int rc = use64 ? dispatch_x3<64>(a, max_mc, pl.cfg, pl.splits, st)
+           : a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
+                            : dispatch_x3<16>(a, max_mc, pl.cfg, pl.splits, st);
   if (rc || pl.splits == 1) return rc;
   const int64_t E = total_m * a.ny;
   int blocks = (int)((E + 255) / 256);

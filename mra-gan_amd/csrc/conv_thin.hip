@@ -554,14 +554,16 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     return check_launch("thin_n");
   }
   // ≤ 32 contraction channels (one quad per lane, 8 taps × NY float4 of weights in registers):
-  // the D-first data gradient (ndf ≤ 32).  The UNet outermost upconv at 2·ngf = 64 stays on
-  // thin_n_class — it is a forward layer, and the f32 step-parity envelopes of the 64³ UNet
-  // fixture were measured with its summation order.
-  if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && a.cx <= 32 && ceil_div(a.k, a.s) == 2 &&
+  // the D-first data gradient (ndf ≤ 32).  The UNet outermost upconv (2·ngf = 64 channels: two
+  // quads per lane) joins it in the 16-bit MFMA modes (262 µs per 2×32³ → 64³ launch on
+  // thin_n_class, r04final); in exact f32 it stays on thin_n_class — a forward layer, and the f32
+  // step-parity envelopes of the 64³ UNet fixture were measured with its summation order (§2).
+  const bool wide8 = a.cx > 32 && a.cx <= 64 && a.rnd != 0;
+  if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && (a.cx <= 32 || wide8) && ceil_div(a.k, a.s) == 2 &&
       (int64_t)a.N * a.Do * a.Ho * a.Wo < ((int64_t)1 << 31) &&
       (int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx < ((int64_t)1 << 31)) {
     static const bool no_tile8 = getenv("MRAGAN_NO_TILE8") != nullptr;   // A/B switch
-    if (a.s == 2 && !no_tile8) {
+    if (a.s == 2 && !no_tile8 && !wide8) {
       const int tiles_d = ceil_div(a.Do, kT8), tiles_h = ceil_div(a.Ho, kT8), tiles_w = ceil_div(a.Wo, kT8);
       const int64_t blocks = (int64_t)a.N * tiles_d * tiles_h * tiles_w;
       const size_t lds = (size_t)kT8Halo * kT8Halo * kT8Halo * (a.cx / 4) * sizeof(float4);
@@ -579,6 +581,15 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     int64_t gx = ceil_div(maxq, 32 * 4);             // ≈ 4 voxels per lane group: the weights load once per 4
     if (gx > 4096) gx = 4096;
     dim3 grid((unsigned)gx, a.s * a.s * a.s);
+    if (wide8) {
+      switch (a.ny) {
+        case 1: hipLaunchKernelGGL((thin_n_class8_kernel<1, 2>), grid, dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((thin_n_class8_kernel<2, 2>), grid, dim3(256), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((thin_n_class8_kernel<3, 2>), grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL((thin_n_class8_kernel<4, 2>), grid, dim3(256), 0, st, a); break;
+      }
+      return check_launch("thin_n_class8");
+    }
     switch (a.ny) {
       case 1: hipLaunchKernelGGL((thin_n_class8_kernel<1, 1>), grid, dim3(256), 0, st, a); break;
       case 2: hipLaunchKernelGGL((thin_n_class8_kernel<2, 1>), grid, dim3(256), 0, st, a); break;

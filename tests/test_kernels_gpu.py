@@ -215,6 +215,23 @@ def check_rounded(got, ref_rounded, ref_exact):
     if mode in ROUNDED_MIN_DIFF:
         assert rel(got, ref_exact) > ROUNDED_MIN_DIFF[mode], "operands were not rounded"
 
+@pytest.mark.parametrize("N,cin,cout,S,k", [(2, 64, 1, 8, 4), (1, 64, 2, 5, 4), (1, 48, 1, 6, 4), (1, 64, 1, 7, 3)])
+def test_thin_class8_wide_modes(x3, N, cin, cout, S, k):
+    """The UNet outermost upconv shape (2·ngf = 64 → nc, ConvTranspose3d k4 s2 p1; networks3D.py
+    UnetSkipConnectionBlock outermost) on thin_n_class8 with two channel quads per lane in the MFMA
+    modes (round 4; it took 262 µs per launch on thin_n_class): the fp64 result on the mode's
+    rounded operands."""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 3 + cin + cout + S)
+    x = torch.randn(N, cin, S, S + 1, S, generator=g, dtype=torch.float64)
+    w = torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) * 0.1
+    op = 1 if k == 3 else 0
+    y = F.conv_transpose3d(x, w, stride=2, padding=1, output_padding=op)
+    y_r = F.conv_transpose3d(R(x), R(w), stride=2, padding=1, output_padding=op)
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, True, False), cout, k, 2, 1, y.shape[2:], transposed=True)
+    check_rounded(ncdhw(out), y_r, y)
+
+
 X3_CASES = [
     # N, cin, cout, S, k, s, p   (every tile shape of conv_igemm_x3.hip's dispatch)
     (2, 128, 128, 6, 3, 1, 0),
