@@ -340,7 +340,9 @@ constexpr int kT8 = 8, kT8Halo = kT8 / 2 + 3;
 
 __device__ __forceinline__ int floor_div2(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
 
-template <int NY>
+// QPL = 2: 64 contraction channels (the UNet outermost upconv in the MFMA modes), lane j holds
+// channel quads j and j + 8 — the halo takes 88 KB of LDS (one block per CU)
+template <int NY, int QPL>
 __global__ void __launch_bounds__(256) thin_n_tile8_kernel(ThinArgs a, int tiles_d, int tiles_h, int tiles_w) {
   constexpr int s = 2, HE = kT8Halo;
   extern __shared__ float4 hx[];                      // [HE³][CQ], zero outside the input volume
@@ -367,16 +369,19 @@ __global__ void __launch_bounds__(256) thin_n_tile8_kernel(ThinArgs a, int tiles
   const int cls = grp & 7, gi = grp >> 3;             // 4 lane groups per parity class
   const int cw = cls % s, ch = (cls / s) % s, cd = cls / (s * s);
   const int t0d = (cd + a.p) % s, t0h = (ch + a.p) % s, t0w = (cw + a.p) % s;
-  float4 wr[8][NY];
+  float4 wr[8][QPL][NY];
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int td = t0d + s * (t >> 2), th = t0h + s * ((t >> 1) & 1), tw = t0w + s * (t & 1);
     const bool tok = td < k && th < k && tw < k;
     const float* wt = a.w + (int64_t)((min(td, k - 1) * k + min(th, k - 1)) * k + min(tw, k - 1)) * NY * a.cx;
 #pragma unroll
-    for (int n = 0; n < NY; ++n)
-      wr[t][n] = (tok && j < CQ) ? op_round4(*reinterpret_cast<const float4*>(wt + n * a.cx + 4 * j), a.rnd)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < QPL; ++u)
+#pragma unroll
+      for (int n = 0; n < NY; ++n)
+        wr[t][u][n] = (tok && j + 8 * u < CQ)
+                          ? op_round4(*reinterpret_cast<const float4*>(wt + n * a.cx + 4 * (j + 8 * u)), a.rnd)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   constexpr int QT = kT8 / s;                         // class outputs per tile dim
@@ -394,13 +399,16 @@ __global__ void __launch_bounds__(256) thin_n_tile8_kernel(ThinArgs a, int tiles
       if (td >= k || th >= k || tw >= k || (unsigned)id >= (unsigned)a.Di || (unsigned)ih >= (unsigned)a.Hi ||
           (unsigned)iw >= (unsigned)a.Wi)
         continue;
-      if (j < CQ) {
-        const float4 xv = hx[(((id - ild) * HE + (ih - ilh)) * HE + (iw - ilw)) * CQ + j];
 #pragma unroll
-        for (int n = 0; n < NY; ++n) {
-          const float4 wv = wr[t][n];
-          acc[n] = fma((double)xv.x, (double)wv.x, fma((double)xv.y, (double)wv.y,
-                       fma((double)xv.z, (double)wv.z, fma((double)xv.w, (double)wv.w, acc[n]))));
+      for (int u = 0; u < QPL; ++u) {
+        if (j + 8 * u < CQ) {
+          const float4 xv = hx[(((id - ild) * HE + (ih - ilh)) * HE + (iw - ilw)) * CQ + j + 8 * u];
+#pragma unroll
+          for (int n = 0; n < NY; ++n) {
+            const float4 wv = wr[t][u][n];
+            acc[n] = fma((double)xv.x, (double)wv.x, fma((double)xv.y, (double)wv.y,
+                         fma((double)xv.z, (double)wv.z, fma((double)xv.w, (double)wv.w, acc[n]))));
+          }
         }
       }
     }
@@ -558,21 +566,36 @@ int conv_thin(ThinArgs a, hipStream_t st) {
   // quads per lane) joins it in the 16-bit MFMA modes (262 µs per 2×32³ → 64³ launch on
   // thin_n_class, r04final); in exact f32 it stays on thin_n_class — a forward layer, and the f32
   // step-parity envelopes of the 64³ UNet fixture were measured with its summation order (§2).
-  const bool wide8 = a.cx > 32 && a.cx <= 64 && a.rnd != 0;
+  const bool wide8 = a.cx > 32 && a.cx <= 64 && a.rnd != 0 && a.ny <= 2;   // ≤ 2 outputs: no spill
   if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && (a.cx <= 32 || wide8) && ceil_div(a.k, a.s) == 2 &&
       (int64_t)a.N * a.Do * a.Ho * a.Wo < ((int64_t)1 << 31) &&
       (int64_t)a.N * a.Di * a.Hi * a.Wi * a.cx < ((int64_t)1 << 31)) {
     static const bool no_tile8 = getenv("MRAGAN_NO_TILE8") != nullptr;   // A/B switch
-    if (a.s == 2 && !no_tile8 && !wide8) {
+    if (a.s == 2 && !no_tile8) {
       const int tiles_d = ceil_div(a.Do, kT8), tiles_h = ceil_div(a.Ho, kT8), tiles_w = ceil_div(a.Wo, kT8);
       const int64_t blocks = (int64_t)a.N * tiles_d * tiles_h * tiles_w;
       const size_t lds = (size_t)kT8Halo * kT8Halo * kT8Halo * (a.cx / 4) * sizeof(float4);
       if (blocks < ((int64_t)1 << 31)) {
-        switch (a.ny) {
-          case 1: hipLaunchKernelGGL((thin_n_tile8_kernel<1>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
-          case 2: hipLaunchKernelGGL((thin_n_tile8_kernel<2>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
-          case 3: hipLaunchKernelGGL((thin_n_tile8_kernel<3>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
-          default: hipLaunchKernelGGL((thin_n_tile8_kernel<4>), dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w); break;
+        static bool attr[2][4] = {};   // one flag per kernel: every instantiation has the same pointer type
+        const int ai = a.ny < 4 ? a.ny - 1 : 3;
+        auto go = [&](void (*kern)(ThinArgs, int, int, int)) {
+          if (!attr[wide8][ai]) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)(kT8Halo * kT8Halo * kT8Halo * 16 * sizeof(float4)));
+            attr[wide8][ai] = true;
+          }
+          hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, st, a, tiles_d, tiles_h, tiles_w);
+        };
+        if (wide8) {
+          if (a.ny == 1) go(thin_n_tile8_kernel<1, 2>);
+          else go(thin_n_tile8_kernel<2, 2>);
+        } else {
+          switch (a.ny) {
+            case 1: go(thin_n_tile8_kernel<1, 1>); break;
+            case 2: go(thin_n_tile8_kernel<2, 1>); break;
+            case 3: go(thin_n_tile8_kernel<3, 1>); break;
+            default: go(thin_n_tile8_kernel<4, 1>); break;
+          }
         }
         return check_launch("thin_n_tile8");
       }
@@ -582,12 +605,8 @@ int conv_thin(ThinArgs a, hipStream_t st) {
     if (gx > 4096) gx = 4096;
     dim3 grid((unsigned)gx, a.s * a.s * a.s);
     if (wide8) {
-      switch (a.ny) {
-        case 1: hipLaunchKernelGGL((thin_n_class8_kernel<1, 2>), grid, dim3(256), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((thin_n_class8_kernel<2, 2>), grid, dim3(256), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((thin_n_class8_kernel<3, 2>), grid, dim3(256), 0, st, a); break;
-        default: hipLaunchKernelGGL((thin_n_class8_kernel<4, 2>), grid, dim3(256), 0, st, a); break;
-      }
+      if (a.ny == 1) hipLaunchKernelGGL((thin_n_class8_kernel<1, 2>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((thin_n_class8_kernel<2, 2>), grid, dim3(256), 0, st, a);
       return check_launch("thin_n_class8");
     }
     switch (a.ny) {
