@@ -512,8 +512,9 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
   }
   if (!a.in_part) a.bs_x = nullptr;     // no partials: the epilogue skips the backward-statistics reads
   // BK 64 (one-plane modes, a multiple of 64 input channels): 8 MFMAs per wave between barriers
-  // instead of 4 — A/B switch MRAGAN_IG_BK64
-  static const bool bk64 = getenv("MRAGAN_IG_BK64") != nullptr;
+  // instead of 4 — G down2 [4×32³] 32.0 → 27.1 µs, up1 / down2-dgrad [2×16³] 37.0 → 33.7 µs, the
+  // UNet leg 5.34 → 5.21 ms (same box, profiles/r04/ab_same_box.json r04y); A/B switch MRAGAN_IG_BK32
+  static const bool bk64 = getenv("MRAGAN_IG_BK32") == nullptr;
   const bool use64 = bk64 && a.cx % 64 == 0 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16);
   int rc = use64 ? dispatch_x3<64>(a, max_mc, pl.cfg, pl.splits, st)
            : a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
