@@ -159,32 +159,53 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   }
   int kc = ks0 % kchunks, tap0 = ks0 / kchunks;
   int kjw = tap0 % gw.ntap, kjh = (tap0 / gw.ntap) % gh.ntap, kjd = tap0 / gw.ntap / gh.ntap;
+  // the step's tap offsets (input: toff bytes, weights: wso bytes) and tap displacements are kept
+  // incrementally — one add per carry level instead of ~25 scalar multiplies per K-step (PMC r04:
+  // 21.8 SALU per MFMA in G down1); the deltas are block constants
+  const int rs_ = a.cx * ESA, rwo = a.ny * a.cx * 4;                       // one input voxel / weight tap
+  const int dC_t = BK * ESA, dC_w = BK * 4;
+  const int rC_t = (kchunks - 1) * dC_t, rC_w = (kchunks - 1) * dC_w;      // chunk wrap
+  const int dW_t = gw.sign * rs_, dW_w = gw.tstep * rwo;
+  const int dH_t = gh.sign * a.Wi * rs_, dH_w = gh.tstep * a.k * rwo;
+  const int dD_t = gd.sign * a.Hi * a.Wi * rs_, dD_w = gd.tstep * a.k * a.k * rwo;
+  const int rW_t = (gw.ntap - 1) * dW_t, rW_w = (gw.ntap - 1) * dW_w;
+  const int rH_t = (gh.ntap - 1) * dH_t, rH_w = (gh.ntap - 1) * dH_w;
+  int dd = gd.sign * kjd, dh = gh.sign * kjh, dw = gw.sign * kjw;
+  int toff = (((dd * a.Hi + dh) * a.Wi + dw) * a.cx + kc * BK) * ESA;
+  int wso = ((((gd.t0 + gd.tstep * kjd) * a.k + gh.t0 + gh.tstep * kjh) * a.k + gw.t0 + gw.tstep * kjw) * a.ny * a.cx +
+             kc * BK) * 4;
   auto advance = [&]() __attribute__((always_inline)) {
+    toff += dC_t; wso += dC_w;
     if (++kc == kchunks) {
       kc = 0;
-      if (++kjw == gw.ntap) { kjw = 0; if (++kjh == gh.ntap) { kjh = 0; ++kjd; } }
+      toff += dW_t - rC_t - dC_t; wso += dW_w - rC_w - dC_w; dw += gw.sign;
+      if (++kjw == gw.ntap) {
+        kjw = 0;
+        toff += dH_t - rW_t - dW_t; wso += dH_w - rW_w - dW_w; dw = 0; dh += gh.sign;
+        if (++kjh == gh.ntap) {
+          kjh = 0;
+          toff += dD_t - rH_t - dH_t; wso += dD_w - rH_w - dH_w; dh = 0; dd += gd.sign;
+          ++kjd;
+        }
+      }
     }
   };
 
   auto load_tiles = [&](RegA (&ra_)[A_LOADS], float4 (&rb_)[B_LOADS]) __attribute__((always_inline)) {
-    const int c0 = kc * BK;
-    const int td = gd.t0 + gd.tstep * kjd, th = gh.t0 + gh.tstep * kjh, tw = gw.t0 + gw.tstep * kjw;
-    const int wt = (td * a.k + th) * a.k + tw;
-    const int dd = gd.sign * kjd, dh = gh.sign * kjh, dw = gw.sign * kjw;
-    const int toff = __builtin_amdgcn_readfirstlane((((dd * a.Hi + dh) * a.Wi + dw) * a.cx + c0) * ESA);
+    const int toffu = __builtin_amdgcn_readfirstlane(toff);
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
       const int id = a_bd[i] + dd, ih = a_bh[i] + dh, iw = a_bw[i] + dw;
       const bool ok = a_nb[i] >= 0 && (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi &&
                       (unsigned)iw < (unsigned)a.Wi;
-      const buf_f32x4 v = buf_load_16b(xrs, ok ? a_base[i] + toff : (int)kOobOffset, 0);
+      const buf_f32x4 v = buf_load_16b(xrs, ok ? a_base[i] + toffu : (int)kOobOffset, 0);
       if constexpr (X16) ra_[i] = __builtin_bit_cast(uint4, v);
       else ra_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
-    const int wso = __builtin_amdgcn_readfirstlane((wt * a.ny * a.cx + c0) * 4);
+    const int wsou = __builtin_amdgcn_readfirstlane(wso);
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
-      const buf_f32x4 v = buf_load_16b(wrs, b_voff[i], wso);
+      const buf_f32x4 v = buf_load_16b(wrs, b_voff[i], wsou);
       rb_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
     advance();

@@ -188,8 +188,6 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       if constexpr (X16G) {
         const bool ok8 = rok && g8 && !(w_edge && q8 == 0);
         rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, ok8 ? glane_al8 + wrun : (int)kOobOffset, gso));
-        if constexpr (kG8X)
-          if (g8x) rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, rok ? glane_al8x + wrun : (int)kOobOffset, gso));
         continue;
       }
 #pragma unroll
@@ -203,6 +201,18 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       const bool okx = rok && !(w_edge && qx == 0);
       const buf_f32x4 v = buf_load_16b(gr, okx ? glane_alx + wrun : (int)kOobOffset, gso);
       rgx[r] = make_float4(v.x, v.y, v.z, v.w);
+    }
+    if constexpr (kG8X) {
+      // the 33rd fine position (wave 0's first GO lanes): one branch for the stage's 8 loads
+      if (g8x) {
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          const int rr = r / nsw, wr = r - rr * nsw;
+          const bool rok = dok && (gh0 >= 0 || rr > 0);
+          const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
+          rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, rok ? glane_al8x + 32 * wr * a.Cg * ESG : (int)kOobOffset, gso));
+        }
+      }
     }
   };
   auto load = [&](int st) __attribute__((always_inline)) {
@@ -313,6 +323,9 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int tq = (lane & 15) >> 2, tp = lane & 3, tgi = (lane >> 4) & 1;
   const int trA = (8 * lh + tq) * RBD + 16 * (((wm0 + 16 * tgi) / 8 + (tp >> 1)) ^ tr_swz<RBD>(tq)) + 8 * (tp & 1);
   const int trB = (8 * lh + tq) * RBG + 16 * (((wn0 + 16 * tgi) / 8 + (tp >> 1)) ^ tr_swz<RBG>(tq)) + 8 * (tp & 1);
+  constexpr int KSTEP = TG == 32 ? 2 : 1, NKS = (kSegW / 2) / KSTEP;
+  const int kp = TG == 32 ? __builtin_amdgcn_readfirstlane(kpar) : 0;
+  const int trA_k = trA + 16 * kp * RBD, trB_k = trB + 16 * kp * RBG;
   auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
     Ds = smem + b * tr_stage<TG>();
     Gs = Ds + kTrRowsD * RBD;
@@ -358,27 +371,30 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         load(st + 1);
       }
     }
+    // TG = 32: this wave's K half is the K-steps ks ≡ kp (mod 2) — a loop over them with the
+    // wave-uniform kp folded into the base offsets (a per-step `continue` on the wave index compiled
+    // to exec-mask branches around every step: no LDS read could run ahead of the previous MFMAs)
 #pragma unroll
-    for (int ks = 0; ks < kSegW / 2; ++ks) {
-      if (TG == 32 && (ks & 1) != kpar) continue;   // K half of this wave
+    for (int ki = 0; ki < NKS; ++ki) {
+      const int ks = KSTEP * ki;                    // + kp (in the bases)
       // K-step ks: coarse w = 2ks + lh × 8 segments
       bf16x8 fa[2], fb[3][2];
       // tap kw: kw = 1 → E[w] (slot w), kw = 0 → O[w − 1] (slot 16 + w), kw = 2 → O[w] (slot 17 + w)
       if constexpr (kTr) {
         // rows 16ks … 16ks+15 (slots 2ks, 2ks+1 × 8 segments): two 4-row reads per operand
-        const char* ar = Ds + trA + (16 * ks) * RBD;
+        const char* ar = Ds + trA_k + (16 * ks) * RBD;
         const tr_v4s a0 = tr_read(ar), a1 = tr_read(ar + 4 * RBD);
         fa[0] = fa[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
         constexpr int kslot[3] = {16, 0, 17};
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
-          const char* br = Gs + trB + (16 * ks + kR * kslot[kw]) * RBG;
+          const char* br = Gs + trB_k + (16 * ks + kR * kslot[kw]) * RBG;
           const tr_v4s b0 = tr_read(br), b1 = tr_read(br + 4 * RBG);
           fb[kw][0] = fb[kw][1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
         }
       } else {
-        const char* arow = Ds + (wm0 + li) * kDRow + lh * 16;
-        const char* brow = Gs + (wn0 + li) * kGRow + lh * 16;
+        const char* arow = Ds + (wm0 + li) * kDRow + lh * 16 + 32 * kp;
+        const char* brow = Gs + (wn0 + li) * kGRow + lh * 16 + 32 * kp;
         fa[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
         fa[1] = prec::has_lo<PM>() ? *reinterpret_cast<const bf16x8*>(arow + ks * 32 + kDHalf) : fa[0];
         constexpr int koff[3] = {16 * 16, 0, 17 * 16};
