@@ -72,10 +72,18 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const int kz = blockIdx.x / ntiles;                 // split-K slice
   int L = blockIdx.x - kz * ntiles, tile = L;
   if ((ntiles & 7) == 0) tile = (L & 7) * (ntiles >> 3) + (L >> 3);
-  const int nb_idx = tile % gn;
-  int rest = tile / gn;
-  const int mb_idx = rest % gm;
-  const int cls = rest / gm;
+  // parity classes fastest (transposed s2): the classes of one output region read the same input
+  // region, so each XCD's contiguous tile range holds every class — with the classes outermost, one
+  // XCD got the 8-tap class (every dim odd) and another the 1-tap one: the kernel took as long as
+  // 1/8 of the chip doing 8/27 of the work.  Heaviest class first within a group.
+  int rest = tile;
+  int cls = 0;
+  if (a.nclass > 1) {
+    cls = a.nclass - 1 - rest % a.nclass;
+    rest /= a.nclass;
+  }
+  const int nb_idx = rest % gn;
+  const int mb_idx = rest / gn;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
