@@ -153,8 +153,10 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   // SGPR soffset.  K-steps advance (channel chunk, kw, kh, kd) with carries: no per-step
   // divisions, no 64-bit address arithmetic.
   constexpr int ESA = X16 ? 2 : 4;          // bytes per input element
-  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * ESA));
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4));
+  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * ESA / (a.tmode == 2 ? 2 : 1)));
+  // a.tmode (timing-only A/B, MRAGAN_IG_TIMING): 1 — the weight descriptor covers the first half
+  // of the packed taps (the rest read as zeros: no memory traffic), 2 — the input's first half
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4 / (a.tmode == 1 ? 2 : 1)));
   int a_base[A_LOADS];
 #pragma unroll
   for (int i = 0; i < A_LOADS; ++i)
@@ -544,6 +546,8 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
   // instead of 4 — G down2 [4×32³] 32.0 → 27.1 µs, up1 / down2-dgrad [2×16³] 37.0 → 33.7 µs, the
   // UNet leg 5.34 → 5.21 ms (same box, profiles/r04/ab_same_box.json r04y); A/B switch MRAGAN_IG_BK32
   static const bool bk64 = getenv("MRAGAN_IG_BK32") == nullptr;
+  static const int tmode = [] { const char* e = getenv("MRAGAN_IG_TIMING"); return e ? atoi(e) : 0; }();
+  a.tmode = tmode;
   const bool use64 = bk64 && a.cx % 64 == 0 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16);
   int rc = use64 ? dispatch_x3<64>(a, max_mc, pl.cfg, pl.splits, st)
            : a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)

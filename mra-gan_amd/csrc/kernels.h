@@ -28,6 +28,7 @@ struct IgemmArgs {
   // optional with in_part (ABI 15): finalize the statistics in the launch where the kernel can
   // (BrickArgs::tick …); *in_finalized = 1 when it did, else left 0 (the caller finalizes)
   unsigned* in_tick = nullptr; float* in_fin0 = nullptr; float* in_fin1 = nullptr; int* in_finalized = nullptr;
+  int tmode = 0;    // conv_igemm_x3 timing-only A/B (MRAGAN_IG_TIMING; wrong results by design)
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);
