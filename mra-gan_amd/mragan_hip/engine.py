@@ -145,7 +145,8 @@ class ConvLayer:
         N, D, H, W, _ = x16.shape
         osp = self.out_spatial(D, H, W)
         part = None if _NO_IN_STATS else ops.in_partials_buffer(N, osp, self.cout, x16.device)
-        y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part)
+        y, chunks = ops.conv3d_op16(x16, self.wp_fwd, self.cout, self.k, self.s, self.p, osp, self.ws_fwd, part,
+                                    transposed=self.transposed)
         return y, part, chunks
 
     def forward_in_stats_op16_fin(self, x16):
@@ -353,6 +354,10 @@ class NetPlan:
             ypad = self._next_prepad(i)
             # a ResnetBlock next: its input's operand plane beside the fp32 tensor (the skip add)
             want16 = op16 and i + 1 < len(self.stages) and self.stages[i + 1].kind == "block"
+            # a ConvTranspose3d with a norm next (G up1): it reads its input's plane too (round 4)
+            nxt_ = self.stages[i + 1] if i + 1 < len(self.stages) else None
+            up16 = (op16 and not _NO_S2_PLANES and ypad == 0 and nxt_ is not None and nxt_.kind != "block"
+                    and nxt_.norm is not None and not nxt_.prepad and nxt_.conv.transposed and nxt_.conv.cin % 32 == 0)
             out16 = None
             if st.kind == "block":
                 if cur16 is not None:
@@ -363,6 +368,13 @@ class NetPlan:
                     _, sc.z1, sc.mean1, sc.rstd1 = ops.instnorm_fwd_op16(sc.h1, act="relu", ypad=1, part=part,
                                                                           chunks=chunks, stats=stats)
                     if want16:
+                        sc.h, part, chunks, stats = st.conv2.forward_in_stats_op16_fin(sc.z1)
+                        sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=None, ypad=ypad, resid=cur,
+                                                                                rpad=1, part=part, chunks=chunks,
+                                                                                want_f32=True, stats=stats)
+                    elif up16:
+                        # the last block before G up1: its output's plane feeds up1's implicit GEMM, the
+                        # fp32 copy up1's weight gradient
                         sc.h, part, chunks, stats = st.conv2.forward_in_stats_op16_fin(sc.z1)
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=None, ypad=ypad, resid=cur,
                                                                                 rpad=1, part=part, chunks=chunks,
@@ -382,7 +394,8 @@ class NetPlan:
                 bias = st.conv.m.bias if (st.use_bias and st.conv.m.bias is not None) else None
                 if st.norm is not None:
                     # the conv's epilogue leaves the norm's statistics partials where it can
-                    if cur is None:                  # the input exists only as its plane (only16 below)
+                    if cur is None or (cur16 is not None and st.conv.transposed):
+                        # the input exists only as its plane (only16 below), or also as one (up16)
                         sc.h, part, chunks = st.conv.forward_in_stats_op16(cur16)
                     else:
                         sc.h, part, chunks = st.conv.forward_in_stats(cur)
