@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 15
+#define MRAGAN_ABI_VERSION 16
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -226,6 +226,14 @@ int mragan_conv3d_op16_dgrad_in_stats_fin(const void* dy16, int N, int Di, int H
                                           const float* x_in, const float* mean, const float* rstd, int act, double* part,
                                           size_t part_bytes, int* chunks, unsigned* tickets, float* coef, int* finalized,
                                           void* stream);
+/* ABI 16: mragan_conv3d_presplit_bwd_stats on the 16-bit operand plane of its input (bf16 / fp16
+ * modes; the stride-2 implicit GEMM, a multiple of 32 input channels): the data gradient of G up1 /
+ * up2 (ConvTranspose3d k3 s2, networks3D.py:203-209) from the plane of the IN backward's dx, with the
+ * backward statistics of the IN in front; results bit-identical to the fp32-input form. */
+int mragan_conv3d_op16_bwd_stats(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked, int cout,
+                                  int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
+                                  size_t ws_bytes, const float* x_in, const float* mean, const float* rstd, int act,
+                                  double* part, size_t part_bytes, int* chunks, void* stream);
 int mragan_instnorm_apply_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
                                const float* resid, int rpad, const float* mean, const float* rstd, void* stream);
 int mragan_instnorm_bwd_apply_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,

@@ -314,6 +314,28 @@ int mragan_conv3d_presplit_bwd_stats(const float* x, int N, int Di, int Hi, int 
   return conv_igemm(a, static_cast<hipStream_t>(stream));
 }
 
+int mragan_conv3d_op16_bwd_stats(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, int cout,
+                                  int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
+                                  size_t ws_bytes, const float* x_in, const float* mean, const float* rstd, int act,
+                                  double* part, size_t part_bytes, int* chunks, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x16 && w && y && x_in && mean && rstd && part && chunks, "conv3d_op16_bwd_stats: null pointer");
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_op16_bwd_stats: transposed must be 0/1");
+  MRAGAN_CHECK_ARG(act == kActNone || act == kActRelu || act == kActLrelu, "conv3d_op16_bwd_stats: act %d", act);
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv3d_op16_bwd_stats: bad input shape");
+  MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv3d_op16_bwd_stats: bad output shape");
+  MRAGAN_CHECK_ARG(k >= 1 && stride >= 2 && pad >= 0 && !thin_side(cin, cout) && cin % 32 == 0,
+                   "conv3d_op16_bwd_stats: the stride-2 implicit GEMM (a multiple of 32 input channels) only");
+  const size_t bound = (size_t)N * Do * ceil_div(Ho, 4) * ceil_div(Wo, 6) * cout * 2 * sizeof(double);
+  MRAGAN_CHECK_ARG(part_bytes >= bound, "conv3d_op16_bwd_stats: partials %zu < %zu bytes", part_bytes, bound);
+  *chunks = 0;
+  IgemmArgs a{static_cast<const float*>(x16), w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, k, stride, pad,
+              transposed, kActNone, 1, g_conv_precision, static_cast<float*>(ws), ws_bytes, nullptr, part, chunks};
+  a.x16 = 1;
+  a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act;
+  return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
 int mragan_instnorm_bwd_partials(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W, int C,
                                  const float* dy, int dypad, const float* dy_add, int act, float* dx, float* g_out,
                                  const double* part, int chunks, void* ws, size_t ws_bytes, void* stream) {

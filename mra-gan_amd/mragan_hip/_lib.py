@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -97,6 +97,9 @@ SIGNATURES = {
                                                     i32, vp, sz, vp, vp, vp, vp, vp]),
     "mragan_instnorm_apply_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, i32, vp, vp, vp]),
     "mragan_instnorm_bwd_apply_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp]),
+    # ABI 16: the stride-2 data gradient with backward statistics on the plane of its input
+    "mragan_conv3d_op16_bwd_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp, i32, i32, i32, i32,
+                                           vp, sz, vp, vp, vp, i32, vp, sz, vp, vp]),
     # ABI 12: the G head's data gradient with the backward statistics of the IN in front of it
     "mragan_conv3d_dgrad_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, sz, vp, vp, vp, i32, i32,
                                            vp, sz, vp, vp]),

@@ -242,6 +242,14 @@ class ConvLayer:
         return (not self.transposed and self.k == 3 and self.s == 2 and self.p == 1 and self.cin % 32 == 0
                 and self.cout % 64 == 0 and W_in % 32 == 0)
 
+    def transposed_plane_bwd_ok(self, W_in):
+        """A ConvTranspose3d k3 s2 p1 (G up1 / up2) whose backward can run on the plane of its output
+        gradient: the data gradient is a forward-form implicit GEMM over Cout (% 32) input channels,
+        the weight gradient wgrad3s2 with the plane as its gathered operand (Cin % 64 dense
+        channels, coarse rows of 16: the input width W_in % 16)."""
+        return (self.transposed and self.k == 3 and self.s == 2 and self.p == 1 and self.cout % 32 == 0
+                and (self.cout == 32 or self.cout % 64 == 0) and self.cin % 64 == 0 and W_in % 16 == 0)
+
     def wgrad(self, x, dy, accumulate=True):
         g = self.m.weight.grad
         if not self.transposed:
@@ -484,6 +492,34 @@ class NetPlan:
                 gpad, gadd = 1, G
                 continue
             conv = st.conv
+            # G up1 / up2 in the one-plane modes (ABI 16): the IN backward writes dY only as its plane;
+            # the data gradient (forward-form implicit GEMM) and the weight gradient (its gathered
+            # operand) read the plane — neither needs the fp32 tensor
+            plane_bwd = (st.norm is not None and sc.inp is not None and conv.transposed_plane_bwd_ok(sc.inp.shape[3])
+                         and self._op16_active() and not _NO_S2_PLANES and not st.use_bias)
+            dh16 = None
+            if plane_bwd:
+                if bstats is not None:
+                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                else:
+                    dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
+                in_spatial = sc.inp.shape[1:4]
+                if need_wgrad:
+                    ops.conv3d_wgrad_g16(sc.inp, dh16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
+                bstats = None
+                if want_dgrad:
+                    nxt = self.stages[i - 1] if i > 0 else None
+                    if (nxt is not None and nxt.kind != "block" and nxt.norm is not None and not st.prepad
+                            and conv.dgrad_bwd_stats_ok()):
+                        nsc = ctx.stages[i - 1]
+                        part = ops.in_partials_buffer(dh16.shape[0], in_spatial, conv.cin, dh16.device)
+                        g, bchunks = ops.conv3d_op16_bwd_stats(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p,
+                                                               in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act, part)
+                        bstats = (part, bchunks) if bchunks else None
+                    else:
+                        g = ops.conv3d_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, in_spatial, None)[0]
+                    gpad, gadd = st.prepad, None
+                continue
             if st.norm is not None:
                 if bstats is not None:
                     dh = ops.instnorm_bwd_partials(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)

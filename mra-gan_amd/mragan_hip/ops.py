@@ -691,6 +691,31 @@ def conv3d_bwd_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: in
     return out, chunks.value
 
 
+def conv3d_op16_bwd_stats(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
+                          out_spatial: Sequence[int], x_in: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, act,
+                          part: torch.Tensor, transposed: bool = False):
+    """conv3d_bwd_stats on the operand plane x16 of its input (ABI 16).  Returns (out, chunks)."""
+    _check16(x16, "conv3d_op16_bwd_stats.x16")
+    _check(x_in, "bwd_stats.x_in")
+    N, Di, Hi, Wi, cin = x16.shape
+    Do, Ho, Wo = out_spatial
+    if tuple(x_in.shape) != (N, Do, Ho, Wo, cout):
+        raise ValueError(f"bwd_stats: x_in shape {tuple(x_in.shape)} != {(N, Do, Ho, Wo, cout)}")
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError("bwd_stats: packed weight size mismatch")
+    if part.dtype != torch.float64 or not part.is_cuda:
+        raise ValueError("bwd_stats: part must be a float64 device tensor")
+    out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
+    chunks = _ct.c_int(0)
+    fn = lambda: call("mragan_conv3d_op16_bwd_stats", _ptr(x16), N, Di, Hi, Wi, cin, _ptr(wp), cout, k, s, p, _ptr(out),
+                      Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act],
+                      _ptr(part), part.numel() * 8, _ct.byref(chunks), _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
+    return out, chunks.value
+
+
 def instnorm_bwd_partials(x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, dy: torch.Tensor, dypad: int,
                           dy_add: Optional[torch.Tensor], act, part: torch.Tensor, chunks: int,
                           g_out: Optional[torch.Tensor] = None):

@@ -651,6 +651,31 @@ def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
     assert rel(gw.view(cout, cin, 3, 3, 3), gw64) < 2e-5
 
 
+@pytest.mark.parametrize("N,cin,cout,S,act", [(2, 32, 64, 32, "relu"), (1, 64, 128, 16, "relu"), (2, 32, 64, 16, "lrelu")])
+def test_op16_stride2_dgrad_backward_statistics(op16, N, cin, cout, S, act):
+    """ABI 16: the data gradient of G up2 / up1 (a forward-form k3 s2 conv over the plane of the IN
+    backward's dx) with the backward statistics of the IN in front: output and partials bit-identical
+    to the fp32-input form of the same mode."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 23 + cin + cout + S)
+    x16 = ndhwc(torch.randn(N, cin, S, S, S, generator=g).float()).cuda().to(dt)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp = pack(ops, w, False, False)
+    o = S // 2
+    osp = (o, o, o)
+    xin = ndhwc(torch.randn(N, cout, o, o, o, generator=g).float()).cuda()
+    _, mean, rstd = ops.instnorm_fwd(xin, act=act)
+    part_ref = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y_ref, ch_ref = ops.conv3d_bwd_stats(x16.float(), wp, cout, 3, 2, 1, osp, None, xin, mean, rstd, act, part_ref)
+    part = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y, ch = ops.conv3d_op16_bwd_stats(x16, wp, cout, 3, 2, 1, osp, xin, mean, rstd, act, part)
+    assert ch == ch_ref
+    assert torch.equal(y, y_ref)
+    n = N * ch * cout * 2
+    assert torch.equal(part[:n], part_ref[:n])
+
+
 def test_op16_stride2_plane_rejected_outside_one_plane_modes(ops):
     """ABI 14: the 16-bit gathered operand of wgrad3s2 exists only in the bf16 / fp16 modes."""
     from mragan_hip import MraganError
