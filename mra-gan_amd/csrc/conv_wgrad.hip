@@ -414,8 +414,8 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   }
   static const bool no_w3 = getenv("MRAGAN_NO_WGRAD3") != nullptr;   // A/B switch
   const bool w3 = !no_w3 && wgrad3_x3_applicable(a), w3s2 = !no_w3 && !w3 && wgrad3s2_x3_applicable(a);
-  MRAGAN_CHECK_ARG(!a.in16 || w3, "conv_wgrad: 16-bit operand planes are supported by the k3 s1 valid weight "
-                   "gradient (wgrad3_x3) only");
+  MRAGAN_CHECK_ARG(!a.in16 || w3 || w3s2, "conv_wgrad: 16-bit operand planes are supported by the k3 s1 valid weight "
+                   "gradient (wgrad3_x3) and the k3 s2 one (wgrad3s2_x3) only");
   MRAGAN_CHECK_ARG(!a.in16g || w3s2, "conv_wgrad: a 16-bit gathered-operand plane is supported by the k3 s2 weight "
                    "gradient (wgrad3s2_x3) only");
   if (w3 || w3s2) {

@@ -88,13 +88,17 @@ struct Wgrad3s2Args {
 };
 
 // X16G: G is the producer's 16-bit operand plane (bf16 / fp16 words): its staging units are
-// (fine position, 8-channel octet), one 16-B load each, stored as they are (one-plane modes)
+// (fine position, 8-channel octet), one 16-B load each, stored as they are (one-plane modes);
+// X16G = 2: D too (ABI 16: G down2's weight gradient, whose dY exists only as its plane) — D units
+// (coarse w, octet, segment half): 4 segments × 16 B per thread
 template <int TG, int PM, int AL, int X16G>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kTr = !prec::has_lo<PM>();
   static_assert(!X16G || kTr, "16-bit operand planes exist in the one-plane modes only");
+  constexpr bool kDp = X16G == 2;         // D as a 16-bit plane too
   constexpr int ESG = X16G ? 2 : 4;       // bytes per G element
+  constexpr int ESD = kDp ? 2 : 4;        // bytes per D element
   constexpr int RBD = kTD * 2, RBG = TG * 2;        // tr: row bytes of the D / G images
   char* Ds = smem;
   char* Gs = smem + (kTr ? kTrRowsD * RBD : kTD * kDRow);
@@ -143,14 +147,17 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const bool g8x = kG8X && q8x < kGPos;
 
   float4 rd[kR], rg[2][kR], rgx[kR];
+  uint4 rd8[kDp ? kR / 2 : 1];
+  const int uwd = (tid & 127) >> 3, od8 = tid & 7, rhd = __builtin_amdgcn_readfirstlane(tid >> 7);
   uint4 rg8[X16G ? kR : 1], rg8x[kG8X ? kR : 1];
   // D / G rows through buffer descriptors: segment / row parts of the offsets are wave-uniform
   // (SGPR soffset); out-of-range rows and positions read zeros through an out-of-range voffset
   // (no select on the loaded values, no 64-bit address arithmetic)
-  const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.d, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * 4));
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.d, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * ESD));
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.g, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * ESG));
   const int dlane = (uw * a.Cd + dn0 + 4 * cq) * 4;
-  const int dseg = kSegW * a.Cd * 4;
+  const int dlane8 = (uwd * a.Cd + dn0 + 8 * od8) * 2;             // kDp: octet od8 of coarse voxel uwd
+  const int dseg = kSegW * a.Cd * ESD;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
   auto bump = [&](int& w_, int& h_, int& d_, int& n_) __attribute__((always_inline)) {
     if (++w_ == nsw) { w_ = 0; if (++h_ == a.H) { h_ = 0; if (++d_ == a.D) { d_ = 0; ++n_; } } }
@@ -173,10 +180,17 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
     const bool dok = (unsigned)gd < (unsigned)Dg;
     const int gh0 = 2 * sh - 1 + kh;                                 // fine row of segment 0
     const int gbase = __builtin_amdgcn_readfirstlane(((sn * Dg + (dok ? gd : 0)) * Hg + (gh0 < 0 ? 0 : gh0)) * gplane_b);
+    if constexpr (kDp) {
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j)
+        rd8[j] = __builtin_bit_cast(uint4, buf_load_16b(dr, dlane8, dso0 + (kR / 2 * rhd + j) * dseg));
+    }
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      const buf_f32x4 dv = buf_load_16b(dr, dlane, dso0 + r * dseg);
-      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      if constexpr (!kDp) {
+        const buf_f32x4 dv = buf_load_16b(dr, dlane, dso0 + r * dseg);
+        rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      }
       const int rr = r / nsw, wr = r - rr * nsw;                     // coarse row / run of the segment
       const bool rok = dok && (gh0 >= 0 || rr > 0);
       // gh0 < 0 only for segment rows rr = 0 (then invalid): rows rr > 0 start at fine row gh0 + 2rr.
@@ -220,6 +234,15 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       load_al(st);
       return;
     }
+    if constexpr (kDp) {
+#pragma unroll
+      for (int j = 0; j < kR / 2; ++j) {
+        const int seg = seg_lo + st * kR + kR / 2 * rhd + j;
+        const bool ok = seg < seg_hi;
+        const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
+        rd8[j] = __builtin_bit_cast(uint4, buf_load_16b(dr, ok ? dlane8 : (int)kOobOffset, dso));
+      }
+    }
     int cw = sw, chh = sh, cdd = sd, cn = sn;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
@@ -229,9 +252,11 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       const int w0 = (ok ? cw : 0) * kSegW;
       bump(cw, chh, cdd, cn);
       // D segments are contiguous 16-voxel runs: offset linear in the segment index
-      const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
-      const buf_f32x4 dv = buf_load_16b(dr, ok ? dlane : (int)kOobOffset, dso);
-      rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      if constexpr (!kDp) {
+        const int dso = __builtin_amdgcn_readfirstlane(ok ? seg * dseg : 0);
+        const buf_f32x4 dv = buf_load_16b(dr, ok ? dlane : (int)kOobOffset, dso);
+        rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
+      }
       const int gd = 2 * d - 1 + kd, gh = 2 * h - 1 + kh;
       const bool rok = ok && (unsigned)gd < (unsigned)Dg && (unsigned)gh < (unsigned)Hg;
       const int gso = __builtin_amdgcn_readfirstlane(rok ? ((n * Dg + gd) * Hg + gh) * Wg * a.Cg * ESG : 0);
@@ -300,7 +325,16 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   };
   auto store = [&]() __attribute__((always_inline)) {
     if constexpr (kTr) {
-      put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+      if constexpr (kDp) {
+        // unit (coarse w uwd, octet od8) → rows uwd·8 + 4·rhd + j, the 16 B at chunk od8 (swizzled)
+#pragma unroll
+        for (int j = 0; j < kR / 2; ++j) {
+          const int row = uwd * kR + kR / 2 * rhd + j;
+          *reinterpret_cast<uint4*>(Ds + row * RBD + 16 * (od8 ^ tr_swz<RBD>(row))) = rd8[j];
+        }
+      } else {
+        put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+      }
       if constexpr (X16G) {
         if (g8) put8(Gs, gslot(q8), go, rg8);
         if constexpr (kG8X)
@@ -497,11 +531,12 @@ static void launch_w3s2_as(const Wgrad3s2Args& a, int blocks, size_t lds, hipStr
 }
 
 template <int TG, int PM, int AL>
-static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, bool g16, hipStream_t st) {
+static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, int planes, hipStream_t st) {
   if constexpr (prec::has_lo<PM>()) {
-    launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);      // (g16 rejected by the caller)
+    launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);      // (planes rejected by the caller)
   } else {
-    if (g16) launch_w3s2_as<TG, PM, AL, 1>(a, blocks, lds, st);
+    if (planes == 2) launch_w3s2_as<TG, PM, AL, 2>(a, blocks, lds, st);
+    else if (planes == 1) launch_w3s2_as<TG, PM, AL, 1>(a, blocks, lds, st);
     else launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);
   }
 }
@@ -525,17 +560,18 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
   static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
-  if (g.in16g && g.x3 != kPrecBf16 && g.x3 != kPrecF16) {
+  if ((g.in16g || g.in16) && g.x3 != kPrecBf16 && g.x3 != kPrecF16) {
     set_error("wgrad3s2_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
     return -kBadArg;
   }
+  const int planes = g.in16 ? 2 : g.in16g ? 1 : 0;       // both operands / G only / none
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
-      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, g.in16g != 0, st);
-      else launch_w3s2<64, PM, 0>(a, blocks, lds, g.in16g != 0, st);
+      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, planes, st);
+      else launch_w3s2<64, PM, 0>(a, blocks, lds, planes, st);
     } else {
-      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, g.in16g != 0, st);
-      else launch_w3s2<32, PM, 0>(a, blocks, lds, g.in16g != 0, st);
+      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, planes, st);
+      else launch_w3s2<32, PM, 0>(a, blocks, lds, planes, st);
     }
     return nsplit;
   })

@@ -497,15 +497,23 @@ class NetPlan:
             # operand) read the plane — neither needs the fp32 tensor
             plane_bwd = (st.norm is not None and sc.inp is not None and conv.transposed_plane_bwd_ok(sc.inp.shape[3])
                          and self._op16_active() and not _NO_S2_PLANES and not st.use_bias)
+            # G down2 (its input only a plane already): dY as a plane too — the weight gradient reads
+            # both planes, the data gradient (transposed implicit GEMM) dY's; not down1, whose data
+            # gradient is brickT's (32 output channels, fp32 input)
+            plane_bwd_fwd = (st.norm is not None and sc.inp is None and sc.inp16 is not None and not st.use_bias
+                             and not conv.transposed and conv.cin != 32 and conv.s2_plane_ok(sc.inp16.shape[3])
+                             and self._op16_active() and not _NO_S2_PLANES)
             dh16 = None
-            if plane_bwd:
+            if plane_bwd or plane_bwd_fwd:
                 if bstats is not None:
                     dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
-                in_spatial = sc.inp.shape[1:4]
-                if need_wgrad:
+                in_spatial = (sc.inp if plane_bwd else sc.inp16).shape[1:4]
+                if need_wgrad and plane_bwd:
                     ops.conv3d_wgrad_g16(sc.inp, dh16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
+                elif need_wgrad:
+                    ops.conv3d_wgrad_op16(dh16, sc.inp16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
                 bstats = None
                 if want_dgrad:
                     nxt = self.stages[i - 1] if i > 0 else None
@@ -514,10 +522,12 @@ class NetPlan:
                         nsc = ctx.stages[i - 1]
                         part = ops.in_partials_buffer(dh16.shape[0], in_spatial, conv.cin, dh16.device)
                         g, bchunks = ops.conv3d_op16_bwd_stats(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p,
-                                                               in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act, part)
+                                                               in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act, part,
+                                                               transposed=not conv.transposed)
                         bstats = (part, bchunks) if bchunks else None
                     else:
-                        g = ops.conv3d_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, in_spatial, None)[0]
+                        g = ops.conv3d_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, in_spatial, None,
+                                            transposed=not conv.transposed)[0]
                     gpad, gadd = st.prepad, None
                 continue
             if st.norm is not None:

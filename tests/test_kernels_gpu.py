@@ -645,6 +645,11 @@ def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
     gw = torch.full_like(gw_ref, float("nan"))
     ops.conv3d_wgrad_g16(dy, x16, 3, 2, 1, gw, False)
     assert torch.equal(gw, gw_ref)
+    # ABI 16: both operands as planes (G down2's weight gradient: dY exists only as its plane)
+    if cout % 64 == 0 and dims[2] // 2 % 16 == 0:
+        gw2 = torch.full_like(gw_ref, float("nan"))
+        ops.conv3d_wgrad_op16(dy.to(dt), x16, 3, 2, 1, gw2, False)
+        assert torch.equal(gw2, gw_ref)
     # and against fp64 on the rounded operands (the mode's definition)
     gw64 = torch.nn.grad.conv3d_weight(ncdhw(x.double().cpu()), (cout, cin, 3, 3, 3),
                                        ncdhw(dy.to(dt).double().cpu()), stride=2, padding=1)
