@@ -90,15 +90,20 @@ def test_graph_step_changing_batch_and_no_identity(tmp_path):
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
 def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
-    """ABI 14: in the one-plane modes the stem's and down1's InstanceNorm outputs (G down1's and
-    down2's inputs; 64³: 32- and 64-channel planes, both wgrad3s2 tile widths) exist only as 16-bit
-    operand planes; the stride-2 convs' forwards and weight gradients read the planes.  The step must
+    """ABI 14 / 16: in the one-plane modes the stride-2 layers' operands exist as 16-bit planes —
+    the stem's and down1's IN outputs (down1 / down2 inputs), the last block's output (up1's
+    input), the IN-backward outputs of up1 / up2 / down2 — read by the implicit GEMMs and wgrad3s2.  The step must
     agree bit for bit with the step that keeps that tensor in fp32 (the kernels round it to the very
     same words) — and the plane path must actually have run."""
     from mragan_hip import engine, ops
     calls = []
-    wg = engine.ConvLayer.wgrad_g16
-    monkeypatch.setattr(engine.ConvLayer, "wgrad_g16", lambda self, *a, **k: (calls.append(self.cin), wg(self, *a, **k)))
+    g16, op16 = ops.conv3d_wgrad_g16, ops.conv3d_wgrad_op16
+    monkeypatch.setattr(ops, "conv3d_wgrad_g16",
+                        lambda dense, gath, k, s, *a, **kw: (calls.append(("g16", gath.shape[-1])),
+                                                             g16(dense, gath, k, s, *a, **kw))[1])
+    monkeypatch.setattr(ops, "conv3d_wgrad_op16",
+                        lambda dense, gath, k, s, *a, **kw: (s == 2 and calls.append(("both", gath.shape[-1])),
+                                                             op16(dense, gath, k, s, *a, **kw))[1])
     extra = ["--ngf", "32"]
     try:
         monkeypatch.setattr(engine, "_NO_S2_PLANES", True)
@@ -109,7 +114,8 @@ def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
     finally:
         ops.set_conv_precision("f32")
         ops.set_loss_scale(1.0)
-    assert set(calls) == {32, 64}, f"the stride-2 plane path did not run for both layers: {set(calls)}"
+    # down1 / up2 (32-channel gathered plane), up1 (64), down2 (both operands as planes)
+    assert set(calls) == {("g16", 32), ("g16", 64), ("both", 64)}, f"plane paths that ran: {set(calls)}"
     assert torch.equal(lr, lp), (lr - lp).abs().max()
     for k in sr:
         assert torch.equal(sr[k], sp[k]), k
