@@ -106,10 +106,17 @@ struct BrickTArgs {
   double* part;                            // optional: the next InstanceNorm's Σy / Σy² per brick
 };
 
-template <int K, int PM>
+// X16 (round 4, one-plane modes): the input is the producer's 16-bit operand plane — a halo
+// position's 32-channel chunk is four 16-B units copied to LDS as they are (G up2 on up1's IN plane,
+// G down1's data gradient on the plane of its dY)
+template <int K, int PM, int X16>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(prec::has_lo<PM>() ? 1 : 2, prec::has_lo<PM>() ? 1 : 2)))
 brickT_x3_kernel(BrickTArgs a) {
+  static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
   constexpr int kHRow = halo_row<PM>();
+  constexpr int ES = X16 ? 2 : 4;                // bytes per input element
+  constexpr int UPP = X16 ? 4 : 8;               // 16-B units per halo position and chunk
+  constexpr int NSL = X16 ? (kHP * 4 + 255) / 256 : kSL;     // units per thread per chunk
   constexpr TSteps<K> ts{};
   constexpr int NS = 2 * TSteps<K>::N;          // (class tap, 16-channel half) steps per chunk
   // weight prefetch distance in steps (divides NS: a ring slot is compile-time in every chunk)
@@ -139,9 +146,9 @@ brickT_x3_kernel(BrickTArgs a) {
     const int hw = pos % kHW, hh = (pos / kHW) % kHH, hd = pos / (kHW * kHH);
     const int id = i0d + hd, ih = i0h + hh, iw = i0w + hw;
     const bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-    hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C * 4 : (int)0x80000000;
+    hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C * ES : (int)0x80000000;
   }
-  const int vol_bytes = a.Di * a.Hi * a.Wi * a.C * 4;     // < 2^31 (brickT_x3_applicable)
+  const int vol_bytes = a.Di * a.Hi * a.Wi * a.C * ES;    // < 2^31 (brickT_x3_applicable)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C, 0, vol_bytes, 0x00020000);
   // uniform scalars (readfirstlane: otherwise the chunk loop bound and every offset derived
@@ -153,17 +160,21 @@ brickT_x3_kernel(BrickTArgs a) {
   __syncthreads();
 
   auto halo_off = [&](int s) __attribute__((always_inline)) {
-    const int e = s * 256 + tid, pos = e >> 3;
+    const int e = s * 256 + tid, pos = e / UPP;
     const int o = pos < kHP ? hoff[pos] : (int)0x80000000;
-    return o + 16 * (e & 7);
+    return o + 16 * (e % UPP);
   };
   auto halo_store = [&](char* buf, int s, const float4& v) __attribute__((always_inline)) {
-    const int e = s * 256 + tid, pos = e >> 3, q = e & 7;
+    const int e = s * 256 + tid, pos = e / UPP, q = e % UPP;
     if (pos < kHP) {
-      uint2 h, lo;
-      prec::split4<PM>(v, h, lo);
-      *reinterpret_cast<uint2*>(buf + pos * kHRow + 8 * q) = h;
-      if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + pos * kHRow + 64 + 8 * q) = lo;
+      if constexpr (X16) {
+        *reinterpret_cast<float4*>(buf + pos * kHRow + 16 * q) = v;    // 8 channels' words, as they are
+      } else {
+        uint2 h, lo;
+        prec::split4<PM>(v, h, lo);
+        *reinterpret_cast<uint2*>(buf + pos * kHRow + 8 * q) = h;
+        if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + pos * kHRow + 64 + 8 * q) = lo;
+      }
     }
   };
   auto bload = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) __attribute__((always_inline)) {
@@ -173,11 +184,11 @@ brickT_x3_kernel(BrickTArgs a) {
 
   // chunk 0's halo: all slices in flight before the first store
   {
-    float4 pv[kSL];
+    float4 pv[NSL];
 #pragma unroll
-    for (int s = 0; s < kSL; ++s) pv[s] = xload(halo_off(s), 0);
+    for (int s = 0; s < NSL; ++s) pv[s] = xload(halo_off(s), 0);
 #pragma unroll
-    for (int s = 0; s < kSL; ++s) halo_store(smem, s, pv[s]);
+    for (int s = 0; s < NSL; ++s) halo_store(smem, s, pv[s]);
   }
 
   // lane li of a class tile = voxel (qd, qh, qw) = (li / 16, (li / 8) & 1, li & 7) of the class
@@ -217,7 +228,7 @@ brickT_x3_kernel(BrickTArgs a) {
     };
     // the next chunk's halo in NB batches (one-plane modes: two, so the 256-register budget of
     // two blocks per CU holds half of it at a time)
-    constexpr int NB = prec::has_lo<PM>() ? 1 : 2, BS = (kSL + NB - 1) / NB;
+    constexpr int NB = prec::has_lo<PM>() ? 1 : 2, BS = (NSL + NB - 1) / NB;
     float4 pv[BS];
     bf16x8 af[2][2];
     a_read(0, af[0]);
@@ -230,12 +241,12 @@ brickT_x3_kernel(BrickTArgs a) {
         if (i == b * (NS / NB)) {
 #pragma unroll
           for (int sl = 0; sl < BS; ++sl)
-            if (b * BS + sl < kSL) pv[sl] = xload(halo_off(b * BS + sl), __builtin_amdgcn_readfirstlane(cn * kBK * 4));
+            if (b * BS + sl < NSL) pv[sl] = xload(halo_off(b * BS + sl), __builtin_amdgcn_readfirstlane(cn * kBK * ES));
         }
         if (i == b * (NS / NB) + kHD) {
 #pragma unroll
           for (int sl = 0; sl < BS; ++sl)
-            if (b * BS + sl < kSL) halo_store(Hn, b * BS + sl, pv[sl]);
+            if (b * BS + sl < NSL) halo_store(Hn, b * BS + sl, pv[sl]);
         }
       }
       const int c = ts.s[i >> 1].c;
@@ -349,7 +360,7 @@ bool brickT_x3_applicable(const IgemmArgs& g) {
 }
 
 // one static per kernel instantiation (the LDS opt-in is per function)
-template <int K, int PM>
+template <int K, int PM, int X16>
 static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
   // halos + offsets; the epilogue rows (4 waves × 32·(8/NP) voxels × kRow) and the statistics
   // reduction after them reuse the same bytes
@@ -359,11 +370,11 @@ static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) 
   const size_t lds = halo > epi ? halo : epi;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM, X16>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((brickT_x3_kernel<K, PM>), dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((brickT_x3_kernel<K, PM, X16>), dim3(blocks), dim3(256), lds, st, a);
 }
 
 size_t brickT_x3_ws_bytes(const IgemmArgs& g) { return (size_t)g.k * g.k * g.k * g.cx * g.ny * sizeof(float); }
@@ -394,9 +405,21 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
     a.part = g.in_part;
     if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
   }
-  if (g.k == 3) launch_brickT<3, PM>(a, (unsigned)blocks, st);
-  else launch_brickT<4, PM>(a, (unsigned)blocks, st);
-  return check_launch("brickT_x3");
+  if constexpr (prec::has_lo<PM>()) {
+    if (g.x16) {
+      set_error("brickT_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
+      return kBadArg;
+    }
+    if (g.k == 3) launch_brickT<3, PM, 0>(a, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 0>(a, (unsigned)blocks, st);
+  } else if (g.x16) {
+    if (g.k == 3) launch_brickT<3, PM, 1>(a, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 1>(a, (unsigned)blocks, st);
+  } else {
+    if (g.k == 3) launch_brickT<3, PM, 0>(a, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 0>(a, (unsigned)blocks, st);
+  }
+  return check_launch(g.x16 ? "brickT_x3(op16)" : "brickT_x3");
 }
 
 int conv_brickT_x3(const IgemmArgs& g, hipStream_t st) { MRAGAN_PREC_DISPATCH(g.x3, return conv_brickT_pm<PM>(g, st)) }

@@ -315,6 +315,8 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
     // 16-bit operand planes: the ResnetBlock convs (forward and whole-grid data gradient) on the
     // brick; the others (the 64³-level stride-2 forward-form convs) on the implicit GEMM
     if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+    // 32-output-channel stride-2 transposed convs (G up2, G down1's data gradient): brickT (round 4)
+    if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
     MRAGAN_CHECK_ARG(a.x3 && a.cx % 32 == 0, "conv: a 16-bit operand plane input needs the bf16 / fp16 implicit GEMM "
                      "(multiples of 32 input channels)");
     return conv_igemm_x3_chunked(a, max_mc, total_m, st);

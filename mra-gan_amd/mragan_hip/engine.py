@@ -410,8 +410,13 @@ class NetPlan:
                     # a stride-2 forward conv next (G down1 / down2): this norm's output only as its
                     # plane — that conv and its weight gradient are its only readers (ABI 14)
                     nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
+                    # — or a 32-output-channel ConvTranspose3d next (G up2: brickT reads the plane, its
+                    # weight gradient takes both operands as planes)
                     only16 = (op16 and not _NO_S2_PLANES and ypad == 0 and nxt is not None and nxt.kind != "block"
-                              and nxt.norm is not None and not nxt.prepad and nxt.conv.s2_plane_ok(sc.h.shape[3]))
+                              and nxt.norm is not None and not nxt.prepad
+                              and (nxt.conv.s2_plane_ok(sc.h.shape[3])
+                                   or (nxt.conv.transposed and nxt.conv.cout == 32
+                                       and nxt.conv.transposed_plane_bwd_ok(sc.h.shape[3]))))
                     if only16:
                         _, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=0, part=part,
                                                                            chunks=chunks)
@@ -495,13 +500,14 @@ class NetPlan:
             # G up1 / up2 in the one-plane modes (ABI 16): the IN backward writes dY only as its plane;
             # the data gradient (forward-form implicit GEMM) and the weight gradient (its gathered
             # operand) read the plane — neither needs the fp32 tensor
-            plane_bwd = (st.norm is not None and sc.inp is not None and conv.transposed_plane_bwd_ok(sc.inp.shape[3])
+            x_any = sc.inp if sc.inp is not None else sc.inp16
+            plane_bwd = (st.norm is not None and x_any is not None and conv.transposed_plane_bwd_ok(x_any.shape[3])
                          and self._op16_active() and not _NO_S2_PLANES and not st.use_bias)
-            # G down2 (its input only a plane already): dY as a plane too — the weight gradient reads
-            # both planes, the data gradient (transposed implicit GEMM) dY's; not down1, whose data
-            # gradient is brickT's (32 output channels, fp32 input)
+            # G down1 / down2 (their inputs only planes already): dY as a plane too — the weight
+            # gradient reads both planes, the data gradient (transposed implicit GEMM, or brickT for
+            # down1's 32 output channels) dY's
             plane_bwd_fwd = (st.norm is not None and sc.inp is None and sc.inp16 is not None and not st.use_bias
-                             and not conv.transposed and conv.cin != 32 and conv.s2_plane_ok(sc.inp16.shape[3])
+                             and not conv.transposed and conv.s2_plane_ok(sc.inp16.shape[3])
                              and self._op16_active() and not _NO_S2_PLANES)
             dh16 = None
             if plane_bwd or plane_bwd_fwd:
@@ -509,9 +515,11 @@ class NetPlan:
                     dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
-                in_spatial = (sc.inp if plane_bwd else sc.inp16).shape[1:4]
-                if need_wgrad and plane_bwd:
+                in_spatial = x_any.shape[1:4]
+                if need_wgrad and plane_bwd and sc.inp is not None:
                     ops.conv3d_wgrad_g16(sc.inp, dh16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
+                elif need_wgrad and plane_bwd:       # G up2 on up1's plane: both operands planes
+                    ops.conv3d_wgrad_op16(sc.inp16, dh16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
                 elif need_wgrad:
                     ops.conv3d_wgrad_op16(dh16, sc.inp16, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
                 bstats = None

@@ -681,6 +681,28 @@ def test_op16_stride2_dgrad_backward_statistics(op16, N, cin, cout, S, act):
     assert torch.equal(part[:n], part_ref[:n])
 
 
+@pytest.mark.parametrize("N,cin,S", [(2, 64, 16), (1, 64, 8), (2, 128, 8)])
+def test_op16_brickT_plane(op16, N, cin, S):
+    """Round 4: brickT (32-output-channel ConvTranspose3d k3 s2 p1 op1: G up2, G down1's data
+    gradient) on the operand plane of its input — output and InstanceNorm partials bit-identical to
+    the fp32-input launch of the same mode."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 29 + cin + S)
+    x16 = ndhwc(torch.randn(N, cin, S, S, S, generator=g).float()).cuda().to(dt)
+    w = torch.randn(cin, 32, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp = pack(ops, w, True, False)
+    osp = (2 * S, 2 * S, 2 * S)
+    part_ref = ops.in_partials_buffer(N, osp, 32, "cuda")
+    y_ref, ch_ref = ops.conv3d_in_stats(x16.float(), wp, 32, 3, 2, 1, osp, None, part_ref, transposed=True)
+    part = ops.in_partials_buffer(N, osp, 32, "cuda")
+    y, ch = ops.conv3d_op16(x16, wp, 32, 3, 2, 1, osp, None, part, transposed=True)
+    assert ch == ch_ref > 0
+    assert torch.equal(y, y_ref)
+    n = N * ch * 32 * 2
+    assert torch.equal(part[:n], part_ref[:n])
+
+
 def test_op16_stride2_plane_rejected_outside_one_plane_modes(ops):
     """ABI 14: the 16-bit gathered operand of wgrad3s2 exists only in the bf16 / fp16 modes."""
     from mragan_hip import MraganError
