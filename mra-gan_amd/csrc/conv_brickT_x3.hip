@@ -150,7 +150,7 @@ brickT_x3_kernel(BrickTArgs a) {
   }
   const int vol_bytes = a.Di * a.Hi * a.Wi * a.C * ES;    // < 2^31 (brickT_x3_applicable)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * a.C, 0, vol_bytes, 0x00020000);
+      const_cast<char*>(reinterpret_cast<const char*>(a.x)) + (int64_t)nb * vol_bytes, 0, vol_bytes, 0x00020000);
   // uniform scalars (readfirstlane: otherwise the chunk loop bound and every offset derived
   // from the chunk index live in VGPRs)
   const int nch = __builtin_amdgcn_readfirstlane(a.C / kBK);
