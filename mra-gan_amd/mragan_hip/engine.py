@@ -35,6 +35,8 @@ _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None   
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
 # A/B switch: MRAGAN_NO_S2_PLANES keeps the stem / down1 InstanceNorm outputs in fp32 (no ABI 14 planes)
 _NO_S2_PLANES = __import__("os").environ.get("MRAGAN_NO_S2_PLANES") is not None
+# brickT on planes (G up2's input, G down1's dY only as planes): MRAGAN_BRICKT_PLANES=0 turns it off
+_BRICKT_PLANES = __import__("os").environ.get("MRAGAN_BRICKT_PLANES", "1") != "0"
 # ABI 15: InstanceNorm statistics finalized in the producing brick's launch (MRAGAN_NO_IN_TICKETS: off)
 _IN_FIN = ops.in_tickets_enabled()
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
@@ -415,7 +417,7 @@ class NetPlan:
                     only16 = (op16 and not _NO_S2_PLANES and ypad == 0 and nxt is not None and nxt.kind != "block"
                               and nxt.norm is not None and not nxt.prepad
                               and (nxt.conv.s2_plane_ok(sc.h.shape[3])
-                                   or (nxt.conv.transposed and nxt.conv.cout == 32
+                                   or (_BRICKT_PLANES and nxt.conv.transposed and nxt.conv.cout == 32
                                        and nxt.conv.transposed_plane_bwd_ok(sc.h.shape[3]))))
                     if only16:
                         _, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=0, part=part,
@@ -508,6 +510,7 @@ class NetPlan:
             # down1's 32 output channels) dY's
             plane_bwd_fwd = (st.norm is not None and sc.inp is None and sc.inp16 is not None and not st.use_bias
                              and not conv.transposed and conv.s2_plane_ok(sc.inp16.shape[3])
+                             and (conv.cin != 32 or _BRICKT_PLANES)
                              and self._op16_active() and not _NO_S2_PLANES)
             dh16 = None
             if plane_bwd or plane_bwd_fwd:

@@ -114,9 +114,10 @@ def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
     finally:
         ops.set_conv_precision("f32")
         ops.set_loss_scale(1.0)
-    # down1 / up2 (32-channel gathered plane: both operands as planes), up1 (64, dense fp32), down2
-    # (both operands as planes, 64-channel gathered)
-    assert set(calls) == {("both", 32), ("g16", 64), ("both", 64)}, f"plane paths that ran: {set(calls)}"
+    # down1 / up2 (32-channel gathered plane; both operands as planes with brickT on planes), up1
+    # (64, dense fp32), down2 (both operands as planes, 64-channel gathered)
+    want = {("both" if engine._BRICKT_PLANES else "g16", 32), ("g16", 64), ("both", 64)}
+    assert set(calls) == want, f"plane paths that ran: {set(calls)}"
     assert torch.equal(lr, lp), (lr - lp).abs().max()
     for k in sr:
         assert torch.equal(sr[k], sp[k]), k
