@@ -1,0 +1,163 @@
+"""`torch.ops.mragan.*`: the C-ABI kernels registered as PyTorch custom operators (SURVEY §7.3,
+§8(b)), for code that composes its own networks from the engine's kernels instead of driving
+the whole CycleGAN step through `models.cycle_gan_model`.
+
+Each op is a `torch.library.custom_op` with a HIP ("cuda") kernel only — there is no CPU kernel,
+so a call on a CPU tensor fails loudly — a fake (meta) kernel for shape propagation, and an
+autograd formula built from the same library's backward kernels.  Activations are NDHWC
+([N, D, H, W, C], fp32, contiguous), the layout of every ops.py call; weights are in torch's own
+layout (Conv3d [Cout][Cin][k][k][k], ConvTranspose3d [Cin][Cout][k][k][k]) and are packed per
+call (one pack launch).  The contraction precision is ops.set_conv_precision's process mode.
+
+  mragan::conv3d           nn.Conv3d / nn.ConvTranspose3d (+ bias, + act)   networks3D.py:185-213
+  mragan::instance_norm    nn.InstanceNorm3d(affine=False) (+ act, + replication-padded output)
+                                                                            networks3D.py:15-24
+  mragan::replication_pad  nn.ReplicationPad3d / the RPad3 of the G stem   networks3D.py:183, 233
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import ops
+
+ACTS = ("none", "relu", "lrelu", "tanh", "sigmoid")
+
+
+def _act(act: str):
+    if act not in ACTS:
+        raise ValueError(f"act must be one of {ACTS}, got {act!r}")
+    return None if act == "none" else act
+
+
+def _conv_geometry(x_shape, weight_shape, stride: int, padding: int, output_padding: int, transposed: bool):
+    N, D, H, W, cin_x = x_shape
+    if len(weight_shape) != 5 or not (weight_shape[2] == weight_shape[3] == weight_shape[4]):
+        raise ValueError(f"conv3d: weight must be [A][B][k][k][k], got {tuple(weight_shape)}")
+    k = weight_shape[2]
+    cin, cout = (weight_shape[0], weight_shape[1]) if transposed else (weight_shape[1], weight_shape[0])
+    if cin != cin_x:
+        raise ValueError(f"conv3d: input has {cin_x} channels, weight expects {cin}")
+    if transposed:
+        f = lambda n: ops.convT_out_size(n, k, stride, padding, output_padding)
+    else:
+        if output_padding:
+            raise ValueError("conv3d: output_padding applies to the transposed form only")
+        f = lambda n: ops.conv_out_size(n, k, stride, padding)
+    return N, (D, H, W), cin, cout, k, (f(D), f(H), f(W))
+
+
+def _packs(weight: torch.Tensor, transposed: bool):
+    """(forward pack, data-gradient pack) of a torch-layout weight, as engine.ConvLayer.packs."""
+    w = weight.contiguous()
+    A, B, T = w.shape[0], w.shape[1], w.shape[2] ** 3
+    wf = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+    wb = torch.empty_like(wf)
+    ops.pack_weight(w, A, B, T, transposed, wf)       # → [t][Cout][Cin]
+    ops.pack_weight(w, A, B, T, not transposed, wb)   # → [t][Cin][Cout]
+    return wf, wb
+
+
+@torch.library.custom_op("mragan::conv3d", mutates_args=(), device_types="cuda")
+def conv3d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
+           output_padding: int, transposed: bool, act: str) -> torch.Tensor:
+    N, _, cin, cout, k, osp = _conv_geometry(x.shape, weight.shape, stride, padding, output_padding, transposed)
+    wf, _ = _packs(weight, transposed)
+    return ops.conv3d(x.contiguous(), wf, cout, k, stride, padding, osp, bias=bias, act=_act(act),
+                      transposed=transposed)
+
+
+@conv3d.register_fake
+def _(x, weight, bias, stride, padding, output_padding, transposed, act):
+    N, _, _, cout, _, osp = _conv_geometry(x.shape, weight.shape, stride, padding, output_padding, transposed)
+    return x.new_empty((N,) + tuple(osp) + (cout,))
+
+
+def _conv_setup(ctx, inputs, output):
+    x, weight, bias, stride, padding, output_padding, transposed, act = inputs
+    ctx.save_for_backward(x, weight, output if act != "none" else None)
+    ctx.cfg = (bias is not None, stride, padding, transposed, act)
+
+
+def _conv_backward(ctx, dy):
+    x, weight, y = ctx.saved_tensors
+    has_bias, stride, padding, transposed, act = ctx.cfg
+    g = dy.contiguous()
+    if act != "none":                                  # act'(y) from the saved output
+        g2 = torch.empty_like(g)
+        ops.act_bwd(y, [g], act, g2)
+        g = g2
+    _, in_sp, cin, cout, k, _ = _conv_geometry(x.shape, weight.shape, stride, padding, 0, transposed)
+    dx = dw = db = None
+    if ctx.needs_input_grad[0]:
+        _, wb = _packs(weight, transposed)
+        dx = ops.conv3d(g, wb, cin, k, stride, padding, in_sp, transposed=not transposed)
+    if ctx.needs_input_grad[1]:
+        dw = torch.empty(weight.shape, device=weight.device, dtype=torch.float32)
+        if transposed:
+            ops.conv3d_wgrad(x.contiguous(), g, k, stride, padding, dw, False)     # dW[Cin][Cout][t]
+        else:
+            ops.conv3d_wgrad(g, x.contiguous(), k, stride, padding, dw, False)     # dW[Cout][Cin][t]
+    if has_bias and ctx.needs_input_grad[2]:
+        db = torch.empty(cout, device=dy.device, dtype=torch.float32)
+        ops.channel_sum(g, db)
+    return dx, dw, db, None, None, None, None, None
+
+
+conv3d.register_autograd(_conv_backward, setup_context=_conv_setup)
+
+
+@torch.library.custom_op("mragan::instance_norm", mutates_args=(), device_types="cuda")
+def instance_norm(x: torch.Tensor, act: str, ypad: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    y, mean, rstd = ops.instnorm_fwd(x.contiguous(), act=_act(act), ypad=ypad)
+    return y, mean, rstd
+
+
+@instance_norm.register_fake
+def _(x, act, ypad):
+    N, D, H, W, C = x.shape
+    return (x.new_empty((N, D + 2 * ypad, H + 2 * ypad, W + 2 * ypad, C)), x.new_empty((N, C)),
+            x.new_empty((N, C)))
+
+
+def _in_setup(ctx, inputs, output):
+    x, act, ypad = inputs
+    _, mean, rstd = output
+    ctx.save_for_backward(x, mean, rstd)
+    ctx.cfg = (act, ypad)
+    ctx.mark_non_differentiable(mean, rstd)
+
+
+def _in_backward(ctx, dy, _dmean, _drstd):
+    x, mean, rstd = ctx.saved_tensors
+    act, ypad = ctx.cfg
+    dx = ops.instnorm_bwd(x.contiguous(), mean, rstd, dy.contiguous(), dypad=ypad, act=_act(act))
+    return dx, None, None
+
+
+instance_norm.register_autograd(_in_backward, setup_context=_in_setup)
+
+
+@torch.library.custom_op("mragan::replication_pad", mutates_args=(), device_types="cuda")
+def replication_pad(x: torch.Tensor, p: int) -> torch.Tensor:
+    return ops.rpad(x.contiguous(), p)
+
+
+@replication_pad.register_fake
+def _(x, p):
+    N, D, H, W, C = x.shape
+    return x.new_empty((N, D + 2 * p, H + 2 * p, W + 2 * p, C))
+
+
+def _rpad_setup(ctx, inputs, output):
+    ctx.p = inputs[1]
+
+
+def _rpad_backward(ctx, dy):
+    return ops.rpad_fold(dy.contiguous(), ctx.p), None
+
+
+replication_pad.register_autograd(_rpad_backward, setup_context=_rpad_setup)
+
+OPS: List[str] = ["conv3d", "instance_norm", "replication_pad"]
