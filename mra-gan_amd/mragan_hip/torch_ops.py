@@ -13,6 +13,12 @@ call (one pack launch).  The contraction precision is ops.set_conv_precision's p
   mragan::instance_norm    nn.InstanceNorm3d(affine=False) (+ act, + replication-padded output)
                                                                             networks3D.py:15-24
   mragan::replication_pad  nn.ReplicationPad3d / the RPad3 of the G stem   networks3D.py:183, 233
+  mragan::l1_loss          nn.L1Loss (the cycle / identity losses)          cycle_gan_model.py:104-105
+  mragan::gan_loss         GANLoss (BCE on D's sigmoid output, or MSE)      networks3D.py:130-150
+  mragan::adam_            torch.optim.Adam step on a flat parameter buffer cycle_gan_model.py:107-110
+
+The loss ops' gradients are the kernels' (sign(a − b)/n, dGANLoss/dp) times the incoming gradient;
+they need the process-wide loss scale at 1 (ops.set_loss_scale), which they check.
 """
 from __future__ import annotations
 
@@ -160,4 +166,87 @@ def _rpad_backward(ctx, dy):
 
 replication_pad.register_autograd(_rpad_backward, setup_context=_rpad_setup)
 
-OPS: List[str] = ["conv3d", "instance_norm", "replication_pad"]
+
+def _unit_loss_scale(name: str):
+    if ops.get_loss_scale() != 1.0:
+        raise RuntimeError(f"mragan::{name} backward: the process-wide loss scale is {ops.get_loss_scale()}, "
+                           "expected 1 (the kernels fold it into the gradient)")
+
+
+@torch.library.custom_op("mragan::l1_loss", mutates_args=(), device_types="cuda")
+def l1_loss(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if a.shape != b.shape:
+        raise ValueError(f"l1_loss: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    loss = torch.empty((), device=a.device, dtype=torch.float32)
+    ops.l1_loss(a.contiguous(), b.contiguous(), 1.0, loss, None)
+    return loss
+
+
+@l1_loss.register_fake
+def _(a, b):
+    return a.new_empty(())
+
+
+def _l1_setup(ctx, inputs, output):
+    ctx.save_for_backward(*inputs)
+
+
+def _l1_backward(ctx, dloss):
+    a, b = ctx.saved_tensors
+    _unit_loss_scale("l1_loss")
+    g = torch.empty(a.shape, device=a.device, dtype=torch.float32)
+    slot = torch.empty((), device=a.device, dtype=torch.float32)
+    ops.l1_loss(a.contiguous(), b.contiguous(), 1.0, slot, g)
+    g = g * dloss
+    return (g if ctx.needs_input_grad[0] else None), (-g if ctx.needs_input_grad[1] else None)
+
+
+l1_loss.register_autograd(_l1_backward, setup_context=_l1_setup)
+
+
+@torch.library.custom_op("mragan::gan_loss", mutates_args=(), device_types="cuda")
+def gan_loss(p: torch.Tensor, target: float, lsgan: bool) -> torch.Tensor:
+    loss = torch.empty((), device=p.device, dtype=torch.float32)
+    ops.gan_loss(p.contiguous(), target, lsgan, 1.0, loss, None)
+    return loss
+
+
+@gan_loss.register_fake
+def _(p, target, lsgan):
+    return p.new_empty(())
+
+
+def _gan_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[0])
+    ctx.cfg = (inputs[1], inputs[2])
+
+
+def _gan_backward(ctx, dloss):
+    (p,) = ctx.saved_tensors
+    target, lsgan = ctx.cfg
+    _unit_loss_scale("gan_loss")
+    dp = torch.empty(p.shape, device=p.device, dtype=torch.float32)
+    slot = torch.empty((), device=p.device, dtype=torch.float32)
+    ops.gan_loss(p.contiguous(), target, lsgan, 1.0, slot, dp)
+    return dp * dloss, None, None
+
+
+gan_loss.register_autograd(_gan_backward, setup_context=_gan_setup)
+
+
+@torch.library.custom_op("mragan::adam_", mutates_args=("param", "exp_avg", "exp_avg_sq"), device_types="cuda")
+def adam_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, lr: float,
+          beta1: float, beta2: float, eps: float, step: int, grad_scale: float) -> None:
+    """One torch.optim.Adam step (amsgrad False, weight_decay 0) in place; `step` counts from 1."""
+    for t, n in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != param.numel():
+            raise ValueError(f"adam_: {n} must be a contiguous float32 tensor of {param.numel()} elements")
+    ops.adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, step, grad_scale)
+
+
+@adam_.register_fake
+def _(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, step, grad_scale):
+    return None
+
+
+OPS: List[str] = ["conv3d", "instance_norm", "replication_pad", "l1_loss", "gan_loss", "adam_"]

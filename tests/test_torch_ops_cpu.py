@@ -37,6 +37,15 @@ def test_instance_norm_and_pad_fake_shapes():
     assert tuple(z.shape) == (2, 22, 22, 22, 128)
 
 
+def test_loss_and_adam_fake():
+    with FakeTensorMode():
+        a = torch.empty(2, 8, 8, 8, 1)
+        assert torch.ops.mragan.l1_loss(a, a).shape == ()
+        assert torch.ops.mragan.gan_loss(a, 1.0, True).shape == ()
+        p = torch.empty(10)
+        assert torch.ops.mragan.adam_(p, p, p, p, 1e-3, 0.5, 0.999, 1e-8, 1, 1.0) is None
+
+
 def test_geometry_errors():
     with FakeTensorMode():
         x = torch.empty(1, 8, 8, 8, 4)

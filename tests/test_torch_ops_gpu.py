@@ -127,3 +127,49 @@ def test_composed_block_matches_torch(tops):
     assert rel(ncdhw(y.detach()), yr.detach()) < TOL
     y.backward(ndhwc(dy.float()).cuda())
     assert rel(ncdhw(xd.grad), xr.grad) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 1000, 262144 + 17])
+def test_l1_loss_op_and_grad(tops, n):
+    g = torch.Generator().manual_seed(n)
+    a, b = torch.randn(n, generator=g, dtype=torch.float64), torch.randn(n, generator=g, dtype=torch.float64)
+    ar, br = a.clone().requires_grad_(), b.clone().requires_grad_()
+    lr_ = F.l1_loss(ar, br)
+    (2.5 * lr_).backward()
+    ad, bd = a.float().cuda().requires_grad_(), b.float().cuda().requires_grad_()
+    loss = torch.ops.mragan.l1_loss(ad, bd)
+    assert abs(float(loss) - float(lr_)) <= 1e-5 * abs(float(lr_))
+    (2.5 * loss).backward()
+    assert rel(ad.grad, ar.grad) < TOL
+    assert rel(bd.grad, br.grad) < TOL
+
+
+@pytest.mark.parametrize("lsgan,target", [(True, 1.0), (True, 0.0), (False, 1.0), (False, 0.0)])
+def test_gan_loss_op_and_grad(tops, lsgan, target):
+    g = torch.Generator().manual_seed(9)
+    p = torch.rand(2, 1, 6, 6, 6, generator=g, dtype=torch.float64) * 0.9 + 0.05
+    pr = p.clone().requires_grad_()
+    t = torch.full_like(p, target)
+    lr_ = F.mse_loss(pr, t) if lsgan else F.binary_cross_entropy(pr, t)
+    lr_.backward()
+    pd = ndhwc(p.float()).cuda().requires_grad_()
+    loss = torch.ops.mragan.gan_loss(pd, target, lsgan)
+    assert abs(float(loss) - float(lr_)) <= 1e-5 * max(abs(float(lr_)), 1e-6)
+    loss.backward()
+    assert rel(ncdhw(pd.grad), pr.grad) < TOL
+
+
+def test_adam_op_matches_torch(tops):
+    g = torch.Generator().manual_seed(4)
+    n = 4097
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) for _ in range(3)]
+    pr = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([pr], lr=2e-4, betas=(0.5, 0.999), eps=1e-8)
+    p, m, v = p0.cuda(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    for step, gr in enumerate(grads, 1):
+        pr.grad = gr.clone()
+        opt.step()
+        torch.ops.mragan.adam_(p, gr.cuda(), m, v, 2e-4, 0.5, 0.999, 1e-8, step, 1.0)
+    assert rel(p, pr.detach()) < 1e-6
+    assert rel(m, opt.state[pr]["exp_avg"]) < 1e-6
