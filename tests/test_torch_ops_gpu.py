@@ -173,3 +173,17 @@ def test_adam_op_matches_torch(tops):
         torch.ops.mragan.adam_(p, gr.cuda(), m, v, 2e-4, 0.5, 0.999, 1e-8, step, 1.0)
     assert rel(p, pr.detach()) < 1e-6
     assert rel(m, opt.state[pr]["exp_avg"]) < 1e-6
+
+
+def test_opcheck_registrations(tops):
+    """torch.library.opcheck: schema (no hidden mutation or aliasing), autograd registration and
+    the fake kernels against the real outputs, one sample per op."""
+    checks = ("test_schema", "test_autograd_registration", "test_faketensor")
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1, 6, 6, 6, 8, generator=g).cuda().requires_grad_()
+    w = (torch.randn(16, 8, 3, 3, 3, generator=g) * 0.1).cuda().requires_grad_()
+    torch.library.opcheck(torch.ops.mragan.conv3d.default, (x, w, None, 2, 1, 0, False, "relu"), test_utils=checks)
+    torch.library.opcheck(torch.ops.mragan.instance_norm.default, (x, "lrelu", 1), test_utils=checks)
+    torch.library.opcheck(torch.ops.mragan.replication_pad.default, (x, 2), test_utils=checks)
+    b = torch.randn(x.shape, generator=g).cuda()
+    torch.library.opcheck(torch.ops.mragan.l1_loss.default, (x, b), test_utils=checks)
