@@ -138,7 +138,7 @@ def test_l1_loss_op_and_grad(tops, n):
     (2.5 * lr_).backward()
     ad, bd = a.float().cuda().requires_grad_(), b.float().cuda().requires_grad_()
     loss = torch.ops.mragan.l1_loss(ad, bd)
-    assert abs(float(loss) - float(lr_)) <= 1e-5 * abs(float(lr_))
+    assert abs(float(loss.detach()) - float(lr_.detach())) <= 1e-5 * abs(float(lr_.detach()))
     (2.5 * loss).backward()
     assert rel(ad.grad, ar.grad) < TOL
     assert rel(bd.grad, br.grad) < TOL
@@ -154,7 +154,7 @@ def test_gan_loss_op_and_grad(tops, lsgan, target):
     lr_.backward()
     pd = ndhwc(p.float()).cuda().requires_grad_()
     loss = torch.ops.mragan.gan_loss(pd, target, lsgan)
-    assert abs(float(loss) - float(lr_)) <= 1e-5 * max(abs(float(lr_)), 1e-6)
+    assert abs(float(loss.detach()) - float(lr_.detach())) <= 1e-5 * max(abs(float(lr_.detach())), 1e-6)
     loss.backward()
     assert rel(ncdhw(pd.grad), pr.grad) < TOL
 
