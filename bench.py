@@ -84,6 +84,9 @@ def parse():
                     help="issue the step on one stream (default: G_A / G_B and D_A / D_B chains on two)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo only for rehearsal")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--full-out", default=os.path.join("gpurun_out", "bench_full.json"),
+                    help="file for the full report (every launch class of every leg); the printed line keeps the "
+                         "largest few and names this path; '' for none")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
     return ap.parse_args()
@@ -273,6 +276,29 @@ def mfma_peak_of(precision):
     return {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x3": MFMA_BF16_PEAK_TFLOPS / 3}.get(precision, MFMA_BF16_PEAK_TFLOPS)
 
 
+VALU_CONV_KERNELS = ("thin_dot", "thin_k", "thin_n", "thin_wgrad", "thin_naive")
+FP64_ACC_KERNELS = ("thin_n_class8", "thin_n_tile8")
+
+
+def kernel_arith(kernels, precision):
+    """The arithmetic the named kernels really run (the roofline label): the thin VALU
+    convolutions are dot products on the vector ALUs (two accumulate in fp64) whatever the
+    contraction mode; InstanceNorm / elementwise kernels move bytes; the rest are MFMA kernels of
+    the mode."""
+    names = [k for k in kernels.split(";") if k]
+    conv = [k for k in names if not k.startswith(("pack", "in_", "wgrad_reduce", "thin_wgrad_reduce", "channel_sum",
+                                                   "conv_splitk_reduce", "thin1_wgrad_reduce"))] or names
+    head = conv[0] if conv else ""
+    rnd = {"f32": "f32", "bf16x3": "f32", "bf16": "bf16-rounded", "fp16": "fp16-rounded"}[precision]
+    if head.startswith(FP64_ACC_KERNELS):
+        return f"VALU dot, {rnd} operands, fp64 accumulate"
+    if head.startswith(VALU_CONV_KERNELS):
+        return f"VALU dot, {rnd} operands, f32 accumulate"
+    if head.startswith(("in_", "rpad", "act_bwd", "concat", "split", "adam", "l1", "gan", "fill")):
+        return "HBM-bound elementwise"
+    return {"bf16x3": "bf16x3 split MFMA", "f32": "f32 MFMA", "bf16": "bf16 MFMA", "fp16": "fp16 MFMA"}[precision]
+
+
 def make_inputs(shape, n, rank):
     g = torch.Generator().manual_seed(1000 + rank)
     return [(torch.randn(shape, generator=g).cuda(), torch.randn(shape, generator=g).cuda()) for _ in range(n)]
@@ -324,7 +350,7 @@ def kernel_classes(model, inputs, reps=10):
     return ops.TIMER.classes(reps)
 
 
-def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_top=40, nc=None, netG=None):
+def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=None, netG=None):
     """One workload: the timed step in `precision`, its launch classes and roofline, and the same
     protocol in each precision of `alts` (a fresh model each)."""
     from mragan_hip import ops
@@ -343,8 +369,7 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
         m = build_model(args, p, batch, nc, netG)
         e, med = time_steps(m, inputs, args.warmup, args.steps, barrier, dist)
         alt[p] = {"value": round(world * batch * args.steps / e, 3), "ms_per_step": round(1e3 * e / args.steps, 3),
-                  "ms_per_step_median": round(med, 3), "dtype": DTYPE[p], "dtype_detail": DTYPE_DETAIL[p],
-                  "timing": "same protocol as the leg's headline (barrier + synchronize around K steps, max over ranks)"}
+                  "ms_per_step_median": round(med, 3), "dtype": DTYPE[p]}
         del m
         torch.cuda.empty_cache()
     ops.set_conv_precision(precision)
@@ -381,8 +406,8 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
     if alt:
         leg["alt_precisions"] = alt
     if classes:
-        prec = {"bf16x3": "bf16x3 split MFMA", "f32": "f32 MFMA", "bf16": "bf16 MFMA", "fp16": "fp16 MFMA"}[precision]
         dom_cls, dom = next(iter(classes.items()))
+        prec = kernel_arith(dom["kernels"], precision)
         if dom["flops"]:
             achieved = dom["flops"] / (dom["mean_ms"] / 1e3) / 1e12
             peak, unit, bound = mfma_peak, "TFLOP/s", "mfma"
@@ -404,9 +429,56 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, n_to
                  mean_us=round(1e3 * v["mean_ms"], 2),
                  frac=round((v["flops"] / (v["mean_ms"] / 1e3) / 1e12) / mfma_peak if v["flops"] else
                             (v["bytes"] / (v["mean_ms"] / 1e3) / 1e9) / HBM_PEAK_GBS, 4))
-            for c, v in list(classes.items())[:n_top]]
+            for c, v in classes.items()]
         leg["kernel_ms_per_step_serial"] = round(sum(v["total_ms"] for v in classes.values()), 3)
     return leg
+
+
+LINE_CAP = 7000        # bytes: the driver keeps the last 8000 bytes of stdout; the line must fit whole
+
+
+def compact_line(res, full_out, n_head=10, n_leg=4):
+    """The printed line: the full report (every launch class of every leg, all fields) goes to
+    `full_out`, named in the line; the line keeps the headline's `n_head` and each leg's `n_leg`
+    largest launch classes as compact rows [class, kernels, launches/step, us/launch, frac], drops
+    the legs' explanatory strings, and trims rows further until it fits LINE_CAP."""
+    full_path = None
+    if full_out:
+        if not os.path.isabs(full_out):
+            full_out = os.path.join(ROOT, full_out)
+        try:
+            os.makedirs(os.path.dirname(full_out), exist_ok=True)
+            with open(full_out, "w") as fh:
+                json.dump(res, fh, indent=1)
+            full_path = os.path.relpath(full_out, ROOT)
+        except OSError:
+            full_path = None
+
+    def rows(tk, n):
+        return [[r["cls"], r["kernels"], r["launches_per_step"], r["mean_us"], r["frac"]] for r in tk[:n]]
+
+    out = json.loads(json.dumps(res))
+    out["top_kernels_full"] = full_path
+    out["top_kernels_cols"] = ["class", "kernels", "launches_per_step", "us_per_launch", "frac"]
+    for leg in out.get("legs", {}).values():
+        for k in ("dtype_detail", "kernel_ms_per_step_serial", "workload", "step_launch", "step_tflop"):
+            leg.pop(k, None)
+        for k in ("formula", "note", "BW_hbm_gbs", "P_mfma_tflops", "F_tflop", "B_ew_elem_bytes"):
+            leg.get("step_roofline", {}).pop(k, None)
+        for k in ("timing", "traffic_source", "flop_per_launch", "bytes_per_launch", "ms_per_step"):
+            leg.get("roofline", {}).pop(k, None)
+    for nh, nl in ((n_head, n_leg), (8, 3), (6, 2), (5, 1), (4, 0), (3, 0), (0, 0)):
+        if "top_kernels" in res:
+            out["top_kernels"] = rows(res["top_kernels"], nh)
+        for key, leg in res.get("legs", {}).items():
+            if "top_kernels" in leg:
+                if nl:
+                    out["legs"][key]["top_kernels"] = rows(leg["top_kernels"], nl)
+                else:
+                    out["legs"][key].pop("top_kernels", None)
+        if len(json.dumps(out)) <= LINE_CAP:
+            break
+    return out
 
 
 def main():
@@ -452,7 +524,7 @@ def main():
         key = f"{S}^3 b{bsz}" + (f" nc{nc}" if nc != args.nc else "") + (f" {netG}" if netG != args.netG else "") + \
             (f" {prec}" if prec != args.precision else "")
         alt_l = [p for p in args.leg_alt_precisions.split(",") if p and p != prec] if prec == args.precision else []
-        legs[key] = run_leg(args, S, bsz, prec, alt_l, barrier, dist, world, rank, n_top=12, nc=nc, netG=netG)
+        legs[key] = run_leg(args, S, bsz, prec, alt_l, barrier, dist, world, rank, nc=nc, netG=netG)
         legs[key]["config"] = {"patch": S, "batch": bsz, "nc": nc, "netG": netG, "conv_precision": prec}
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
@@ -492,7 +564,7 @@ def main():
         res["legs"] = legs
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_child(args)
-    print(json.dumps(res), flush=True)
+    print(json.dumps(compact_line(res, args.full_out)), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

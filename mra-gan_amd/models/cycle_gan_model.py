@@ -151,6 +151,9 @@ class _Lanes:
         from mragan_hip import ops
         self._ops = ops
         cur = torch.cuda.current_stream()
+        if ops.in_tickets_enabled():
+            # the ticket pool's zero-fill must precede both lanes' first ticket draw
+            ops.ensure_ticket_pool(cur.device)
         self.s = [cur, aux if parallel else cur]
         self.parallel = parallel
         if parallel:

@@ -225,14 +225,27 @@ def in_tickets_enabled() -> bool:
     return not _NO_IN_TICKETS
 
 
-def _ticket_ptr(n: int, device) -> int:
+def ensure_ticket_pool(device) -> torch.Tensor:
+    """The device's zeroed ticket pool, created on the device's default stream and synchronized
+    before it is returned: every lane's first kernel that draws a ticket runs after the fill,
+    whichever stream it is on (call before forking lanes; _ticket_ptr falls back to it)."""
     dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     pool = _tickets.get(dev)
     if pool is None:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("in-launch InstanceNorm finalize: the ticket pool must be allocated before a graph "
                                "capture (run one eager step first)")
-        pool = _tickets[dev] = torch.zeros(_TICKET_SLOTS, device=dev, dtype=torch.int32)
+        with torch.cuda.stream(torch.cuda.default_stream(dev)):
+            pool = torch.zeros(_TICKET_SLOTS, device=dev, dtype=torch.int32)
+        torch.cuda.synchronize(dev)
+        _tickets[dev] = pool
+    return pool
+
+
+def _ticket_ptr(n: int, device) -> int:
+    pool = ensure_ticket_pool(device)
     if n > _TICKET_SLOTS:
         raise ValueError(f"in-launch finalize: {n} ticket slots > the pool's {_TICKET_SLOTS}")
     if _ticket_next[0] + n > _TICKET_SLOTS:

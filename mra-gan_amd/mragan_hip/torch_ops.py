@@ -7,7 +7,8 @@ so a call on a CPU tensor fails loudly — a fake (meta) kernel for shape propag
 autograd formula built from the same library's backward kernels.  Activations are NDHWC
 ([N, D, H, W, C], fp32, contiguous), the layout of every ops.py call; weights are in torch's own
 layout (Conv3d [Cout][Cin][k][k][k], ConvTranspose3d [Cin][Cout][k][k][k]) and are packed per
-call (one pack launch).  The contraction precision is ops.set_conv_precision's process mode.
+call (one pack launch in the forward, one for the data gradient in the backward).  Every tensor
+argument must be float32 on the input's device (checked: the kernels take raw pointers).  The contraction precision is ops.set_conv_precision's process mode.
 
   mragan::conv3d           nn.Conv3d / nn.ConvTranspose3d (+ bias, + act)   networks3D.py:185-213
   mragan::instance_norm    nn.InstanceNorm3d(affine=False) (+ act, + replication-padded output)
@@ -54,22 +55,37 @@ def _conv_geometry(x_shape, weight_shape, stride: int, padding: int, output_padd
     return N, (D, H, W), cin, cout, k, (f(D), f(H), f(W))
 
 
-def _packs(weight: torch.Tensor, transposed: bool):
-    """(forward pack, data-gradient pack) of a torch-layout weight, as engine.ConvLayer.packs."""
+def _need_f32(t: Optional[torch.Tensor], name: str, device: torch.device, numel: Optional[int] = None):
+    """The kernels take raw fp32 device pointers: refuse any other dtype, a tensor on another
+    device (a host pointer handed to a device kernel) or a wrong element count before the call."""
+    if t is None:
+        return
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name} must be on {device}, got {t.device}")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} must have {numel} elements, got {t.numel()}")
+
+
+def _pack(weight: torch.Tensor, transposed: bool, data_gradient: bool) -> torch.Tensor:
+    """One pack of a torch-layout weight, as engine.ConvLayer.packs: the forward pack
+    [t][Cout][Cin] (data_gradient False) or the data-gradient pack [t][Cin][Cout] — one launch."""
     w = weight.contiguous()
     A, B, T = w.shape[0], w.shape[1], w.shape[2] ** 3
-    wf = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
-    wb = torch.empty_like(wf)
-    ops.pack_weight(w, A, B, T, transposed, wf)       # → [t][Cout][Cin]
-    ops.pack_weight(w, A, B, T, not transposed, wb)   # → [t][Cin][Cout]
-    return wf, wb
+    wp = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+    ops.pack_weight(w, A, B, T, transposed != data_gradient, wp)
+    return wp
 
 
 @torch.library.custom_op("mragan::conv3d", mutates_args=(), device_types="cuda")
 def conv3d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
            output_padding: int, transposed: bool, act: str) -> torch.Tensor:
     N, _, cin, cout, k, osp = _conv_geometry(x.shape, weight.shape, stride, padding, output_padding, transposed)
-    wf, _ = _packs(weight, transposed)
+    _need_f32(x, "conv3d: x", x.device)
+    _need_f32(weight, "conv3d: weight", x.device)
+    _need_f32(bias, "conv3d: bias", x.device, cout)
+    wf = _pack(weight, transposed, data_gradient=False)
     return ops.conv3d(x.contiguous(), wf, cout, k, stride, padding, osp, bias=bias, act=_act(act),
                       transposed=transposed)
 
@@ -90,6 +106,7 @@ def _conv_backward(ctx, dy):
     x, weight, y = ctx.saved_tensors
     has_bias, stride, padding, transposed, act = ctx.cfg
     g = dy.contiguous()
+    _need_f32(g, "conv3d backward: grad_output", x.device)
     if act != "none":                                  # act'(y) from the saved output
         g2 = torch.empty_like(g)
         ops.act_bwd(y, [g], act, g2)
@@ -97,7 +114,7 @@ def _conv_backward(ctx, dy):
     _, in_sp, cin, cout, k, _ = _conv_geometry(x.shape, weight.shape, stride, padding, 0, transposed)
     dx = dw = db = None
     if ctx.needs_input_grad[0]:
-        _, wb = _packs(weight, transposed)
+        wb = _pack(weight, transposed, data_gradient=True)
         dx = ops.conv3d(g, wb, cin, k, stride, padding, in_sp, transposed=not transposed)
     if ctx.needs_input_grad[1]:
         dw = torch.empty(weight.shape, device=weight.device, dtype=torch.float32)
@@ -177,6 +194,8 @@ def _unit_loss_scale(name: str):
 def l1_loss(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if a.shape != b.shape:
         raise ValueError(f"l1_loss: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    _need_f32(a, "l1_loss: a", a.device)
+    _need_f32(b, "l1_loss: b", a.device)
     loss = torch.empty((), device=a.device, dtype=torch.float32)
     ops.l1_loss(a.contiguous(), b.contiguous(), 1.0, loss, None)
     return loss
@@ -206,6 +225,7 @@ l1_loss.register_autograd(_l1_backward, setup_context=_l1_setup)
 
 @torch.library.custom_op("mragan::gan_loss", mutates_args=(), device_types="cuda")
 def gan_loss(p: torch.Tensor, target: float, lsgan: bool) -> torch.Tensor:
+    _need_f32(p, "gan_loss: p", p.device)
     loss = torch.empty((), device=p.device, dtype=torch.float32)
     ops.gan_loss(p.contiguous(), target, lsgan, 1.0, loss, None)
     return loss

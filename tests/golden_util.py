@@ -73,3 +73,17 @@ def is_pre_in_bias(net, key, n_layers_D=3):
 def _is_g_head(key):
     # the head conv is the last conv of the generator; its index depends on n_blocks
     return key in ("model.26.bias", "model.23.bias")
+
+
+def over_envelope(err, env) -> bool:
+    """A per-tensor gate's verdict: True unless err is a finite number within env.  A NaN error
+    compares False against any bound, so `err > env` would let a NaN tensor through; this does not."""
+    return not (np.isfinite(err) and err <= env)
+
+
+def assert_finite(label, *arrays):
+    """Every value finite (a NaN / Inf anywhere fails the gate, whatever its error norm says)."""
+    for a in arrays:
+        a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+        bad = int((~np.isfinite(a)).sum())
+        assert bad == 0, f"{label}: {bad} non-finite values"

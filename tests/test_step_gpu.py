@@ -37,7 +37,8 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import CASE_KW, available_cases, inputs, is_pre_in_bias, load, rel_err, sampled
+from golden_util import (CASE_KW, assert_finite, available_cases, inputs, is_pre_in_bias, load, over_envelope, rel_err,
+                         sampled)
 
 pytestmark = pytest.mark.gpu
 
@@ -69,12 +70,12 @@ PARAMS = [(c, p) for p in PRECISIONS for c in CASES]
 # rounded-operand step (below)
 REDUCED = ("bf16", "fp16")
 # per-tensor gradient outlier budget (all gradient gates): at most this fraction of the parameter
-# tensors (and at least 2) may exceed their envelope, none by more than OUTLIER_X×.  Measured
-# (r04g, every case × precision, printed by check_outliers): worst factor 2.73× (fp16 / bf16
-# D-layer biases), so 5× (was 20×); every case ≤ 3 tensors except the exact-f32 UNet 64³ fixture,
-# 6 of 36 at ≤ 2.15× — its fixture holds one perturbed fp64 realisation, which under-states the
-# envelope of its kink-dominated tensors — so the fraction stays 20 %.
-OUTLIER_FRAC, OUTLIER_X = 0.2, 5.0
+# tensors (and at least 2) may exceed their envelope, none by more than OUTLIER_X×.  Both constants
+# are fixed by the protocol, not by a GPU run: the envelope of each tensor is the largest of the
+# reference's fp32 error and the fp64 gradient's movement under ≥ 3 input-perturbation
+# realisations (the BASELINE-size fixtures store three, tools/gen_fixtures.py; the small cases
+# compute three at test time), so a tensor past it is a tail event of an estimated spread.
+OUTLIER_FRAC, OUTLIER_X = 0.1, 5.0
 
 
 def check_outliers(label, bad, n_params):
@@ -82,7 +83,7 @@ def check_outliers(label, bad, n_params):
     print(f"{label}: {len(bad)}/{n_params} parameter tensors over their envelope"
           + (f"; worst {worst[0]}.{worst[1]} at {worst[2] / worst[3]:.2f}x" if worst else ""))
     assert len(bad) <= max(2, int(OUTLIER_FRAC * n_params)), bad
-    assert all(r <= OUTLIER_X * env for _, _, r, env in bad), bad
+    assert all(np.isfinite(r) and r <= OUTLIER_X * env for _, _, r, env in bad), bad
 
 
 @pytest.fixture(scope="module", params=PARAMS, ids=[f"{c}-{p}" for c, p in PARAMS])
@@ -120,6 +121,19 @@ def stepped(request, tmp_path_factory):
     from mragan_hip import ops
     ops.set_conv_precision("f32")
     return name, z, meta, init, history, snap
+
+
+def test_all_finite(stepped):
+    """Every loss, generated volume, gradient, updated parameter and running statistic of the
+    snapshot is finite in full (the sampled gates below see 64-256 elements per tensor)."""
+    name, _, meta, _, history, snap = stepped
+    assert_finite(f"{name} losses", np.stack(history))
+    for vis, t in snap["vis"].items():
+        assert_finite(vis, t)
+    for what in ("grads", "params", "bufs"):
+        for net, d in snap[what].items():
+            for k, t in d.items():
+                assert_finite(f"{what} {net}.{k}", t)
 
 
 def test_init_bit_exact(stepped):
@@ -173,6 +187,7 @@ def _pgap(p, mode, key, got):
     w32 = p[f"{mode}/emu32/{key}/val"]
     gap = max(rel_err(p[f"{mode}/{r}/{key}/val"], w64) for r in _cal_runs(p, mode))
     g = flat[torch.from_numpy(p[f"{mode}/emu64/{key}/idx"])].numpy()
+    assert_finite(key, g)
     return rel_err(g, w64), gap, g, w64, w32
 
 
@@ -260,7 +275,7 @@ def test_reduced_gradients(stepped):
             err, gap, g, w64, w32 = _pgap(p, mode, f"step0/grad/{net}/{k}", gr)
             env = max(REDUCED_MIN, 2 * gap)
             n_params += 1
-            if err > env:
+            if over_envelope(err, env):
                 bad.append((net, k, err, env))
             scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
             ours.append(g * scale)
@@ -331,7 +346,7 @@ PERTURB = {"f32": 4e-6, "bf16x3": 4e-5}
 
 @pytest.fixture(scope="module")
 def conditioning(stepped):
-    """fp64 oracle gradients at inputs perturbed by PERTURB (two realizations): how far the
+    """fp64 oracle gradients at inputs perturbed by PERTURB (three realizations): how far the
     exact gradient moves when the forward pass moves by fp32 rounding.  ReLU / LeakyReLU
     pre-activations within ~1e-5 of 0 flip their derivative under such perturbations, which
     makes the step's gradients 1e-3…1e-2-conditioned (tools/diag_d.py traces it)."""
@@ -341,13 +356,14 @@ def conditioning(stepped):
         return None                 # reduced precisions / emulated bf16x3: test_reduced_gradients
     eps = PERTURB[meta["precision"]]
     pre = {4e-6: "fp64p4e-6", 4e-5: "fp64p4e-5"}[eps]
-    if any(k.startswith(pre + "/") for k in z.files):
-        # BASELINE-size cases: the fixture holds the perturbed fp64 run (same protocol, one
-        # realization, generator seed 77) — returned as sampled vectors keyed like the grads
-        return [{"sampled": pre}]
+    stored = [q for q in (pre, pre + "r1", pre + "r2", pre + "r3") if f"{q}/loss_names" in z.files]
+    if stored:
+        # BASELINE-size cases: the fixture holds the perturbed fp64 runs (same protocol, generator
+        # seeds 77, 78, 79 — tools/gen_fixtures.py) — returned as sampled vectors keyed like the grads
+        return [{"sampled": q} for q in stored]
     A, B = inputs(meta, 0)
     out = []
-    for r in range(2):
+    for r in range(3):
         g = torch.Generator().manual_seed(77 + r)
         Ap = A.double() * (1 + eps * torch.randn(A.shape, generator=g, dtype=torch.float64))
         Bp = B.double() * (1 + eps * torch.randn(B.shape, generator=g, dtype=torch.float64))
@@ -384,9 +400,10 @@ def test_gradients(stepped, conditioning):
             wp = [z[f"{c['sampled']}/step0/grad/{net}/{k}/val"] if "sampled" in c else sampled(z, key64, c[net][k])[0]
                   for c in conditioning]
             env = max(1e-3, 2 * rel_err(w32, w64), *[2 * rel_err(x, w64) for x in wp])
+            assert_finite(f"grad {net}.{k}", g)
             r = rel_err(g, w64)
             n_params += 1
-            if r > env:
+            if over_envelope(r, env):
                 bad.append((net, k, r, env))
             scale = 1.0 / max(float(np.linalg.norm(w64)), 1e-30)
             ours.append(g * scale)
@@ -430,6 +447,7 @@ def test_params_after_adam(stepped):
             if is_pre_in_bias(net, k):
                 continue
             g, w = sampled(z, f"fp64/step0/param/{net}/{k}", p)
+            assert_finite(f"param {net}.{k}", g)
             d = np.abs(g - w)
             assert d.max() <= 2.05 * lr, (net, k, d.max())
             total += d.size

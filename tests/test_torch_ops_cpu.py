@@ -59,3 +59,14 @@ def test_cpu_tensor_refused():
     x = torch.zeros(1, 4, 4, 4, 2)
     with pytest.raises(Exception):
         torch.ops.mragan.replication_pad(x, 1)
+
+
+def test_argument_guard():
+    """_need_f32 is the guard every op runs before handing raw pointers to a kernel."""
+    cpu = torch.device("cpu")
+    tops._need_f32(None, "t", cpu)
+    tops._need_f32(torch.zeros(3), "t", cpu, 3)
+    for bad, numel in ((torch.zeros(3, dtype=torch.bfloat16), None), (torch.zeros(3, dtype=torch.float64), None),
+                       (torch.zeros(3, device="meta"), None), (torch.zeros(4), 3)):
+        with pytest.raises(ValueError):
+            tops._need_f32(bad, "t", cpu, numel)

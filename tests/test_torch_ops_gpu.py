@@ -187,3 +187,24 @@ def test_opcheck_registrations(tops):
     torch.library.opcheck(torch.ops.mragan.replication_pad.default, (x, 2), test_utils=checks)
     b = torch.randn(x.shape, generator=g).cuda()
     torch.library.opcheck(torch.ops.mragan.l1_loss.default, (x, b), test_utils=checks)
+
+
+def test_argument_refusals(tops):
+    """Wrong dtype, device or size is refused before any kernel sees the pointer."""
+    x = torch.randn(1, 6, 6, 6, 8, device="cuda")
+    w = torch.randn(16, 8, 3, 3, 3, device="cuda") * 0.1
+    conv = torch.ops.mragan.conv3d
+    for bad_w in (w.bfloat16(), w.half(), w.double(), w.cpu()):
+        with pytest.raises(ValueError):
+            conv(x, bad_w, None, 1, 1, 0, False, "none")
+    for bad_b in (torch.zeros(15, device="cuda"), torch.zeros(16), torch.zeros(16, device="cuda", dtype=torch.float16)):
+        with pytest.raises(ValueError):
+            conv(x, w, bad_b, 1, 1, 0, False, "none")
+    a = torch.randn(64, device="cuda")
+    for bad in (a.half(), a.bfloat16(), a.double()):
+        with pytest.raises(ValueError):
+            torch.ops.mragan.l1_loss(bad, bad)
+        with pytest.raises(ValueError):
+            torch.ops.mragan.gan_loss(bad, 1.0, False)
+    with pytest.raises(ValueError):
+        torch.ops.mragan.l1_loss(a, a.cpu())

@@ -62,7 +62,13 @@ CKPT_CASES = {
     "ckpt_r6_ngf4": (["--netG", "resnet_6blocks", "--ngf", "4", "--ndf", "4"], 24, 1, 1, 8),
 }
 N_SAMPLES = 256
-DTYPE_PREFIXES = ("fp32", "fp64", "fp64p4e-6", "fp64p4e-5")
+DTYPE_PREFIXES = ("fp32", "fp64", "fp64p4e-6", "fp64p4e-5", "fp64p4e-6r1", "fp64p4e-6r2", "fp64p4e-6r3")
+# further realisations of the exact-f32 mode's input perturbation for the BASELINE-size cases
+# (generator seeds 78, 79; the stored fp64p4e-6 run is seed 77): the per-tensor gradient envelope is the max over realisations, as
+# the small cases compute two at test time (tests/test_step_gpu.py `conditioning`)
+EXTRA_REALISATIONS = ("fp64p4e-6r1", "fp64p4e-6r2")
+BASELINE_SIZE = ("step_r9_s64_b2", "step_unet_s64_b1_ngf32", "step_r9_s96_b1_nc2", "step_r9_s128_b1",
+                 "step_unet256_s256_b1_ngf4")
 
 
 COL_LIMIT = 2 << 30      # bytes of one im2col buffer of an fp64 CPU convolution
@@ -135,13 +141,23 @@ def perturb(x, eps, g):
     return x * (1 + eps * torch.randn(x.shape, generator=g, dtype=torch.float64))
 
 
-def run_case(name, argv, S, B, nc, dtypes, steps, seed):
+def _eps_seed(dt):
+    """fp64p<E>[r<i>]: relative perturbation E, noise generator seed 77 + i."""
+    if not dt.startswith("fp64p"):
+        return 0.0, 77
+    body = dt[len("fp64p"):]
+    e, _, r = body.partition("r")
+    return float(e), 77 + (int(r) if r else 0)
+
+
+def run_case(name, argv, S, B, nc, dtypes, steps, seed, out=None):
     TrainOptions, create_model = import_reference()
     import gc
     import random
-    out = {}
+    first = out is None
+    out = {} if out is None else out
     for dt in dtypes:
-        eps = float(dt[len("fp64p"):]) if dt.startswith("fp64p") else 0.0
+        eps, pseed = _eps_seed(dt)
         gc.collect()
         sys.argv = ["train.py", "--checkpoints_dir", "/tmp/gen_fixtures_ck"] + argv
         opt = TrainOptions().gather_options()
@@ -156,7 +172,7 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
                 getattr(model, "net" + n).double()
             model.criterionGAN.double()
         pre = f"{dt}"
-        if dt == dtypes[0]:
+        if first and dt == dtypes[0]:
             for n in ("G_A", "G_B", "D_A", "D_B"):
                 for k, v in getattr(model, "net" + n).state_dict().items():
                     if v.is_floating_point() and k.endswith("weight"):
@@ -167,7 +183,7 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
             if dt.startswith("fp64"):
                 A, Bt = A.double(), Bt.double()
             if eps:
-                g = torch.Generator().manual_seed(77)
+                g = torch.Generator().manual_seed(pseed)
                 A, Bt = perturb(A, eps, g), perturb(Bt, eps, g)
             model.set_input([A, Bt])
             model.optimize_parameters()
@@ -195,6 +211,7 @@ def run_case(name, argv, S, B, nc, dtypes, steps, seed):
                             sample(b, f"{pre}/step0/buf/{n}/{k}", out, n=16)
         out[f"{pre}/loss_names"] = np.array(model.loss_names)
         del model
+        print(f"  {name}: {dt} done", flush=True)
     meta = dict(argv=" ".join(argv), S=S, B=B, nc=nc, steps=steps, seed=seed, torch=torch.__version__)
     out["meta"] = np.array(repr(meta))
     path = os.path.join(OUT, name + ".npz")
@@ -264,9 +281,25 @@ def run_pool_sequence(name="pool_seq_p2", pool_size=2, seed=123, queries=48):
           "of", len(ids))
 
 
+def add_realisations(name):
+    """Append the EXTRA_REALISATIONS runs to an existing fixture (the stored runs are kept as
+    they are; the new ones sample the same indices)."""
+    argv, S, B, nc, _, steps, seed = CASES[name]
+    path = os.path.join(OUT, name + ".npz")
+    with np.load(path, allow_pickle=False) as z:
+        out = {k: z[k] for k in z.files}
+    todo = [dt for dt in EXTRA_REALISATIONS if f"{dt}/loss_names" not in out]
+    if todo:
+        run_case(name, argv, S, B, nc, todo, steps, seed, out=out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(os.cpu_count())
+    if sys.argv[1:2] == ["--realisations"]:
+        for name in sys.argv[2:] or BASELINE_SIZE:
+            add_realisations(name)
+        return
     which = sys.argv[1:] or list(CASES) + list(CKPT_CASES) + ["pool_seq_p2"]
     for name in which:
         if name == "pool_seq_p2":
