@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 16
+#define MRAGAN_ABI_VERSION 17
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -234,6 +234,21 @@ int mragan_conv3d_op16_bwd_stats(const void* x16, int N, int Di, int Hi, int Wi,
                                   int k, int stride, int pad, float* y, int Do, int Ho, int Wo, int transposed, void* ws,
                                   size_t ws_bytes, const float* x_in, const float* mean, const float* rstd, int act,
                                   double* part, size_t part_bytes, int* chunks, void* stream);
+/* ABI 17: the k7 layers on 16-bit operand planes (bf16 / fp16 modes).
+ *   mragan_conv3d_thin_op16: the 32 → nc (1, 2) k7 s1 convolution from the plane of its 32-channel
+ *       input — the G head forward on ReplicationPad3d(3)(relu(IN(x))) of the last up-conv
+ *       (networks3D.py:211-213) and the G stem's data gradient from the plane of the stem IN
+ *       backward's dx (transposed = 1; networks3D.py:185-189).  Same arguments and results as
+ *       mragan_conv3d_fwd / _transposed on the fp32 tensor (bit-identical).
+ *   mragan_conv3d_wgrad_thin_op16: mragan_conv3d_wgrad of the k7 s1 layers (one side nc = 1 or 2,
+ *       the other 32 channels) with the 32-channel operand as its plane, the nc-channel one fp32:
+ *       the head's dW (gathered = the head input's plane) and the stem's (dense = the plane of dx). */
+int mragan_conv3d_thin_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                            const float* bias, int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho,
+                            int Wo, int transposed, void* ws, size_t ws_bytes, void* stream);
+int mragan_conv3d_wgrad_thin_op16(const void* dense, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered, int Dg,
+                                  int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                                  size_t ws_bytes, void* stream);
 int mragan_instnorm_apply_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
                                const float* resid, int rpad, const float* mean, const float* rstd, void* stream);
 int mragan_instnorm_bwd_apply_op16(const float* x, const float* mean, const float* rstd, int N, int D, int H, int W,

@@ -234,6 +234,36 @@ static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int
   return conv_igemm(a, static_cast<hipStream_t>(stream));
 }
 
+int mragan_conv3d_thin_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias,
+                            int cout, int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int transposed,
+                            void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(x16 && w && y, "conv3d_thin_op16: null pointer");
+  MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_thin_op16: transposed must be 0/1");
+  MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && Do > 0 && Ho > 0 && Wo > 0 && pad >= 0,
+                   "conv3d_thin_op16: bad shape");
+  MRAGAN_CHECK_ARG(thinn_x3_applicable(cin, cout, k, stride, g_conv_precision),
+                   "conv3d_thin_op16: only the 32 -> 1|2-channel k7 s1 convolutions (got %d -> %d, k%d s%d)", cin,
+                   cout, k, stride);
+  ThinArgs a{static_cast<const float*>(x16), N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad,
+             transposed, act, g_conv_precision};
+  a.x16 = 1;
+  return conv_thinn_x3(a, g_conv_precision, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int mragan_conv3d_wgrad_thin_op16(const void* dense, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered, int Dg,
+                                  int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(dense && gathered && dw && ws, "wgrad_thin_op16: null pointer");
+  MRAGAN_CHECK_ARG(thin1_wgrad_x3_applicable(Cd, Cg, k, stride, g_conv_precision) && pad >= 0,
+                   "wgrad_thin_op16: only the k7 s1 layers between nc and 32 channels (got %d, %d, k%d s%d)", Cd, Cg, k,
+                   stride);
+  return conv_thin1_wgrad_x3(static_cast<const float*>(dense), N, Dd, Hd, Wd, Cd, static_cast<const float*>(gathered), Dg,
+                             Hg, Wg, Cg, pad, dw, accumulate, g_conv_precision, ws, ws_bytes,
+                             static_cast<hipStream_t>(stream), 1);
+}
+
 int mragan_instnorm_apply_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
                                const float* resid, int rpad, const float* mean, const float* rstd, void* stream) {
   if (int rc = op16_mode_ok()) return rc;

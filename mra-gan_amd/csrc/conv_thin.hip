@@ -566,6 +566,9 @@ int conv_thin(ThinArgs a, hipStream_t st) {
   // quads per lane) joins it in the 16-bit MFMA modes (262 µs per 2×32³ → 64³ launch on
   // thin_n_class, r04final); in exact f32 it stays on thin_n_class — a forward layer, and the f32
   // step-parity envelopes of the 64³ UNet fixture were measured with its summation order (§2).
+  // the one-plane modes: k4 s2 p1 transposed convs to ≤ 2 channels (the UNet outermost upconv, the
+  // D-first data gradient) run input-centric on MFMA (conv_up4.hip, round 5)
+  if (up4_mfma_applicable(a)) return conv_up4_mfma(a, st);
   const bool wide8 = a.cx > 32 && a.cx <= 64 && a.rnd != 0 && a.ny <= 2;   // ≤ 2 outputs: no spill
   if (a.ny <= 4 && a.trans && a.s > 1 && a.cx % 4 == 0 && (a.cx <= 32 || wide8) && ceil_div(a.k, a.s) == 2 &&
       (int64_t)a.N * a.Do * a.Ho * a.Wo < ((int64_t)1 << 31) &&

@@ -30,6 +30,8 @@
 #include "kernels.h"
 #include "prec.h"
 
+#include <type_traits>
+
 namespace mragan {
 
 namespace {
@@ -513,8 +515,14 @@ struct Thin1RWArgs {
 // (brick rows 2kq, 2kq + 1 of each step)
 constexpr int kWT0 = 7;                 // tiles of group 0 (group 1: kMT − 7 = 6)
 
-template <int PM>
+// P16 (one-plane modes, round 5): P is the 16-bit operand plane of the 32-channel operand (the words
+// the staging would round it to): 8-B loads, the channel pairs of two voxels re-packed by bit ops —
+// bit-identical to the fp32 path (tests/test_kernels_gpu.py::test_k7_planes_bit_identical)
+template <int PM, int P16>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) thin1r_wgrad_kernel(Thin1RWArgs a) {
+  static_assert(!P16 || !prec::has_lo<PM>(), "operand planes exist in the one-plane modes only");
+  constexpr uint32_t PES = P16 ? 2u : 4u;     // bytes per P element
+  using PV = typename std::conditional<P16 != 0, uint2, float4>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);                     // [kRing][kPlaneE]
   bf16x8* ringL = ringH + kRing * kPlaneE;
@@ -536,16 +544,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // P staging unit of this thread: voxel pair vp = tid & 63 (voxels 2vp, 2vp + 1 of the brick:
   // row vp / 8, columns 2(vp % 8) …), channel quad cq = tid >> 6
   const int vp = tid & 63, cq = tid >> 6;
-  auto p_load = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, float4& v0, float4& v1)
+  auto p_load = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, PV& v0, PV& v1)
                     __attribute__((always_inline)) {
     const int ph = vh0 + (vp >> 3), pw = vw0 + 2 * (vp & 7);
     const bool okr = vd < a.Dp && ph < a.Hp;
     const bool ok0 = okr && pw < a.Wp, ok1 = okr && pw + 1 < a.Wp;
-    const uint32_t b0 = (uint32_t)((((int64_t)vd * a.Hp + ph) * a.Wp + pw) * kC + 4 * cq) * 4u;
-    v0 = buf_load_f32x4(pr, ok0 ? b0 : kOobOffset);
-    v1 = buf_load_f32x4(pr, ok1 ? b0 + kC * 4u : kOobOffset);
+    const uint32_t b0 = (uint32_t)((((int64_t)vd * a.Hp + ph) * a.Wp + pw) * kC + 4 * cq) * PES;
+    if constexpr (P16) {
+      v0 = buf_load_8b(pr, (int)(ok0 ? b0 : kOobOffset), 0);
+      v1 = buf_load_8b(pr, (int)(ok1 ? b0 + kC * PES : kOobOffset), 0);
+    } else {
+      v0 = buf_load_f32x4(pr, ok0 ? b0 : kOobOffset);
+      v1 = buf_load_f32x4(pr, ok1 ? b0 + kC * PES : kOobOffset);
+    }
   };
-  auto p_store = [&](int buf, const float4 v0, const float4 v1) __attribute__((always_inline)) {
+  auto p_store = [&](int buf, const PV v0, const PV v1) __attribute__((always_inline)) {
     __bf16* ph = pt + (size_t)buf * 2 * kC * kPS;
     __bf16* pl = ph + kC * kPS;
     auto put = [&](int q, float x0, float x1) __attribute__((always_inline)) {
@@ -555,10 +568,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       *reinterpret_cast<uint32_t*>(ph + idx) = h;
       if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint32_t*>(pl + idx) = l;
     };
-    put(0, v0.x, v1.x);
-    put(1, v0.y, v1.y);
-    put(2, v0.z, v1.z);
-    put(3, v0.w, v1.w);
+    if constexpr (P16) {
+      // channel q of voxels 2vp, 2vp + 1: the 16-bit words (v0, v1) of that channel, low half first
+      auto put16 = [&](int q, uint32_t w) __attribute__((always_inline)) {
+        *reinterpret_cast<uint32_t*>(ph + (4 * cq + q) * kPS + 2 * vp) = w;
+      };
+      put16(0, (v0.x & 0xffffu) | (v1.x << 16));
+      put16(1, (v0.x >> 16) | (v1.x & 0xffff0000u));
+      put16(2, (v0.y & 0xffffu) | (v1.y << 16));
+      put16(3, (v0.y >> 16) | (v1.y & 0xffff0000u));
+    } else {
+      put(0, v0.x, v1.x);
+      put(1, v0.y, v1.y);
+      put(2, v0.z, v1.z);
+      put(3, v0.w, v1.w);
+    }
   };
 
   for (int item = blockIdx.x; item < a.items; item += gridDim.x) {
@@ -572,15 +596,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int nplanes = nsteps + kK - 1;
     const __amdgpu_buffer_rsrc_t qr =
         make_rsrc(a.Q + (int64_t)nb * a.Dq * a.Hq * a.Wq * a.qC, (uint32_t)a.Dq * a.Hq * a.Wq * a.qC * 4u);
-    const __amdgpu_buffer_rsrc_t pr =
-        make_rsrc(a.P + (int64_t)nb * a.Dp * a.Hp * a.Wp * kC, (uint32_t)a.Dp * a.Hp * a.Wp * kC * 4u);
+    const __amdgpu_buffer_rsrc_t pr = make_rsrc(reinterpret_cast<const char*>(a.P) + (int64_t)nb * a.Dp * a.Hp * a.Wp * kC * PES,
+                                                (uint32_t)a.Dp * a.Hp * a.Wp * kC * PES);
     const int d0 = vd0 - a.pe, h0 = vh0 - a.pe, w0 = vw0 - a.pe;
     const int erow = tid / kBW, epos = tid % kBW;      // this thread's X8 entry (tid < 224)
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 0] = __builtin_amdgcn_s_memtime();
 
     // prologue: P of step 0 → buffer 0, Q planes 0..6 → slots 0..6
     {
-      float4 v0, v1;
+      PV v0, v1;
       p_load(pr, vd0, vh0, vw0, v0, v1);
       if (tid < kPlaneE) {
         float v[7][8];
@@ -597,7 +621,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int s = 0; s < nsteps; ++s) {
       // P(s + 1) and Q plane s + 7 → registers before the MFMAs, → the free buffer / slot after
       const bool more_q = s + kK < nplanes && tid < kPlaneE, more_p = s + 1 < nsteps;
-      float4 v0 = {}, v1 = {};
+      PV v0 = {}, v1 = {};
       f32x8 q = {};
       if (more_q) q = load_row8v(qr, a.Dq, a.Hq, a.Wq, d0 + s + kK, h0 + erow, w0 + epos, a.qC, a.qc);
       if (more_p) p_load(pr, vd0 + s + 1, vh0, vw0, v0, v1);
@@ -684,6 +708,18 @@ __global__ void __launch_bounds__(256) thin1_wgrad_reduce_kernel(const float* __
   }
 }
 
+template <int PM, int P16>
+static int launch_thin1w(const Thin1RWArgs& a, int grid, size_t lds, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_wgrad_kernel<PM, P16>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((thin1r_wgrad_kernel<PM, P16>), dim3(grid), dim3(512), lds, st, a);
+  return check_launch(P16 ? "thin1_wgrad_x3(op16)" : "thin1_wgrad_x3");
+}
+
 // 2-channel single side (nc = 2) in the one-plane modes: one pass per channel of that side
 bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s, int mode) {
   const bool one_plane = mode == kPrecBf16 || mode == kPrecF16;
@@ -695,7 +731,10 @@ size_t thin1_wgrad_x3_ws_bytes() { return (size_t)cu_count() * kT * kC * sizeof(
 
 // Same argument convention as conv_wgrad: dW[dn][gn][t] = Σ_m D[m][dn] · G[m − p + t][gn]
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
-                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
+                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st,
+                        int wide16) {
+  MRAGAN_CHECK_ARG(!wide16 || mode == kPrecBf16 || mode == kPrecF16,
+                   "thin1_wgrad_x3: a 16-bit operand plane needs the bf16 / fp16 mode");
   Thin1RWArgs a{};
   static const int stamps = getenv("MRAGAN_STAMPS") ? 1 : 0;
   a.stamp = stamps;
@@ -715,7 +754,7 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
                    "thin1_wgrad_x3: %d single-side channels in precision mode %d", nq, mode);
   a.N = N;
   a.qC = nq;
-  MRAGAN_CHECK_ARG((int64_t)a.Dp * a.Hp * a.Wp * kC * 4 < (int64_t)kOobOffset &&
+  MRAGAN_CHECK_ARG((int64_t)a.Dp * a.Hp * a.Wp * kC * (wide16 ? 2 : 4) < (int64_t)kOobOffset &&
                        (int64_t)a.Dq * a.Hq * a.Wq * nq * 4 < (int64_t)kOobOffset,
                    "thin1_wgrad_x3: volume too large");
   a.nbh = ceil_div(a.Hp, kBH); a.nbw = ceil_div(a.Wp, kBW);
@@ -738,17 +777,14 @@ int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, c
   for (int qc = 0; qc < nq; ++qc) {
     a.qc = qc;
     int rc = kOk;
-    MRAGAN_PREC_DISPATCH(mode, {
-      static bool attr_set = false;
-      if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_wgrad_kernel<PM>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL(thin1r_wgrad_kernel<PM>, dim3(grid), dim3(512), lds, st, a);
-      rc = check_launch("thin1_wgrad_x3");
-      break;
-    })
+    if (wide16) {
+      rc = mode == kPrecF16 ? launch_thin1w<kPrecF16, 1>(a, grid, lds, st) : launch_thin1w<kPrecBf16, 1>(a, grid, lds, st);
+    } else {
+      MRAGAN_PREC_DISPATCH(mode, {
+        rc = launch_thin1w<PM, 0>(a, grid, lds, st);
+        break;
+      })
+    }
     if (rc) return rc;
     hipLaunchKernelGGL(thin1_wgrad_reduce_kernel, dim3(kT), dim3(256), 0, st, a.slab, grid, flip, out, ocs,
                        qc * qstride, accumulate);

@@ -29,6 +29,8 @@
 #include "kernels.h"
 #include "prec.h"
 
+#include <type_traits>
+
 namespace mragan {
 
 namespace {
@@ -82,7 +84,7 @@ __global__ void thinn_x3_pack_kernel(const float* __restrict__ wp, int flip, int
 }  // namespace
 
 struct ThinnArgs {
-  const float* x; int N, Di, Hi, Wi;      // [N][Di][Hi][Wi][32]
+  const float* x; int N, Di, Hi, Wi;      // [N][Di][Hi][Wi][32] (fp32, or the 16-bit operand plane: X16)
   const __bf16* wx;
   const float* bias;
   float* y; int Do, Ho, Wo, ny;           // [N][Do][Ho][Wo][ny]
@@ -99,9 +101,14 @@ __device__ __forceinline__ int thinn_rot(int pos) { return (pos ^ (pos >> 2)) & 
 
 constexpr int kScratch = kMW * 17;      // floats of a wave's epilogue scratch ([80][16] padded)
 
-template <int PM>
+// X16 (one-plane modes, round 5): x is the 16-bit operand plane of the input — the bf16 / fp16 words
+// the staging below would round it to — so a staged element is one 8-B load stored as it is
+// (bit-identical to the fp32-input path, tests/test_kernels_gpu.py::test_k7_planes_bit_identical)
+template <int PM, int X16>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 thinn_x3_kernel(ThinnArgs a) {
+  static_assert(!X16 || !prec::has_lo<PM>(), "operand planes exist in the one-plane modes only");
+  constexpr uint32_t ES = X16 ? 2u : 4u;    // bytes per input element
   extern __shared__ __attribute__((aligned(16))) char smem[];   // [kUnitBytes] | [8][kScratch]
   char* buf = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -116,7 +123,8 @@ thinn_x3_kernel(ThinnArgs a) {
   const int od0 = 2 * a.P * seg, oh0 = r * kBH, ow0 = cw * kOW;
   const int npairs = min(a.P, (a.Do - od0 + 1) / 2);
   const int nunits = 2 * (2 * npairs + kK - 1);
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (int64_t)nb * a.Di * a.Hi * a.Wi * kC, (uint32_t)a.Di * a.Hi * a.Wi * kC * 4u);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const char*>(a.x) + (int64_t)nb * a.Di * a.Hi * a.Wi * kC * ES,
+                                              (uint32_t)a.Di * a.Hi * a.Wi * kC * ES);
 
   // staging of one unit (plane, channel half) into registers / LDS; per-thread element offsets
   // inside an input plane (−1: outside the input), fixed per block
@@ -130,25 +138,30 @@ thinn_x3_kernel(ThinnArgs a) {
     poff[l] = ok ? (h * a.Wi + w) * kC + 4 * cq : -1;
   }
   const uint32_t plane = (uint32_t)a.Hi * a.Wi * kC;
-  auto stage_load = [&](int u, float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
+  using SV = typename std::conditional<X16 != 0, uint2, float4>::type;
+  auto stage_load = [&](int u, SV (&sv)[kF4PT]) __attribute__((always_inline)) {
     const int d = od0 + (u >> 1) - a.pe, half = u & 1;
     const bool dok = (unsigned)d < (unsigned)a.Di;          // planes outside the input read 0
     const uint32_t base = (uint32_t)(dok ? d : 0) * plane + 16u * half;
 #pragma unroll
-    for (int l = 0; l < kF4PT; ++l)
-      sv[l] = buf_load_f32x4(xr, (!dok || poff[l] < 0) ? kOobOffset : (base + poff[l]) * 4u);
+    for (int l = 0; l < kF4PT; ++l) {
+      const uint32_t off = (!dok || poff[l] < 0) ? kOobOffset : (base + poff[l]) * ES;
+      if constexpr (X16) sv[l] = buf_load_8b(xr, (int)off, 0);
+      else sv[l] = buf_load_f32x4(xr, off);
+    }
   };
   // element l of this thread sits at position 128l + tid/4 (channels 4(tid&3)…): its chunk
   // rotation depends on tid only, so every store is base + 8192·l
   const int cq = tid & 3, srot = thinn_rot(tid >> 2);
   const int st_hi = (tid >> 2) * kRec + 16 * ((cq >> 1) ^ srot) + 8 * (cq & 1);
   const int st_lo = (tid >> 2) * kRec + 16 * ((2 + (cq >> 1)) ^ srot) + 8 * (cq & 1);
-  auto stage_store = [&](const float4 (&sv)[kF4PT]) __attribute__((always_inline)) {
+  auto stage_store = [&](const SV (&sv)[kF4PT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < kF4PT; ++l) {
       if (l * kThreads + tid < kNF4) {
         uint2 h, lo;
-        prec::split4<PM>(sv[l], h, lo);
+        if constexpr (X16) h = sv[l];
+        else prec::split4<PM>(sv[l], h, lo);
         *reinterpret_cast<uint2*>(buf + l * (kThreads / 4) * kRec + st_hi) = h;
         if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(buf + l * (kThreads / 4) * kRec + st_lo) = lo;
       }
@@ -192,7 +205,7 @@ thinn_x3_kernel(ThinnArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);
   };
 
-  float4 sv[kF4PT];
+  SV sv[kF4PT];
   stage_load(0, sv);
   for (int u = 0; u < nunits; ++u) {
     __syncthreads();                            // every wave is done with the previous unit
@@ -259,7 +272,7 @@ bool thinn_x3_applicable(int cx, int ny, int k, int s, int mode) {
 
 size_t thinn_x3_ws_bytes(int ny) { return (size_t)ny * kPackElems * sizeof(__bf16); }
 
-template <int PM>
+template <int PM, int X16>
 static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream_t st) {
   if (!(t.ny == 1 || (t.ny == 2 && !prec::has_lo<PM>()))) {
     set_error("thinn_x3: %d output channels in precision mode %d", t.ny, PM);
@@ -300,22 +313,27 @@ static int conv_thinn_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
     if (P >= nq) break;
   }
   const int64_t blocks = cols * a.nseg;
-  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * kC * 4 < (int64_t)kOobOffset, "thinn_x3: input volume too large");
+  MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * kC * (X16 ? 2 : 4) < (int64_t)kOobOffset, "thinn_x3: input volume too large");
   a.total = (int)blocks;
   a.per = (int)ceil_div(blocks, 8);
   const size_t lds = (size_t)kUnitBytes + (size_t)kBH * kScratch * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel<PM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thinn_x3_kernel<PM, X16>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(thinn_x3_kernel<PM>, dim3((unsigned)(8 * a.per)), dim3(kThreads), lds, st, a);
-  return check_launch("thinn_x3");
+  hipLaunchKernelGGL((thinn_x3_kernel<PM, X16>), dim3((unsigned)(8 * a.per)), dim3(kThreads), lds, st, a);
+  return check_launch(X16 ? "thinn_x3(op16)" : "thinn_x3");
 }
 
 int conv_thinn_x3(const ThinArgs& t, int mode, void* ws, size_t ws_bytes, hipStream_t st) {
-  MRAGAN_PREC_DISPATCH(mode, return conv_thinn_pm<PM>(t, ws, ws_bytes, st))
+  if (t.x16) {
+    if (mode == kPrecF16) return conv_thinn_pm<kPrecF16, 1>(t, ws, ws_bytes, st);
+    MRAGAN_CHECK_ARG(mode == kPrecBf16, "thinn_x3: a 16-bit operand plane needs the bf16 / fp16 mode");
+    return conv_thinn_pm<kPrecBf16, 1>(t, ws, ws_bytes, st);
+  }
+  MRAGAN_PREC_DISPATCH(mode, return conv_thinn_pm<PM, 0>(t, ws, ws_bytes, st))
 }
 
 }  // namespace mragan

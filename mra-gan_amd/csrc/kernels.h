@@ -99,8 +99,12 @@ struct ThinArgs {
   // InstanceNorm(+act) of bs_x whose output, replication-padded by bs_fold, was the conv's input
   const float* bs_x = nullptr; const float* bs_mean = nullptr; const float* bs_rstd = nullptr;
   int bs_act = 0, bs_fold = 0;
+  int x16 = 0;                 // x is a 16-bit operand plane (thinn_x3 only, the one-plane modes)
 };
 int conv_thin(ThinArgs a, hipStream_t st);
+// ConvTranspose3d k4 s2 p1 to 1-2 channels on MFMA, one-plane modes (conv_up4.hip)
+bool up4_mfma_applicable(const ThinArgs& a);
+int conv_up4_mfma(const ThinArgs& a, hipStream_t st);
 // MFMA path for 1 → 32-channel k7 s1 convolutions (conv_thin1_ring.hip); 2 → 32 in the one-plane
 // modes (mode = the precision code)
 bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode);
@@ -114,8 +118,10 @@ int conv_thinn_x3(const ThinArgs& a, int mode, void* ws, size_t ws_bytes, hipStr
 // bf16x3 MFMA weight gradient of the 1-channel k7 s1 convolutions (conv_thin1_wgrad_x3.hip)
 bool thin1_wgrad_x3_applicable(int Cd, int Cg, int k, int s, int mode);
 size_t thin1_wgrad_x3_ws_bytes();
+// wide16: the 32-channel operand is the 16-bit operand plane of the mode (one-plane modes)
 int conv_thin1_wgrad_x3(const float* D, int N, int Dd, int Hd, int Wd, int Cd, const float* G, int Dg, int Hg, int Wg,
-                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st);
+                        int Cg, int p, float* out, int accumulate, int mode, void* ws, size_t ws_bytes, hipStream_t st,
+                        int wide16 = 0);
 
 struct WgradArgs {
   const float* D; int N, Dd, Hd, Wd, Cd;

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -100,6 +100,11 @@ SIGNATURES = {
     # ABI 16: the stride-2 data gradient with backward statistics on the plane of its input
     "mragan_conv3d_op16_bwd_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp, i32, i32, i32, i32,
                                            vp, sz, vp, vp, vp, i32, vp, sz, vp, vp]),
+    # ABI 17: the k7 layers on 16-bit operand planes
+    "mragan_conv3d_thin_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32,
+                                      i32, vp, sz, vp]),
+    "mragan_conv3d_wgrad_thin_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32,
+                                            vp, sz, vp]),
     # ABI 12: the G head's data gradient with the backward statistics of the IN in front of it
     "mragan_conv3d_dgrad_in_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, sz, vp, vp, vp, i32, i32,
                                            vp, sz, vp, vp]),

@@ -37,6 +37,9 @@ _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
 _NO_S2_PLANES = __import__("os").environ.get("MRAGAN_NO_S2_PLANES") is not None
 # brickT on planes (G up2's input, G down1's dY only as planes): MRAGAN_BRICKT_PLANES=0 turns it off
 _BRICKT_PLANES = __import__("os").environ.get("MRAGAN_BRICKT_PLANES", "1") != "0"
+# ABI 17: the k7 layers' 32-channel operands (the head input, the stem IN backward's dx) only as planes
+# in the one-plane modes; MRAGAN_NO_K7_PLANES=1 keeps them fp32 (A/B)
+_NO_K7_PLANES = __import__("os").environ.get("MRAGAN_NO_K7_PLANES") is not None
 # ABI 15: InstanceNorm statistics finalized in the producing brick's launch (MRAGAN_NO_IN_TICKETS: off)
 _IN_FIN = ops.in_tickets_enabled()
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
@@ -234,8 +237,19 @@ class ConvLayer:
         return dz, part, chunks
 
     def wgrad_g16(self, x16, dy, accumulate=True):
-        """wgrad of a forward-form k3 s2 conv whose input exists only as its operand plane (ABI 14)."""
-        ops.conv3d_wgrad_g16(dy, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
+        """wgrad of a forward-form conv whose input exists only as its operand plane: the k3 s2 convs
+        (ABI 14) and the G head (k7, 32 → nc; ABI 17)."""
+        if self.k == 7:
+            ops.conv3d_wgrad_thin_op16(dy, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
+        else:
+            ops.conv3d_wgrad_g16(dy, x16, self.k, self.s, self.p, self.m.weight.grad, accumulate)
+
+    def k7_wide16_ok(self):
+        """A k7 s1 layer between nc (1, 2) and 32 channels whose 32-channel operand can be its 16-bit
+        operand plane in every kernel that reads it (thinn_x3, thin1 weight gradient; ABI 17)."""
+        return (not _NO_K7_PLANES and ops.get_conv_precision() in ("bf16", "fp16") and not self.transposed
+                and self.k == 7 and self.s == 1
+                and ((self.cin == 32 and self.cout in (1, 2)) or (self.cout == 32 and self.cin in (1, 2))))
 
     def s2_plane_ok(self, W_in):
         """A forward-form k3 s2 p1 conv (G down1 / down2) that can read its input of width W_in as
@@ -412,15 +426,19 @@ class NetPlan:
                     # a stride-2 forward conv next (G down1 / down2): this norm's output only as its
                     # plane — that conv and its weight gradient are its only readers (ABI 14)
                     nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
+                    # the G head next (k7, 32 → nc, ABI 17): its input only as the plane — the head's
+                    # forward (thinn_x3) and weight gradient are its only readers
+                    head16 = (op16 and nxt is not None and nxt.kind != "block" and nxt.norm is None
+                              and nxt.prepad == ypad and nxt.conv.cin == 32 and nxt.conv.k7_wide16_ok())
                     # — or a 32-output-channel ConvTranspose3d next (G up2: brickT reads the plane, its
                     # weight gradient takes both operands as planes)
-                    only16 = (op16 and not _NO_S2_PLANES and ypad == 0 and nxt is not None and nxt.kind != "block"
+                    only16 = head16 or (op16 and not _NO_S2_PLANES and ypad == 0 and nxt is not None and nxt.kind != "block"
                               and nxt.norm is not None and not nxt.prepad
                               and (nxt.conv.s2_plane_ok(sc.h.shape[3])
                                    or (_BRICKT_PLANES and nxt.conv.transposed and nxt.conv.cout == 32
                                        and nxt.conv.transposed_plane_bwd_ok(sc.h.shape[3]))))
                     if only16:
-                        _, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=0, part=part,
+                        _, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad, part=part,
                                                                            chunks=chunks)
                     elif want16 and self._op16_blocks_ok(sc.h.shape[3], sc.h.shape[2]):
                         sc.out, out16, sc.mean, sc.rstd = ops.instnorm_fwd_op16(sc.h, act=st.act, ypad=ypad,
@@ -430,7 +448,13 @@ class NetPlan:
                         sc.out, sc.mean, sc.rstd = ops.instnorm_fwd(sc.h, act=st.act, ypad=ypad, part=part,
                                                                     chunks=chunks)
                 else:
-                    sc.h = st.conv.forward(cur, bias=bias, act=st.act)     # activated output
+                    if cur is None:
+                        # the G head on its input's plane (ABI 17)
+                        c = st.conv
+                        sc.h = ops.conv3d_thin_op16(cur16, c.wp_fwd, c.cout, c.k, c.s, c.p, c.out_spatial(*cur16.shape[1:4]),
+                                                    bias=bias, act=st.act)
+                    else:
+                        sc.h = st.conv.forward(cur, bias=bias, act=st.act)     # activated output
                     sc.out = ops.rpad(sc.h, ypad) if ypad else sc.h
             ctx.stages.append(sc)
             cur, cur16 = sc.out, out16
@@ -539,6 +563,22 @@ class NetPlan:
                     else:
                         g = ops.conv3d_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, in_spatial, None,
                                             transposed=not conv.transposed)[0]
+                    gpad, gadd = st.prepad, None
+                continue
+            if (st.norm is not None and sc.inp is not None and self._op16_active() and conv.cout == 32
+                    and conv.k7_wide16_ok()):
+                # the G stem (k7, nc → 32; ABI 17): its IN backward writes dx only as the plane — the
+                # stem's weight gradient and data gradient (thinn_x3) are its only readers
+                if bstats is not None:
+                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                else:
+                    dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
+                bstats = None
+                if need_wgrad:
+                    ops.conv3d_wgrad_thin_op16(dh16, sc.inp, conv.k, conv.s, conv.p, conv.m.weight.grad, True)
+                if want_dgrad:
+                    g = ops.conv3d_thin_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, sc.inp.shape[1:4],
+                                             transposed=True)
                     gpad, gadd = st.prepad, None
                 continue
             if st.norm is not None:

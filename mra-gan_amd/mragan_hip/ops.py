@@ -789,6 +789,45 @@ def conv3d_wgrad_g16(dense: torch.Tensor, gathered16: torch.Tensor, k: int, s: i
     return dw
 
 
+def conv3d_thin_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
+                     bias: Optional[torch.Tensor] = None, act=None, transposed: bool = False) -> torch.Tensor:
+    """conv3d of the 32 → nc k7 layers (G head forward, G stem data gradient) from the operand
+    plane of their 32-channel input (ABI 17): bit-identical to conv3d on the fp32 tensor."""
+    _check16(x16, "conv3d_thin_op16.x16")
+    N, Di, Hi, Wi, cin = x16.shape
+    Do, Ho, Wo = out_spatial
+    if wp.numel() != k ** 3 * cin * cout:
+        raise ValueError(f"conv3d_thin_op16: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
+    nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
+    ws = WS.get(nbytes) if nbytes else None
+    fn = lambda: call("mragan_conv3d_thin_op16", _ptr(x16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(bias), cout, k, s, p,
+                      ACT[act], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _stream())
+    _timed(lambda: _conv_info(cin, cout, k, s, p, transposed, N, (Di, Hi, Wi), (Do, Ho, Wo)), fn)
+    return out
+
+
+def conv3d_wgrad_thin_op16(dense, gathered, k: int, s: int, p: int, dw: torch.Tensor, accumulate: bool) -> torch.Tensor:
+    """conv3d_wgrad of the k7 layers (nc ↔ 32 channels) with the 32-channel operand as its 16-bit
+    plane and the nc-channel one fp32 (ABI 17)."""
+    N, Dd, Hd, Wd, Cd = dense.shape
+    Ng, Dg, Hg, Wg, Cg = gathered.shape
+    if Ng != N:
+        raise ValueError("wgrad: batch mismatch")
+    wide, thin = (dense, gathered) if Cd >= Cg else (gathered, dense)
+    _check16(wide, "wgrad_thin_op16.wide")
+    _check(thin, "wgrad_thin_op16.thin")
+    if dw.numel() != Cd * Cg * k ** 3 or not dw.is_contiguous():
+        raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
+    nbytes = query("mragan_conv3d_wgrad_workspace", N, Dd, Hd, Wd, Cd, Cg, k, s)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_conv3d_wgrad_thin_op16", _ptr(dense), N, Dd, Hd, Wd, Cd, _ptr(gathered), Dg, Hg, Wg, Cg,
+                      k, s, p, _ptr(dw), int(accumulate), _ptr(ws), ws.numel(), _stream())
+    _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}x{Dd}x{Hd}x{Wd}] op16",
+                        flops=2.0 * N * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)
+    return dw
+
+
 def rpad(x: torch.Tensor, p: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _check(x, "rpad.x")
     N, D, H, W, C = x.shape

@@ -232,6 +232,30 @@ def test_thin_class8_wide_modes(x3, N, cin, cout, S, k):
     check_rounded(ncdhw(out), y_r, y)
 
 
+@pytest.mark.parametrize("N,cin,cout,dims,act,bias", [
+    (2, 64, 1, (8, 8, 8), "tanh", True),        # UNet outermost upconv (2·ngf → nc, + bias, Tanh)
+    (1, 64, 2, (5, 6, 7), "tanh", True),        # nc = 2, partial output bricks
+    (2, 32, 1, (9, 8, 10), None, False),        # D-first data gradient shape (ndf → nc)
+    (1, 32, 2, (4, 4, 4), None, False),
+    (2, 64, 1, (2, 2, 3), None, True),          # smaller than one brick: most of the halo is padding
+])
+def test_up4_mfma(x3, N, cin, cout, dims, act, bias):
+    """ConvTranspose3d k4 s2 p1 to ≤ 2 channels (conv_up4.hip, the one-plane modes' MFMA path;
+    bf16x3 keeps thin_n_tile8): the fp64 transposed convolution of the mode's rounded operands,
+    bias and activation after."""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 5 + cin + cout + sum(dims))
+    x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
+    w = torch.randn(cin, cout, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64) if bias else None
+    f = {None: lambda t: t, "tanh": torch.tanh}[act]
+    y = f(F.conv_transpose3d(x, w, b, stride=2, padding=1))
+    y_r = f(F.conv_transpose3d(R(x), R(w), b, stride=2, padding=1))
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, True, False), cout, 4, 2, 1, y.shape[2:],
+                     bias=b.float().cuda() if bias else None, act=act, transposed=True)
+    check_rounded(ncdhw(out), y_r, y)
+
+
 X3_CASES = [
     # N, cin, cout, S, k, s, p   (every tile shape of conv_igemm_x3.hip's dispatch)
     (2, 128, 128, 6, 3, 1, 0),
@@ -654,6 +678,65 @@ def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
     gw64 = torch.nn.grad.conv3d_weight(ncdhw(x.double().cpu()), (cout, cin, 3, 3, 3),
                                        ncdhw(dy.to(dt).double().cpu()), stride=2, padding=1)
     assert rel(gw.view(cout, cin, 3, 3, 3), gw64) < 2e-5
+
+
+@pytest.mark.parametrize("N,nc,S,W", [(2, 1, 20, 20), (1, 2, 17, 23), (1, 1, 64, 64)])
+def test_k7_planes_bit_identical(op16, N, nc, S, W):
+    """ABI 17: the k7 layers on the 16-bit operand plane of their 32-channel operand — the G head
+    forward (thinn_x3 on the RPad3 input's plane, + bias, Tanh), the G stem data gradient (thinn_x3,
+    transposed form, on the plane of the IN backward's dx) and both weight gradients (thin1 wgrad,
+    the 32-channel side a plane) — equal the same kernels on the fp32 tensor in the same mode bit for
+    bit, and the fp64 convolution of the rounded operands to 2e-5."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 11 + nc + S + W)
+    Sp, Wp = S + 6, W + 6
+    # head: 32 → nc on the padded input
+    x16 = ndhwc(torch.randn(N, 32, Sp, Sp, Wp, generator=g).float()).cuda().to(dt)
+    x = x16.float()
+    w_head = torch.randn(nc, 32, 7, 7, 7, generator=g, dtype=torch.float64) * 0.02
+    b = torch.randn(nc, generator=g).float().cuda()
+    wp = pack(ops, w_head, False, False)
+    y_ref = ops.conv3d(x, wp, nc, 7, 1, 0, (S, S, W), bias=b, act="tanh")
+    y = ops.conv3d_thin_op16(x16, wp, nc, 7, 1, 0, (S, S, W), bias=b, act="tanh")
+    assert torch.equal(y, y_ref)
+    y64 = torch.tanh(F.conv3d(ncdhw(x.double().cpu()), R(w_head), b.double().cpu()))
+    assert rel(ncdhw(y), y64) < 2e-5
+    # head weight gradient: dense = dz (nc channels, fp32), gathered = the input plane
+    dz = ndhwc(torch.randn(N, nc, S, S, W, generator=g).float()).cuda()
+    gw_ref = torch.empty(nc * 32 * 343, device="cuda")
+    ops.conv3d_wgrad(dz, x, 7, 1, 0, gw_ref, False)
+    gw = torch.full_like(gw_ref, float("nan"))
+    ops.conv3d_wgrad_thin_op16(dz, x16, 7, 1, 0, gw, False)
+    assert torch.equal(gw, gw_ref)
+    # stem: nc → 32; its data gradient and weight gradient from the plane of dx (dense, 32 channels)
+    dh16 = ndhwc(torch.randn(N, 32, S, S, W, generator=g).float()).cuda().to(dt)
+    dh = dh16.float()
+    w_stem = torch.randn(32, nc, 7, 7, 7, generator=g, dtype=torch.float64) * 0.02
+    wb = pack(ops, w_stem, False, True)
+    gx_ref = ops.conv3d(dh, wb, nc, 7, 1, 0, (Sp, Sp, Wp), transposed=True)
+    gx = ops.conv3d_thin_op16(dh16, wb, nc, 7, 1, 0, (Sp, Sp, Wp), transposed=True)
+    assert torch.equal(gx, gx_ref)
+    xs = ndhwc(torch.randn(N, nc, Sp, Sp, Wp, generator=g).float()).cuda()
+    gws_ref = torch.empty(32 * nc * 343, device="cuda")
+    ops.conv3d_wgrad(dh, xs, 7, 1, 0, gws_ref, False)
+    gws = torch.full_like(gws_ref, float("nan"))
+    ops.conv3d_wgrad_thin_op16(dh16, xs, 7, 1, 0, gws, False, )
+    assert torch.equal(gws, gws_ref)
+    gw64 = torch.nn.grad.conv3d_weight(R(ncdhw(xs.double().cpu())), (32, nc, 7, 7, 7), ncdhw(dh.double().cpu()))
+    assert rel(gws.view(32, nc, 7, 7, 7), gw64) < 2e-5
+
+
+def test_k7_planes_rejected(op16):
+    """conv3d_thin_op16 takes only the 32 → nc k7 shapes, wgrad_thin_op16 only nc ↔ 32 k7."""
+    ops = op16
+    dt = ops.op16_dtype()
+    x16 = torch.zeros(1, 10, 10, 10, 64, device="cuda", dtype=dt)
+    with pytest.raises(RuntimeError):
+        ops.conv3d_thin_op16(x16, torch.zeros(343 * 64, device="cuda"), 1, 7, 1, 0, (4, 4, 4))
+    with pytest.raises(RuntimeError):
+        ops.conv3d_wgrad_thin_op16(torch.zeros(1, 4, 4, 4, 1, device="cuda"), x16, 7, 1, 0,
+                                   torch.zeros(64 * 343, device="cuda"), False)
 
 
 @pytest.mark.parametrize("N,cin,cout,S,act", [(2, 32, 64, 32, "relu"), (1, 64, 128, 16, "relu"), (2, 32, 64, 16, "lrelu")])
