@@ -521,6 +521,9 @@ int conv_thin(ThinArgs a, hipStream_t st) {
   MRAGAN_CHECK_ARG(a.k >= 1 && a.k <= 7, "conv_thin: k=%d unsupported", a.k);
   if (a.N == 0 || a.ny == 0) return kOk;
   const bool s1 = a.s == 1;
+  // the one-plane modes: k4 s2 p1 convs from 1-2 channels (the PatchGAN first layer, the UNet
+  // outermost downconv and upconv data gradient) on MFMA (conv_down4.hip, round 5)
+  if (down4_mfma_applicable(a)) return conv_down4_mfma(a, st);
   if (a.cx <= 4 && (!a.trans || s1)) {
     int td = ceil_div(a.Do, TK_OD), th = ceil_div(a.Ho, TK_OH), tw = ceil_div(a.Wo, TK_OW);
     int RD, RH, RW;

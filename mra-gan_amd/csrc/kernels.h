@@ -105,6 +105,9 @@ int conv_thin(ThinArgs a, hipStream_t st);
 // ConvTranspose3d k4 s2 p1 to 1-2 channels on MFMA, one-plane modes (conv_up4.hip)
 bool up4_mfma_applicable(const ThinArgs& a);
 int conv_up4_mfma(const ThinArgs& a, hipStream_t st);
+// Conv3d k4 s2 p1 from 1-2 to 32 | 64 channels on MFMA, one-plane modes (conv_down4.hip)
+bool down4_mfma_applicable(const ThinArgs& a);
+int conv_down4_mfma(const ThinArgs& a, hipStream_t st);
 // MFMA path for 1 → 32-channel k7 s1 convolutions (conv_thin1_ring.hip); 2 → 32 in the one-plane
 // modes (mode = the precision code)
 bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode);

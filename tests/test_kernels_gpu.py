@@ -256,6 +256,28 @@ def test_up4_mfma(x3, N, cin, cout, dims, act, bias):
     check_rounded(ncdhw(out), y_r, y)
 
 
+@pytest.mark.parametrize("N,cin,cout,dims,act,bias", [
+    (2, 1, 32, (16, 16, 32), "lrelu", True),    # PatchGAN first layer / UNet outermost downconv
+    (1, 2, 32, (10, 18, 22), "lrelu", True),    # nc = 2, partial output bricks
+    (1, 1, 64, (12, 10, 8), None, False),       # UNet outermost upconv's data gradient (1 → 2·ngf)
+    (2, 2, 64, (4, 6, 2), None, True),          # smaller than one brick
+])
+def test_down4_mfma(x3, N, cin, cout, dims, act, bias):
+    """Conv3d k4 s2 p1 from 1-2 channels (conv_down4.hip, the one-plane modes' MFMA path; bf16x3
+    keeps thin_k): the fp64 convolution of the mode's rounded operands, bias and activation after."""
+    ops = x3
+    g = torch.Generator().manual_seed(N * 3 + cin + cout + sum(dims))
+    x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    b = torch.randn(cout, generator=g, dtype=torch.float64) if bias else None
+    f = {None: lambda t: t, "lrelu": lambda t: F.leaky_relu(t, 0.2)}[act]
+    y = f(F.conv3d(x, w, b, stride=2, padding=1))
+    y_r = f(F.conv3d(R(x), R(w), b, stride=2, padding=1))
+    out = ops.conv3d(ndhwc(x.float()).cuda(), pack(ops, w, False, False), cout, 4, 2, 1, y.shape[2:],
+                     bias=b.float().cuda() if bias else None, act=act)
+    check_rounded(ncdhw(out), y_r, y)
+
+
 X3_CASES = [
     # N, cin, cout, S, k, s, p   (every tile shape of conv_igemm_x3.hip's dispatch)
     (2, 128, 128, 6, 3, 1, 0),

@@ -71,6 +71,9 @@ def main():
     w_dn2 = rnd(27 * 2 * ngf * c4) * 0.01
     x_d2 = rnd(N, s2, s2, s2, ngf)                        # PatchGAN layer 2 Conv3d(ndf -> 2ndf, k4 s2 p1) input
     w_d2 = rnd(64 * ngf * 2 * ngf) * 0.01
+    x_df = rnd(N, S, S, S, 1)                            # D first layer input (1 channel)
+    w_dfw = rnd(64 * ngf) * 0.01
+    b_df = rnd(ngf)
     x_uo = rnd(N, s2, s2, s2, 2 * ngf)                    # UNet outermost upconv input (2·ngf channels)
     w_uo = rnd(64 * 2 * ngf) * 0.01
     b_uo = rnd(1)
@@ -108,6 +111,7 @@ def main():
         "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
         "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
+        "dfirst_fwd": lambda: ops.conv3d(x_df, w_dfw, ngf, 4, 2, 1, (s2, s2, s2), bias=b_df, act="lrelu"),
         "unet_up": lambda: ops.conv3d(x_uo, w_uo, 1, 4, 2, 1, (S, S, S), bias=b_uo, act="tanh", transposed=True),
         "dfirst_dgrad": lambda: ops.conv3d(dy_df, w_df, 1, 4, 2, 1, (S, S, S), transposed=True),
         "down1_wgrad": lambda: ops.conv3d_wgrad(dy_dn1, x_dn1, 3, 2, 1, gw_dn1, False),
