@@ -6,7 +6,7 @@
 // The contraction is one voxel's 4³ taps × nc channels — K = 64·nc — against C = 32 or 64 output
 // channels: an MFMA GEMM with M = output voxels, N = C.  The VALU kernel (thin_k: one thread per
 // voxel × 32 channels, 2048 FMAs each) took 26–39 µs per launch at 64³.
-// A block owns a 4 × 8 × 16 output brick of one instance; its (2·4 + 2) × (2·8 + 2) × (2·16 + 2)
+// A block owns a 2 × 8 × 16 output brick of one instance; its (2·2 + 2) × (2·8 + 2) × (2·16 + 2)
 // input region is staged in LDS as 16-bit operands (RNE, as every kernel of the mode rounds), and
 // an A fragment — 8 consecutive K of one voxel — is gathered from it:
 //   nc = 1: K = (kd·4 + kh)·4 + kw; a lane's 8 K are two kh rows × the 4 kw taps: two runs of 4
@@ -31,9 +31,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kDD = 4, kDH = 8, kDW = 16;                     // output brick
-constexpr int kRD = 2 * kDD + 2, kRH = 2 * kDH + 2, kRW = 2 * kDW + 2;   // input region 10 × 18 × 34
-constexpr int kDRT = kDD * kDH * kDW / 32;                    // 16 row tiles of 32 voxels
+// output brick 2 × 8 × 16 (512 blocks for a 4 × 32³ output: two per CU hide each other's
+// staging and store phases; 4 × 8 × 16 bricks — 256 blocks, one per CU — took 20 µs)
+constexpr int kDD = 2, kDH = 8, kDW = 16;
+constexpr int kRD = 2 * kDD + 2, kRH = 2 * kDH + 2, kRW = 2 * kDW + 2;   // input region 6 × 18 × 34
+constexpr int kDRT = kDD * kDH * kDW / 32;                    // 8 row tiles of 32 voxels
 
 template <int NC>
 constexpr int down4_row_bytes() { return ((kRW * NC * 2 + 15) / 16) * 16 + 8; }   // 72 (nc 1) / 152 (nc 2)

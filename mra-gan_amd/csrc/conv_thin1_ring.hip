@@ -235,7 +235,10 @@ constexpr int kFRed = 4 * kC * 2 * 8;   // + [4 waves][32 channels][Σ, Σ²] do
 
 // C2: a two-channel input (one-plane modes): channel 1's X8 planes and weights sit where the lo
 // splits of bf16x3 do, and each K-step issues one MFMA per channel
-template <int PM, int C2>
+// EPI (compile-time epilogue, round 5): 0 = bias (+ activation); 1 = the next InstanceNorm's Σy, Σy²
+// (a.part); 2 = backward statistics (a.part with a.sx).  With the three in one body the compiler
+// kept every path's registers live (accumulator-file spills, 11 VALU per MFMA: PMC r05g).
+template <int PM, int C2, int EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_fwd_kernel(Thin1RArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);       // [kRing][kFPlaneE]
@@ -250,7 +253,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   const int co = ((li >> 2) & 1) * 16 + (li >> 3) * 4 + (li & 3);
   float bias[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) bias[q] = a.bias ? a.bias[16 * lh + q] : 0.f;
+  for (int q = 0; q < 16; ++q) bias[q] = (EPI == 0 && a.bias) ? a.bias[16 * lh + q] : 0.f;
   // this lane's voxels (B columns): brick rows 4·wave + 2i + li/16 (tile i), column li % 16
   const int bh0 = 4 * wave + (li >> 4), bw = li & 15;
 
@@ -288,14 +291,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     // voxels; fp64 throughout, y² formed in fp64 as the other producers do (fp32 sums of y and y²
     // lose var = E[y²] − E[y]² to cancellation by mean² / var — the stem reads a non-centred
     // volume).  One wave per SIMD by design: the 32 extra registers cost no occupancy.
-    double ps[16], pq[16];
-    float smu[16], srs[16];
+    constexpr int NS = EPI ? 16 : 1;
+    double ps[NS], pq[NS];
+    float smu[NS], srs[NS];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < NS; ++q) {
       ps[q] = pq[q] = 0.0;
       smu[q] = srs[q] = 0.f;
     }
-    if (a.part && a.sx) {
+    if constexpr (EPI == 2) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         smu[q] = a.smean[nb * kC + 16 * lh + q];
@@ -311,8 +315,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       // backward statistics: this step's x̂ operands, loaded before the MFMAs so their latency hides
       // under them (loaded in the epilogue they stalled every depth step: +0.17 ms per step)
-      float4 sxv[2][4];
-      if (a.part && a.sx) {
+      float4 sxv[2][EPI == 2 ? 4 : 1];
+      if constexpr (EPI == 2) {
         const int Sd = a.Do - 2 * a.sfold, Sh = a.Ho - 2 * a.sfold, Sw = a.Wo - 2 * a.sfold;
         const int cd = min(max(od0 + s - a.sfold, 0), Sd - 1), cw = min(max(ow0 + bw - a.sfold, 0), Sw - 1);
 #pragma unroll
@@ -358,16 +362,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           float* yv = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * kC + 16 * lh;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            float4 v = make_float4(acc[i][4 * q] + bias[4 * q], acc[i][4 * q + 1] + bias[4 * q + 1],
-                                   acc[i][4 * q + 2] + bias[4 * q + 2], acc[i][4 * q + 3] + bias[4 * q + 3]);
-            if (a.act != kActNone)
-              v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
+            float4 v = make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
+            if constexpr (EPI == 0) {
+              v = make_float4(v.x + bias[4 * q], v.y + bias[4 * q + 1], v.z + bias[4 * q + 2], v.w + bias[4 * q + 3]);
+              if (a.act != kActNone)
+                v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
+            }
             *reinterpret_cast<float4*>(yv + 4 * q) = v;
-            if (a.part && !a.sx) {
+            if constexpr (EPI == 1) {
               ps[4 * q] += v.x; ps[4 * q + 1] += v.y; ps[4 * q + 2] += v.z; ps[4 * q + 3] += v.w;
               pq[4 * q] += (double)v.x * v.x; pq[4 * q + 1] += (double)v.y * v.y;
               pq[4 * q + 2] += (double)v.z * v.z; pq[4 * q + 3] += (double)v.w * v.w;
-            } else if (a.part) {
+            } else if constexpr (EPI == 2) {
               const float4 xv = sxv[i][q];
               const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -384,7 +390,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       __syncthreads();
     }
-    if (a.part) {
+    if constexpr (EPI != 0) {
       // item = nb · (items per instance) + (chunk · nbh + chh) · nbw + cw: the partials' chunk order
       double* red = reinterpret_cast<double*>(smem + kFLds);
 #pragma unroll
@@ -432,15 +438,22 @@ bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode) {
 
 size_t thin1_x3_ws_bytes(int ny) { return (size_t)kGroups * 2 * ny * 8 * sizeof(__bf16); }
 
-template <int PM, int C2>
-static void launch_thin1_fwd(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
+template <int PM, int C2, int EPI>
+static void launch_thin1_fwd_e(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM, C2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM, C2, EPI>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((thin1r_fwd_kernel<PM, C2>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((thin1r_fwd_kernel<PM, C2, EPI>), dim3(grid), dim3(256), lds, st, a);
+}
+
+template <int PM, int C2>
+static void launch_thin1_fwd(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
+  if (!a.part) launch_thin1_fwd_e<PM, C2, 0>(a, grid, lds, st);
+  else if (!a.sx) launch_thin1_fwd_e<PM, C2, 1>(a, grid, lds, st);
+  else launch_thin1_fwd_e<PM, C2, 2>(a, grid, lds, st);
 }
 
 template <int PM>

@@ -16,9 +16,9 @@ import torch  # noqa: E402
 from mragan_hip import ops  # noqa: E402
 from mragan_hip._lib import lib  # noqa: E402
 
-ops.set_conv_precision("bf16x3")
 S, N, ngf = 64, int(sys.argv[1]) if len(sys.argv) > 1 else 2, 32
 which = sys.argv[2] if len(sys.argv) > 2 else "fwd"
+ops.set_conv_precision(sys.argv[3] if len(sys.argv) > 3 else "bf16x3")
 x = torch.randn(N, S + 6, S + 6, S + 6, 1, device="cuda")
 w = torch.randn(343 * ngf, device="cuda") * 0.01
 dh = torch.randn(N, S, S, S, ngf, device="cuda")

@@ -74,6 +74,11 @@ def main():
     x_df = rnd(N, S, S, S, 1)                            # D first layer input (1 channel)
     w_dfw = rnd(64 * ngf) * 0.01
     b_df = rnd(ngf)
+    part_stem = ops.in_partials_buffer(N, (S, S, S), ngf, dev)
+    h_up2 = rnd(N, S, S, S, ngf)                         # G up2's conv output (the head's IN input)
+    m_up2 = rnd(N, ngf) * 0.1
+    r_up2 = torch.rand(N, ngf, device=dev) + 0.5
+    part_head = ops.in_partials_buffer(N, (S + 6, S + 6, S + 6), ngf, dev)
     x_uo = rnd(N, s2, s2, s2, 2 * ngf)                    # UNet outermost upconv input (2·ngf channels)
     w_uo = rnd(64 * 2 * ngf) * 0.01
     b_uo = rnd(1)
@@ -112,6 +117,9 @@ def main():
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
         "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
         "dfirst_fwd": lambda: ops.conv3d(x_df, w_dfw, ngf, 4, 2, 1, (s2, s2, s2), bias=b_df, act="lrelu"),
+        "stem_fwd_st": lambda: ops.conv3d_in_stats(x_stem, w_stem, ngf, 7, 1, 0, (S, S, S), None, part_stem),
+        "head_dgrad_st": lambda: ops.conv3d_dgrad_in_stats(dz, w_stem, ngf, 7, h_up2, m_up2, r_up2, "relu", 3,
+                                                           part_head),
         "unet_up": lambda: ops.conv3d(x_uo, w_uo, 1, 4, 2, 1, (S, S, S), bias=b_uo, act="tanh", transposed=True),
         "dfirst_dgrad": lambda: ops.conv3d(dy_df, w_df, 1, 4, 2, 1, (S, S, S), transposed=True),
         "down1_wgrad": lambda: ops.conv3d_wgrad(dy_dn1, x_dn1, 3, 2, 1, gw_dn1, False),
