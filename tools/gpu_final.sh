@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-4 evidence at HEAD: all -m gpu tests, smoke, the default (driver) bench line, a kernel trace
-# of the headline workload (traced durations include the other lane's contention), and PMC passes
-# (FETCH_SIZE / WRITE_SIZE; instruction mix) of the res-block operand-plane kernels (bf16, N = 4).
-#   bash tools/gpu_r04_final.sh TAG [notests]
+# Evidence at HEAD: all -m gpu tests, smoke, the default (driver) bench line (full report to a file),
+# a kernel trace of the headline workload (traced durations include the other lane's contention),
+# and PMC passes (FETCH_SIZE / WRITE_SIZE; instruction mix) of the res-block operand-plane kernels
+# (bf16, N = 4).
+#   bash tools/gpu_final.sh TAG [notests]
 set -eo pipefail
 TAG=${1:-r04final}
 NOTESTS=${2:-}
@@ -18,7 +19,7 @@ if [ -z "$NOTESTS" ]; then
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
   tail -2 "$O/smoke.log"
 fi
-step bench 700 python3 bench.py > "$O/bench.json" 2> "$O/bench.err"
+step bench 700 python3 bench.py --full-out "gpurun_out/$TAG/bench_full.json" > "$O/bench.json" 2> "$O/bench.err"
 cut -c1-400 "$O/bench.json"
 cd /tmp && export TMPDIR=/tmp
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o bench \

@@ -117,6 +117,10 @@ def main():
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
         "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
         "dfirst_fwd": lambda: ops.conv3d(x_df, w_dfw, ngf, 4, 2, 1, (s2, s2, s2), bias=b_df, act="lrelu"),
+        "head_fwd16": lambda: ops.conv3d_thin_op16(x_head.to(dt16), w_head, 1, 7, 1, 0, (S, S, S), act="tanh"),
+        "stem_dgrad16": lambda: ops.conv3d_thin_op16(dh1.to(dt16), w_head, 1, 7, 1, 0, (S + 6,) * 3, transposed=True),
+        "head_wgrad16": lambda: ops.conv3d_wgrad_thin_op16(dz, x_head.to(dt16), 7, 1, 0, gw_head, False),
+        "stem_wgrad16": lambda: ops.conv3d_wgrad_thin_op16(dh1.to(dt16), x_stem, 7, 1, 0, gw_head, False),
         "stem_fwd_st": lambda: ops.conv3d_in_stats(x_stem, w_stem, ngf, 7, 1, 0, (S, S, S), None, part_stem),
         "head_dgrad_st": lambda: ops.conv3d_dgrad_in_stats(dz, w_stem, ngf, 7, h_up2, m_up2, r_up2, "relu", 3,
                                                            part_head),
