@@ -291,12 +291,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     // voxels; fp64 throughout, y² formed in fp64 as the other producers do (fp32 sums of y and y²
     // lose var = E[y²] − E[y]² to cancellation by mean² / var — the stem reads a non-centred
     // volume).  One wave per SIMD by design: the 32 extra registers cost no occupancy.
+    // The backward statistics (EPI 2: Σg, Σg·x̂ — no variance formula, nothing cancels against a
+    // square) accumulate in fp32 over the item's ≤ 32 values per lane and channel and join the fp64
+    // sums at the item's end: 4 VALU fewer per value than fp64 throughout (r05i PMC: 10 VALU per MFMA)
     constexpr int NS = EPI ? 16 : 1;
-    double ps[NS], pq[NS];
+    using AccT = typename std::conditional<EPI == 2, float, double>::type;
+    AccT ps[NS], pq[NS];
     float smu[NS], srs[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      ps[q] = pq[q] = 0.0;
+      ps[q] = pq[q] = AccT(0);
       smu[q] = srs[q] = 0.f;
     }
     if constexpr (EPI == 2) {
@@ -382,7 +386,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
                 const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
                                  : (a.sact == kActLrelu && !(xh > 0.f)) ? vs[e] * kLreluSlope : vs[e];
                 ps[4 * q + e] += gv;
-                pq[4 * q + e] += (double)gv * xh;
+                pq[4 * q + e] = fmaf(gv, xh, pq[4 * q + e]);
               }
             }
           }
@@ -395,7 +399,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       double* red = reinterpret_cast<double*>(smem + kFLds);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        double s2 = ps[q], q2 = pq[q];
+        double s2 = (double)ps[q], q2 = (double)pq[q];
 #pragma unroll
         for (int m = 1; m < 32; m <<= 1) {
           s2 += __shfl_xor(s2, m);
