@@ -28,6 +28,7 @@
 // Work items = (column, depth chunk of L steps); L is chosen on the host so that the items
 // divide evenly over the CUs (one 4-wave block per CU, grid ≤ CU count, items strided).
 #include "kernels.h"
+#include "lane_ops.h"
 #include "prec.h"
 
 #include <type_traits>
@@ -251,11 +252,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   // A row li (weights) holds channel perm(li) = 16·((li>>2)&1) + 4·(li>>3) + (li&3), so
   // accumulator 4q + e of lane (li, lh) is channel 16·lh + 4q + e: 64 contiguous bytes per lane
   const int co = ((li >> 2) & 1) * 16 + (li >> 3) * 4 + (li & 3);
+  // WREG (one-plane, one channel): the 25 A fragments live in registers for the whole kernel
+  // (100 VGPRs; one wave per SIMD leaves room) — per MFMA only the ring's B fragment is read from
+  // LDS.  The r05 form re-read the weights from LDS every K-step and issued each MFMA right behind
+  // its two reads (s_waitcnt lgkmcnt(0) per MFMA: one LDS latency per 32-cycle MFMA, ≈ 8 k cycles
+  // per depth step against 1.6 k of MFMA, stamps r05g).
+  constexpr bool WREG = !prec::has_lo<PM>() && !C2 && EPI != 2;   // EPI 2: its registers go to the statistics
+  bf16x8 wreg[WREG ? kKS : 1];
+  if constexpr (WREG) {
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) wreg[ks] = wsm[((2 * ks + lh) * 2 + 0) * kC + co];
+  }
   float bias[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) bias[q] = (EPI == 0 && a.bias) ? a.bias[16 * lh + q] : 0.f;
   // this lane's voxels (B columns): brick rows 4·wave + 2i + li/16 (tile i), column li % 16
   const int bh0 = 4 * wave + (li >> 4), bw = li & 15;
+  // store layout (quad transposes): lane 4m + k handles piece k (channels 16·lh + 4k …) of the
+  // voxels 4m … 4m + 3 — the same tile row as its own voxel, columns bwq … bwq + 3
+  const int kq4 = li & 3, bwq = bw & ~3;
 
   for (int item = blockIdx.x; item < a.items; item += gridDim.x) {
     int r = item;
@@ -314,44 +330,76 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const bool more = s + kK < nplanes;
       float n0[8], n1[8], m0[8], m1[8];
       if (more) {
+#ifdef MRAGAN_EXP_NOLOAD            // bottleneck experiments (variant builds only, tools/)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) n0[j] = n1[j] = m0[j] = m1[j] = 0.f;
+#else
         load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er0, w0 + ep, n0, m0);
         if (e1) load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + s + kK, h0 + er1, w0 + ep, n1, m1);
+#endif
       }
       // backward statistics: this step's x̂ operands, loaded before the MFMAs so their latency hides
       // under them (loaded in the epilogue they stalled every depth step: +0.17 ms per step)
+      // Loaded in the store layout (below): lane (4m + k, lh) reads the 16-B piece k of the four
+      // voxels 4m … 4m + 3 of its tile row — each load instruction then covers 8 voxels' whole
+      // 128-B rows instead of 16-B pieces of 32 rows — and a quad transpose after the MFMAs
+      // turns them into this lane's own voxel's pieces
       float4 sxv[2][EPI == 2 ? 4 : 1];
       if constexpr (EPI == 2) {
         const int Sd = a.Do - 2 * a.sfold, Sh = a.Ho - 2 * a.sfold, Sw = a.Wo - 2 * a.sfold;
-        const int cd = min(max(od0 + s - a.sfold, 0), Sd - 1), cw = min(max(ow0 + bw - a.sfold, 0), Sw - 1);
+        const int cd = min(max(od0 + s - a.sfold, 0), Sd - 1);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int ch = min(max(oh0 + bh0 + 2 * i - a.sfold, 0), Sh - 1);
-          const float* xp = a.sx + ((((int64_t)nb * Sd + cd) * Sh + ch) * Sw + cw) * kC + 16 * lh;
+          const float* xrow = a.sx + (((int64_t)nb * Sd + cd) * Sh + ch) * (int64_t)Sw * kC + 16 * lh + 4 * kq4;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) sxv[i][q] = *reinterpret_cast<const float4*>(xp + 4 * q);
+          for (int j = 0; j < 4; ++j) {
+            const int cw = min(max(ow0 + bwq + j - a.sfold, 0), Sw - 1);
+            sxv[i][j] = *reinterpret_cast<const float4*>(xrow + (int64_t)cw * kC);
+          }
         }
       }
       f32x16 acc[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-      for (int ks = 0; ks < kKS; ++ks) {
-        // this lane's group 2ks + lh → (kd, kh); the zero group 49 reads group 48's entries
+      // fragments of K-step ks: this lane's group 2ks + lh → (kd, kh) (the zero group 49 reads
+      // group 48's ring entries); software-pipelined one K-step ahead, so each MFMA waits on reads
+      // issued a whole K-step earlier
+      constexpr bool kTwo = prec::has_lo<PM>() || C2;
+      auto frag = [&](int ks, bf16x8& ah, bf16x8& al, bf16x8 (&xh)[2], bf16x8 (&xl)[2]) __attribute__((always_inline)) {
         const int g = 2 * ks + lh;
         const int g0 = 2 * ks, g1 = 2 * ks + 1 < kK * kK ? 2 * ks + 1 : kK * kK - 1;
         const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
-        const bf16x8 ah = wsm[(g * 2 + 0) * kC + co];
-        const bf16x8 al = (prec::has_lo<PM>() || C2) ? wsm[(g * 2 + 1) * kC + co] : ah;
+        if constexpr (!WREG) {
+          ah = wsm[(g * 2 + 0) * kC + co];
+          al = kTwo ? wsm[(g * 2 + 1) * kC + co] : ah;
+        }
         const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<0>(bh0 + kh, bw, 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 xh = ringH[base + 2 * i * kBW];
-          const bf16x8 xl = (prec::has_lo<PM>() || C2) ? ringL[base + 2 * i * kBW] : xh;
+          xh[i] = ringH[base + 2 * i * kBW];
+          xl[i] = kTwo ? ringL[base + 2 * i * kBW] : xh[i];
+        }
+      };
+      bf16x8 fah[2], fal[2], fxh[2][2], fxl[2][2];
+      frag(0, fah[0], fal[0], fxh[0], fxl[0]);
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) {
+#ifdef MRAGAN_EXP_NOMFMA
+        if (ks > 0) break;
+#endif
+        const int c = ks & 1;
+        if (ks + 1 < kKS) frag(ks + 1, fah[c ^ 1], fal[c ^ 1], fxh[c ^ 1], fxl[c ^ 1]);
+        const bf16x8 ah = WREG ? wreg[WREG ? ks : 0] : fah[c];
+        const bf16x8 al = WREG ? ah : fal[c];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
           if constexpr (C2) {
-            acc[i] = prec::mma<PM>(ah, ah, xh, xh, acc[i]);
-            acc[i] = prec::mma<PM>(al, al, xl, xl, acc[i]);
+            acc[i] = prec::mma<PM>(ah, ah, fxh[c][i], fxh[c][i], acc[i]);
+            acc[i] = prec::mma<PM>(al, al, fxl[c][i], fxl[c][i], acc[i]);
           } else {
-            acc[i] = prec::mma<PM>(ah, al, xh, xl, acc[i]);
+            acc[i] = prec::mma<PM>(ah, al, fxh[c][i], fxl[c][i], acc[i]);
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (more) {
         store_x8c<PM, C2>(ringH, ringL, kFPlaneE, (s + kK) & (kRing - 1), tid, n0, m0);
@@ -359,37 +407,97 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
 
       const int od = od0 + s, ow = ow0 + bw;
+      // the statistics run on every lane (a voxel outside the output adds 0), all of them before
+      // the first store, and only the stores are predicated: on gfx9 vmcnt counts stores too, so a
+      // wait for an sx load issued before some output stores also waits for those stores (the r05
+      // form interleaved them and made every depth step wait for its own output stores)
+      bool in[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int oh = oh0 + bh0 + 2 * i;
-        if (oh < a.Ho && ow < a.Wo) {
-          float* yv = a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * kC + 16 * lh;
+      for (int i = 0; i < 2; ++i) in[i] = oh0 + bh0 + 2 * i < a.Ho && ow < a.Wo;
+      if constexpr (EPI == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float v = acc[i][e] + bias[e];
+            acc[i][e] = a.act != kActNone ? act_fwd(v, a.act) : v;
+          }
+      } else if constexpr (EPI == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float u = in[i] ? acc[i][e] : 0.f;
+            ps[e] += u;
+            pq[e] += (double)u * u;
+          }
+      } else {
+        // sx pieces from the store layout to this lane's own voxel (component-wise quad transposes:
+        // lane k held piece k of voxels 0 … 3 of its quad, now pieces 0 … 3 of voxel k)
+        float4 own[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          f32x4v t[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            f32x4v v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = c == 0 ? sxv[i][j].x : c == 1 ? sxv[i][j].y : c == 2 ? sxv[i][j].z : sxv[i][j].w;
+            t[c] = quad_transpose(v, kq4);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) own[i][q] = make_float4(t[0][q], t[1][q], t[2][q], t[3][q]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            float4 v = make_float4(acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]);
-            if constexpr (EPI == 0) {
-              v = make_float4(v.x + bias[4 * q], v.y + bias[4 * q + 1], v.z + bias[4 * q + 2], v.w + bias[4 * q + 3]);
-              if (a.act != kActNone)
-                v = make_float4(act_fwd(v.x, a.act), act_fwd(v.y, a.act), act_fwd(v.z, a.act), act_fwd(v.w, a.act));
-            }
-            *reinterpret_cast<float4*>(yv + 4 * q) = v;
-            if constexpr (EPI == 1) {
-              ps[4 * q] += v.x; ps[4 * q + 1] += v.y; ps[4 * q + 2] += v.z; ps[4 * q + 3] += v.w;
-              pq[4 * q] += (double)v.x * v.x; pq[4 * q + 1] += (double)v.y * v.y;
-              pq[4 * q + 2] += (double)v.z * v.z; pq[4 * q + 3] += (double)v.w * v.w;
-            } else if constexpr (EPI == 2) {
-              const float4 xv = sxv[i][q];
-              const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, vs[4] = {v.x, v.y, v.z, v.w};
+            const float4 xv = own[i][q];
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float xh = (xs[e] - smu[4 * q + e]) * srs[4 * q + e];
-                const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
-                                 : (a.sact == kActLrelu && !(xh > 0.f)) ? vs[e] * kLreluSlope : vs[e];
-                ps[4 * q + e] += gv;
-                pq[4 * q + e] = fmaf(gv, xh, pq[4 * q + e]);
-              }
+            for (int e = 0; e < 4; ++e) {
+              const float vs = acc[i][4 * q + e];
+              const float xh = (xs[e] - smu[4 * q + e]) * srs[4 * q + e];
+              const float g0 = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
+                               : (a.sact == kActLrelu && !(xh > 0.f)) ? vs * kLreluSlope : vs;
+              const float gv = in[i] ? g0 : 0.f;
+              ps[4 * q + e] += gv;
+              pq[4 * q + e] = fmaf(gv, xh, pq[4 * q + e]);
             }
           }
+      }
+      if constexpr (EPI == 2) {
+        // the compiler sinks the statistics below the stores; this empty asm reads the sx values
+        // (so their wait is placed here) and the memory clobber keeps the stores after it
+        asm volatile("" ::"v"(sxv[0][0].x), "v"(sxv[0][1].x), "v"(sxv[0][2].x), "v"(sxv[0][3].x), "v"(sxv[1][0].x),
+                     "v"(sxv[1][1].x), "v"(sxv[1][2].x), "v"(sxv[1][3].x)
+                     : "memory");
+      }
+      // stores in the store layout: after component-wise quad transposes lane (4m + k, lh) holds
+      // piece k of voxels 4m … 4m + 3, so store j writes 8 voxels' whole 128-B rows (the lanes of
+      // a quad: 64 contiguous bytes per half) instead of 16-B pieces of 32 rows — 4× fewer cache
+      // lines per store instruction (the stores were a third of the stem forward's time, r05r)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f32x4v t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          f32x4v v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[i][4 * q + c];
+          t[c] = quad_transpose(v, kq4);
+        }
+        const int oh = oh0 + bh0 + 2 * i;
+        float* yrow = a.y + (((int64_t)nb * a.Do + od) * a.Ho + oh) * (int64_t)a.Wo * kC + 16 * lh + 4 * kq4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int owj = ow0 + bwq + j;
+#ifdef MRAGAN_EXP_NOSTORE
+          if (oh < a.Ho && owj < a.Wo && a.Do < 0)
+#else
+          if (oh < a.Ho && owj < a.Wo)
+#endif
+            *reinterpret_cast<float4*>(yrow + (int64_t)owj * kC) = make_float4(t[0][j], t[1][j], t[2][j], t[3][j]);
         }
       }
       __syncthreads();
@@ -645,6 +753,33 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 
       const __bf16* ph = pt + (size_t)(s & 1) * 2 * kC * kPS;
       const __bf16* pl = ph + kC * kPS;
+      if constexpr (!prec::has_lo<PM>()) {
+        // one-plane modes: both K-steps' fragments are read before their MFMAs (K-step 1's while
+        // K-step 0's MFMAs run) instead of each MFMA waiting on its own ring read (r05 PMC: 13.6
+        // VALU per MFMA, every MFMA behind an s_waitcnt lgkmcnt(0))
+        bf16x8 fa[2][kWT0], fb[2];
+        auto fragw = [&](int kss, bf16x8 (&A)[kWT0], bf16x8& B) __attribute__((always_inline)) {
+          B = *reinterpret_cast<const bf16x8*>(ph + li * kPS + (2 * kq + kss) * kBW + 8 * lh);
+#pragma unroll
+          for (int i = 0; i < kWT0; ++i) {
+            if (i < nt) {
+              const int g = min(4 * (t0 + i) + (li >> 3), kK * kK - 1);
+              const int kd = g / kK, kh = g - kd * kK;
+              const int row = 2 * kq + kss + kh;
+              A[i] = ringH[((s + kd) & (kRing - 1)) * kPlaneE + row * kBW +
+                           ((8 * lh + kw_l) ^ (((row + kd + s) & 1) << 3))];
+            }
+          }
+        };
+        fragw(0, fa[0], fb[0]);
+        fragw(1, fa[1], fb[1]);
+#pragma unroll
+        for (int kss = 0; kss < 2; ++kss) {
+#pragma unroll
+          for (int i = 0; i < kWT0; ++i)
+            if (i < nt) acc[i] = prec::mma<PM>(fa[kss][i], fa[kss][i], fb[kss], fb[kss], acc[i]);
+        }
+      } else
 #pragma unroll
       for (int kss = 0; kss < 2; ++kss) {
         // K-step: brick row 2·kq + kss, voxels 8·lh … +7 of its 16

@@ -579,6 +579,197 @@ static int launch_in_bwd_apply(const InBwdArgs& a, const InShape& s, const doubl
   return check_launch(a.dx16 ? "in_bwd_apply(op16)" : "in_bwd_apply");
 }
 
+// ---- small instances: statistics and apply in ONE launch ----------------------------------
+// The three-launch form (statistics partials → finalize → apply) costs three dependent launches
+// whatever the size; on the small tensors (the UNet's 8³ / 4³ / 2³ levels, the PatchGAN's 8³ / 7³
+// layers, ≤ 64 KB per channel group) each launch is a few µs of dispatch and ramp for a few KB of
+// data, and the chain of a lane is what the step waits for (UNet 64³ b1 step: 240 of its ≈ 680
+// launches were InstanceNorm).  Here a block owns 4·CQB channels of one instance: pass 1 sums
+// (Σx, Σx²) — or the backward's (Σg, Σg·x̂) — in fp64 over every voxel, a fixed xor butterfly
+// over the wave's voxel slots and a fixed 4-wave sum give the statistics (deterministic), pass 2
+// re-reads the block's (L2-resident) slice and applies.  No partials, no finalize launch.
+// Thread = (voxel slot vt, channel quad q of the block), q fastest: lane = vt·CQB + q.
+constexpr int kInSmallBytes = 64 * 1024;          // per block and pass
+static int in_small_cqb(const InShape& s) {
+  static const int64_t max_s = [] {                 // A/B: MRAGAN_IN_SMALL=0 off, =S the largest S
+    const char* e = getenv("MRAGAN_IN_SMALL");
+    return e ? (int64_t)atoll(e) : (int64_t)1 << 20;
+  }();
+  // a block reads whole 128-B lines of each voxel (32 channels, or all of a narrower tensor): with
+  // fewer channels per block every line is fetched by several blocks on different XCDs — the
+  // 4-channel slices of a 16³ C128 norm ran the 64³ b2 step at 13.2 instead of 11.1 ms (r05o)
+  const int CQ = s.C / 4;
+  int cqb = 8;
+  while (cqb > 1 && (cqb > CQ || CQ % cqb)) cqb >>= 1;           // narrower tensors: 4, 2 or 1 quads
+  if (s.S() > max_s || s.N < 1 || (cqb < 8 && s.C >= 32)) return 0;
+  return s.S() * cqb * 16 <= kInSmallBytes ? cqb : 0;
+}
+
+// fixed-order block sum of 4 channel values (per thread: its quad's 4 components) over the voxel
+// slots: xor butterfly over the lane bits above the quad index, then the 4 waves in order
+template <int CQB>
+__device__ __forceinline__ void in_small_reduce(double (&a)[4], double (&b)[4], double* red /* [4][CQB*4][2] */) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = tid % CQB;
+#pragma unroll
+  for (int off = CQB; off < 64; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] += __shfl_xor(a[j], off);
+      b[j] += __shfl_xor(b[j], off);
+    }
+  if (lane < CQB)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[((wave * CQB + q) * 4 + j) * 2] = a[j];
+      red[((wave * CQB + q) * 4 + j) * 2 + 1] = b[j];
+    }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double A = 0, B = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      A += red[((w * CQB + q) * 4 + j) * 2];
+      B += red[((w * CQB + q) * 4 + j) * 2 + 1];
+    }
+    a[j] = A;
+    b[j] = B;
+  }
+}
+
+template <int CQB>
+__global__ void __launch_bounds__(256) in_small_fwd_kernel(const float* __restrict__ x, InShape s, float* __restrict__ mean,
+                                                           float* __restrict__ rstd, int act,
+                                                           const float* __restrict__ resid, int rpad,
+                                                           float* __restrict__ y, int ypad, uint2* __restrict__ y16,
+                                                           int mode) {
+  __shared__ double red[4 * CQB * 4 * 2];
+  constexpr int VS = 256 / CQB;
+  const int n = blockIdx.y, tid = threadIdx.x, q = tid % CQB, vt = tid / CQB;
+  const int CQ = s.C / 4, qg = blockIdx.x * CQB + q;              // this thread's channel quad
+  const int S = (int)s.S();
+  const float4* xv = reinterpret_cast<const float4*>(x) + (size_t)n * S * CQ + qg;
+  double sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+#pragma unroll 4
+  for (int v = vt; v < S; v += VS) {
+    const float4 t = xv[(size_t)v * CQ];
+    sa[0] += t.x; sa[1] += t.y; sa[2] += t.z; sa[3] += t.w;
+    sb[0] += (double)t.x * t.x; sb[1] += (double)t.y * t.y; sb[2] += (double)t.z * t.z; sb[3] += (double)t.w * t.w;
+  }
+  in_small_reduce<CQB>(sa, sb, red);
+  float mu[4], rs[4];
+  const double Sd = (double)S;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double m = sa[j] / Sd;
+    double var = sb[j] / Sd - m * m;
+    if (var < 0) var = 0;
+    mu[j] = (float)m;
+    rs[j] = (float)(1.0 / sqrt(var + (double)kInEps));
+  }
+  if (vt == 0) {
+    reinterpret_cast<float4*>(mean + n * s.C)[qg] = make_float4(mu[0], mu[1], mu[2], mu[3]);
+    reinterpret_cast<float4*>(rstd + n * s.C)[qg] = make_float4(rs[0], rs[1], rs[2], rs[3]);
+  }
+  const int Dp = s.D + 2 * ypad, Hp = s.H + 2 * ypad, Wp = s.W + 2 * ypad, P = Dp * Hp * Wp;
+  const int Dr = s.D + 2 * rpad, Hr = s.H + 2 * rpad, Wr = s.W + 2 * rpad;
+  const float4* rv = resid ? reinterpret_cast<const float4*>(resid) + (size_t)n * Dr * Hr * Wr * CQ + qg : nullptr;
+  float4* yv = y ? reinterpret_cast<float4*>(y) + (size_t)n * P * CQ + qg : nullptr;
+  uint2* y16v = y16 ? y16 + (size_t)n * P * CQ + qg : nullptr;
+  for (int pv = vt; pv < P; pv += VS) {
+    const int wp = pv % Wp, t = pv / Wp, hp = t % Hp, dp = t / Hp;
+    const int sd = min(max(dp - ypad, 0), s.D - 1), sh = min(max(hp - ypad, 0), s.H - 1), sw = min(max(wp - ypad, 0), s.W - 1);
+    const int sv = (sd * s.H + sh) * s.W + sw;
+    float4 v = xv[(size_t)sv * CQ];
+    v = make_float4((v.x - mu[0]) * rs[0], (v.y - mu[1]) * rs[1], (v.z - mu[2]) * rs[2], (v.w - mu[3]) * rs[3]);
+    v = f4_act(v, act);
+    if (rv) {
+      const float4 r = rv[(size_t)(((sd + rpad) * Hr + sh + rpad) * Wr + sw + rpad) * CQ];
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    if (yv) yv[(size_t)pv * CQ] = v;
+    if (y16v) y16v[(size_t)pv * CQ] = f4_op16(v, mode);
+  }
+}
+
+template <int CQB, int P>
+__global__ void __launch_bounds__(256) in_small_bwd_kernel(InBwdArgs a, InShape s) {
+  __shared__ double red[4 * CQB * 4 * 2];
+  constexpr int VS = 256 / CQB;
+  const int n = blockIdx.y, tid = threadIdx.x, q = tid % CQB, vt = tid / CQB;
+  const int CQ = s.C / 4, qg = blockIdx.x * CQB + q;
+  const int S = (int)s.S();
+  double sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  for (int v = vt; v < S; v += VS) {
+    const int w = v % s.W, t = v / s.W, h = t % s.H, d = t / s.H;
+    const InRow row = in_bwd_row(a, s, n, d, h, qg);
+    float4 g, xh;
+    in_bwd_voxel<P>(a, s, row, w, g, xh);
+    sa[0] += g.x; sa[1] += g.y; sa[2] += g.z; sa[3] += g.w;
+    sb[0] += (double)g.x * xh.x; sb[1] += (double)g.y * xh.y; sb[2] += (double)g.z * xh.z; sb[3] += (double)g.w * xh.w;
+  }
+  in_small_reduce<CQB>(sa, sb, red);
+  const double Sd = (double)S;
+  float mg[4], mgx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mg[j] = (float)(sa[j] / Sd);
+    mgx[j] = (float)(sb[j] / Sd);
+  }
+  float4* dx = reinterpret_cast<float4*>(a.dx);
+  uint2* dx16 = reinterpret_cast<uint2*>(a.dx16);
+  float4* gout = reinterpret_cast<float4*>(a.g_out);
+  for (int v = vt; v < S; v += VS) {
+    const int w = v % s.W, t = v / s.W, h = t % s.H, d = t / s.H;
+    const InRow row = in_bwd_row(a, s, n, d, h, qg);
+    float4 g, xh, graw;
+    in_bwd_voxel<P>(a, s, row, w, g, xh, &graw);
+    const size_t o = ((size_t)n * S + v) * CQ + qg;
+    if (gout) gout[o] = graw;
+    float4 r;
+    r.x = row.rs.x * (g.x - mg[0] - xh.x * mgx[0]);
+    r.y = row.rs.y * (g.y - mg[1] - xh.y * mgx[1]);
+    r.z = row.rs.z * (g.z - mg[2] - xh.z * mgx[2]);
+    r.w = row.rs.w * (g.w - mg[3] - xh.w * mgx[3]);
+    if (dx) dx[o] = r;
+    if (dx16) dx16[o] = f4_op16(r, a.mode16);
+  }
+}
+
+static int launch_in_small_fwd(int cqb, const float* x, const InShape& s, float* mean, float* rstd, int act,
+                               const float* resid, int rpad, float* y, int ypad, void* y16, int mode16, hipStream_t st) {
+  const dim3 g(s.C / 4 / cqb, s.N);
+  uint2* o16 = static_cast<uint2*>(y16);
+  switch (cqb) {
+    case 8: hipLaunchKernelGGL(in_small_fwd_kernel<8>, g, dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad, o16, mode16); break;
+    case 4: hipLaunchKernelGGL(in_small_fwd_kernel<4>, g, dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad, o16, mode16); break;
+    case 2: hipLaunchKernelGGL(in_small_fwd_kernel<2>, g, dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad, o16, mode16); break;
+    default: hipLaunchKernelGGL(in_small_fwd_kernel<1>, g, dim3(256), 0, st, x, s, mean, rstd, act, resid, rpad, y, ypad, o16, mode16); break;
+  }
+  return check_launch(y16 ? "in_small_fwd(op16)" : "in_small_fwd");
+}
+
+template <int CQB>
+static void launch_in_small_bwd_c(const InBwdArgs& a, const InShape& s, hipStream_t st) {
+  const dim3 g(s.C / 4 / CQB, s.N);
+  switch (a.dypad) {
+    case 0: hipLaunchKernelGGL((in_small_bwd_kernel<CQB, 0>), g, dim3(256), 0, st, a, s); break;
+    case 1: hipLaunchKernelGGL((in_small_bwd_kernel<CQB, 1>), g, dim3(256), 0, st, a, s); break;
+    case 3: hipLaunchKernelGGL((in_small_bwd_kernel<CQB, 3>), g, dim3(256), 0, st, a, s); break;
+    default: hipLaunchKernelGGL((in_small_bwd_kernel<CQB, -1>), g, dim3(256), 0, st, a, s); break;
+  }
+}
+
+static int launch_in_small_bwd(int cqb, const InBwdArgs& a, const InShape& s, hipStream_t st) {
+  switch (cqb) {
+    case 8: launch_in_small_bwd_c<8>(a, s, st); break;
+    case 4: launch_in_small_bwd_c<4>(a, s, st); break;
+    case 2: launch_in_small_bwd_c<2>(a, s, st); break;
+    default: launch_in_small_bwd_c<1>(a, s, st); break;
+  }
+  return check_launch(a.dx16 ? "in_small_bwd(op16)" : "in_small_bwd");
+}
+
 // ---- running statistics (composite of the reference's sequential calls) ------------------
 // One entry per IN layer: the segments (one per reference call, in call order) of per-instance
 // mean/rstd.  r ← (1−m)·r + m·avg_call(μ_n + bias), rv ← (1−m)·rv + m·avg_call(σ²_n · S/(S−1)).
@@ -632,6 +823,7 @@ int instnorm_fwd(const float* x, InShape s, float* y, int ypad, int act, const f
   }
   const int chunks = in_chunks(s);
   if (instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C) > ws_bytes) { set_error("instnorm: workspace too small"); return kWorkspace; }
+  if (const int cqb = in_small_cqb(s)) return launch_in_small_fwd(cqb, x, s, mean, rstd, act, resid, rpad, y, ypad, y16, mode16, st);
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, s.N), dim3(256), 0, st, x, s, chunks, part);
   int rc = check_launch("in_stats");
@@ -686,6 +878,7 @@ int instnorm_bwd(const InBwdArgs& a, InShape s, void* ws, size_t ws_bytes, hipSt
   const int chunks = in_chunks(s);
   const size_t need = instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C) + (size_t)s.N * s.C * 2 * sizeof(float);
   if (need > ws_bytes) { set_error("instnorm_bwd: workspace too small"); return kWorkspace; }
+  if (const int cqb = in_small_cqb(s)) return launch_in_small_bwd(cqb, a, s, st);
   double* part = static_cast<double*>(ws);
   float* coef = reinterpret_cast<float*>(static_cast<char*>(ws) + instnorm_ws_bytes(s.N, s.D, s.H, s.W, s.C));
   const int rows = s.N * s.D * s.H;

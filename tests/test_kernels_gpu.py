@@ -441,7 +441,8 @@ def _in_ref(x, act):
     return y
 
 
-@pytest.mark.parametrize("N,C,S", [(2, 32, 9), (1, 128, 6), (3, 8, 5), (1, 256, 3), (2, 24, 6), (5, 4, 7), (1, 32, 40)])
+@pytest.mark.parametrize("N,C,S", [(2, 32, 9), (1, 128, 6), (3, 8, 5), (1, 256, 3), (2, 24, 6), (5, 4, 7), (1, 32, 40),
+                                   (2, 128, 15), (2, 256, 7), (1, 12, 5)])
 @pytest.mark.parametrize("act", [None, "relu", "lrelu"])
 @pytest.mark.parametrize("ypad", [0, 1, 3])
 def test_instnorm_fwd(ops, N, C, S, act, ypad):
@@ -460,7 +461,8 @@ def test_instnorm_fwd(ops, N, C, S, act, ypad):
     assert rel(mean, x.mean(dim=(2, 3, 4))) < 1e-6
 
 
-@pytest.mark.parametrize("N,C,S", [(2, 32, 7), (1, 128, 5), (2, 8, 6), (2, 24, 5), (1, 32, 33)])
+@pytest.mark.parametrize("N,C,S", [(2, 32, 7), (1, 128, 5), (2, 8, 6), (2, 24, 5), (1, 32, 33), (2, 128, 15), (2, 256, 7),
+                                   (1, 12, 5)])
 @pytest.mark.parametrize("act", [None, "relu", "lrelu"])
 @pytest.mark.parametrize("dypad", [0, 1, 3])
 @pytest.mark.parametrize("with_add", [False, True])
