@@ -65,6 +65,15 @@ __device__ __forceinline__ tr_v4s tr_read(const char* p) {
 template <int TG>
 constexpr int tr_stage() { return kTrRowsD * kTD * 2 + kTrRowsG * TG * 2; }
 
+// KW = 4: the k4 s2 p1 convolutions (PatchGAN layers 2-3, networks3D.py:389-400; the UNet's down
+// convs and, as G = dY, its k4 s2 p1 transposed up convs, networks3D.py:300-330), one-plane modes.
+// Along w the four taps read the fine positions 2w − 1 … 2w + 2 = O[w − 1], E[w], O[w], E[w + 1]:
+// the segment stages 34 fine positions (2w0 − 1 … 2w0 + 32), E in slots 0 … 16, O from slot 17.
+template <int KW> constexpr int gpos() { return 2 * kSegW + KW - 2; }      // 33 | 34
+template <int KW> constexpr int obase() { return KW == 3 ? 16 : 17; }      // first O-phase slot
+template <int KW> __device__ __forceinline__ int gslot_k(int q) { return (q & 1) ? (q - 1) >> 1 : obase<KW>() + (q >> 1); }
+template <int TG, int KW> constexpr int tr_stage_k() { return kTrRowsD * kTD * 2 + gpos<KW>() * kR * TG * 2; }
+
 // one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half
 template <int PM>
 __device__ __forceinline__ void split8_store(char* p, int half, float v0, float v1, float v2, float v3, float v4,
@@ -91,10 +100,12 @@ struct Wgrad3s2Args {
 // (fine position, 8-channel octet), one 16-B load each, stored as they are (one-plane modes);
 // X16G = 2: D too (ABI 16: G down2's weight gradient, whose dY exists only as its plane) — D units
 // (coarse w, octet, segment half): 4 segments × 16 B per thread
-template <int TG, int PM, int AL, int X16G>
+template <int TG, int PM, int AL, int X16G, int KW>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kTr = !prec::has_lo<PM>();
+  static_assert(KW == 3 || (kTr && !X16G), "k4: the one-plane modes on fp32 operands");
+  constexpr int kGPos = gpos<KW>();       // shadows the file constant (33) in this kernel
   static_assert(!X16G || kTr, "16-bit operand planes exist in the one-plane modes only");
   constexpr bool kDp = X16G == 2;         // D as a 16-bit plane too
   constexpr int ESG = X16G ? 2 : 4;       // bytes per G element
@@ -115,10 +126,10 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   int L = blockIdx.x;
   if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
   const int tile = L % (ndn * ngn);
-  const int kk9 = (L / (ndn * ngn)) % 9;
-  const int z = L / (ndn * ngn * 9);
+  const int kk9 = (L / (ndn * ngn)) % (KW * KW);
+  const int z = L / (ndn * ngn * KW * KW);
   const int dn0 = (tile / ngn) * kTD, gn0 = (tile % ngn) * TG;
-  const int kd = kk9 / 3, kh = kk9 % 3;
+  const int kd = kk9 / KW, kh = kk9 % KW;
   const int seg_lo = z * a.seg_per_split;
   if (seg_lo >= a.nseg) return;                    // grid padding (a multiple of 8 blocks)
   const int seg_hi = min(a.nseg, seg_lo + a.seg_per_split);
@@ -192,13 +203,15 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         rd[r] = make_float4(dv.x, dv.y, dv.z, dv.w);
       }
       const int rr = r / nsw, wr = r - rr * nsw;                     // coarse row / run of the segment
-      const bool rok = dok && (gh0 >= 0 || rr > 0);
+      // (KW 4: the fine row past the last, 2H, on the last coarse row with kh = 3)
+      const bool rok = dok && (gh0 >= 0 || rr > 0) && (KW == 3 || gh0 + 2 * rr < Hg);
       // gh0 < 0 only for segment rows rr = 0 (then invalid): rows rr > 0 start at fine row gh0 + 2rr.
       // The soffset carries the row only; the run's w start goes into the (non-negative) voffset:
       // the range check must see the lane's real offset
       const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
       const int wrun = 32 * wr * a.Cg * ESG;
       const bool w_edge = wr == 0;                                   // fine voxel −1 is outside
+      const bool w_redge = KW == 4 && wr == nsw - 1;                 // KW 4: fine voxel 2W too
       if constexpr (X16G) {
         const bool ok8 = rok && g8 && !(w_edge && q8 == 0);
         rg8[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, ok8 ? glane_al8 + wrun : (int)kOobOffset, gso));
@@ -207,12 +220,12 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass) {
         const int q = pass * GP + gq;
-        const bool ok = rok && !(w_edge && q == 0);
+        const bool ok = rok && !(w_edge && q == 0) && !(w_redge && q == kGPos - 1);
         const buf_f32x4 v = buf_load_16b(gr, ok ? glane_al + wrun + pass * GP * a.Cg * 4 : (int)kOobOffset, gso);
         rg[pass][r] = make_float4(v.x, v.y, v.z, v.w);
       }
       const int qx = gx ? gqx : gq;
-      const bool okx = rok && !(w_edge && qx == 0);
+      const bool okx = rok && !(w_edge && qx == 0) && !(w_redge && qx == kGPos - 1);
       const buf_f32x4 v = buf_load_16b(gr, okx ? glane_alx + wrun : (int)kOobOffset, gso);
       rgx[r] = make_float4(v.x, v.y, v.z, v.w);
     }
@@ -336,21 +349,21 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
       }
       if constexpr (X16G) {
-        if (g8) put8(Gs, gslot(q8), go, rg8);
+        if (g8) put8(Gs, gslot_k<KW>(q8), go, rg8);
         if constexpr (kG8X)
-          if (g8x) put8(Gs, gslot(q8x), go, rg8x);
+          if (g8x) put8(Gs, gslot_k<KW>(q8x), go, rg8x);
         return;
       }
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass)
-        put16(Gs, std::integral_constant<int, RBG>{}, gslot(pass * GP + gq), gcq, rg[pass]);
-      if (gx) put16(Gs, std::integral_constant<int, RBG>{}, gslot(gqx), gcq, rgx);
+        put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW>(pass * GP + gq), gcq, rg[pass]);
+      if (gx) put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW>(gqx), gcq, rgx);
       return;
     }
     put(Ds, kDRow, kDHalf, uw, cq, rd);
 #pragma unroll
-    for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot(pass * GP + gq), gcq, rg[pass]);
-    if (gx) put(Gs, kGRow, kGHalf, gslot(gqx), gcq, rgx);
+    for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot_k<KW>(pass * GP + gq), gcq, rg[pass]);
+    if (gx) put(Gs, kGRow, kGHalf, gslot_k<KW>(gqx), gcq, rgx);
   };
   // tr read offsets: lane 4q+p of its 16-lane group g (lane bit 4) reads row 8h + q (+ the read's
   // K offset) and channels (sub-tile base + 16g + 4p … +3)
@@ -361,13 +374,13 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int kp = TG == 32 ? __builtin_amdgcn_readfirstlane(kpar) : 0;
   const int trA_k = trA + 16 * kp * RBD, trB_k = trB + 16 * kp * RBG;
   auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
-    Ds = smem + b * tr_stage<TG>();
+    Ds = smem + b * tr_stage_k<TG, KW>();
     Gs = Ds + kTrRowsD * RBD;
   };
 
-  f32x16 acc[3];
+  f32x16 acc[KW];
 #pragma unroll
-  for (int t = 0; t < 3; ++t) acc[t] = f32x16{};
+  for (int t = 0; t < KW; ++t) acc[t] = f32x16{};
 
   auto advance = [&]() __attribute__((always_inline)) {
     if constexpr (AL) {           // whole rows: one carry chain per stage
@@ -412,21 +425,22 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
     for (int ki = 0; ki < NKS; ++ki) {
       const int ks = KSTEP * ki;                    // + kp (in the bases)
       // K-step ks: coarse w = 2ks + lh × 8 segments
-      bf16x8 fa[2], fb[3][2];
-      // tap kw: kw = 1 → E[w] (slot w), kw = 0 → O[w − 1] (slot 16 + w), kw = 2 → O[w] (slot 17 + w)
+      bf16x8 fa[2], fb[KW][2];
+      // tap kw: kw = 1 → E[w] (slot w), kw = 0 → O[w − 1] (slot ob + w), kw = 2 → O[w] (slot ob + 1 + w),
+      // kw = 3 (KW 4) → E[w + 1] (slot w + 1); ob = the first O slot (16 | 17)
       if constexpr (kTr) {
         // rows 16ks … 16ks+15 (slots 2ks, 2ks+1 × 8 segments): two 4-row reads per operand
         const char* ar = Ds + trA_k + (16 * ks) * RBD;
         const tr_v4s a0 = tr_read(ar), a1 = tr_read(ar + 4 * RBD);
         fa[0] = fa[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
-        constexpr int kslot[3] = {16, 0, 17};
+        constexpr int kslot[4] = {obase<KW>(), 0, obase<KW>() + 1, 1};
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
+        for (int kw = 0; kw < KW; ++kw) {
           const char* br = Gs + trB_k + (16 * ks + kR * kslot[kw]) * RBG;
           const tr_v4s b0 = tr_read(br), b1 = tr_read(br + 4 * RBG);
           fb[kw][0] = fb[kw][1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-      } else {
+      } else if constexpr (KW == 3) {
         const char* arow = Ds + (wm0 + li) * kDRow + lh * 16 + 32 * kp;
         const char* brow = Gs + (wn0 + li) * kGRow + lh * 16 + 32 * kp;
         fa[0] = *reinterpret_cast<const bf16x8*>(arow + ks * 32);
@@ -439,7 +453,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         }
       }
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) acc[kw] = prec::mma<PM>(fa[0], fa[1], fb[kw][0], fb[kw][1], acc[kw]);
+      for (int kw = 0; kw < KW; ++kw) acc[kw] = prec::mma<PM>(fa[0], fa[1], fb[kw][0], fb[kw][1], acc[kw]);
     }
     if constexpr (kTr) {
       if (st + 1 < nstage) {
@@ -458,26 +472,26 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   // TG = 32: the odd-K waves' partial sums join the even-K waves' through LDS (fixed order)
   if constexpr (TG == 32) {
     if constexpr (kTr) __syncthreads();             // every wave is past its last stage's reads
-    float* red = reinterpret_cast<float*>(smem);    // [2 dn halves][3 taps][16][64 lanes]
+    float* red = reinterpret_cast<float*>(smem);    // [2 dn halves][KW taps][16][64 lanes]
     if (kpar == 1) {
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
+      for (int kw = 0; kw < KW; ++kw)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) red[(((wave >> 1) * 3 + kw) * 16 + r) * 64 + lane] = acc[kw][r];
+        for (int r = 0; r < 16; ++r) red[(((wave >> 1) * KW + kw) * 16 + r) * 64 + lane] = acc[kw][r];
     }
     __syncthreads();
     if (kpar == 1) return;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
+    for (int kw = 0; kw < KW; ++kw)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[kw][r] += red[(((wave >> 1) * 3 + kw) * 16 + r) * 64 + lane];
+      for (int r = 0; r < 16; ++r) acc[kw][r] += red[(((wave >> 1) * KW + kw) * 16 + r) * 64 + lane];
   }
 
   // slab[z][t][dn][gn]: lane li = gn column, register r = dn row (r & 3) + 8 (r >> 2) + 4 lh
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    const int t = (kd * 3 + kh) * 3 + kw;
-    float* slab = a.ws + ((int64_t)z * 27 + t) * a.Cd * a.Cg;
+  for (int kw = 0; kw < KW; ++kw) {
+    const int t = (kd * KW + kh) * KW + kw;
+    float* slab = a.ws + ((int64_t)z * KW * KW * KW + t) * a.Cd * a.Cg;
     const int col = gn0 + wn0 + li;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -488,7 +502,9 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
 }
 
 bool wgrad3s2_x3_applicable(const WgradArgs& a) {
-  return a.x3 && a.k == 3 && a.s == 2 && a.p == 1 && a.Wd % kSegW == 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
+  static const bool no_k4 = getenv("MRAGAN_NO_W4S2") != nullptr;   // A/B switch
+  const bool k4 = !no_k4 && a.k == 4 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16) && !a.in16 && !a.in16g;
+  return a.x3 && (a.k == 3 || k4) && a.s == 2 && a.p == 1 && a.Wd % kSegW == 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
          a.Wg == 2 * a.Wd && a.Cd % kTD == 0 && (a.Cg % 64 == 0 || a.Cg == 32) &&
          (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg * 4 < ((int64_t)1 << 31) &&     // byte offsets are 32-bit
          (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd * 4 < ((int64_t)1 << 31);
@@ -496,7 +512,8 @@ bool wgrad3s2_x3_applicable(const WgradArgs& a) {
 
 static int s2_tg(const WgradArgs& a) { return a.Cg % 64 == 0 ? 64 : 32; }
 
-static size_t s2_lds(int tg, bool tr) {
+static size_t s2_lds(int tg, bool tr, int kw) {
+  if (tr && kw == 4) return (size_t)2 * (tg == 64 ? tr_stage_k<64, 4>() : tr_stage_k<32, 4>());
   if (tr) return (size_t)2 * (tg == 64 ? tr_stage<64>() : tr_stage<32>());
   return (size_t)kTD * kDRow + (size_t)tg * kGRow;
 }
@@ -506,7 +523,7 @@ static size_t s2_lds(int tg, bool tr) {
 int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   const int tg = s2_tg(a);
   const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
-  const int tiles = (a.Cd / kTD) * (a.Cg / tg) * 9;
+  const int tiles = (a.Cd / kTD) * (a.Cg / tg) * a.k * a.k;
   static const int scale = [] {                               // A/B switch: MRAGAN_W3S2_BUDGET (percent)
     const char* e = getenv("MRAGAN_W3S2_BUDGET");
     return e ? atoi(e) : 100;
@@ -519,25 +536,26 @@ int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TG, int PM, int AL, int X16G>
+template <int TG, int PM, int AL, int X16G, int KW>
 static void launch_w3s2_as(const Wgrad3s2Args& a, int blocks, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL, X16G>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL, X16G>), dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW>), dim3(blocks), dim3(256), lds, st, a);
 }
 
 template <int TG, int PM, int AL>
-static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, int planes, hipStream_t st) {
+static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, int planes, int kw, hipStream_t st) {
   if constexpr (prec::has_lo<PM>()) {
-    launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);      // (planes rejected by the caller)
+    launch_w3s2_as<TG, PM, AL, 0, 3>(a, blocks, lds, st);   // (planes and k4 rejected by the caller)
   } else {
-    if (planes == 2) launch_w3s2_as<TG, PM, AL, 2>(a, blocks, lds, st);
-    else if (planes == 1) launch_w3s2_as<TG, PM, AL, 1>(a, blocks, lds, st);
-    else launch_w3s2_as<TG, PM, AL, 0>(a, blocks, lds, st);
+    if (kw == 4) launch_w3s2_as<TG, PM, AL, 0, 4>(a, blocks, lds, st);
+    else if (planes == 2) launch_w3s2_as<TG, PM, AL, 2, 3>(a, blocks, lds, st);
+    else if (planes == 1) launch_w3s2_as<TG, PM, AL, 1, 3>(a, blocks, lds, st);
+    else launch_w3s2_as<TG, PM, AL, 0, 3>(a, blocks, lds, st);
   }
 }
 
@@ -552,14 +570,19 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   a.seg_per_split = per;
   const int nsplit = (a.nseg + per - 1) / per;
   const int tg = s2_tg(g);
-  const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * 9 * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
-  const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16);
+  const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * g.k * g.k * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
+  const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16, g.k);
   // aligned stages: whole coarse rows of one plane per stage, every stage full
   const int nsw = g.Wd / kSegW;
   static const bool no_al = getenv("MRAGAN_W3S2_NO_AL") != nullptr;   // A/B switch
   const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
   static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
+  static_assert(2 * 4 * 16 * 64 * 4 <= 2 * tr_stage_k<32, 4>(), "the K-half reduction fits the tr stages (k4)");
+  if (g.k == 4 && (g.x3 == kPrecBf16x3 || g.in16 || g.in16g)) {
+    set_error("wgrad3s2_x3: k4 runs the one-plane modes on fp32 operands");
+    return -kBadArg;
+  }
   if ((g.in16g || g.in16) && g.x3 != kPrecBf16 && g.x3 != kPrecF16) {
     set_error("wgrad3s2_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
     return -kBadArg;
@@ -567,11 +590,11 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const int planes = g.in16 ? 2 : g.in16g ? 1 : 0;       // both operands / G only / none
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
-      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, planes, st);
-      else launch_w3s2<64, PM, 0>(a, blocks, lds, planes, st);
+      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, planes, g.k, st);
+      else launch_w3s2<64, PM, 0>(a, blocks, lds, planes, g.k, st);
     } else {
-      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, planes, st);
-      else launch_w3s2<32, PM, 0>(a, blocks, lds, planes, st);
+      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, planes, g.k, st);
+      else launch_w3s2<32, PM, 0>(a, blocks, lds, planes, g.k, st);
     }
     return nsplit;
   })

@@ -375,6 +375,42 @@ def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
     check_rounded(dwt, dwt_rnd, dwt_ref)
 
 
+@pytest.mark.parametrize("N,cin,cout,dims", [(1, 32, 64, (8, 10, 32)), (2, 64, 128, (6, 4, 64)), (1, 32, 128, (4, 2, 32)),
+                                             # aligned stages (whole coarse rows per 8-segment stage)
+                                             (1, 32, 64, (4, 16, 32)), (2, 64, 128, (4, 8, 64)),
+                                             (1, 32, 64, (6, 16, 64))])
+def test_wgrad_s2_four_tap(x3, N, cin, cout, dims):
+    """Weight gradients of the k4 s2 p1 convs (PatchGAN layers 2-3, networks3D.py:389-400; the
+    UNet's down convs) and of the k4 s2 p1 transposed up convs (networks3D.py:300-330) on the
+    4-kw-tap even/odd-phase kernel (conv_wgrad3s2_x3.hip, KW 4, one-plane modes: 34 staged fine
+    positions, fine row / voxel 2H / 2W read as zeros), vs fp64; bf16x3 keeps the generic kernel."""
+    ops = x3
+    g = torch.Generator().manual_seed(29 + N + cin + cout)
+    x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    y = F.conv3d(x, w, stride=2, padding=1)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    dw_ref = torch.nn.grad.conv3d_weight(x, w.shape, dy, stride=2, padding=1)
+    dw_rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), stride=2, padding=1)
+    dw = torch.full((cout, cin, 4, 4, 4), 3.0, device="cuda")
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 4, 2, 1, dw, accumulate=False)
+    check_rounded(dw, dw_rnd, dw_ref)
+    ops.conv3d_wgrad(ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda(), 4, 2, 1, dw, accumulate=True)
+    check_rounded(dw, 2 * dw_rnd, 2 * dw_ref)
+    # transposed: ConvTranspose3d(cout → cin, k4 s2 p1) on the coarse grid of y
+    xt = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    wt = (torch.randn(cout, cin, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+    yt = F.conv_transpose3d(xt, wt, stride=2, padding=1)
+    assert tuple(yt.shape[2:]) == tuple(dims)
+    dyt = torch.randn(yt.shape, generator=g, dtype=torch.float64)
+    (dwt_ref,) = torch.autograd.grad(yt, wt, dyt)
+    wr = R(wt).requires_grad_()
+    (dwt_rnd,) = torch.autograd.grad(F.conv_transpose3d(R(xt), wr, stride=2, padding=1), wr, R(dyt))
+    dwt = torch.zeros((cout, cin, 4, 4, 4), device="cuda")
+    ops.conv3d_wgrad(ndhwc(xt.float()).cuda(), ndhwc(dyt.float()).cuda(), 4, 2, 1, dwt, accumulate=False)
+    check_rounded(dwt, dwt_rnd, dwt_ref)
+
+
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
 def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
     ops = x3
