@@ -42,10 +42,14 @@ constexpr int kRow = 144;                  // LDS row: hi 64 B, lo 64 B, 16 B pa
 // MFMAs (the store stream bounded the one-block-per-CU kernel: 132 µs with stores, 60 without)
 template <int PM>
 constexpr int halo_row() { return prec::has_lo<PM>() ? 144 : 80; }
-constexpr int kOD = 4, kOH = 16, kOW = 16; // output brick
-constexpr int kHD = 4, kHH = 10, kHW = 10; // input halo (k ≤ 4, p = 1)
-constexpr int kHP = kHD * kHH * kHW;       // 400 positions
-constexpr int kSL = (kHP * 8 + 255) / 256; // float4 per thread per chunk (13)
+// output brick 4 × 4·NW × 16 for NW waves (each wave 4 × 4 × 16: one 32-voxel tile of each parity
+// class); NW = 4 on the large layers, 2 or 1 where 4-wave bricks would leave most CUs idle (the
+// UNet's 16³ → 32³ up convs: 32 bricks at N = 1, 34.9 µs)
+constexpr int kOD = 4, kOW = 16;
+constexpr int kHD = 4, kHW = 10;           // input halo (k ≤ 4, p = 1): 4 × (2·NW + 2) × 10
+template <int NW> constexpr int oh_t() { return 4 * NW; }
+template <int NW> constexpr int hh_t() { return 2 * NW + 2; }
+template <int NW> constexpr int hp_t() { return kHD * hh_t<NW>() * kHW; }   // 400 positions at NW 4
 
 // packed [T][ny][C] fp32 → [T][chunk][kk][hi|lo][ny][lh][8] bf16 (one thread per 8 channels)
 template <int PM>
@@ -109,14 +113,16 @@ struct BrickTArgs {
 // X16 (round 4, one-plane modes): the input is the producer's 16-bit operand plane — a halo
 // position's 32-channel chunk is four 16-B units copied to LDS as they are (G up2 on up1's IN plane,
 // G down1's data gradient on the plane of its dY)
-template <int K, int PM, int X16>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(prec::has_lo<PM>() ? 1 : 2, prec::has_lo<PM>() ? 1 : 2)))
+template <int K, int PM, int X16, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(prec::has_lo<PM>() ? 1 : 2, prec::has_lo<PM>() ? 1 : 2)))
 brickT_x3_kernel(BrickTArgs a) {
   static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
+  constexpr int NT = 64 * NW;                    // threads
+  constexpr int kOH = oh_t<NW>(), kHH = hh_t<NW>(), kHP = hp_t<NW>();
   constexpr int kHRow = halo_row<PM>();
   constexpr int ES = X16 ? 2 : 4;                // bytes per input element
   constexpr int UPP = X16 ? 4 : 8;               // 16-B units per halo position and chunk
-  constexpr int NSL = X16 ? (kHP * 4 + 255) / 256 : kSL;     // units per thread per chunk
+  constexpr int NSL = (kHP * UPP + NT - 1) / NT; // units per thread per chunk
   constexpr TSteps<K> ts{};
   constexpr int NS = 2 * TSteps<K>::N;          // (class tap, 16-channel half) steps per chunk
   // weight prefetch distance in steps (divides NS: a ring slot is compile-time in every chunk)
@@ -142,7 +148,7 @@ brickT_x3_kernel(BrickTArgs a) {
             i0w = floordiv2(o0w + a.p - (a.k - 1));
   // byte offsets into this instance's volume; out-of-volume positions get an offset past the
   // descriptor's range, so the buffer load returns zeros (the transposed conv's implicit padding)
-  for (int pos = tid; pos < kHP; pos += 256) {
+  for (int pos = tid; pos < kHP; pos += NT) {
     const int hw = pos % kHW, hh = (pos / kHW) % kHH, hd = pos / (kHW * kHH);
     const int id = i0d + hd, ih = i0h + hh, iw = i0w + hw;
     const bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
@@ -160,12 +166,12 @@ brickT_x3_kernel(BrickTArgs a) {
   __syncthreads();
 
   auto halo_off = [&](int s) __attribute__((always_inline)) {
-    const int e = s * 256 + tid, pos = e / UPP;
+    const int e = s * NT + tid, pos = e / UPP;
     const int o = pos < kHP ? hoff[pos] : (int)0x80000000;
     return o + 16 * (e % UPP);
   };
   auto halo_store = [&](char* buf, int s, const float4& v) __attribute__((always_inline)) {
-    const int e = s * 256 + tid, pos = e / UPP, q = e % UPP;
+    const int e = s * NT + tid, pos = e / UPP, q = e % UPP;
     if (pos < kHP) {
       if constexpr (X16) {
         *reinterpret_cast<float4*>(buf + pos * kHRow + 16 * q) = v;    // 8 channels' words, as they are
@@ -228,7 +234,8 @@ brickT_x3_kernel(BrickTArgs a) {
     };
     // the next chunk's halo in NB batches (one-plane modes: two, so the 256-register budget of
     // two blocks per CU holds half of it at a time)
-    constexpr int NB = prec::has_lo<PM>() ? 1 : 2, BS = (NSL + NB - 1) / NB;
+    // (one-wave blocks: four — their lanes carry 20 fp32 slices per chunk)
+    constexpr int NB = prec::has_lo<PM>() ? 1 : NW == 1 ? 4 : 2, BS = (NSL + NB - 1) / NB;
     float4 pv[BS];
     bf16x8 af[2][2];
     a_read(0, af[0]);
@@ -328,7 +335,7 @@ brickT_x3_kernel(BrickTArgs a) {
         pq[k] += __shfl_xor(pq[k], m);
       }
     }
-    double* red = reinterpret_cast<double*>(smem + 4 * VPW * kRow);   // [4 waves][32 channels][2]
+    double* red = reinterpret_cast<double*>(smem + NW * VPW * kRow);  // [NW waves][32 channels][2]
     if (lane < 8) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -340,7 +347,7 @@ brickT_x3_kernel(BrickTArgs a) {
     if (tid < 32) {
       double s2 = 0.0, q2 = 0.0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         s2 += red[(w * 32 + tid) * 2];
         q2 += red[(w * 32 + tid) * 2 + 1];
       }
@@ -360,24 +367,48 @@ bool brickT_x3_applicable(const IgemmArgs& g) {
 }
 
 // one static per kernel instantiation (the LDS opt-in is per function)
-template <int K, int PM, int X16>
-static void launch_brickT(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
-  // halos + offsets; the epilogue rows (4 waves × 32·(8/NP) voxels × kRow) and the statistics
+template <int K, int PM, int X16, int NW>
+static void launch_brickT_nw(const BrickTArgs& a, unsigned blocks, hipStream_t st) {
+  // halos + offsets; the epilogue rows (NW waves × 32·(8/NP) voxels × kRow) and the statistics
   // reduction after them reuse the same bytes
   constexpr int NP = prec::has_lo<PM>() ? 2 : 4;
-  const size_t halo = (size_t)2 * kHP * halo_row<PM>() + kHP * sizeof(int);
-  const size_t epi = (size_t)4 * 32 * (8 / NP) * kRow + 4 * 32 * 2 * sizeof(double);
+  const size_t halo = (size_t)2 * hp_t<NW>() * halo_row<PM>() + hp_t<NW>() * sizeof(int);
+  const size_t epi = (size_t)NW * 32 * (8 / NP) * kRow + NW * 32 * 2 * sizeof(double);
   const size_t lds = halo > epi ? halo : epi;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM, X16>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(brickT_x3_kernel<K, PM, X16, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((brickT_x3_kernel<K, PM, X16>), dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((brickT_x3_kernel<K, PM, X16, NW>), dim3(blocks), dim3(64 * NW), lds, st, a);
+}
+
+template <int K, int PM, int X16>
+static void launch_brickT(const BrickTArgs& a, int nw, unsigned blocks, hipStream_t st) {
+  if (nw == 4) {
+    launch_brickT_nw<K, PM, X16, 4>(a, blocks, st);
+  } else if constexpr (K == 3) {
+    // no one-wave form for k3 (fp32 input: its 20 slices per lane spill; and a plane launch must
+    // pick the same bricks as the fp32 one — bit-identical outputs and statistics partials)
+    launch_brickT_nw<K, PM, X16, 2>(a, blocks, st);
+  } else {
+    if (nw == 2) launch_brickT_nw<K, PM, X16, 2>(a, blocks, st);
+    else launch_brickT_nw<K, PM, X16, 1>(a, blocks, st);
+  }
 }
 
 size_t brickT_x3_ws_bytes(const IgemmArgs& g) { return (size_t)g.k * g.k * g.k * g.cx * g.ny * sizeof(float); }
+
+static int brickT_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
 
 template <int PM>
 static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
@@ -397,7 +428,19 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   a.wx = reinterpret_cast<const __bf16*>(g.ws);
   a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
   a.k = g.k; a.p = g.p; a.act = g.act;
-  a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, kOH); a.nbw = ceil_div(g.Wo, kOW);
+  // waves per block: 4, unless that leaves fewer bricks than CUs (then 2, or 1)
+  static const int force_nw = [] {                   // A/B switch: MRAGAN_BRICKT_NW=1|2|4
+    const char* e = getenv("MRAGAN_BRICKT_NW");
+    return e ? atoi(e) : 0;
+  }();
+  int nw = 4;
+  if (force_nw == 1 || force_nw == 2 || force_nw == 4) {
+    nw = force_nw;
+  } else {
+    while (nw > 1 && (int64_t)g.N * ceil_div(g.Do, kOD) * ceil_div(g.Ho, 4 * nw) * ceil_div(g.Wo, kOW) < brickT_cus()) nw >>= 1;
+  }
+  if (nw == 1 && g.k == 3) nw = 2;
+  a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, 4 * nw); a.nbw = ceil_div(g.Wo, kOW);
   const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
   if (blocks == 0) return kOk;
   static const bool no_stats = getenv("MRAGAN_NO_BRICKT_STATS") != nullptr;   // A/B switch
@@ -410,14 +453,14 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
       set_error("brickT_x3: a 16-bit operand plane needs the bf16 or fp16 mode");
       return kBadArg;
     }
-    if (g.k == 3) launch_brickT<3, PM, 0>(a, (unsigned)blocks, st);
-    else launch_brickT<4, PM, 0>(a, (unsigned)blocks, st);
+    if (g.k == 3) launch_brickT<3, PM, 0>(a, nw, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 0>(a, nw, (unsigned)blocks, st);
   } else if (g.x16) {
-    if (g.k == 3) launch_brickT<3, PM, 1>(a, (unsigned)blocks, st);
-    else launch_brickT<4, PM, 1>(a, (unsigned)blocks, st);
+    if (g.k == 3) launch_brickT<3, PM, 1>(a, nw, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 1>(a, nw, (unsigned)blocks, st);
   } else {
-    if (g.k == 3) launch_brickT<3, PM, 0>(a, (unsigned)blocks, st);
-    else launch_brickT<4, PM, 0>(a, (unsigned)blocks, st);
+    if (g.k == 3) launch_brickT<3, PM, 0>(a, nw, (unsigned)blocks, st);
+    else launch_brickT<4, PM, 0>(a, nw, (unsigned)blocks, st);
   }
   return check_launch(g.x16 ? "brickT_x3(op16)" : "brickT_x3");
 }

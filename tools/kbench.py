@@ -76,6 +76,7 @@ def main():
     x_ut = rnd(N, s4, s4, s4, c4)                        # UNet up conv ConvTranspose3d(128 -> 32, k4 s2) input
     dy_ut = rnd(N, s2, s2, s2, ngf)                      # and its output gradient
     gw_ut = torch.empty(64 * c4 * ngf, device=dev)
+    w_ut = rnd(64 * c4 * ngf) * 0.01                      # ConvTranspose3d(128 -> 32, k4 s2 p1) weights
     x_df = rnd(N, S, S, S, 1)                            # D first layer input (1 channel)
     w_dfw = rnd(64 * ngf) * 0.01
     b_df = rnd(ngf)
@@ -121,6 +122,7 @@ def main():
         "up1_fwd": lambda: ops.conv3d(x_up1, w_up1, 2 * ngf, 3, 2, 1, (s2, s2, s2), transposed=True),
         "down2_fwd": lambda: ops.conv3d(x_dn2, w_dn2, c4, 3, 2, 1, (s4, s4, s4)),
         "d2_fwd": lambda: ops.conv3d(x_d2, w_d2, 2 * ngf, 4, 2, 1, (S // 4, S // 4, S // 4)),
+        "unet_ct": lambda: ops.conv3d(x_ut, w_ut, ngf, 4, 2, 1, (s2, s2, s2), transposed=True),
         "d2_wgrad": lambda: ops.conv3d_wgrad(dy_d2, x_d2, 4, 2, 1, gw_d2, False),
         "unet_up_wgrad": lambda: ops.conv3d_wgrad(x_ut, dy_ut, 4, 2, 1, gw_ut, False),
         "dfirst_fwd": lambda: ops.conv3d(x_df, w_dfw, ngf, 4, 2, 1, (s2, s2, s2), bias=b_df, act="lrelu"),
