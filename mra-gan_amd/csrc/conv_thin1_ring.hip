@@ -647,7 +647,7 @@ template <int PM, int P16>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) thin1r_wgrad_kernel(Thin1RWArgs a) {
   static_assert(!P16 || !prec::has_lo<PM>(), "operand planes exist in the one-plane modes only");
   constexpr uint32_t PES = P16 ? 2u : 4u;     // bytes per P element
-  using PV = typename std::conditional<P16 != 0, uint2, float4>::type;
+  using PV = typename std::conditional<P16 != 0, uint4, float4>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);                     // [kRing][kPlaneE]
   bf16x8* ringL = ringH + kRing * kPlaneE;
@@ -669,16 +669,25 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // P staging unit of this thread: voxel pair vp = tid & 63 (voxels 2vp, 2vp + 1 of the brick:
   // row vp / 8, columns 2(vp % 8) …), channel quad cq = tid >> 6
   const int vp = tid & 63, cq = tid >> 6;
+  // P16: thread = (voxel vi = tid / 4 of the brick, 16-B chunk ck = tid % 4 = channels 8ck … 8ck+7):
+  // a wave's load is 16 voxels' whole 64-B rows (1 KB contiguous); the voxel-pair / channel-quad
+  // form touched 64 lines per load instruction for 8 B each
+  const int vi16 = tid >> 2, ck16 = tid & 3;
   auto p_load = [&](__amdgpu_buffer_rsrc_t pr, int vd, int vh0, int vw0, PV& v0, PV& v1)
                     __attribute__((always_inline)) {
+    if constexpr (P16) {
+      const int ph = vh0 + (vi16 >> 4), pw = vw0 + (vi16 & 15);
+      const bool ok = vd < a.Dp && ph < a.Hp && pw < a.Wp;
+      const uint32_t b = (uint32_t)((((int64_t)vd * a.Hp + ph) * a.Wp + pw) * kC + 8 * ck16) * PES;
+      v0 = __builtin_bit_cast(uint4, buf_load_16b(pr, (int)(ok ? b : kOobOffset), 0));
+      v1 = v0;
+      return;
+    }
     const int ph = vh0 + (vp >> 3), pw = vw0 + 2 * (vp & 7);
     const bool okr = vd < a.Dp && ph < a.Hp;
     const bool ok0 = okr && pw < a.Wp, ok1 = okr && pw + 1 < a.Wp;
     const uint32_t b0 = (uint32_t)((((int64_t)vd * a.Hp + ph) * a.Wp + pw) * kC + 4 * cq) * PES;
-    if constexpr (P16) {
-      v0 = buf_load_8b(pr, (int)(ok0 ? b0 : kOobOffset), 0);
-      v1 = buf_load_8b(pr, (int)(ok1 ? b0 + kC * PES : kOobOffset), 0);
-    } else {
+    if constexpr (!P16) {
       v0 = buf_load_f32x4(pr, ok0 ? b0 : kOobOffset);
       v1 = buf_load_f32x4(pr, ok1 ? b0 + kC * PES : kOobOffset);
     }
@@ -694,14 +703,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint32_t*>(pl + idx) = l;
     };
     if constexpr (P16) {
-      // channel q of voxels 2vp, 2vp + 1: the 16-bit words (v0, v1) of that channel, low half first
-      auto put16 = [&](int q, uint32_t w) __attribute__((always_inline)) {
-        *reinterpret_cast<uint32_t*>(ph + (4 * cq + q) * kPS + 2 * vp) = w;
-      };
-      put16(0, (v0.x & 0xffffu) | (v1.x << 16));
-      put16(1, (v0.x >> 16) | (v1.x & 0xffff0000u));
-      put16(2, (v0.y & 0xffffu) | (v1.y << 16));
-      put16(3, (v0.y >> 16) | (v1.y & 0xffff0000u));
+      // channel 8ck + j of voxel vi: the 16-bit word j of the chunk
+      uint16_t* col = reinterpret_cast<uint16_t*>(ph) + (8 * ck16) * kPS + vi16;
+      const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        col[(2 * j) * kPS] = (uint16_t)(w[j] & 0xffffu);
+        col[(2 * j + 1) * kPS] = (uint16_t)(w[j] >> 16);
+      }
     } else {
       put(0, v0.x, v1.x);
       put(1, v0.y, v1.y);
