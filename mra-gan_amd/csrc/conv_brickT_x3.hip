@@ -104,10 +104,14 @@ struct BrickTArgs {
   const float* x; int N, Di, Hi, Wi, C;    // C = contraction channels (multiple of 32)
   const __bf16* wx;                        // brickT_pack output
   const float* bias;
-  float* y; int Do, Ho, Wo, ny;            // ny = 32
+  float* y; int Do, Ho, Wo, ny;            // ny: a multiple of 32, one 32-channel group per block
+  int gn;                                  // channel groups (ny / 32)
   int k, p, act;
   int nbd, nbh, nbw;
   double* part;                            // optional: the next InstanceNorm's Σy / Σy² per brick
+  // optional with part (ABI 12 form): backward statistics instead — y is the gradient of the
+  // InstanceNorm(+sact) of sx (same grid, no fold): Σ g, Σ g·x̂ with g = y·act'(x̂)
+  const float* sx; const float* smean; const float* srstd; int sact;
 };
 
 // X16 (round 4, one-plane modes): the input is the producer's 16-bit operand plane — a halo
@@ -140,8 +144,9 @@ brickT_x3_kernel(BrickTArgs a) {
   int blk = blockIdx.x;
   const int bw_i = blk % a.nbw; blk /= a.nbw;
   const int bh_i = blk % a.nbh; blk /= a.nbh;
-  const int bd_i = blk % a.nbd;
-  const int nb = blk / a.nbd;
+  const int bd_i = blk % a.nbd; blk /= a.nbd;
+  const int nb = blk % a.N;
+  const int n0 = (blk / a.N) * 32;               // this block's 32 output channels
   const int o0d = bd_i * kOD, o0h = bh_i * kOH, o0w = bw_i * kOW;
   // halo origin: lowest input index any output of the brick reads (tap k−1)
   const int i0d = floordiv2(o0d + a.p - (a.k - 1)), i0h = floordiv2(o0h + a.p - (a.k - 1)),
@@ -202,7 +207,7 @@ brickT_x3_kernel(BrickTArgs a) {
   // i0 + [q + (o0 − 2·i0 + c + p − t)/2] → lane part q, the rest wave-uniform.
   const int qd = li >> 4, qh = (li >> 3) & 1, qw = li & 7;
   const int lane_row = ((qd * kHH) + qh + 2 * wave) * kHW + qw;     // halo position (tap part added)
-  const int wlane = li * 32 + lh * 16;                               // this lane's 16 B of a fragment
+  const int wlane = (n0 + li) * 32 + lh * 16;                        // this lane's 16 B of a fragment
 
   f32x16 acc[8];
 #pragma unroll
@@ -281,7 +286,12 @@ brickT_x3_kernel(BrickTArgs a) {
   char* ew = smem + wave * (VPW * kRow);
   const int q = lane & 7;                                   // read-back: channel quad 4q … 4q+3
   float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + 4 * q);
+  if (a.bias) bq = *reinterpret_cast<const float4*>(a.bias + n0 + 4 * q);
+  float4 smu = make_float4(0.f, 0.f, 0.f, 0.f), srs = smu;
+  if (a.sx) {
+    smu = *reinterpret_cast<const float4*>(a.smean + nb * a.ny + n0 + 4 * q);
+    srs = *reinterpret_cast<const float4*>(a.srstd + nb * a.ny + n0 + 4 * q);
+  }
   double ps[4] = {0.0, 0.0, 0.0, 0.0}, pq[4] = {0.0, 0.0, 0.0, 0.0};   // InstanceNorm partials (a.part)
 #pragma unroll
   for (int pass = 0; pass < NP; ++pass) {
@@ -311,11 +321,24 @@ brickT_x3_kernel(BrickTArgs a) {
       if (od < a.Do && oh < a.Ho && ow < a.Wo) {
         const float4 r = make_float4(act_fwd(t[0] + bq.x, a.act), act_fwd(t[1] + bq.y, a.act),
                                      act_fwd(t[2] + bq.z, a.act), act_fwd(t[3] + bq.w, a.act));
-        float4* dst = reinterpret_cast<float4*>(a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * a.ny + 4 * q);
+        float4* dst = reinterpret_cast<float4*>(a.y + ((((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow) * a.ny + n0 + 4 * q);
         // non-temporal: the 134 MB output stream otherwise evicts the weight fragments every
         // block re-reads from L2 (measured 165 → 132 µs at 4 × 64³ × 32)
         __builtin_nontemporal_store(f32x4{r.x, r.y, r.z, r.w}, reinterpret_cast<f32x4*>(dst));
-        if (a.part) {
+        if (a.part && a.sx) {
+          const int64_t vo = (((int64_t)nb * a.Do + od) * a.Ho + oh) * a.Wo + ow;
+          const float4 xs = *reinterpret_cast<const float4*>(a.sx + vo * a.ny + n0 + 4 * q);
+          const float xv[4] = {xs.x, xs.y, xs.z, xs.w}, rv[4] = {r.x, r.y, r.z, r.w};
+          const float mv[4] = {smu.x, smu.y, smu.z, smu.w}, sv[4] = {srs.x, srs.y, srs.z, srs.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xh = (xv[e] - mv[e]) * sv[e];
+            const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
+                             : (a.sact == kActLrelu && !(xh > 0.f)) ? rv[e] * kLreluSlope : rv[e];
+            ps[e] += gv;
+            pq[e] += (double)gv * xh;
+          }
+        } else if (a.part) {
           ps[0] += r.x; ps[1] += r.y; ps[2] += r.z; ps[3] += r.w;
           pq[0] += (double)r.x * r.x; pq[1] += (double)r.y * r.y; pq[2] += (double)r.z * r.z; pq[3] += (double)r.w * r.w;
         }
@@ -352,7 +375,7 @@ brickT_x3_kernel(BrickTArgs a) {
         q2 += red[(w * 32 + tid) * 2 + 1];
       }
       const int chunks = a.nbd * a.nbh * a.nbw, brick = (bd_i * a.nbh + bh_i) * a.nbw + bw_i;
-      double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + tid) * 2;
+      double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + n0 + tid) * 2;
       dst[0] = s2;
       dst[1] = q2;
     }
@@ -360,9 +383,15 @@ brickT_x3_kernel(BrickTArgs a) {
 }
 
 bool brickT_x3_applicable(const IgemmArgs& g) {
-  // ny = 32 only: at 64 output channels the 16 class accumulators take the whole AGPR file
-  // and the halo prefetch spills (those layers stay on conv_igemm_x3)
-  return g.x3 && g.trans && g.s == 2 && g.p == 1 && (g.k == 3 || g.k == 4) && g.cx % kBK == 0 && g.ny == 32 &&
+  // 32 output channels per block (at 64 per block the 16 class accumulators would take the whole
+  // AGPR file and the halo prefetch spill): wider layers (G up1, 128 → 64) run one block per
+  // 32-channel group, re-reading the halo per group (A/B switch MRAGAN_BRICKT_WIDE=0: ny = 32 only).
+  static const bool wide = [] {
+    const char* e = getenv("MRAGAN_BRICKT_WIDE");
+    return !(e && atoi(e) == 0);
+  }();
+  return g.x3 && g.trans && g.s == 2 && g.p == 1 && (g.k == 3 || g.k == 4) && g.cx % kBK == 0 &&
+         (g.ny == 32 || (wide && g.ny % 32 == 0 && g.ny > 0)) &&
          (int64_t)g.Di * g.Hi * g.Wi * g.cx * 4 < ((int64_t)1 << 31);
 }
 
@@ -437,15 +466,20 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   if (force_nw == 1 || force_nw == 2 || force_nw == 4) {
     nw = force_nw;
   } else {
-    while (nw > 1 && (int64_t)g.N * ceil_div(g.Do, kOD) * ceil_div(g.Ho, 4 * nw) * ceil_div(g.Wo, kOW) < brickT_cus()) nw >>= 1;
+    while (nw > 1 && (int64_t)g.N * (g.ny / 32) * ceil_div(g.Do, kOD) * ceil_div(g.Ho, 4 * nw) * ceil_div(g.Wo, kOW) < brickT_cus())
+      nw >>= 1;
   }
   if (nw == 1 && g.k == 3) nw = 2;
   a.nbd = ceil_div(g.Do, kOD); a.nbh = ceil_div(g.Ho, 4 * nw); a.nbw = ceil_div(g.Wo, kOW);
-  const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw;
+  a.gn = g.ny / 32;
+  const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw * a.gn;
   if (blocks == 0) return kOk;
   static const bool no_stats = getenv("MRAGAN_NO_BRICKT_STATS") != nullptr;   // A/B switch
-  if (g.in_part && !no_stats && !g.bs_x) {   // conv3d_in_stats: the following InstanceNorm's partials
+  if (g.in_part && !no_stats) {
+    // conv3d_in_stats: the following InstanceNorm's partials; conv3d_bwd_stats (a stride-2 data
+    // gradient, ABI 12): the backward statistics of the InstanceNorm in front (same grid)
     a.part = g.in_part;
+    if (g.bs_x) { a.sx = g.bs_x; a.smean = g.bs_mean; a.srstd = g.bs_rstd; a.sact = g.bs_act; }
     if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
   }
   if constexpr (prec::has_lo<PM>()) {

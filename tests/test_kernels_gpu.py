@@ -922,11 +922,11 @@ def test_head_dgrad_backward_statistics(x3, N, S, act, nc):
     (2, 128, 64, 16, 3, True, "relu", True),     # G down2's data gradient (convT form) → down1's IN
     (2, 32, 64, 16, 3, True, "lrelu", True),     # convT form, 32 → 64 channels
     (2, 32, 64, 32, 3, False, "relu", True),     # G up2's data gradient (forward form) → up1's IN
-    (1, 64, 32, 8, 3, True, "lrelu", False),     # 32 output channels: brickT, no epilogue → stats pass
+    (1, 64, 32, 8, 3, True, "lrelu", True),      # 32 output channels: brickT's epilogue (round 5)
     (2, 64, 32, 8, 4, True, "lrelu", None),      # PatchGAN layer 2's data gradient (k4 s2 p1, convT form, 8³ → 16³)
     (2, 128, 64, 4, 4, True, "lrelu", None),     # PatchGAN layer 3's data gradient (4³ → 8³)
     (2, 32, 64, 16, 4, False, "lrelu", None),    # k4 s2 p1 in the forward form
-    (1, 128, 64, 5, 3, True, "relu", False),     # ragged: 5³ → 9³ (output padding 0): uneven parity classes
+    (1, 128, 64, 5, 3, True, "relu", True),      # ragged: 5³ → 9³ (output padding 0): brickT's partial bricks
 ])
 def test_stride2_dgrad_backward_statistics(x3, N, cin, cout, S, k, tr, act, expect):
     """ABI 12: the stride-2 data gradient's implicit-GEMM epilogue leaves the backward statistics of
@@ -940,7 +940,8 @@ def test_stride2_dgrad_backward_statistics(x3, N, cin, cout, S, k, tr, act, expe
         torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.05
     wp = pack(ops, w, tr, False)
     # the data gradient of Conv3d(k, s2, p1) from an even size (k4: output padding 0); the ragged
-    # case (S = 5, k3, output padding 0: 9³ outputs, parity classes of 5 and 4) must not produce partials
+    # case (S = 5, k3, output padding 0: 9³ outputs, parity classes of 5 and 4): on brickT since
+    # round 5, whose partial bricks count only the voxels inside the output
     op = 0 if (k == 4 or S % 2) else 1
     o = ops.convT_out_size(S, k, 2, 1, op) if tr else ops.conv_out_size(S, k, 2, 1)
     osp = (o, o, o)
