@@ -607,7 +607,15 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   MRAGAN_CHECK_ARG(best_s >= 0, "conv_brick_ks: %d output channels are not a multiple of 32", ny);
   // more than one round of CU slots (the 18³ data gradient at N = 4: 864 blocks): the r03 brick's
   // 128×128 eight-wave tiles are faster there (30.0 vs 36.2 µs, r04c) — the caller falls back
-  if (!force && best[0] > 2.0) return kUnsupported;
+  // Large grids (≥ 3 rounds: the 128³ / 96³ configurations' 34³ / 26³ data gradients) with the
+  // backward-statistics epilogue run here all the same: the K-split brick's epilogue beats the
+  // 8-wave brick's there (125.6 vs 135.7 µs at 2 × 32³ → 34³, r05z); A/B switch MRAGAN_KS_BIG=0
+  static const bool ks_big = [] {
+    const char* e = getenv("MRAGAN_KS_BIG");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool big_bs = ks_big && a.sx && best[0] >= 6.0;
+  if (!force && best[0] > 2.0 && !big_bs) return kUnsupported;
   const int* b = shapes[best_s];
   const Var& V = vars[best_v];
   a.BD = b[0]; a.BH = b[1]; a.BW = b[2];

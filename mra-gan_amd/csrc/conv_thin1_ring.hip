@@ -232,23 +232,33 @@ constexpr int kFH = 16;
 constexpr int kFRH = kFH + kK - 1;      // 22 X8 rows per plane
 constexpr int kFPlaneE = kFRH * kBW;    // 352 entries per plane (hi or lo)
 constexpr int kFLds = 2 * kRing * kFPlaneE * 16 + kGroups * 2 * kC * 16;   // ring + weights: 141 312 B
-constexpr int kFRed = 4 * kC * 2 * 8;   // + [4 waves][32 channels][Σ, Σ²] doubles (a.part)
+constexpr int kFRed = 4 * kC * 2 * 8 + 2 * kC * 4;   // + [4 waves][32 ch][Σ, Σ²] doubles (a.part), μ / rstd of sx
+// TW = 2 (one-plane modes, one input channel): no lo ring, hi weights only — 69 KB, so two blocks
+// share a CU (two waves per SIMD: one block's loads and barrier waits under the other's MFMAs)
+constexpr int kFLdsC = kRing * kFPlaneE * 16 + kGroups * kC * 16;              // 70 656 B
 
 // C2: a two-channel input (one-plane modes): channel 1's X8 planes and weights sit where the lo
 // splits of bf16x3 do, and each K-step issues one MFMA per channel
 // EPI (compile-time epilogue, round 5): 0 = bias (+ activation); 1 = the next InstanceNorm's Σy, Σy²
 // (a.part); 2 = backward statistics (a.part with a.sx).  With the three in one body the compiler
 // kept every path's registers live (accumulator-file spills, 11 VALU per MFMA: PMC r05g).
-template <int PM, int C2, int EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) thin1r_fwd_kernel(Thin1RArgs a) {
+template <int PM, int C2, int EPI, int TW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW))) thin1r_fwd_kernel(Thin1RArgs a) {
+  static_assert(TW == 1 || (!prec::has_lo<PM>() && !C2), "two waves per SIMD: one-plane, one channel");
+  constexpr bool CMP = TW == 2;                          // compact LDS: hi ring and hi weights only
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* ringH = reinterpret_cast<bf16x8*>(smem);       // [kRing][kFPlaneE]
-  bf16x8* ringL = ringH + kRing * kFPlaneE;
-  bf16x8* wsm = ringL + kRing * kFPlaneE;                // [kGroups][hi|lo][kC]: the packed table
+  bf16x8* ringL = CMP ? ringH : ringH + kRing * kFPlaneE;
+  bf16x8* wsm = ringH + (CMP ? 1 : 2) * kRing * kFPlaneE;  // [kGroups][hi|lo][kC] (CMP: [kGroups][kC])
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
+  auto wsel = [&](int g, int hl, int c) __attribute__((always_inline)) { return CMP ? g * kC + c : (g * 2 + hl) * kC + c; };
 
-  for (int e = tid; e < kGroups * 2 * kC; e += 256) wsm[e] = reinterpret_cast<const bf16x8*>(a.wx)[e];
+  if constexpr (CMP) {
+    for (int e = tid; e < kGroups * kC; e += 256) wsm[e] = reinterpret_cast<const bf16x8*>(a.wx)[(e / kC) * 2 * kC + e % kC];
+  } else {
+    for (int e = tid; e < kGroups * 2 * kC; e += 256) wsm[e] = reinterpret_cast<const bf16x8*>(a.wx)[e];
+  }
   // A row li (weights) holds channel perm(li) = 16·((li>>2)&1) + 4·(li>>3) + (li&3), so
   // accumulator 4q + e of lane (li, lh) is channel 16·lh + 4q + e: 64 contiguous bytes per lane
   const int co = ((li >> 2) & 1) * 16 + (li >> 3) * 4 + (li & 3);
@@ -257,12 +267,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   // LDS.  The r05 form re-read the weights from LDS every K-step and issued each MFMA right behind
   // its two reads (s_waitcnt lgkmcnt(0) per MFMA: one LDS latency per 32-cycle MFMA, ≈ 8 k cycles
   // per depth step against 1.6 k of MFMA, stamps r05g).
-  constexpr bool WREG = !prec::has_lo<PM>() && !C2 && EPI != 2;   // EPI 2: its registers go to the statistics
+  // (EPI 2: its registers go to the statistics; TW 2: 256 registers per wave in all)
+  constexpr bool WREG = !prec::has_lo<PM>() && !C2 && EPI != 2 && TW == 1;
   bf16x8 wreg[WREG ? kKS : 1];
   if constexpr (WREG) {
     __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < kKS; ++ks) wreg[ks] = wsm[((2 * ks + lh) * 2 + 0) * kC + co];
+    for (int ks = 0; ks < kKS; ++ks) wreg[ks] = wsm[wsel(2 * ks + lh, 0, co)];
   }
   float bias[16];
 #pragma unroll
@@ -291,14 +302,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     const int er0 = tid / kBW, er1 = (tid + 256) / kBW, ep = tid % kBW;
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 0] = __builtin_amdgcn_s_memtime();
 
-    // prologue: planes 0..6 → slots 0..6
+    // the item's instance's μ / rstd of the backward statistics' x̂ (EPI 2), read from LDS in the
+    // epilogue (32 registers fewer: the two-waves-per-SIMD form fits 256)
+    float* sstat = reinterpret_cast<float*>(smem + (CMP ? kFLdsC : kFLds) + 4 * kC * 2 * 8);
+    if constexpr (EPI == 2) {
+      if (tid < 2 * kC) sstat[tid] = tid < kC ? a.smean[nb * kC + tid] : a.srstd[nb * kC + tid - kC];
+    }
+    // prologue: planes 0..6 → slots 0..6, every load in flight before the first store (one load
+    // latency per item instead of seven)
+    // (in batches of PB planes: all 7 at once for one wave per SIMD and one channel)
+    constexpr int PB = (TW == 2 || C2) ? 4 : kK;
 #pragma unroll
-    for (int rp = 0; rp < kK; ++rp) {
-      float v0[8], v1[8], u0[8], u1[8];
-      load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er0, w0 + ep, v0, u0);
-      if (e1) load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + rp, h0 + er1, w0 + ep, v1, u1);
-      store_x8c<PM, C2>(ringH, ringL, kFPlaneE, rp, tid, v0, u0);
-      if (e1) store_x8c<PM, C2>(ringH, ringL, kFPlaneE, rp, tid + 256, v1, u1);
+    for (int b0 = 0; b0 < kK; b0 += PB) {
+      float v0[PB][8], v1[PB][8], u0[PB][8], u1[PB][8];
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        if (b0 + j < kK) {
+          load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + b0 + j, h0 + er0, w0 + ep, v0[j], u0[j]);
+          if (e1) load_rows<C2>(xr, a.Di, a.Hi, a.Wi, d0 + b0 + j, h0 + er1, w0 + ep, v1[j], u1[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        if (b0 + j < kK) {
+          store_x8c<PM, C2>(ringH, ringL, kFPlaneE, b0 + j, tid, v0[j], u0[j]);
+          if (e1) store_x8c<PM, C2>(ringH, ringL, kFPlaneE, b0 + j, tid + 256, v1[j], u1[j]);
+        }
+      }
     }
     __syncthreads();
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
@@ -313,19 +343,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr int NS = EPI ? 16 : 1;
     using AccT = typename std::conditional<EPI == 2, float, double>::type;
     AccT ps[NS], pq[NS];
-    float smu[NS], srs[NS];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      ps[q] = pq[q] = AccT(0);
-      smu[q] = srs[q] = 0.f;
-    }
-    if constexpr (EPI == 2) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        smu[q] = a.smean[nb * kC + 16 * lh + q];
-        srs[q] = a.srstd[nb * kC + 16 * lh + q];
-      }
-    }
+    for (int q = 0; q < NS; ++q) ps[q] = pq[q] = AccT(0);
     for (int s = 0; s < nsteps; ++s) {
       const bool more = s + kK < nplanes;
       float n0[8], n1[8], m0[8], m1[8];
@@ -369,8 +388,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int g0 = 2 * ks, g1 = 2 * ks + 1 < kK * kK ? 2 * ks + 1 : kK * kK - 1;
         const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
         if constexpr (!WREG) {
-          ah = wsm[(g * 2 + 0) * kC + co];
-          al = kTwo ? wsm[(g * 2 + 1) * kC + co] : ah;
+          ah = wsm[wsel(g, 0, co)];
+          al = kTwo ? wsm[wsel(g, 1, co)] : ah;
         }
         const int base = ((s + kd) & (kRing - 1)) * kFPlaneE + x8_entry<0>(bh0 + kh, bw, 0);
 #pragma unroll
@@ -453,11 +472,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float4 xv = own[i][q];
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            const float4 mu4 = *reinterpret_cast<const float4*>(sstat + 16 * lh + 4 * q);
+            const float4 rs4 = *reinterpret_cast<const float4*>(sstat + kC + 16 * lh + 4 * q);
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, smu[4] = {mu4.x, mu4.y, mu4.z, mu4.w},
+                        srs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float vs = acc[i][4 * q + e];
-              const float xh = (xs[e] - smu[4 * q + e]) * srs[4 * q + e];
+              const float xh = (xs[e] - smu[e]) * srs[e];
               const float g0 = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
                                : (a.sact == kActLrelu && !(xh > 0.f)) ? vs * kLreluSlope : vs;
               const float gv = in[i] ? g0 : 0.f;
@@ -504,7 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     if constexpr (EPI != 0) {
       // item = nb · (items per instance) + (chunk · nbh + chh) · nbw + cw: the partials' chunk order
-      double* red = reinterpret_cast<double*>(smem + kFLds);
+      double* red = reinterpret_cast<double*>(smem + (CMP ? kFLdsC : kFLds));
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         double s2 = (double)ps[q], q2 = (double)pq[q];
@@ -550,22 +572,32 @@ bool thin1_x3_applicable(int cx, int ny, int k, int s, int mode) {
 
 size_t thin1_x3_ws_bytes(int ny) { return (size_t)kGroups * 2 * ny * 8 * sizeof(__bf16); }
 
-template <int PM, int C2, int EPI>
-static void launch_thin1_fwd_e(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
+template <int PM, int C2, int EPI, int TW>
+static void launch_thin1_fwd_e(const Thin1RArgs& a, int grid, hipStream_t st) {
+  const size_t lds = (TW == 2 ? kFLdsC : kFLds) + kFRed;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM, C2, EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(thin1r_fwd_kernel<PM, C2, EPI, TW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((thin1r_fwd_kernel<PM, C2, EPI>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((thin1r_fwd_kernel<PM, C2, EPI, TW>), dim3(grid), dim3(256), lds, st, a);
 }
 
-template <int PM, int C2>
-static void launch_thin1_fwd(const Thin1RArgs& a, int grid, size_t lds, hipStream_t st) {
-  if (!a.part) launch_thin1_fwd_e<PM, C2, 0>(a, grid, lds, st);
-  else if (!a.sx) launch_thin1_fwd_e<PM, C2, 1>(a, grid, lds, st);
-  else launch_thin1_fwd_e<PM, C2, 2>(a, grid, lds, st);
+template <int PM, int C2, int TW>
+static void launch_thin1_fwd(const Thin1RArgs& a, int grid, hipStream_t st) {
+  if (!a.part) launch_thin1_fwd_e<PM, C2, 0, TW>(a, grid, st);
+  else if (!a.sx) launch_thin1_fwd_e<PM, C2, 1, TW>(a, grid, st);
+  else launch_thin1_fwd_e<PM, C2, 2, 1>(a, grid, st);   // (the caller picks TW 1: its registers spill at 256)
+}
+
+// two blocks per CU in the one-plane one-channel case (A/B switch: MRAGAN_THIN1_TW=1)
+static int thin1_tw() {
+  static const int tw = [] {
+    const char* e = getenv("MRAGAN_THIN1_TW");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return tw;
 }
 
 template <int PM>
@@ -597,24 +629,28 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
   if (columns == 0 || t.Do == 0) return kOk;
   MRAGAN_CHECK_ARG((int64_t)t.Di * t.Hi * t.Wi * t.cx * 4 < (int64_t)kOobOffset, "thin1_x3: input volume too large");
   int grid = 1;
-  pick_chunk(columns, t.Do, cu_count(), a.L, a.nch, grid);
-  a.items = (int)(columns * a.nch);
   static const bool no_stats = getenv("MRAGAN_NO_THIN1_STATS") != nullptr;   // A/B switch
-  if (t.in_part && !no_stats && t.act == kActNone && !t.bias &&
-      (t.bs_x ? (t.trans && t.bs_fold >= 0 && t.Do > 2 * t.bs_fold && t.Ho > 2 * t.bs_fold && t.Wo > 2 * t.bs_fold)
-              : !t.trans)) {
+  const bool stats = t.in_part && !no_stats && t.act == kActNone && !t.bias &&
+                     (t.bs_x ? (t.trans && t.bs_fold >= 0 && t.Do > 2 * t.bs_fold && t.Ho > 2 * t.bs_fold && t.Wo > 2 * t.bs_fold)
+                             : !t.trans);
+  // two blocks per CU for the plain and forward-statistics forms (the backward-statistics one
+  // needs more than 256 registers)
+  const int tw = (!prec::has_lo<PM>() && !c2 && !(stats && t.bs_x)) ? thin1_tw() : 1;
+  pick_chunk(columns, t.Do, tw * cu_count(), a.L, a.nch, grid);
+  a.items = (int)(columns * a.nch);
+  if (stats) {
     // conv3d_in_stats: the stem InstanceNorm's partials; conv3d_dgrad_in_stats (the G head's data
     // gradient): the backward statistics of the InstanceNorm in front of the head
     a.part = t.in_part;
     a.sx = t.bs_x; a.smean = t.bs_mean; a.srstd = t.bs_rstd; a.sact = t.bs_act; a.sfold = t.bs_fold;
     if (t.in_chunks) *t.in_chunks = a.nch * a.nbh * a.nbw;
   }
-  const size_t lds = kFLds + kFRed;
   if constexpr (!prec::has_lo<PM>()) {
-    if (c2) launch_thin1_fwd<PM, 1>(a, grid, lds, st);
-    else launch_thin1_fwd<PM, 0>(a, grid, lds, st);
+    if (c2) launch_thin1_fwd<PM, 1, 1>(a, grid, st);
+    else if (tw == 2) launch_thin1_fwd<PM, 0, 2>(a, grid, st);
+    else launch_thin1_fwd<PM, 0, 1>(a, grid, st);
   } else {
-    launch_thin1_fwd<PM, 0>(a, grid, lds, st);
+    launch_thin1_fwd<PM, 0, 1>(a, grid, st);
   }
   return check_launch("thin1_x3");
 }

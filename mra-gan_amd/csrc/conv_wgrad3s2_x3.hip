@@ -69,10 +69,16 @@ constexpr int tr_stage() { return kTrRowsD * kTD * 2 + kTrRowsG * TG * 2; }
 // convs and, as G = dY, its k4 s2 p1 transposed up convs, networks3D.py:300-330), one-plane modes.
 // Along w the four taps read the fine positions 2w − 1 … 2w + 2 = O[w − 1], E[w], O[w], E[w + 1]:
 // the segment stages 34 fine positions (2w0 − 1 … 2w0 + 32), E in slots 0 … 16, O from slot 17.
-template <int KW> constexpr int gpos() { return 2 * kSegW + KW - 2; }      // 33 | 34
-template <int KW> constexpr int obase() { return KW == 3 ? 16 : 17; }      // first O-phase slot
-template <int KW> __device__ __forceinline__ int gslot_k(int q) { return (q & 1) ? (q - 1) >> 1 : obase<KW>() + (q >> 1); }
-template <int TG, int KW> constexpr int tr_stage_k() { return kTrRowsD * kTD * 2 + gpos<KW>() * kR * TG * 2; }
+// SW = 8: 8-voxel coarse segments for the 8-wide levels (the UNet's 8³, the PatchGAN's layer-3
+// gradient), one-plane modes on fp32 operands; a stage is then 64 K rows (4 K-steps)
+template <int KW, int SW = kSegW> constexpr int gpos() { return 2 * SW + KW - 2; }      // 33 | 34 (SW 16)
+template <int KW, int SW = kSegW> constexpr int obase() { return SW + (KW == 4 ? 1 : 0); }   // first O-phase slot
+template <int KW, int SW = kSegW> __device__ __forceinline__ int gslot_k(int q) {
+  return (q & 1) ? (q - 1) >> 1 : obase<KW, SW>() + (q >> 1);
+}
+template <int TG, int KW, int SW = kSegW> constexpr int tr_stage_k() {
+  return SW * kR * kTD * 2 + gpos<KW, SW>() * kR * TG * 2;
+}
 
 // one channel of the 8 segments → 16 B hi at p, 16 B lo at p + half
 template <int PM>
@@ -100,12 +106,15 @@ struct Wgrad3s2Args {
 // (fine position, 8-channel octet), one 16-B load each, stored as they are (one-plane modes);
 // X16G = 2: D too (ABI 16: G down2's weight gradient, whose dY exists only as its plane) — D units
 // (coarse w, octet, segment half): 4 segments × 16 B per thread
-template <int TG, int PM, int AL, int X16G, int KW>
+template <int TG, int PM, int AL, int X16G, int KW, int SW>
 __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool kTr = !prec::has_lo<PM>();
   static_assert(KW == 3 || (kTr && !X16G), "k4: the one-plane modes on fp32 operands");
-  constexpr int kGPos = gpos<KW>();       // shadows the file constant (33) in this kernel
+  static_assert(SW == kSegW || (kTr && !X16G), "8-voxel segments: the one-plane modes on fp32 operands");
+  constexpr int kGPos = gpos<KW, SW>();   // shadows the file constant (33) in this kernel
+  constexpr int kSegW = SW;               // (and the segment width)
+  constexpr int kTrRowsD = SW * kR;       // D rows per stage
   static_assert(!X16G || kTr, "16-bit operand planes exist in the one-plane modes only");
   constexpr bool kDp = X16G == 2;         // D as a 16-bit plane too
   constexpr int ESG = X16G ? 2 : 4;       // bytes per G element
@@ -144,6 +153,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   constexpr int GP = 256 / GQ;                     // positions per pass: 16 (TG 64) or 32 (TG 32)
   constexpr int GPASS = kGPos / GP;                // full passes: 2 or 1
   const int cq = tid & 15, uw = tid >> 4;
+  const bool dact = uw < SW;                       // SW 8: threads 128 … 255 stage no D unit
   const int gcq = tid % GQ, gq = tid / GQ;
   const int gqx = GPASS * GP + gq;                 // the remainder pass (q = 32 …)
   const bool gx = gqx < kGPos;
@@ -166,7 +176,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   // (no select on the loaded values, no 64-bit address arithmetic)
   const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.d, __builtin_amdgcn_readfirstlane(a.N * a.D * a.H * a.W * a.Cd * ESD));
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.g, __builtin_amdgcn_readfirstlane(a.N * Dg * Hg * Wg * a.Cg * ESG));
-  const int dlane = (uw * a.Cd + dn0 + 4 * cq) * 4;
+  const int dlane = dact ? (uw * a.Cd + dn0 + 4 * cq) * 4 : (int)kOobOffset;
   const int dlane8 = (uwd * a.Cd + dn0 + 8 * od8) * 2;             // kDp: octet od8 of coarse voxel uwd
   const int dseg = kSegW * a.Cd * ESD;
   int sw = seg_lo % nsw, sh = (seg_lo / nsw) % a.H, sd = (seg_lo / nsw / a.H) % a.D, sn = seg_lo / nsw / a.H / a.D;
@@ -209,7 +219,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
       // The soffset carries the row only; the run's w start goes into the (non-negative) voffset:
       // the range check must see the lane's real offset
       const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
-      const int wrun = 32 * wr * a.Cg * ESG;
+      const int wrun = 2 * SW * wr * a.Cg * ESG;
       const bool w_edge = wr == 0;                                   // fine voxel −1 is outside
       const bool w_redge = KW == 4 && wr == nsw - 1;                 // KW 4: fine voxel 2W too
       if constexpr (X16G) {
@@ -237,7 +247,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
           const int rr = r / nsw, wr = r - rr * nsw;
           const bool rok = dok && (gh0 >= 0 || rr > 0);
           const int gso = __builtin_amdgcn_readfirstlane(gbase + (gh0 < 0 ? 2 * rr - 1 : 2 * rr) * gplane_b);
-          rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, rok ? glane_al8x + 32 * wr * a.Cg * ESG : (int)kOobOffset, gso));
+          rg8x[r] = __builtin_bit_cast(uint4, buf_load_16b(gr, rok ? glane_al8x + 2 * SW * wr * a.Cg * ESG : (int)kOobOffset, gso));
         }
       }
     }
@@ -346,24 +356,24 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
           *reinterpret_cast<uint4*>(Ds + row * RBD + 16 * (od8 ^ tr_swz<RBD>(row))) = rd8[j];
         }
       } else {
-        put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
+        if (dact) put16(Ds, std::integral_constant<int, RBD>{}, uw, cq, rd);
       }
       if constexpr (X16G) {
-        if (g8) put8(Gs, gslot_k<KW>(q8), go, rg8);
+        if (g8) put8(Gs, gslot_k<KW, SW>(q8), go, rg8);
         if constexpr (kG8X)
-          if (g8x) put8(Gs, gslot_k<KW>(q8x), go, rg8x);
+          if (g8x) put8(Gs, gslot_k<KW, SW>(q8x), go, rg8x);
         return;
       }
 #pragma unroll
       for (int pass = 0; pass < GPASS; ++pass)
-        put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW>(pass * GP + gq), gcq, rg[pass]);
-      if (gx) put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW>(gqx), gcq, rgx);
+        put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW, SW>(pass * GP + gq), gcq, rg[pass]);
+      if (gx) put16(Gs, std::integral_constant<int, RBG>{}, gslot_k<KW, SW>(gqx), gcq, rgx);
       return;
     }
     put(Ds, kDRow, kDHalf, uw, cq, rd);
 #pragma unroll
-    for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot_k<KW>(pass * GP + gq), gcq, rg[pass]);
-    if (gx) put(Gs, kGRow, kGHalf, gslot_k<KW>(gqx), gcq, rgx);
+    for (int pass = 0; pass < GPASS; ++pass) put(Gs, kGRow, kGHalf, gslot_k<KW, SW>(pass * GP + gq), gcq, rg[pass]);
+    if (gx) put(Gs, kGRow, kGHalf, gslot_k<KW, SW>(gqx), gcq, rgx);
   };
   // tr read offsets: lane 4q+p of its 16-lane group g (lane bit 4) reads row 8h + q (+ the read's
   // K offset) and channels (sub-tile base + 16g + 4p … +3)
@@ -374,7 +384,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   const int kp = TG == 32 ? __builtin_amdgcn_readfirstlane(kpar) : 0;
   const int trA_k = trA + 16 * kp * RBD, trB_k = trB + 16 * kp * RBG;
   auto use_buf = [&](int b) __attribute__((always_inline)) {       // tr: select stage buffer b
-    Ds = smem + b * tr_stage_k<TG, KW>();
+    Ds = smem + b * tr_stage_k<TG, KW, SW>();
     Gs = Ds + kTrRowsD * RBD;
   };
 
@@ -433,7 +443,7 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
         const char* ar = Ds + trA_k + (16 * ks) * RBD;
         const tr_v4s a0 = tr_read(ar), a1 = tr_read(ar + 4 * RBD);
         fa[0] = fa[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
-        constexpr int kslot[4] = {obase<KW>(), 0, obase<KW>() + 1, 1};
+        constexpr int kslot[4] = {obase<KW, SW>(), 0, obase<KW, SW>() + 1, 1};
 #pragma unroll
         for (int kw = 0; kw < KW; ++kw) {
           const char* br = Gs + trB_k + (16 * ks + kR * kslot[kw]) * RBG;
@@ -501,10 +511,19 @@ __global__ void __launch_bounds__(256) wgrad3s2_x3_kernel(Wgrad3s2Args a) {
   }
 }
 
+// coarse voxels per segment: 16, or 8 for the 8-wide levels (one-plane modes, fp32 operands;
+// A/B switch MRAGAN_NO_W3S2_SW8)
+static int s2_segw(const WgradArgs& a) {
+  static const bool no_sw8 = getenv("MRAGAN_NO_W3S2_SW8") != nullptr;
+  if (a.Wd % kSegW == 0) return kSegW;
+  if (!no_sw8 && a.Wd % 8 == 0 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16) && !a.in16 && !a.in16g) return 8;
+  return 0;
+}
+
 bool wgrad3s2_x3_applicable(const WgradArgs& a) {
   static const bool no_k4 = getenv("MRAGAN_NO_W4S2") != nullptr;   // A/B switch
   const bool k4 = !no_k4 && a.k == 4 && (a.x3 == kPrecBf16 || a.x3 == kPrecF16) && !a.in16 && !a.in16g;
-  return a.x3 && (a.k == 3 || k4) && a.s == 2 && a.p == 1 && a.Wd % kSegW == 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
+  return a.x3 && (a.k == 3 || k4) && a.s == 2 && a.p == 1 && s2_segw(a) != 0 && a.Dg == 2 * a.Dd && a.Hg == 2 * a.Hd &&
          a.Wg == 2 * a.Wd && a.Cd % kTD == 0 && (a.Cg % 64 == 0 || a.Cg == 32) &&
          (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg * 4 < ((int64_t)1 << 31) &&     // byte offsets are 32-bit
          (int64_t)a.N * a.Dd * a.Hd * a.Wd * a.Cd * 4 < ((int64_t)1 << 31);
@@ -512,7 +531,11 @@ bool wgrad3s2_x3_applicable(const WgradArgs& a) {
 
 static int s2_tg(const WgradArgs& a) { return a.Cg % 64 == 0 ? 64 : 32; }
 
-static size_t s2_lds(int tg, bool tr, int kw) {
+static size_t s2_lds(int tg, bool tr, int kw, int sw) {
+  if (tr && sw == 8) {
+    if (kw == 4) return (size_t)2 * (tg == 64 ? tr_stage_k<64, 4, 8>() : tr_stage_k<32, 4, 8>());
+    return (size_t)2 * (tg == 64 ? tr_stage_k<64, 3, 8>() : tr_stage_k<32, 3, 8>());
+  }
   if (tr && kw == 4) return (size_t)2 * (tg == 64 ? tr_stage_k<64, 4>() : tr_stage_k<32, 4>());
   if (tr) return (size_t)2 * (tg == 64 ? tr_stage<64>() : tr_stage<32>());
   return (size_t)kTD * kDRow + (size_t)tg * kGRow;
@@ -522,7 +545,7 @@ static size_t s2_lds(int tg, bool tr, int kw) {
 // never more than the generic plan's (its workspace query sizes the slabs)
 int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   const int tg = s2_tg(a);
-  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / kSegW);
+  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / s2_segw(a));
   const int tiles = (a.Cd / kTD) * (a.Cg / tg) * a.k * a.k;
   static const int scale = [] {                               // A/B switch: MRAGAN_W3S2_BUDGET (percent)
     const char* e = getenv("MRAGAN_W3S2_BUDGET");
@@ -536,23 +559,26 @@ int wgrad3s2_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TG, int PM, int AL, int X16G, int KW>
+template <int TG, int PM, int AL, int X16G, int KW, int SW = kSegW>
 static void launch_w3s2_as(const Wgrad3s2Args& a, int blocks, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW, SW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW>), dim3(blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((wgrad3s2_x3_kernel<TG, PM, AL, X16G, KW, SW>), dim3(blocks), dim3(256), lds, st, a);
 }
 
 template <int TG, int PM, int AL>
-static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, int planes, int kw, hipStream_t st) {
+static void launch_w3s2(const Wgrad3s2Args& a, int blocks, size_t lds, int planes, int kw, int sw, hipStream_t st) {
   if constexpr (prec::has_lo<PM>()) {
-    launch_w3s2_as<TG, PM, AL, 0, 3>(a, blocks, lds, st);   // (planes and k4 rejected by the caller)
+    launch_w3s2_as<TG, PM, AL, 0, 3>(a, blocks, lds, st);   // (planes, k4 and 8-wide rejected by the caller)
   } else {
-    if (kw == 4) launch_w3s2_as<TG, PM, AL, 0, 4>(a, blocks, lds, st);
+    if (sw == 8) {
+      if (kw == 4) launch_w3s2_as<TG, PM, AL, 0, 4, 8>(a, blocks, lds, st);
+      else launch_w3s2_as<TG, PM, AL, 0, 3, 8>(a, blocks, lds, st);
+    } else if (kw == 4) launch_w3s2_as<TG, PM, AL, 0, 4>(a, blocks, lds, st);
     else if (planes == 2) launch_w3s2_as<TG, PM, AL, 2, 3>(a, blocks, lds, st);
     else if (planes == 1) launch_w3s2_as<TG, PM, AL, 1, 3>(a, blocks, lds, st);
     else launch_w3s2_as<TG, PM, AL, 0, 3>(a, blocks, lds, st);
@@ -564,21 +590,27 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   a.d = g.D; a.N = g.N; a.D = g.Dd; a.H = g.Hd; a.W = g.Wd; a.Cd = g.Cd;
   a.g = g.G; a.Cg = g.Cg;
   a.ws = g.ws;
-  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / kSegW);
+  const int segw = s2_segw(g);
+  if (!segw) {
+    set_error("wgrad3s2_x3: coarse width %d is not a multiple of 16 (8 in the one-plane modes)", g.Wd);
+    return -kBadArg;
+  }
+  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / segw);
   int per = (a.nseg + splits - 1) / splits;
   per = (per + kR - 1) / kR * kR;
   a.seg_per_split = per;
   const int nsplit = (a.nseg + per - 1) / per;
   const int tg = s2_tg(g);
   const int blocks = ((g.Cd / kTD) * (g.Cg / tg) * g.k * g.k * nsplit + 7) / 8 * 8;   // XCD remap needs % 8
-  const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16, g.k);
+  const size_t lds = s2_lds(tg, g.x3 == kPrecBf16 || g.x3 == kPrecF16, g.k, segw);
   // aligned stages: whole coarse rows of one plane per stage, every stage full
-  const int nsw = g.Wd / kSegW;
+  const int nsw = g.Wd / segw;
   static const bool no_al = getenv("MRAGAN_W3S2_NO_AL") != nullptr;   // A/B switch
   const bool al = !no_al && kR % nsw == 0 && g.Hd % (kR / nsw) == 0 && a.nseg % kR == 0 && per % kR == 0;
   static_assert(2 * 3 * 16 * 64 * 4 <= kTD * kDRow, "the K-half reduction fits the D tile");
   static_assert(2 * 3 * 16 * 64 * 4 <= 2 * tr_stage<32>(), "the K-half reduction fits the tr stages");
   static_assert(2 * 4 * 16 * 64 * 4 <= 2 * tr_stage_k<32, 4>(), "the K-half reduction fits the tr stages (k4)");
+  static_assert(2 * 4 * 16 * 64 * 4 <= 2 * tr_stage_k<32, 3, 8>(), "the K-half reduction fits the tr stages (8-wide)");
   if (g.k == 4 && (g.x3 == kPrecBf16x3 || g.in16 || g.in16g)) {
     set_error("wgrad3s2_x3: k4 runs the one-plane modes on fp32 operands");
     return -kBadArg;
@@ -590,11 +622,11 @@ int conv_wgrad3s2_x3(const WgradArgs& g, int splits, hipStream_t st) {
   const int planes = g.in16 ? 2 : g.in16g ? 1 : 0;       // both operands / G only / none
   MRAGAN_PREC_DISPATCH(g.x3, {
     if (tg == 64) {
-      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, planes, g.k, st);
-      else launch_w3s2<64, PM, 0>(a, blocks, lds, planes, g.k, st);
+      if (al) launch_w3s2<64, PM, 1>(a, blocks, lds, planes, g.k, segw, st);
+      else launch_w3s2<64, PM, 0>(a, blocks, lds, planes, g.k, segw, st);
     } else {
-      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, planes, g.k, st);
-      else launch_w3s2<32, PM, 0>(a, blocks, lds, planes, g.k, st);
+      if (al) launch_w3s2<32, PM, 1>(a, blocks, lds, planes, g.k, segw, st);
+      else launch_w3s2<32, PM, 0>(a, blocks, lds, planes, g.k, segw, st);
     }
     return nsplit;
   })

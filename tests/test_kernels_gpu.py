@@ -322,7 +322,11 @@ def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
 
 
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1),
-                                                   (2, 64, 32, 10, 3, 2, 1), (3, 32, 64, 11, 3, 2, 1)])
+                                                   (2, 64, 32, 10, 3, 2, 1), (3, 32, 64, 11, 3, 2, 1),
+                                                   # one split: the kernel writes the gradient itself (no slab /
+                                                   # reduce) — the UNet's inner layers
+                                                   (1, 256, 256, 4, 4, 2, 1), (2, 128, 64, 5, 4, 2, 1),
+                                                   (1, 96, 160, 3, 3, 1, 1)])
 def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
     ops = x3
     g = torch.Generator().manual_seed(13 + N * 10 + cin + cout)
@@ -343,7 +347,10 @@ def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
                                              (3, 64, 64, (2, 6, 32)),
                                              # aligned stages (whole coarse rows per 8-segment stage)
                                              (1, 32, 64, (4, 16, 32)), (2, 64, 128, (4, 8, 64)),
-                                             (1, 32, 64, (6, 16, 64))])
+                                             (1, 32, 64, (6, 16, 64)),
+                                             # 8-voxel segments (coarse w 8 / 24: one-plane modes)
+                                             (1, 32, 64, (8, 6, 16)), (2, 64, 128, (16, 16, 16)),
+                                             (1, 32, 64, (4, 6, 48))])
 def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
     """Weight gradients of the k3 s2 p1 down convs (networks3D.py:192-197) and of the transposed
     up convs (op 1, networks3D.py:203-210) on the 3-kw-tap even/odd-phase kernel
@@ -378,7 +385,10 @@ def test_wgrad_s2_three_tap(x3, N, cin, cout, dims):
 @pytest.mark.parametrize("N,cin,cout,dims", [(1, 32, 64, (8, 10, 32)), (2, 64, 128, (6, 4, 64)), (1, 32, 128, (4, 2, 32)),
                                              # aligned stages (whole coarse rows per 8-segment stage)
                                              (1, 32, 64, (4, 16, 32)), (2, 64, 128, (4, 8, 64)),
-                                             (1, 32, 64, (6, 16, 64))])
+                                             (1, 32, 64, (6, 16, 64)),
+                                             # 8-voxel segments (coarse w 8 / 24)
+                                             (1, 32, 64, (8, 6, 16)), (2, 64, 128, (16, 16, 16)),
+                                             (1, 32, 64, (4, 6, 48))])
 def test_wgrad_s2_four_tap(x3, N, cin, cout, dims):
     """Weight gradients of the k4 s2 p1 convs (PatchGAN layers 2-3, networks3D.py:389-400; the
     UNet's down convs) and of the k4 s2 p1 transposed up convs (networks3D.py:300-330) on the
