@@ -385,11 +385,16 @@ brickT_x3_kernel(BrickTArgs a) {
 bool brickT_x3_applicable(const IgemmArgs& g) {
   // 32 output channels per block (at 64 per block the 16 class accumulators would take the whole
   // AGPR file and the halo prefetch spill): wider layers (G up1, 128 → 64) run one block per
-  // 32-channel group, re-reading the halo per group (A/B switch MRAGAN_BRICKT_WIDE=0: ny = 32 only).
-  static const bool wide = [] {
+  // 32-channel group, re-reading the halo per group — on grids of at least 64 four-wave bricks
+  // only: the UNet's coarse wide layers (≤ 16³ outputs, up to 512 contraction channels) are a few
+  // dozen long blocks there and run faster on the implicit GEMM (r05ab: UNet leg 5.24 ms with them
+  // on brickT).  A/B switch MRAGAN_BRICKT_WIDE=<min bricks> (0: ny = 32 only).
+  static const int wide_min = [] {
     const char* e = getenv("MRAGAN_BRICKT_WIDE");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 64;
   }();
+  const int64_t bricks4 = (int64_t)g.N * ceil_div(g.Do, kOD) * ceil_div(g.Ho, 16) * ceil_div(g.Wo, kOW);
+  const bool wide = wide_min > 0 && bricks4 >= wide_min;
   return g.x3 && g.trans && g.s == 2 && g.p == 1 && (g.k == 3 || g.k == 4) && g.cx % kBK == 0 &&
          (g.ny == 32 || (wide && g.ny % 32 == 0 && g.ny > 0)) &&
          (int64_t)g.Di * g.Hi * g.Wi * g.cx * 4 < ((int64_t)1 << 31);

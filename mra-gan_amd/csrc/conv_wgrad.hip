@@ -23,20 +23,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // XCDs in flattened-id order; remapping id L → (L mod 8)·(B/8) + L/8 gives each XCD a contiguous
 // range of splits with all their taps, so its L2 holds 1/8 of the voxel range instead of
 // every XCD streaming all of it (the taps re-read the same dy/x rows).
-// tap_fast (one split, direct output): the taps are the fastest logical index instead, so the taps
-// of one (dn, gn) — contiguous in the torch layout — are written from one XCD's L2
-__device__ __forceinline__ void wgrad_block(int& bx, int& by, int& bz, bool tap_fast = false) {
+__device__ __forceinline__ void wgrad_block(int& bx, int& by, int& bz) {
   const int gx = gridDim.x, gy = gridDim.y;
   const int B = gx * gy * gridDim.z;
   int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   if ((B & 7) == 0) L = (L & 7) * (B >> 3) + (L >> 3);
-  if (tap_fast) {
-    by = L % gy;
-    bx = (L / gy) % gx;
-  } else {
-    bx = L % gx;
-    by = (L / gx) % gy;
-  }
+  bx = L % gx;
+  by = (L / gx) % gy;
   bz = L / (gx * gy);
 }
 
@@ -199,7 +192,7 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   const int li = lane & 31, lh = lane >> 5;
   const int ntn = (a.Cg + BN - 1) / BN;
   int bx, by, bz;
-  wgrad_block(bx, by, bz, a.out != nullptr);
+  wgrad_block(bx, by, bz);
   const int dn0 = (bx / ntn) * BM, gn0 = (bx % ntn) * BN;
   const int t = by;
   const int tw = t % a.k, th = (t / a.k) % a.k, td = t / (a.k * a.k);
@@ -307,27 +300,6 @@ conv_wgrad_x3_kernel(WgradArgs a) {
   }
 
   const int T = a.k * a.k * a.k;
-  if (a.out) {
-    // one split: out[dn][gn][t] (=|+=) the tile itself — what wgrad_reduce would write from a
-    // one-slab workspace (0 + v = v), bit for bit
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = gn0 + wn0 + j * 32 + li;
-      if (col >= a.Cg) continue;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = dn0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < a.Cd) {
-            float* dst = a.out + ((int64_t)row * a.Cg + col) * T + t;
-            const float v = acc[i][j][r];
-            *dst = a.acc ? *dst + v : v;
-          }
-        }
-    }
-    return;
-  }
   float* slab = a.ws + ((int64_t)bz * T + t) * a.Cd * a.Cg;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -457,15 +429,6 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   const bool idx32 = M * a.Cd < ((int64_t)1 << 31) &&
                      (int64_t)a.N * a.Dg * a.Hg * a.Wg * a.Cg < ((int64_t)1 << 31);
   const bool x3 = a.x3 && a.Cd % 32 == 0 && a.Cg % 32 == 0 && idx32;
-  // one split on the MFMA kernel: it writes the gradient itself (the UNet's ≤ 4³ inner layers,
-  // whose 256 × 256 × 64 weights dwarf their activations: no 16.8 MB slab, no reduce pass;
-  // A/B switch MRAGAN_WGRAD_NO_DIRECT)
-  static const bool no_direct = getenv("MRAGAN_WGRAD_NO_DIRECT") != nullptr;
-  const bool direct = x3 && a.splits == 1 && !no_direct;
-  if (direct) {
-    a.out = out;
-    a.acc = accumulate;
-  }
   if (x3) {
     auto grid_of = [&](int bm, int bn) { return dim3(ceil_div(a.Cd, bm) * ceil_div(a.Cg, bn), T, a.splits); };
     MRAGAN_PREC_DISPATCH(a.x3, {
@@ -494,7 +457,6 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
   }
   int rc = check_launch(x3 ? "conv_wgrad_x3" : "conv_wgrad_f32");
   if (rc) return rc;
-  if (direct) return kOk;
   return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, a.splits, accumulate, st);
 }
 

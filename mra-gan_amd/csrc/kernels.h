@@ -137,8 +137,6 @@ struct WgradArgs {
   int in16;        // D and G are 16-bit operand planes (wgrad3_x3 in the bf16 / fp16 modes only)
   int in16g = 0;   // only G is a 16-bit operand plane (wgrad3s2_x3, the one-plane modes: the fine-grid
                    // operand of the 64³-level stride-2 layers)
-  float* out = nullptr;   // set by conv_wgrad: one split — conv_wgrad_x3 writes the torch-layout
-  int acc = 0;            // gradient itself (=|+=), no slab and no wgrad_reduce
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
 // bf16x3 weight gradient of valid k3 s1 convs on padded inputs, 3 kw taps per block (conv_wgrad3_x3.hip)

@@ -323,8 +323,7 @@ def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
 
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1),
                                                    (2, 64, 32, 10, 3, 2, 1), (3, 32, 64, 11, 3, 2, 1),
-                                                   # one split: the kernel writes the gradient itself (no slab /
-                                                   # reduce) — the UNet's inner layers
+                                                   # one split (the UNet's inner layers)
                                                    (1, 256, 256, 4, 4, 2, 1), (2, 128, 64, 5, 4, 2, 1),
                                                    (1, 96, 160, 3, 3, 1, 1)])
 def test_conv3d_bf16x3_wgrad(x3, N, cin, cout, S, k, s, p):
@@ -936,7 +935,7 @@ def test_head_dgrad_backward_statistics(x3, N, S, act, nc):
     (2, 64, 32, 8, 4, True, "lrelu", None),      # PatchGAN layer 2's data gradient (k4 s2 p1, convT form, 8³ → 16³)
     (2, 128, 64, 4, 4, True, "lrelu", None),     # PatchGAN layer 3's data gradient (4³ → 8³)
     (2, 32, 64, 16, 4, False, "lrelu", None),    # k4 s2 p1 in the forward form
-    (1, 128, 64, 5, 3, True, "relu", True),      # ragged: 5³ → 9³ (output padding 0): brickT's partial bricks
+    (1, 128, 32, 5, 3, True, "relu", True),      # ragged: 5³ → 9³ (output padding 0): brickT's partial bricks
 ])
 def test_stride2_dgrad_backward_statistics(x3, N, cin, cout, S, k, tr, act, expect):
     """ABI 12: the stride-2 data gradient's implicit-GEMM epilogue leaves the backward statistics of
