@@ -590,6 +590,7 @@ static int launch_in_bwd_apply(const InBwdArgs& a, const InShape& s, const doubl
 // re-reads the block's (L2-resident) slice and applies.  No partials, no finalize launch.
 // Thread = (voxel slot vt, channel quad q of the block), q fastest: lane = vt·CQB + q.
 constexpr int kInSmallBytes = 64 * 1024;          // per block and pass
+constexpr int kInSmallU = 8;                      // voxels per thread whose loads are in flight together
 static int in_small_cqb(const InShape& s) {
   static const int64_t max_s = [] {                 // A/B: MRAGAN_IN_SMALL=0 off, =S the largest S
     const char* e = getenv("MRAGAN_IN_SMALL");
@@ -676,19 +677,59 @@ __global__ void __launch_bounds__(256) in_small_fwd_kernel(const float* __restri
   const float4* rv = resid ? reinterpret_cast<const float4*>(resid) + (size_t)n * Dr * Hr * Wr * CQ + qg : nullptr;
   float4* yv = y ? reinterpret_cast<float4*>(y) + (size_t)n * P * CQ + qg : nullptr;
   uint2* y16v = y16 ? y16 + (size_t)n * P * CQ + qg : nullptr;
-  for (int pv = vt; pv < P; pv += VS) {
-    const int wp = pv % Wp, t = pv / Wp, hp = t % Hp, dp = t / Hp;
-    const int sd = min(max(dp - ypad, 0), s.D - 1), sh = min(max(hp - ypad, 0), s.H - 1), sw = min(max(wp - ypad, 0), s.W - 1);
-    const int sv = (sd * s.H + sh) * s.W + sw;
-    float4 v = xv[(size_t)sv * CQ];
-    v = make_float4((v.x - mu[0]) * rs[0], (v.y - mu[1]) * rs[1], (v.z - mu[2]) * rs[2], (v.w - mu[3]) * rs[3]);
-    v = f4_act(v, act);
-    if (rv) {
-      const float4 r = rv[(size_t)(((sd + rpad) * Hr + sh + rpad) * Wr + sw + rpad) * CQ];
-      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  // kInSmallU voxels' loads issued before their stores (the stores may alias the loads as far as
+  // the compiler knows: a one-voxel loop waited a full load latency per voxel)
+  const float4* rvp = rv ? rv : xv;
+  for (int pv0 = vt; pv0 < P; pv0 += kInSmallU * VS) {
+    float4 v[kInSmallU], r[kInSmallU];
+#pragma unroll
+    for (int u = 0; u < kInSmallU; ++u) {
+      const int pv = min(pv0 + u * VS, P - 1);
+      const int wp = pv % Wp, t = pv / Wp, hp = t % Hp, dp = t / Hp;
+      const int sd = min(max(dp - ypad, 0), s.D - 1), sh = min(max(hp - ypad, 0), s.H - 1), sw = min(max(wp - ypad, 0), s.W - 1);
+      v[u] = xv[(size_t)((sd * s.H + sh) * s.W + sw) * CQ];
+      r[u] = rvp[(size_t)(rv ? ((sd + rpad) * Hr + sh + rpad) * Wr + sw + rpad : 0) * CQ];   // (no branch)
     }
-    if (yv) yv[(size_t)pv * CQ] = v;
-    if (y16v) y16v[(size_t)pv * CQ] = f4_op16(v, mode);
+#pragma unroll
+    for (int u = 0; u < kInSmallU; ++u) {
+      const int pv = pv0 + u * VS;
+      if (pv >= P) break;
+      float4 t = make_float4((v[u].x - mu[0]) * rs[0], (v[u].y - mu[1]) * rs[1], (v[u].z - mu[2]) * rs[2],
+                             (v[u].w - mu[3]) * rs[3]);
+      t = f4_act(t, act);
+      if (rv) { t.x += r[u].x; t.y += r[u].y; t.z += r[u].z; t.w += r[u].w; }
+      if (yv) yv[(size_t)pv * CQ] = t;
+      if (y16v) y16v[(size_t)pv * CQ] = f4_op16(t, mode);
+    }
+  }
+}
+
+// the unpadded backward (P = 0: dY on the voxel grid) for kInSmallU voxels: every load first, in
+// straight-line code (no branch between them: the add operand's pointer is a select, its value
+// zeroed when absent), then the arithmetic — the compiler waited for each voxel's loads before the
+// next voxel's act / add branches otherwise (vmcnt(0) per voxel)
+template <int U>
+__device__ __forceinline__ void in_small_voxels0(const InBwdArgs& a, const float4* dyp, const float4* xp,
+                                                 const float4* addp, bool has_add, const size_t (&o)[U],
+                                                 const float4& mu, const float4& rs, float4 (&g)[U],
+                                                 float4 (&xh)[U], float4 (&graw)[U]) {
+  float4 dv[U], xv[U], ev[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    dv[u] = dyp[o[u]];
+    xv[u] = xp[o[u]];
+    ev[u] = addp[o[u]];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float4 t = dv[u];
+    if (has_add) f4_add(t, ev[u]);
+    graw[u] = t;
+    xh[u] = make_float4((xv[u].x - mu.x) * rs.x, (xv[u].y - mu.y) * rs.y, (xv[u].z - mu.z) * rs.z,
+                        (xv[u].w - mu.w) * rs.w);
+    t.x *= dact_from_xhat(xh[u].x, a.act); t.y *= dact_from_xhat(xh[u].y, a.act);
+    t.z *= dact_from_xhat(xh[u].z, a.act); t.w *= dact_from_xhat(xh[u].w, a.act);
+    g[u] = t;
   }
 }
 
@@ -700,13 +741,39 @@ __global__ void __launch_bounds__(256) in_small_bwd_kernel(InBwdArgs a, InShape 
   const int CQ = s.C / 4, qg = blockIdx.x * CQB + q;
   const int S = (int)s.S();
   double sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
-  for (int v = vt; v < S; v += VS) {
-    const int w = v % s.W, t = v / s.W, h = t % s.H, d = t / s.H;
-    const InRow row = in_bwd_row(a, s, n, d, h, qg);
-    float4 g, xh;
-    in_bwd_voxel<P>(a, s, row, w, g, xh);
-    sa[0] += g.x; sa[1] += g.y; sa[2] += g.z; sa[3] += g.w;
-    sb[0] += (double)g.x * xh.x; sb[1] += (double)g.y * xh.y; sb[2] += (double)g.z * xh.z; sb[3] += (double)g.w * xh.w;
+  const float4* dyp = reinterpret_cast<const float4*>(a.dy);
+  const float4* xp = reinterpret_cast<const float4*>(a.x);
+  const bool has_add = a.dy_add != nullptr;
+  const float4* addp = has_add ? reinterpret_cast<const float4*>(a.dy_add) : dyp;
+  const float4 mu = reinterpret_cast<const float4*>(a.mean + n * s.C)[qg];
+  const float4 rsq = reinterpret_cast<const float4*>(a.rstd + n * s.C)[qg];
+  // kInSmallU voxels' loads together, summed in voxel order (the one-voxel loop's order)
+  auto voxels = [&](int v0, float4 (&g)[kInSmallU], float4 (&xh)[kInSmallU], float4 (&graw)[kInSmallU])
+      __attribute__((always_inline)) {
+    if constexpr (P == 0) {
+      size_t o[kInSmallU];
+#pragma unroll
+      for (int u = 0; u < kInSmallU; ++u) o[u] = ((size_t)n * S + min(v0 + u * VS, S - 1)) * CQ + qg;
+      in_small_voxels0<kInSmallU>(a, dyp, xp, addp, has_add, o, mu, rsq, g, xh, graw);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kInSmallU; ++u) {
+        const int v = min(v0 + u * VS, S - 1);
+        const int w = v % s.W, t = v / s.W, h = t % s.H, d = t / s.H;
+        in_bwd_voxel<P>(a, s, in_bwd_row(a, s, n, d, h, qg), w, g[u], xh[u], &graw[u]);
+      }
+    }
+  };
+  for (int v0 = vt; v0 < S; v0 += kInSmallU * VS) {
+    float4 g[kInSmallU], xh[kInSmallU], graw[kInSmallU];
+    voxels(v0, g, xh, graw);
+#pragma unroll
+    for (int u = 0; u < kInSmallU; ++u) {
+      if (v0 + u * VS >= S) break;
+      sa[0] += g[u].x; sa[1] += g[u].y; sa[2] += g[u].z; sa[3] += g[u].w;
+      sb[0] += (double)g[u].x * xh[u].x; sb[1] += (double)g[u].y * xh[u].y;
+      sb[2] += (double)g[u].z * xh[u].z; sb[3] += (double)g[u].w * xh[u].w;
+    }
   }
   in_small_reduce<CQB>(sa, sb, red);
   const double Sd = (double)S;
@@ -719,20 +786,23 @@ __global__ void __launch_bounds__(256) in_small_bwd_kernel(InBwdArgs a, InShape 
   float4* dx = reinterpret_cast<float4*>(a.dx);
   uint2* dx16 = reinterpret_cast<uint2*>(a.dx16);
   float4* gout = reinterpret_cast<float4*>(a.g_out);
-  for (int v = vt; v < S; v += VS) {
-    const int w = v % s.W, t = v / s.W, h = t % s.H, d = t / s.H;
-    const InRow row = in_bwd_row(a, s, n, d, h, qg);
-    float4 g, xh, graw;
-    in_bwd_voxel<P>(a, s, row, w, g, xh, &graw);
-    const size_t o = ((size_t)n * S + v) * CQ + qg;
-    if (gout) gout[o] = graw;
-    float4 r;
-    r.x = row.rs.x * (g.x - mg[0] - xh.x * mgx[0]);
-    r.y = row.rs.y * (g.y - mg[1] - xh.y * mgx[1]);
-    r.z = row.rs.z * (g.z - mg[2] - xh.z * mgx[2]);
-    r.w = row.rs.w * (g.w - mg[3] - xh.w * mgx[3]);
-    if (dx) dx[o] = r;
-    if (dx16) dx16[o] = f4_op16(r, a.mode16);
+  for (int v0 = vt; v0 < S; v0 += kInSmallU * VS) {
+    float4 g[kInSmallU], xh[kInSmallU], graw[kInSmallU];
+    voxels(v0, g, xh, graw);
+#pragma unroll
+    for (int u = 0; u < kInSmallU; ++u) {
+      const int v = v0 + u * VS;
+      if (v >= S) break;
+      const size_t o = ((size_t)n * S + v) * CQ + qg;
+      if (gout) gout[o] = graw[u];
+      float4 r;
+      r.x = rsq.x * (g[u].x - mg[0] - xh[u].x * mgx[0]);
+      r.y = rsq.y * (g[u].y - mg[1] - xh[u].y * mgx[1]);
+      r.z = rsq.z * (g[u].z - mg[2] - xh[u].z * mgx[2]);
+      r.w = rsq.w * (g[u].w - mg[3] - xh[u].w * mgx[3]);
+      if (dx) dx[o] = r;
+      if (dx16) dx16[o] = f4_op16(r, a.mode16);
+    }
   }
 }
 
