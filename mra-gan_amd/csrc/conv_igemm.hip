@@ -19,6 +19,7 @@
 // MFMA K-order: lane half h supplies k = 4h+s at step s, so each lane reads ONE float4 of
 // A and of B per 8-deep chunk and feeds 4 MFMAs from it.
 #include "kernels.h"
+#include "prec.h"
 #include "conv_geo.h"
 
 #include <cstdlib>
@@ -232,17 +233,25 @@ static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hi
 }
 
 static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
-// A/B switch, off by default: measured on MI355X (bf16, 64³ b2 bench, r03c) the interior brick
-// (~25 µs at N = 4, the forward's time) plus the shell pass (~28 µs: 252 blocks × 36 serial K-steps,
-// latency-bound) lost to the whole-grid brick (~41 µs)
-static const bool g_split_off = getenv("MRAGAN_DGRAD_SPLIT") == nullptr;
+// Interior + shell data gradient (below): measured on MI355X (bf16, r03c / r05bb) the interior
+// brick plus the shell pass (252 blocks × 36 serial K-steps at 4 × 16³, latency-bound) lose to the
+// whole-grid brick on the 64³ configuration's 16³ blocks (N = 4: 42.9 vs 32.7 µs; N = 2: 36.8 vs
+// 32.7) and at 1 × 32³ (59.2 vs 55.6), and win from 2 × 32³ on (the 128³ configuration's cycle-free
+// passes: 92.9 vs 109.6 µs — the 34³ output grid fits no brick shape, the 32³ interior fits the
+// forward's).  MRAGAN_DGRAD_SPLIT=1 / 0 forces it on / off for A/B.
+static const int g_split_env = [] {
+  const char* e = getenv("MRAGAN_DGRAD_SPLIT");
+  return e ? (atoi(e) ? 1 : 0) : -1;
+}();
 static int x3_instances_per_launch(const IgemmArgs& a);
 
 // data gradient of a valid k3 s1 conv (transposed form p = 0, output = input + 2): the 16-bit
 // modes compute it as interior + shell (the whole-grid brick spent 42 % of its rows on outputs
 // whose taps mostly read zero padding and on padded brick rows)
 bool full_dgrad_split_applicable(const IgemmArgs& a) {
-  return !g_brick_off && !g_split_off && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
+  const bool big = (int64_t)a.N * a.Di * a.Hi * a.Wi >= 65536 && a.Di >= 32;
+  const bool on = g_split_env >= 0 ? g_split_env == 1 : (big && (a.x3 == kPrecBf16 || a.x3 == kPrecF16));
+  return !g_brick_off && on && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
          a.Ho == a.Hi + 2 && a.Wo == a.Wi + 2 && a.Do == a.Ho && a.Ho == a.Wo && a.Di >= 2 && a.cx % 16 == 0 &&
          conv_brick_x3_active(a) && x3_instances_per_launch(a) >= a.N;
 }
@@ -314,6 +323,10 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
   if (a.x16) {
     // 16-bit operand planes: the ResnetBlock convs (forward and whole-grid data gradient) on the
     // brick; the others (the 64³-level stride-2 forward-form convs) on the implicit GEMM
+    if (full_dgrad_split_applicable(a)) {
+      const int rc = conv_brick(a, st, true);
+      return rc ? rc : conv_igemm_x3_shell(a, st);
+    }
     if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
     // 32-output-channel stride-2 transposed convs (G up2, G down1's data gradient): brickT (round 4)
     if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);

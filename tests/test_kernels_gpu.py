@@ -660,6 +660,28 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
+@pytest.mark.parametrize("N,S", [(2, 32), (1, 32)])
+def test_op16_res_dgrad_interior_shell(op16, N, S):
+    """The ResnetBlock whole-grid data gradient from 2 × 32³ on runs as the interior brick (the 32³
+    "same" conv written one voxel in) plus the shell pass (conv_igemm.hip full_dgrad_split_applicable;
+    1 × 32³ keeps the whole-grid brick): fp64 on the rounded operands, and bit-identical between the
+    plane and the fp32 input."""
+    ops = op16
+    dt = ops.op16_dtype()
+    C = 128
+    g = torch.Generator().manual_seed(N * 3 + S)
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_b, ws_b = pack(ops, w, False, True), _presplit(ops, w, C, C, True)
+    dy = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()
+    osp = (S + 2,) * 3
+    dx, _ = ops.conv3d_op16(dy.to(dt), wp_b, C, 3, 1, 0, osp, ws_b, transposed=True)
+    dx32 = ops.conv3d(dy, wp_b, C, 3, 1, 0, osp, transposed=True, wsplit=ws_b)
+    assert torch.isfinite(dx).all()
+    assert torch.equal(dx, dx32)
+    ref = F.conv_transpose3d(ncdhw(dy.to(dt).double().cpu()), w.float().to(dt).double())
+    assert rel(ncdhw(dx.double().cpu()), ref) < 2e-5
+
+
 @pytest.mark.parametrize("N,S", [(2, 16), (4, 16), (1, 12)])
 def test_in_launch_finalize(op16, N, S):
     """ABI 15: the K-split brick's last block per (instance, column tile) finalizes the InstanceNorm
