@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 17
+#define MRAGAN_ABI_VERSION 18
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -226,6 +226,20 @@ int mragan_conv3d_op16_dgrad_in_stats_fin(const void* dy16, int N, int Di, int H
                                           const float* x_in, const float* mean, const float* rstd, int act, double* part,
                                           size_t part_bytes, int* chunks, unsigned* tickets, float* coef, int* finalized,
                                           void* stream);
+/* ABI 18: mragan_conv3d_op16_dgrad_in_stats(_fin) with a gradient x_add ([N][Di][Hi][Wi][cout]
+ * fp32) that joins the fold before act': the IN backward in front then reads g = fold(dz) + x_add
+ * (mragan_instnorm_bwd_partials_op16 with dy_add = x_add).  In the ResnetBlock chain
+ * (networks3D.py:241-263, out = x + block(x)) conv1's data gradient dz of block i+1 and the block
+ * output gradient G of block i+1 (the skip path) meet at block i's second InstanceNorm, whose
+ * backward statistics Σ g, Σ g·x̂ then come from this epilogue (x_add read at the padded outputs
+ * that map one to one onto an interior voxel) and its statistics pass goes.  Brick kernels only
+ * (bf16 / fp16, whole-grid k3 s1): elsewhere *chunks = 0 (run the statistics pass).  tickets may be
+ * null (then as the non-_fin form; coef / finalized unused). */
+int mragan_conv3d_op16_dgrad_in_stats_add(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* wpacked,
+                                          const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes,
+                                          const float* x_in, const float* mean, const float* rstd, int act,
+                                          const float* x_add, double* part, size_t part_bytes, int* chunks,
+                                          unsigned* tickets, float* coef, int* finalized, void* stream);
 /* ABI 16: mragan_conv3d_presplit_bwd_stats on the 16-bit operand plane of its input (bf16 / fp16
  * modes; the stride-2 implicit GEMM, a multiple of 32 input channels): the data gradient of G up1 /
  * up2 (ConvTranspose3d k3 s2, networks3D.py:203-209) from the plane of the IN backward's dx, with the

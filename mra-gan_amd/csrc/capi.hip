@@ -191,7 +191,8 @@ static int conv3d_op16_impl(const void* x16, int N, int Di, int Hi, int Wi, int 
 static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
                                     const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
                                     const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
-                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream);
+                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream,
+                                    const float* x_add = nullptr);
 
 int mragan_conv3d_op16_dgrad_in_stats(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
                                       const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
@@ -211,10 +212,22 @@ int mragan_conv3d_op16_dgrad_in_stats_fin(const void* dy16, int N, int Di, int H
                                   part, part_bytes, chunks, tickets, coef, finalized, stream);
 }
 
+int mragan_conv3d_op16_dgrad_in_stats_add(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
+                                          const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes,
+                                          const float* x_in, const float* mean, const float* rstd, int act,
+                                          const float* x_add, double* part, size_t part_bytes, int* chunks,
+                                          unsigned* tickets, float* coef, int* finalized, void* stream) {
+  MRAGAN_CHECK_ARG(x_add, "conv3d_op16_dgrad_in_stats_add: null x_add");
+  MRAGAN_CHECK_ARG(!tickets || (coef && finalized), "conv3d_op16_dgrad_in_stats_add: tickets need coef and finalized");
+  return op16_dgrad_in_stats_impl(dy16, N, Di, Hi, Wi, cin, w, wsplit, cout, y, ws, ws_bytes, x_in, mean, rstd, act,
+                                  part, part_bytes, chunks, tickets, coef, finalized, stream, x_add);
+}
+
 static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int Wi, int cin, const float* w,
                                     const void* wsplit, int cout, float* y, void* ws, size_t ws_bytes, const float* x_in,
                                     const float* mean, const float* rstd, int act, double* part, size_t part_bytes,
-                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream) {
+                                    int* chunks, unsigned* tickets, float* coef, int* finalized, void* stream,
+                                    const float* x_add) {
   if (int rc = op16_mode_ok()) return rc;
   if (finalized) *finalized = 0;
   MRAGAN_CHECK_ARG(dy16 && w && wsplit && y && x_in && mean && rstd && part && chunks,
@@ -229,7 +242,7 @@ static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int
   IgemmArgs a{static_cast<const float*>(dy16), w, nullptr, y, N, Di, Hi, Wi, cin, Do, Ho, Wo, cout, 3, 1, 0, 1, kActNone,
               1, g_conv_precision, static_cast<float*>(ws), ws_bytes, wsplit, part, chunks};
   a.x16 = 1;
-  a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act;
+  a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act; a.bs_add = x_add;
   if (tickets) { a.in_tick = tickets; a.in_fin0 = coef; a.in_fin1 = nullptr; a.in_finalized = finalized; }
   return conv_igemm(a, static_cast<hipStream_t>(stream));
 }

@@ -399,7 +399,7 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
     // backward statistics (see BrickArgs::sx): only for the whole-grid data gradient (output = input + 2)
     MRAGAN_CHECK_ARG(g.in_part && g.trans && g.Do == g.Di + 2 && g.Ho == g.Hi + 2 && g.Wo == g.Wi + 2 && g.bs_mean &&
                      g.bs_rstd && !interior, "conv_brick: backward statistics need the whole-grid data gradient");
-    a.sx = g.bs_x; a.smean = g.bs_mean; a.srstd = g.bs_rstd; a.sact = g.bs_act;
+    a.sx = g.bs_x; a.smean = g.bs_mean; a.srstd = g.bs_rstd; a.sact = g.bs_act; a.sadd = g.bs_add;
   }
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps
   a.flip = g.trans ? 1 : 0;

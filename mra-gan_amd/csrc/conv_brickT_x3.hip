@@ -480,7 +480,7 @@ static int conv_brickT_pm(const IgemmArgs& g, hipStream_t st) {
   const int64_t blocks = (int64_t)g.N * a.nbd * a.nbh * a.nbw * a.gn;
   if (blocks == 0) return kOk;
   static const bool no_stats = getenv("MRAGAN_NO_BRICKT_STATS") != nullptr;   // A/B switch
-  if (g.in_part && !no_stats) {
+  if (g.in_part && !no_stats && !g.bs_add) {     // bs_add (ABI 18): brick epilogues only
     // conv3d_in_stats: the following InstanceNorm's partials; conv3d_bwd_stats (a stride-2 data
     // gradient, ABI 12): the backward statistics of the InstanceNorm in front (same grid)
     a.part = g.in_part;

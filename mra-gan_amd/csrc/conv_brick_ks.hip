@@ -196,6 +196,8 @@ conv_brick_ks_kernel(BrickArgs a) {
           const int cd = min(max(od - 1, 0), a.Do - 3), ch = min(max(oh - 1, 0), a.Ho - 3),
                     cw = min(max(ow - 1, 0), a.Wo - 3);
           xoff[r] = (int)((((int64_t)nb * (a.Do - 2) + cd) * (a.Ho - 2) + ch) * (a.Wo - 2) + cw);
+          // bit 30: the padded output is the interior voxel's own (no clamp) — where sadd joins
+          if (od >= 1 && od <= a.Do - 2 && oh >= 1 && oh <= a.Ho - 2 && ow >= 1 && ow <= a.Wo - 2) xoff[r] |= 1 << 30;
         }
       }
     }
@@ -354,7 +356,7 @@ conv_brick_ks_kernel(BrickArgs a) {
     orow[q] = out_off[row];
     xrow[q] = a.sx ? xoff[row] : 0;
   }
-  float4 bq[TN], mu[TN], rsd[TN], xs[TN][4];
+  float4 bq[TN], mu[TN], rsd[TN], xs[TN][4], xa[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int c0 = n0 + j * 32 + 4 * m4;
@@ -363,9 +365,12 @@ conv_brick_ks_kernel(BrickArgs a) {
       mu[j] = *reinterpret_cast<const float4*>(a.smean + nb * a.ny + c0);
       rsd[j] = *reinterpret_cast<const float4*>(a.srstd + nb * a.ny + c0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        xs[j][q] = orow[q] >= 0 ? *reinterpret_cast<const float4*>(a.sx + (int64_t)xrow[q] * a.ny + c0)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < 4; ++q) {
+        const int64_t xi = (int64_t)(xrow[q] & ((1 << 30) - 1)) * a.ny + c0;
+        xs[j][q] = orow[q] >= 0 ? *reinterpret_cast<const float4*>(a.sx + xi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        xa[j][q] = (a.sadd && orow[q] >= 0 && (xrow[q] >> 30)) ? *reinterpret_cast<const float4*>(a.sadd + xi)
+                                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
   // K reduction: every wave leaves the partials of the three fragment rows it does not finish
@@ -443,10 +448,12 @@ conv_brick_ks_kernel(BrickArgs a) {
         }
       } else {
         const float xv[4] = {xs[j][q].x, xs[j][q].y, xs[j][q].z, xs[j][q].w};
+        const float av[4] = {xa[j][q].x, xa[j][q].y, xa[j][q].z, xa[j][q].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float xh = (xv[e] - muv[e]) * rsv[e];
-          const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? v[e] * kLreluSlope : v[e];
+          const float gin = v[e] + av[e];    // + 0 where no skip gradient joins: the same float
+          const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? gin * kLreluSlope : gin;
           ps[j][e] += gv;
           pq[j][e] += (double)gv * xh;
         }

@@ -158,6 +158,8 @@ conv_brick_x3_kernel(BrickArgs a) {
           const int cd = min(max(od - 1, 0), a.Do - 3), ch = min(max(oh - 1, 0), a.Ho - 3),
                     cw = min(max(ow - 1, 0), a.Wo - 3);
           xoff[r] = (int)((((int64_t)nb * (a.Do - 2) + cd) * (a.Ho - 2) + ch) * (a.Wo - 2) + cw);
+          // bit 30: the padded output is the interior voxel's own (no clamp) — where sadd joins
+          if (od >= 1 && od <= a.Do - 2 && oh >= 1 && oh <= a.Ho - 2 && ow >= 1 && ow <= a.Wo - 2) xoff[r] |= 1 << 30;
         }
       }
     }
@@ -348,8 +350,11 @@ conv_brick_x3_kernel(BrickArgs a) {
           if (off >= 0) {
             const float v = acc[i][j][r];
             a.y[(int64_t)off * a.ny + col] = v;
-            const float xh = (a.sx[(int64_t)xoff[row] * a.ny + col] - mu) * rs;
-            const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? v * kLreluSlope : v;
+            const int xo = xoff[row];
+            const int64_t xi = (int64_t)(xo & ((1 << 30) - 1)) * a.ny + col;
+            const float xh = (a.sx[xi] - mu) * rs;
+            const float gin = (a.sadd && (xo >> 30)) ? v + a.sadd[xi] : v;
+            const float gv = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f : (a.sact == kActLrelu && !(xh > 0.f)) ? gin * kLreluSlope : gin;
             ps[j] += gv;
             pq[j] += (double)gv * xh;
           }

@@ -520,6 +520,9 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
                        (int64_t)a.k * a.k * a.k * a.ny * a.cx * 4 < ((int64_t)1 << 31),
                    "conv (16-bit MFMA modes): input of %d×%d×%d×%d×%d too large for one launch", a.N, a.Di, a.Hi, a.Wi,
                    a.cx);
+  // a skip gradient joining the backward statistics (ABI 18) exists in the brick epilogues only:
+  // no partials here (chunks stays 0, the caller runs the statistics pass)
+  if (a.bs_add) a.in_part = nullptr;
   X3Plan pl = x3_plan(a, total_m);
   if (pl.splits > 1) {
     const size_t need = (size_t)pl.splits * total_m * a.ny * sizeof(float);

@@ -25,6 +25,7 @@ struct IgemmArgs {
   int x16;          // x is a 16-bit operand plane (bf16 / fp16 words of the precision mode), not fp32
   // with in_part, backward statistics instead (BrickArgs::sx): the producing IN's x, μ, rstd, act
   const float* bs_x; const float* bs_mean; const float* bs_rstd; int bs_act;
+  const float* bs_add = nullptr;   // ABI 18, brick kernels only: BrickArgs::sadd
   // optional with in_part (ABI 15): finalize the statistics in the launch where the kernel can
   // (BrickArgs::tick …); *in_finalized = 1 when it did, else left 0 (the caller finalizes)
   unsigned* in_tick = nullptr; float* in_fin0 = nullptr; float* in_fin1 = nullptr; int* in_finalized = nullptr;
@@ -57,6 +58,10 @@ struct BrickArgs {
   // ([N][Do−2][Ho−2][Wo−2][ny] fp32, statistics smean / srstd [N][ny]): part = Σ_p g, Σ_p g·x̂
   // with g = dz_p·act'(x̂) at the interior voxel p folds into (conv_brick_x3 only)
   const float* sx; const float* smean; const float* srstd; int sact;
+  // optional with sx (ABI 18): a gradient added to the fold before act' — the ResnetBlock skip
+  // gradient ([N][Do−2][Ho−2][Wo−2][ny] fp32; each interior voxel counted once, at the padded
+  // output that maps onto it one to one)
+  const float* sadd;
   int stamp;        // diagnostics: record s_memtime phase stamps (conv_brick_ks only)
   // optional with part (ABI 15, conv_brick_ks only): finalize in the launch (in_ticket.h) —
   // tick: N·gn zeroed counters; fin_mode 0: μ → fin0, rstd → fin1 ([N][ny]); 1: the backward

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -95,6 +95,9 @@ SIGNATURES = {
                                      sz, vp, sz, vp, vp, vp, vp, vp, vp]),
     "mragan_conv3d_op16_dgrad_in_stats_fin": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, sz, vp, vp, vp,
                                                     i32, vp, sz, vp, vp, vp, vp, vp]),
+    # ABI 18: the ResnetBlock skip gradient joining the data-gradient epilogue's backward statistics
+    "mragan_conv3d_op16_dgrad_in_stats_add": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, sz, vp, vp, vp,
+                                                    i32, vp, vp, sz, vp, vp, vp, vp, vp]),
     "mragan_instnorm_apply_op16": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, i32, vp, vp, vp]),
     "mragan_instnorm_bwd_apply_op16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp]),
     # ABI 16: the stride-2 data gradient with backward statistics on the plane of its input

@@ -30,6 +30,8 @@ from ._lib import call
 _NO_IN_STATS = bool(int(__import__("os").environ.get("MRAGAN_NO_IN_STATS", "0") or "0"))
 _NO_HEAD_STATS = __import__("os").environ.get("MRAGAN_NO_HEAD_STATS") is not None   # A/B: head dgrad without IN statistics
 _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None       # A/B: stride-2 dgrads without them
+# A/B: a ResnetBlock's second-IN backward statistics from the next block's conv1 data gradient (ABI 18)
+_NO_SKIP_STATS = __import__("os").environ.get("MRAGAN_NO_SKIP_STATS") is not None
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -187,6 +189,20 @@ class ConvLayer:
             return dz, part, chunks, coef
         dz, chunks = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean, rstd, act,
                                                     part)
+        return dz, part, chunks, None
+
+    def dgrad_op16_in_stats_add(self, dy16, norm_x, mean, rstd, act, add):
+        """dgrad_op16_in_stats for an InstanceNorm whose backward input is fold(dz) + add (ABI 18):
+        conv1 of ResnetBlock i+1, whose input gradient meets block i+1's output gradient G (the
+        skip path) at block i's second IN.  Returns (dz, part, chunks, coef) as dgrad_op16_in_stats."""
+        N, D, H, W, _ = dy16.shape
+        part = ops.in_partials_buffer(N, (D + 2, H + 2, W + 2), self.cin, dy16.device)
+        if _IN_FIN:
+            dz, chunks, coef = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean,
+                                                              rstd, act, part, fin=True, x_add=add)
+            return dz, part, chunks, coef
+        dz, chunks = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean, rstd, act,
+                                                    part, x_add=add)
         return dz, part, chunks, None
 
     def wgrad_op16(self, x16, dy16, accumulate=True):
@@ -484,9 +500,16 @@ class NetPlan:
             want_dgrad = i > 0 or need_input_grad
             if st.kind == "block" and sc.inp16 is not None:
                 # 16-bit operand planes: the IN backwards write dY only as planes (the convs' sole use)
+                skip = bstats if (bstats is not None and len(bstats) == 3 and gpad == 1 and gadd is not None) else None
+                bstats = None
                 if gpad == 0 and gadd is None:
                     G = g
                     dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                elif skip is not None:
+                    # statistics from the next block's conv1 data-gradient epilogue (ABI 18)
+                    G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
+                    dh2 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, None, skip[0], skip[1],
+                                                         g_out=G, coef=skip[2])
                 else:
                     G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                     dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
@@ -501,7 +524,21 @@ class NetPlan:
                     dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
                     st.conv1.wgrad_op16(sc.inp16, dh1)
-                g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
+                nxt = self.stages[i - 1] if i > 0 else None
+                nsc = ctx.stages[i - 1] if i > 0 else None
+                # the IN in front: the previous block's IN2 (no activation), or G down2's IN + ReLU
+                skip_in = nxt is not None and (
+                    (nxt.kind == "block" and nsc.inp16 is not None)
+                    or (nxt.kind != "block" and nxt.norm is not None and nsc.h is not None
+                        and tuple(nsc.h.shape) == tuple(G.shape)))
+                if skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS:
+                    # conv1's data gradient also accumulates that IN's backward statistics, with this
+                    # block's output gradient G joining at the skip (ABI 18)
+                    act_in = None if nxt.kind == "block" else nxt.act
+                    g, part, chunks, coef = st.conv1.dgrad_op16_in_stats_add(dh1, nsc.h, nsc.mean, nsc.rstd, act_in, G)
+                    bstats = (part, chunks, coef) if chunks else None
+                else:
+                    g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue
             if st.kind == "block":
@@ -539,7 +576,8 @@ class NetPlan:
             dh16 = None
             if plane_bwd or plane_bwd_fwd:
                 if bstats is not None:
-                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2],
+                                                          coef=bstats[2] if len(bstats) > 2 else None)
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
                 in_spatial = x_any.shape[1:4]
@@ -570,7 +608,8 @@ class NetPlan:
                 # the G stem (k7, nc → 32; ABI 17): its IN backward writes dx only as the plane — the
                 # stem's weight gradient and data gradient (thinn_x3) are its only readers
                 if bstats is not None:
-                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                    dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2],
+                                                          coef=bstats[2] if len(bstats) > 2 else None)
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
                 bstats = None
@@ -583,7 +622,7 @@ class NetPlan:
                 continue
             if st.norm is not None:
                 if bstats is not None:
-                    dh = ops.instnorm_bwd_partials(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats)
+                    dh = ops.instnorm_bwd_partials(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2])
                 else:
                     dh = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
             else:

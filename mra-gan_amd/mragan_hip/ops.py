@@ -564,18 +564,24 @@ def _conv3d_op16_fin(x16, wp, cout, k, s, p, out_spatial, wsplit, part, transpos
 
 def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, wsplit: torch.Tensor,
                                x_in: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, act, part: torch.Tensor,
-                               fin: bool = False):
+                               fin: bool = False, x_add: Optional[torch.Tensor] = None):
     """Whole-grid data gradient (k3 s1 p0 transposed form, output = input + 2 per dim) from the
     plane dy16 that also leaves, in `part`, the backward-statistics partials of the InstanceNorm
     (+act) whose output was this conv's input: x_in (pre-norm, [N, D, H, W, cout]), mean, rstd.
     Returns (dz, chunks); chunks = 0: no partials (run instnorm_bwd_op16).  With fin (ABI 15):
     (dz, chunks, coef) — coef [N, cout, 2] when the launch finalized the IN backward's coefficients
-    (then instnorm_bwd_partials_op16(coef=…)), else None."""
+    (then instnorm_bwd_partials_op16(coef=…)), else None.  x_add (ABI 18, same shape as x_in): a
+    gradient that joins the fold before act' — the statistics are then those of fold(dz) + x_add
+    (instnorm_bwd_partials_op16 with dy_add=x_add); chunks = 0 where no brick epilogue runs."""
     _check16(dy16, "dgrad_in_stats.dy16")
     _check(x_in, "dgrad_in_stats.x_in")
     N, Di, Hi, Wi, cin = dy16.shape
     if tuple(x_in.shape) != (N, Di, Hi, Wi, cout):
         raise ValueError(f"dgrad_in_stats: x_in shape {tuple(x_in.shape)} != {(N, Di, Hi, Wi, cout)}")
+    if x_add is not None:
+        _check(x_add, "dgrad_in_stats.x_add")
+        if tuple(x_add.shape) != tuple(x_in.shape):
+            raise ValueError(f"dgrad_in_stats: x_add shape {tuple(x_add.shape)} != {tuple(x_in.shape)}")
     if wp.numel() != 27 * cin * cout or wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
         raise ValueError("dgrad_in_stats: packed / pre-split weight size mismatch")
     if part.dtype != torch.float64 or not part.is_cuda:
@@ -585,6 +591,18 @@ def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, 
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, 3, 1, 0, *osp, 1)
     ws = WS.get(nbytes) if nbytes else None
     chunks = _ct.c_int(0)
+    if x_add is not None:
+        coef = torch.empty((N, cout, 2), device=dy16.device, dtype=torch.float32) if fin else None
+        tick = _ticket_ptr(N * max(1, cout // 32), dy16.device) if fin else None
+        done = _ct.c_int(0)
+        fn = lambda: call("mragan_conv3d_op16_dgrad_in_stats_add", _ptr(dy16), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit),
+                          cout, _ptr(out), _ptr(ws), nbytes, _ptr(x_in), _ptr(mean), _ptr(rstd), ACT[act], _ptr(x_add),
+                          _ptr(part), part.numel() * 8, _ct.byref(chunks), tick, _ptr(coef),
+                          _ct.byref(done) if fin else None, _stream())
+        _timed(lambda: _conv_info(cin, cout, 3, 1, 0, True, N, (Di, Hi, Wi), osp), fn)
+        if fin:
+            return out, chunks.value, (coef if done.value else None)
+        return out, chunks.value
     if fin:
         coef = torch.empty((N, cout, 2), device=dy16.device, dtype=torch.float32)
         tick = _ticket_ptr(N * max(1, cout // 32), dy16.device)

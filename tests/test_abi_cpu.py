@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
     assert set(header_functions()) == set(mragan_hip.exported_symbols())
-    assert lib.mragan_abi_version() == 17
+    assert lib.mragan_abi_version() == 18
 
 
 def test_library_built_for_gfx950():

@@ -682,6 +682,43 @@ def test_op16_res_dgrad_interior_shell(op16, N, S):
     assert rel(ncdhw(dx.double().cpu()), ref) < 2e-5
 
 
+@pytest.mark.parametrize("N,S,act,fin", [(4, 16, None, True), (2, 16, None, True), (2, 16, None, False),
+                                          (1, 32, None, True), (2, 16, "relu", True)])
+def test_op16_dgrad_skip_statistics(op16, N, S, act, fin):
+    """ABI 18: conv1's data gradient of ResnetBlock i+1 leaves the backward statistics of block i's
+    second InstanceNorm, whose input gradient is fold(dz) + G (G: block i+1's output gradient, the
+    skip path): dz bit-identical to the plain data gradient (fp32 noise where the statistics brick
+    differs), G written by the IN backward bit-identical, dx within fp64 summation-order noise of the
+    statistics-pass IN backward on the same dz — for the
+    8-wave brick (N = 4), the K-split brick with and without in-launch finalize, the large grid."""
+    ops = op16
+    dt = ops.op16_dtype()
+    C = 128
+    g = torch.Generator().manual_seed(N * 13 + S)
+    w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_b, ws_b = pack(ops, w, False, True), _presplit(ops, w, C, C, True)
+    h = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()          # block i's conv2 output
+    _, m, r = ops.instnorm_fwd(h, act=act)
+    dh1 = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda().to(dt)  # block i+1's IN1 dx plane
+    G1 = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()         # block i+1's output gradient
+    dz_ref, _ = ops.conv3d_op16(dh1, wp_b, C, 3, 1, 0, (S + 2,) * 3, ws_b, transposed=True)
+    part = ops.in_partials_buffer(N, (S + 2,) * 3, C, "cuda")
+    res = ops.conv3d_op16_dgrad_in_stats(dh1, wp_b, C, ws_b, h, m, r, act, part, fin=fin, x_add=G1)
+    dz, chunks = res[0], res[1]
+    coef = res[2] if fin else None
+    assert chunks > 0
+    # the plain data gradient of a large grid may run another brick (summation order): same to fp32 noise
+    assert torch.equal(dz, dz_ref) if N * S ** 3 < 32768 else rel(dz, dz_ref) < 1e-6
+    G_ref = torch.empty_like(h)
+    dx_ref = ops.instnorm_bwd_op16(h, m, r, dz, 1, G1, act=act, g_out=G_ref)
+    G = torch.full_like(h, float("nan"))
+    dx = ops.instnorm_bwd_partials_op16(h, m, r, dz, 1, G1, act, part, chunks, g_out=G, coef=coef)
+    assert torch.equal(G, G_ref)
+    assert torch.isfinite(dx.float()).all()
+    assert (dx != dx_ref).float().mean().item() < 1e-3        # only round-half cases of ~1e-7 shifts
+    assert rel(dx, dx_ref) < 1e-5
+
+
 @pytest.mark.parametrize("N,S", [(2, 16), (4, 16), (1, 12)])
 def test_in_launch_finalize(op16, N, S):
     """ABI 15: the K-split brick's last block per (instance, column tile) finalizes the InstanceNorm
