@@ -501,10 +501,15 @@ class NetPlan:
             if st.kind == "block" and sc.inp16 is not None:
                 # 16-bit operand planes: the IN backwards write dY only as planes (the convs' sole use)
                 skip = bstats if (bstats is not None and len(bstats) == 3 and gpad == 1 and gadd is not None) else None
+                own = bstats if (bstats is not None and gpad == 0 and gadd is None) else None
                 bstats = None
                 if gpad == 0 and gadd is None:
                     G = g
-                    dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
+                    if own is not None:      # statistics from G up1's data-gradient epilogue
+                        dh2 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, G, 0, None, None, *own[:2],
+                                                             coef=own[2] if len(own) > 2 else None)
+                    else:
+                        dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
                 elif skip is not None:
                     # statistics from the next block's conv1 data-gradient epilogue (ABI 18)
                     G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
@@ -590,12 +595,17 @@ class NetPlan:
                 bstats = None
                 if want_dgrad:
                     nxt = self.stages[i - 1] if i > 0 else None
-                    if (nxt is not None and nxt.kind != "block" and nxt.norm is not None and not st.prepad
-                            and conv.dgrad_bwd_stats_ok()):
+                    # the IN in front: a down / up conv's IN(+act), or (G up1) the last ResnetBlock's
+                    # IN2 — no activation, no fold, its output gradient is this data gradient alone
+                    blk_in = (nxt is not None and nxt.kind == "block" and ctx.stages[i - 1].inp16 is not None
+                              and not _NO_SKIP_STATS and tuple(ctx.stages[i - 1].h.shape[1:4]) == tuple(in_spatial))
+                    in_ok = blk_in or (nxt is not None and nxt.kind != "block" and nxt.norm is not None)
+                    if in_ok and not st.prepad and conv.dgrad_bwd_stats_ok():
                         nsc = ctx.stages[i - 1]
                         part = ops.in_partials_buffer(dh16.shape[0], in_spatial, conv.cin, dh16.device)
                         g, bchunks = ops.conv3d_op16_bwd_stats(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p,
-                                                               in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act, part,
+                                                               in_spatial, nsc.h, nsc.mean, nsc.rstd,
+                                                               None if blk_in else nxt.act, part,
                                                                transposed=not conv.transposed)
                         bstats = (part, bchunks) if bchunks else None
                     else:
