@@ -32,6 +32,19 @@ _NO_HEAD_STATS = __import__("os").environ.get("MRAGAN_NO_HEAD_STATS") is not Non
 _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None       # A/B: stride-2 dgrads without them
 # A/B: a ResnetBlock's second-IN backward statistics from the next block's conv1 data gradient (ABI 18)
 _NO_SKIP_STATS = __import__("os").environ.get("MRAGAN_NO_SKIP_STATS") is not None
+_SPLIT_ENV = __import__("os").environ.get("MRAGAN_DGRAD_SPLIT")
+
+
+def _dgrad_split(N, D, H, W):
+    """Mirror of conv_igemm.hip full_dgrad_split_applicable's size rule: from 2 × 32³ on the plain
+    ResnetBlock data gradient runs as interior brick + shell pass (faster than any whole-grid brick
+    there, and than the backward-statistics brick plus the saved statistics pass: 128³ step
+    29.07 / 29.10 ms with it against 29.40 / 29.44 with the statistics brick, r05bg).  The skip
+    statistics (ABI 18) are used below 32³ only: at 1 × 32³ too the statistics brick (K-split, large
+    grid) costs about what the statistics pass saves (r05bh: 29.12 / 29.22 vs 29.08 / 29.07 ms)."""
+    if _SPLIT_ENV is not None:
+        return _SPLIT_ENV not in ("", "0")
+    return N * D * H * W >= 65536 and D >= 32 and ops.get_conv_precision() in ("bf16", "fp16")
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -536,7 +549,8 @@ class NetPlan:
                     (nxt.kind == "block" and nsc.inp16 is not None)
                     or (nxt.kind != "block" and nxt.norm is not None and nsc.h is not None
                         and tuple(nsc.h.shape) == tuple(G.shape)))
-                if skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS:
+                if (skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS and dh1.shape[1] < 32
+                        and not _dgrad_split(*dh1.shape[:4])):
                     # conv1's data gradient also accumulates that IN's backward statistics, with this
                     # block's output gradient G joining at the skip (ABI 18)
                     act_in = None if nxt.kind == "block" else nxt.act
