@@ -33,6 +33,9 @@ _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None   
 # A/B: a ResnetBlock's second-IN backward statistics from the next block's conv1 data gradient (ABI 18)
 _NO_SKIP_STATS = __import__("os").environ.get("MRAGAN_NO_SKIP_STATS") is not None
 _SPLIT_ENV = __import__("os").environ.get("MRAGAN_DGRAD_SPLIT")
+# conv2's data gradient where the split runs: plain (split) + IN1's statistics pass, not the
+# backward-statistics brick (128³ step 29.10 / 29.02 vs 29.52 / 29.30 ms, r05bi); A/B switch
+_IN1_STATS_BIG = __import__("os").environ.get("MRAGAN_IN1_STATS_BIG") is not None
 
 
 def _dgrad_split(N, D, H, W):
@@ -534,7 +537,10 @@ class NetPlan:
                 if need_wgrad:
                     st.conv2.wgrad_op16(sc.z1, dh2)
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
-                dz1, part, chunks, coef = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
+                if not _IN1_STATS_BIG and _dgrad_split(*dh2.shape[:4]):
+                    dz1, part, chunks, coef = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4]), None, 0, None
+                else:
+                    dz1, part, chunks, coef = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
                 if chunks:
                     dh1 = ops.instnorm_bwd_partials_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, "relu", part, chunks,
                                                          coef=coef)
