@@ -238,7 +238,10 @@ static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B s
 // whole-grid brick on the 64³ configuration's 16³ blocks (N = 4: 42.9 vs 32.7 µs; N = 2: 36.8 vs
 // 32.7) and at 1 × 32³ (59.2 vs 55.6), and win from 2 × 32³ on (the 128³ configuration's cycle-free
 // passes: 92.9 vs 109.6 µs — the 34³ output grid fits no brick shape, the 32³ interior fits the
-// forward's).  MRAGAN_DGRAD_SPLIT=1 / 0 forces it on / off for A/B.
+// forward's).  Opt-in (MRAGAN_DGRAD_SPLIT=1): with the split on for 2 × 32³ only and the 1 × 32³
+// cycle passes on the whole-grid brick, the 128³ step gates failed (G_A gradients of 1e11–1e27,
+// gpurun_out/r05final2, r05bk) while the split everywhere and the whole-grid brick everywhere both
+// pass — not understood yet, so not the default.
 static const int g_split_env = [] {
   const char* e = getenv("MRAGAN_DGRAD_SPLIT");
   return e ? (atoi(e) ? 1 : 0) : -1;
@@ -249,9 +252,7 @@ static int x3_instances_per_launch(const IgemmArgs& a);
 // modes compute it as interior + shell (the whole-grid brick spent 42 % of its rows on outputs
 // whose taps mostly read zero padding and on padded brick rows)
 bool full_dgrad_split_applicable(const IgemmArgs& a) {
-  const bool big = (int64_t)a.N * a.Di * a.Hi * a.Wi >= 65536 && a.Di >= 32;
-  const bool on = g_split_env >= 0 ? g_split_env == 1 : (big && (a.x3 == kPrecBf16 || a.x3 == kPrecF16));
-  return !g_brick_off && on && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
+  return !g_brick_off && g_split_env == 1 && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
          a.Ho == a.Hi + 2 && a.Wo == a.Wi + 2 && a.Do == a.Ho && a.Ho == a.Wo && a.Di >= 2 && a.cx % 16 == 0 &&
          conv_brick_x3_active(a) && x3_instances_per_launch(a) >= a.N;
 }

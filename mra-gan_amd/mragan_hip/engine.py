@@ -45,9 +45,9 @@ def _dgrad_split(N, D, H, W):
     29.07 / 29.10 ms with it against 29.40 / 29.44 with the statistics brick, r05bg).  The skip
     statistics (ABI 18) are used below 32³ only: at 1 × 32³ too the statistics brick (K-split, large
     grid) costs about what the statistics pass saves (r05bh: 29.12 / 29.22 vs 29.08 / 29.07 ms)."""
-    if _SPLIT_ENV is not None:
-        return _SPLIT_ENV not in ("", "0")
-    return N * D * H * W >= 65536 and D >= 32 and ops.get_conv_precision() in ("bf16", "fp16")
+    # opt-in (MRAGAN_DGRAD_SPLIT=1), as in conv_igemm.hip: a split at 2 × 32³ with the whole-grid
+    # brick at 1 × 32³ failed the 128³ step gates (r05final2 / r05bk), not yet understood
+    return _SPLIT_ENV not in (None, "", "0") and ops.get_conv_precision() in ("bf16", "fp16")
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))

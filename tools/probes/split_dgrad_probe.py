@@ -2,7 +2,7 @@
 """ResnetBlock whole-grid data gradient (k3 s1 p0 transposed, 16-bit operand plane of dY) against
 fp64 on the rounded operands, and its HIP-event time — run once with MRAGAN_DGRAD_SPLIT=1 (interior
 brick + shell pass) and once without (whole-grid brick) to compare the two dispatches.
-    python tools/probes/split_dgrad_probe.py [bf16|fp16]"""
+    python tools/probes/split_dgrad_probe.py [bf16|fp16] [NxS,...]"""
 import os
 import sys
 
@@ -19,8 +19,11 @@ def main():
     ops.set_conv_precision(prec)
     dt = ops.op16_dtype()
     C = 128
-    tag = "split" if os.environ.get("MRAGAN_DGRAD_SPLIT") else "whole"
-    for N, S in [(2, 16), (4, 16), (1, 32), (2, 32), (1, 24)]:
+    tag = {"1": "split", "0": "whole"}.get(os.environ.get("MRAGAN_DGRAD_SPLIT", ""), "default")
+    cases = [(2, 16), (4, 16), (1, 32), (2, 32), (1, 24)]
+    if len(sys.argv) > 2:                      # e.g. "2x24,4x24"
+        cases = [tuple(int(v) for v in c.split("x")) for c in sys.argv[2].split(",")]
+    for N, S in cases:
         g = torch.Generator().manual_seed(N * 7 + S)
         w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
         wf = w.float().cuda().contiguous()
