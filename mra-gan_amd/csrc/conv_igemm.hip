@@ -236,12 +236,13 @@ static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B s
 // Interior + shell data gradient (below): measured on MI355X (bf16, r03c / r05bb) the interior
 // brick plus the shell pass (252 blocks × 36 serial K-steps at 4 × 16³, latency-bound) lose to the
 // whole-grid brick on the 64³ configuration's 16³ blocks (N = 4: 42.9 vs 32.7 µs; N = 2: 36.8 vs
-// 32.7) and at 1 × 32³ (59.2 vs 55.6), and win from 2 × 32³ on (the 128³ configuration's cycle-free
+// 32.7) and at 1 × 32³ (59.2 vs 55.6), and win from 2 × 32³ on (the 128³ configuration's first
 // passes: 92.9 vs 109.6 µs — the 34³ output grid fits no brick shape, the 32³ interior fits the
-// forward's).  Opt-in (MRAGAN_DGRAD_SPLIT=1): with the split on for 2 × 32³ only and the 1 × 32³
-// cycle passes on the whole-grid brick, the 128³ step gates failed (G_A gradients of 1e11–1e27,
-// gpurun_out/r05final2, r05bk) while the split everywhere and the whole-grid brick everywhere both
-// pass — not understood yet, so not the default.
+// forward's).  On from N·D·H·W ≥ 2 × 32³ (D ≥ 32) in the one-plane modes; MRAGAN_DGRAD_SPLIT=1 / 0
+// forces it on / off for A/B.  The shell pass reads the fp32 pack `w` (the implicit GEMM rounds it
+// on the fly), which the engine refreshes for a ResnetBlock conv only where this rule holds
+// (engine._dgrad_split — a superset of this function's conditions; r05final2's garbage 128³
+// gradients were that pack left stale).
 static const int g_split_env = [] {
   const char* e = getenv("MRAGAN_DGRAD_SPLIT");
   return e ? (atoi(e) ? 1 : 0) : -1;
@@ -252,7 +253,9 @@ static int x3_instances_per_launch(const IgemmArgs& a);
 // modes compute it as interior + shell (the whole-grid brick spent 42 % of its rows on outputs
 // whose taps mostly read zero padding and on padded brick rows)
 bool full_dgrad_split_applicable(const IgemmArgs& a) {
-  return !g_brick_off && g_split_env == 1 && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
+  const bool big = (int64_t)a.N * a.Di * a.Hi * a.Wi >= 65536 && a.Di >= 32;
+  const bool on = g_split_env >= 0 ? g_split_env == 1 : (big && (a.x3 == kPrecBf16 || a.x3 == kPrecF16));
+  return !g_brick_off && on && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
          a.Ho == a.Hi + 2 && a.Wo == a.Wi + 2 && a.Do == a.Ho && a.Ho == a.Wo && a.Di >= 2 && a.cx % 16 == 0 &&
          conv_brick_x3_active(a) && x3_instances_per_launch(a) >= a.N;
 }

@@ -39,15 +39,17 @@ _IN1_STATS_BIG = __import__("os").environ.get("MRAGAN_IN1_STATS_BIG") is not Non
 
 
 def _dgrad_split(N, D, H, W):
-    """Mirror of conv_igemm.hip full_dgrad_split_applicable's size rule: from 2 × 32³ on the plain
-    ResnetBlock data gradient runs as interior brick + shell pass (faster than any whole-grid brick
-    there, and than the backward-statistics brick plus the saved statistics pass: 128³ step
-    29.07 / 29.10 ms with it against 29.40 / 29.44 with the statistics brick, r05bg).  The skip
+    """Mirror of conv_igemm.hip full_dgrad_split_applicable's size rule (a superset of its
+    conditions): from 2 × 32³ on the plain ResnetBlock data gradient runs as interior brick + shell
+    pass (faster than any whole-grid brick there, and than the backward-statistics brick plus the
+    saved statistics pass: 128³ step 29.07 / 29.10 ms with it against 29.40 / 29.44 with the
+    statistics brick, r05bg).  The shell pass reads the conv's fp32 data-gradient pack, which the
+    per-step repack skips for the brick convs: ConvLayer.fresh_fp32_bwd refreshes it first.  The skip
     statistics (ABI 18) are used below 32³ only: at 1 × 32³ too the statistics brick (K-split, large
     grid) costs about what the statistics pass saves (r05bh: 29.12 / 29.22 vs 29.08 / 29.07 ms)."""
-    # opt-in (MRAGAN_DGRAD_SPLIT=1), as in conv_igemm.hip: a split at 2 × 32³ with the whole-grid
-    # brick at 1 × 32³ failed the 128³ step gates (r05final2 / r05bk), not yet understood
-    return _SPLIT_ENV not in (None, "", "0") and ops.get_conv_precision() in ("bf16", "fp16")
+    if _SPLIT_ENV is not None:
+        return _SPLIT_ENV not in ("", "0")
+    return N * D * H * W >= 65536 and D >= 32 and ops.get_conv_precision() in ("bf16", "fp16")
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -123,12 +125,24 @@ class ConvLayer:
             if self.ws_bwd is None or self.ws_bwd.device != w.device:
                 self.ws_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             out.append((w, A, B, T, base + int(tb), self.ws_bwd))
+        self.fp32_bwd_stale = False
         if prec != "f32" and split_f and split_b and not self.transposed and not _FP32_PACKS:
             # the MFMA-mode brick kernels read only the pre-split copies of a k3 s1 ResnetBlock
             # conv (forward and data gradient): its two fp32 packs are not refreshed (the repack
-            # moves half the bytes; a mode switch repacks, ensure_packed)
+            # moves half the bytes; a mode switch repacks, ensure_packed) — except the data-gradient
+            # pack where the interior + shell split runs (fresh_fp32_bwd)
+            self.fp32_bwd_stale = True
             out = out[2:]
         return out
+
+    def fresh_fp32_bwd(self):
+        """Refresh the fp32 data-gradient pack before a data gradient that may run the interior +
+        shell split (its shell pass reads it): once per repack, on the stream of the first such use
+        (captured into the step graph with it)."""
+        if getattr(self, "fp32_bwd_stale", False):
+            w = self.m.weight.data
+            ops.pack_weight(w, self.cout, self.cin, self.k ** 3, True, self.wp_bwd)
+            self.fp32_bwd_stale = False
 
     def repack(self):
         for src, A, B, T, tr, dst in self.packs():
@@ -538,6 +552,7 @@ class NetPlan:
                     st.conv2.wgrad_op16(sc.z1, dh2)
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
                 if not _IN1_STATS_BIG and _dgrad_split(*dh2.shape[:4]):
+                    st.conv2.fresh_fp32_bwd()
                     dz1, part, chunks, coef = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4]), None, 0, None
                 else:
                     dz1, part, chunks, coef = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
@@ -563,6 +578,8 @@ class NetPlan:
                     g, part, chunks, coef = st.conv1.dgrad_op16_in_stats_add(dh1, nsc.h, nsc.mean, nsc.rstd, act_in, G)
                     bstats = (part, chunks, coef) if chunks else None
                 else:
+                    if _dgrad_split(*dh1.shape[:4]):
+                        st.conv1.fresh_fp32_bwd()
                     g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue

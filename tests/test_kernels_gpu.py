@@ -662,10 +662,11 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
 
 @pytest.mark.parametrize("N,S", [(2, 32), (1, 32)])
 def test_op16_res_dgrad_interior_shell(op16, N, S):
-    """The ResnetBlock whole-grid data gradient at the 128³ configuration's 32³ level — the whole-grid
-    brick, or with MRAGAN_DGRAD_SPLIT=1 the interior brick (the 32³ "same" conv written one voxel
-    in) plus the shell pass (conv_igemm.hip full_dgrad_split_applicable): fp64 on the rounded
-    operands, and bit-identical between the plane and the fp32 input."""
+    """The ResnetBlock whole-grid data gradient from 2 × 32³ on runs as the interior brick (the 32³
+    "same" conv written one voxel in) plus the shell pass (conv_igemm.hip full_dgrad_split_applicable;
+    1 × 32³ keeps the whole-grid brick): fp64 on the rounded operands, and bit-identical between the
+    plane and the fp32 input.  (The shell pass reads the fp32 pack: the engine refreshes it,
+    ConvLayer.fresh_fp32_bwd — this test packs it itself.)"""
     ops = op16
     dt = ops.op16_dtype()
     C = 128
