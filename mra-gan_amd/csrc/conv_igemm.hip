@@ -238,7 +238,9 @@ static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B s
 // whole-grid brick on the 64³ configuration's 16³ blocks (N = 4: 42.9 vs 32.7 µs; N = 2: 36.8 vs
 // 32.7) and at 1 × 32³ (59.2 vs 55.6), and win from 2 × 32³ on (the 128³ configuration's first
 // passes: 92.9 vs 109.6 µs — the 34³ output grid fits no brick shape, the 32³ interior fits the
-// forward's).  On from N·D·H·W ≥ 2 × 32³ (D ≥ 32) in the one-plane modes; MRAGAN_DGRAD_SPLIT=1 / 0
+// forward's), and at the 96³ configuration's 24³ (fp16, r05bj: 2 × 24³ 56.5 vs 61.2, 4 × 24³ 88.5
+// vs 117.4 µs; 2 × 28³ loses, 84.4 vs 63.7: no brick fits 28).  On for N ≥ 2 and interior extents
+// that are multiples of 8 from 24 on, in the one-plane modes; MRAGAN_DGRAD_SPLIT=1 / 0
 // forces it on / off for A/B.  The shell pass reads the fp32 pack `w` (the implicit GEMM rounds it
 // on the fly), which the engine refreshes for a ResnetBlock conv only where this rule holds
 // (engine._dgrad_split — a superset of this function's conditions; r05final2's garbage 128³
@@ -253,7 +255,7 @@ static int x3_instances_per_launch(const IgemmArgs& a);
 // modes compute it as interior + shell (the whole-grid brick spent 42 % of its rows on outputs
 // whose taps mostly read zero padding and on padded brick rows)
 bool full_dgrad_split_applicable(const IgemmArgs& a) {
-  const bool big = (int64_t)a.N * a.Di * a.Hi * a.Wi >= 65536 && a.Di >= 32;
+  const bool big = a.N >= 2 && a.Di >= 24 && a.Di % 8 == 0 && a.Hi % 8 == 0 && a.Wi % 8 == 0;
   const bool on = g_split_env >= 0 ? g_split_env == 1 : (big && (a.x3 == kPrecBf16 || a.x3 == kPrecF16));
   return !g_brick_off && on && !a.bs_x && a.trans && a.s == 1 && a.k == 3 && a.p == 0 && a.Do == a.Di + 2 &&
          a.Ho == a.Hi + 2 && a.Wo == a.Wi + 2 && a.Do == a.Ho && a.Ho == a.Wo && a.Di >= 2 && a.cx % 16 == 0 &&

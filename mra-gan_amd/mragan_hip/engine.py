@@ -40,7 +40,8 @@ _IN1_STATS_BIG = __import__("os").environ.get("MRAGAN_IN1_STATS_BIG") is not Non
 
 def _dgrad_split(N, D, H, W):
     """Mirror of conv_igemm.hip full_dgrad_split_applicable's size rule (a superset of its
-    conditions): from 2 × 32³ on the plain ResnetBlock data gradient runs as interior brick + shell
+    conditions): for N ≥ 2 at 24³ / 32³ (multiples of 8 from 24) the plain ResnetBlock data
+    gradient runs as interior brick + shell
     pass (faster than any whole-grid brick there, and than the backward-statistics brick plus the
     saved statistics pass: 128³ step 29.07 / 29.10 ms with it against 29.40 / 29.44 with the
     statistics brick, r05bg).  The shell pass reads the conv's fp32 data-gradient pack, which the
@@ -49,7 +50,8 @@ def _dgrad_split(N, D, H, W):
     grid) costs about what the statistics pass saves (r05bh: 29.12 / 29.22 vs 29.08 / 29.07 ms)."""
     if _SPLIT_ENV is not None:
         return _SPLIT_ENV not in ("", "0")
-    return N * D * H * W >= 65536 and D >= 32 and ops.get_conv_precision() in ("bf16", "fp16")
+    return (N >= 2 and D >= 24 and D % 8 == 0 and H % 8 == 0 and W % 8 == 0
+            and ops.get_conv_precision() in ("bf16", "fp16"))
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
