@@ -596,10 +596,14 @@ class NetPlan:
                     dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
                     st.conv2.wgrad(sc.z1, dh2)
+                if _dgrad_split(*dh2.shape[:4]):     # the split's shell pass reads the fp32 pack
+                    st.conv2.fresh_fp32_bwd()
                 dz1 = st.conv2.dgrad(dh2, sc.z1.shape[1:4])
                 dh1 = ops.instnorm_bwd(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
                     st.conv1.wgrad(sc.inp, dh1)
+                if _dgrad_split(*dh1.shape[:4]):
+                    st.conv1.fresh_fp32_bwd()
                 g = st.conv1.dgrad(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue

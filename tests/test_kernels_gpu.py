@@ -1458,3 +1458,32 @@ def test_adam_rebias_skipped_steps(ops):
         torch.cuda.synchronize()
         want = torch.tensor(ops.adam_hyper(lr, b1, b2, eps, t - k, scale))
         assert torch.equal(hyper.cpu(), want), (t, k, hyper.cpu(), want)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_fresh_fp32_bwd_pack(ops, prec):
+    """The per-step repack skips a ResnetBlock conv's fp32 packs in the one-plane modes (the bricks
+    read the pre-split copies); the split data gradient's shell pass reads the fp32 data-gradient
+    pack, so the engine refreshes it first (ConvLayer.fresh_fp32_bwd): after a repack the flag is
+    set, and the refresh writes exactly the pack the full repack would."""
+    from mragan_hip import engine
+    ops.set_conv_precision(prec)
+    try:
+        import types
+        torch.manual_seed(0)
+        w = torch.nn.Parameter(torch.randn(64, 64, 3, 3, 3, device="cuda") * 0.05)
+        m = types.SimpleNamespace(weight=w, kernel_size=3, stride=1, padding=0, in_channels=64, out_channels=64)
+        layer = engine.ConvLayer(m, False)
+        for src, A, B, T, tr, dst in layer.packs():
+            ops.pack_weight(src, A, B, T, tr, dst)
+        if engine._FP32_PACKS:
+            pytest.skip("fp32 packs refreshed by every repack in this environment")
+        assert layer.fp32_bwd_stale
+        layer.wp_bwd.fill_(float("nan"))
+        layer.fresh_fp32_bwd()
+        ref = torch.empty_like(layer.wp_bwd)
+        ops.pack_weight(m.weight.data, 64, 64, 27, True, ref)
+        assert not layer.fp32_bwd_stale
+        assert torch.equal(layer.wp_bwd, ref)
+    finally:
+        ops.set_conv_precision("f32")
