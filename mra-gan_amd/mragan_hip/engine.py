@@ -32,6 +32,9 @@ _NO_HEAD_STATS = __import__("os").environ.get("MRAGAN_NO_HEAD_STATS") is not Non
 _NO_S2_STATS = __import__("os").environ.get("MRAGAN_NO_S2_STATS") is not None       # A/B: stride-2 dgrads without them
 # A/B: a ResnetBlock's second-IN backward statistics from the next block's conv1 data gradient (ABI 18)
 _NO_SKIP_STATS = __import__("os").environ.get("MRAGAN_NO_SKIP_STATS") is not None
+# A/B: skip statistics only up to this batch (the N = 4 data gradient runs the 8-wave brick, whose
+# statistics epilogue costs ≈ 5 µs, r05ba)
+_SKIP_STATS_MAXN = int(__import__("os").environ.get("MRAGAN_SKIP_STATS_MAXN", "0") or "0")
 _SPLIT_ENV = __import__("os").environ.get("MRAGAN_DGRAD_SPLIT")
 # conv2's data gradient where the split runs: plain (split) + IN1's statistics pass, not the
 # backward-statistics brick (128³ step 29.10 / 29.02 vs 29.52 / 29.30 ms, r05bi); A/B switch
@@ -573,7 +576,8 @@ class NetPlan:
                     or (nxt.kind != "block" and nxt.norm is not None and nsc.h is not None
                         and tuple(nsc.h.shape) == tuple(G.shape)))
                 if (skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS and dh1.shape[1] < 32
-                        and not _dgrad_split(*dh1.shape[:4])):
+                        and not _dgrad_split(*dh1.shape[:4])
+                        and (_SKIP_STATS_MAXN <= 0 or dh1.shape[0] <= _SKIP_STATS_MAXN)):
                     # conv1's data gradient also accumulates that IN's backward statistics, with this
                     # block's output gradient G joining at the skip (ABI 18)
                     act_in = None if nxt.kind == "block" else nxt.act
