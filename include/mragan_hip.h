@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MRAGAN_ABI_VERSION 18
+#define MRAGAN_ABI_VERSION 19
 
 enum mragan_status { MRAGAN_OK = 0, MRAGAN_EBADARG = 1, MRAGAN_EWORKSPACE = 2, MRAGAN_ELAUNCH = 3, MRAGAN_EUNSUPPORTED = 4 };
 enum mragan_act { MRAGAN_ACT_NONE = 0, MRAGAN_ACT_RELU = 1, MRAGAN_ACT_LRELU = 2, MRAGAN_ACT_TANH = 3, MRAGAN_ACT_SIGMOID = 4 };
@@ -165,7 +165,18 @@ int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, 
  *       of 32 input channels (G down1 / down2 on the stem / down1 InstanceNorm planes);
  *       wsplit nullable (the brick then splits per call); part / chunks nullable (no partials);
  *   conv3d_wgrad_op16: mragan_conv3d_wgrad on the planes of dense and gathered — the k3 s1 valid
- *       weight gradient of the ResnetBlock convs (wgrad3_x3).                                   */
+ *       weight gradient of the ResnetBlock convs (wgrad3_x3).
+ * ABI 19: in mragan_conv3d_presplit(_in_stats), mragan_conv3d_op16(_fin) and the
+ * mragan_conv3d_op16_dgrad_in_stats family `wpacked` may be NULL when `wsplit` is given.  The k3 s1
+ * bricks and both passes of the interior + shell data gradient read only `wsplit` (the shell pass
+ * stages its hi words); every kernel that needs the fp32 pack then fails with MRAGAN_EBADARG
+ * instead of reading it.  A caller that refreshes only the pre-split copy after an optimizer step
+ * (the fp32 pack stale) passes NULL, so no kernel can read stale weights.
+ * mragan_conv3d_dgrad_split: 1 when the whole-grid data gradient of a k3 s1 p0 conv from the plane of
+ * dY ([N][Di][Hi][Wi][cin] → [N][Di+2][Hi+2][Wi+2][cout], transposed form) runs as the interior brick
+ * plus the shell pass in the current mode, else 0 — the rule the engine schedules by (that form
+ * leaves no backward statistics), queried instead of mirrored.                              */
+int mragan_conv3d_dgrad_split(int N, int Di, int Hi, int Wi, int cin, int cout);
 int mragan_instnorm_fwd_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
                              const float* resid, int rpad, float* mean, float* rstd, void* ws, size_t ws_bytes,
                              void* stream);

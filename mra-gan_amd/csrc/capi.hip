@@ -49,12 +49,15 @@ static int conv_common(const float* x, int N, int Di, int Hi, int Wi, int cin, c
                        int k, int stride, int pad, int act, float* y, int Do, int Ho, int Wo, int trans, void* ws,
                        size_t ws_bytes, void* stream, const void* wx3 = nullptr, double* in_part = nullptr,
                        int* in_chunks = nullptr) {
-  MRAGAN_CHECK_ARG(x && w && y, "conv: null pointer");
+  // w may be null when the pre-split copy wx3 is given (a stale fp32 pack is not passed): only the
+  // kernels that read wx3 alone accept that (conv_brick, the shell pass); the others refuse it
+  MRAGAN_CHECK_ARG(x && (w || wx3) && y, "conv: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0, "conv: bad input shape");
   MRAGAN_CHECK_ARG(Do > 0 && Ho > 0 && Wo > 0, "conv: bad output shape");
   MRAGAN_CHECK_ARG(k >= 1 && stride >= 1 && pad >= 0, "conv: bad k/stride/pad");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (thin_side(cin, cout)) {
+    MRAGAN_CHECK_ARG(w, "conv: the thin convolutions need the fp32 weight pack");
     ThinArgs a{x, N, Di, Hi, Wi, cin, w, bias, y, Do, Ho, Wo, cout, k, stride, pad, trans, act, g_conv_precision};
     if (g_conv_precision != MRAGAN_PREC_F32 && thin1_x3_applicable(cin, cout, k, stride, g_conv_precision)) {
       a.in_part = in_part;
@@ -170,7 +173,8 @@ static int conv3d_op16_impl(const void* x16, int N, int Di, int Hi, int Wi, int 
                             float* mean, float* rstd, int* finalized, void* stream) {
   if (int rc = op16_mode_ok()) return rc;
   if (finalized) *finalized = 0;
-  MRAGAN_CHECK_ARG(x16 && w && y, "conv3d_op16: null pointer");   // wsplit: optional (the brick packs per call)
+  // wsplit: optional (the brick packs per call); w: optional when wsplit is given (conv_common)
+  MRAGAN_CHECK_ARG(x16 && (w || wsplit) && y, "conv3d_op16: null pointer");
   MRAGAN_CHECK_ARG(transposed == 0 || transposed == 1, "conv3d_op16: transposed must be 0/1");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && Do > 0 && Ho > 0 && Wo > 0,
                    "conv3d_op16: bad shape");
@@ -230,7 +234,7 @@ static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int
                                     const float* x_add) {
   if (int rc = op16_mode_ok()) return rc;
   if (finalized) *finalized = 0;
-  MRAGAN_CHECK_ARG(dy16 && w && wsplit && y && x_in && mean && rstd && part && chunks,
+  MRAGAN_CHECK_ARG(dy16 && wsplit && y && x_in && mean && rstd && part && chunks,     // w: optional (conv_common)
                    "conv3d_op16_dgrad_in_stats: null pointer");
   MRAGAN_CHECK_ARG(N >= 0 && Di > 0 && Hi > 0 && Wi > 0 && cin > 0 && cout > 0 && !thin_side(cin, cout),
                    "conv3d_op16_dgrad_in_stats: bad shape");
@@ -245,6 +249,17 @@ static int op16_dgrad_in_stats_impl(const void* dy16, int N, int Di, int Hi, int
   a.bs_x = x_in; a.bs_mean = mean; a.bs_rstd = rstd; a.bs_act = act; a.bs_add = x_add;
   if (tickets) { a.in_tick = tickets; a.in_fin0 = coef; a.in_fin1 = nullptr; a.in_finalized = finalized; }
   return conv_igemm(a, static_cast<hipStream_t>(stream));
+}
+
+int mragan_conv3d_dgrad_split(int N, int Di, int Hi, int Wi, int cin, int cout) {
+  // the whole-grid data gradient of a k3 s1 p0 conv from the plane of dY ([N][Di][Hi][Wi][cin]) to
+  // the padded grid of cout channels, as mragan_conv3d_op16(transposed = 1) dispatches it (ABI 19)
+  if (N <= 0 || Di <= 0 || Hi <= 0 || Wi <= 0 || cin <= 0 || cout <= 0) return 0;
+  if (g_conv_precision != MRAGAN_PREC_BF16 && g_conv_precision != MRAGAN_PREC_F16) return 0;
+  IgemmArgs a{nullptr, nullptr, nullptr, nullptr, N, Di, Hi, Wi, cin, Di + 2, Hi + 2, Wi + 2, cout, 3, 1, 0, 1,
+              kActNone, 1, g_conv_precision, nullptr, 0, nullptr, nullptr, nullptr};
+  a.x16 = 1;
+  return full_dgrad_split_applicable(a) ? 1 : 0;
 }
 
 int mragan_conv3d_thin_op16(const void* x16, int N, int Di, int Hi, int Wi, int cin, const float* w, const float* bias,

@@ -389,6 +389,9 @@ bool conv_brick_applicable(const IgemmArgs& a) {
 }
 
 int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
+  // a caller whose fp32 pack is stale passes none (the MFMA bricks read the pre-split copy only)
+  MRAGAN_CHECK_ARG(g.w || (g.wx3 && conv_brick_x3_active(g)),
+                   "conv_brick: needs the fp32 weight pack (no usable pre-split copy was given)");
   BrickArgs a{};
   a.x = g.x; a.N = g.N; a.Di = g.Di; a.Hi = g.Hi; a.Wi = g.Wi; a.C = g.cx;
   a.w = g.w; a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
@@ -399,6 +402,11 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
     // backward statistics (see BrickArgs::sx): only for the whole-grid data gradient (output = input + 2)
     MRAGAN_CHECK_ARG(g.in_part && g.trans && g.Do == g.Di + 2 && g.Ho == g.Hi + 2 && g.Wo == g.Wi + 2 && g.bs_mean &&
                      g.bs_rstd && !interior, "conv_brick: backward statistics need the whole-grid data gradient");
+    // the bricks keep a row's fold index in bits 0-29 of xoff and the skip-add flag in bit 30
+    // (conv_brick_ks.hip, conv_brick_x3.hip): the interior voxel index must fit 30 bits
+    MRAGAN_CHECK_ARG(!g.bs_add || (int64_t)g.N * g.Di * g.Hi * g.Wi < ((int64_t)1 << 30),
+                     "conv_brick: skip-gradient statistics need N·D·H·W < 2^30 (got %d×%d×%d×%d)", g.N, g.Di, g.Hi,
+                     g.Wi);
     a.sx = g.bs_x; a.smean = g.bs_mean; a.srstd = g.bs_rstd; a.sact = g.bs_act; a.sadd = g.bs_add;
   }
   // transposed form with s = 1: y[o] = Σ_t x[o + p − t] Wp[t] = forward form, pad k−1−p, flipped taps

@@ -233,6 +233,11 @@ static int dispatch_tile(const IgemmArgs& a, int64_t max_mc, int64_t total_m, hi
 }
 
 static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B switch for benchmarking
+static int need_fp32_pack(const IgemmArgs& a) {
+  MRAGAN_CHECK_ARG(a.w, "conv: this convolution needs the fp32 weight pack (only a pre-split copy was given)");
+  return kOk;
+}
+
 // Interior + shell data gradient (below): measured on MI355X (bf16, r03c / r05bb) the interior
 // brick plus the shell pass (252 blocks × 36 serial K-steps at 4 × 16³, latency-bound) lose to the
 // whole-grid brick on the 64³ configuration's 16³ blocks (N = 4: 42.9 vs 32.7 µs; N = 2: 36.8 vs
@@ -241,10 +246,10 @@ static const bool g_brick_off = getenv("MRAGAN_NO_BRICK") != nullptr;   // A/B s
 // forward's), and at the 96³ configuration's 24³ (fp16, r05bj: 2 × 24³ 56.5 vs 61.2, 4 × 24³ 88.5
 // vs 117.4 µs; 2 × 28³ loses, 84.4 vs 63.7: no brick fits 28).  On for N ≥ 2 and interior extents
 // that are multiples of 8 from 24 on, in the one-plane modes; MRAGAN_DGRAD_SPLIT=1 / 0
-// forces it on / off for A/B.  The shell pass reads the fp32 pack `w` (the implicit GEMM rounds it
-// on the fly), which the engine refreshes for a ResnetBlock conv only where this rule holds
-// (engine._dgrad_split — a superset of this function's conditions; r05final2's garbage 128³
-// gradients were that pack left stale).
+// forces it on / off for A/B.  Both passes read the pre-split weights (the shell pass through the
+// implicit GEMM's W16 staging), so the fp32 pack — which the engine does not refresh for the
+// ResnetBlock convs in these modes and then does not pass at all — is never read here (r05final2's
+// garbage 128³ gradients were a stale fp32 pack read by the shell pass).
 static const int g_split_env = [] {
   const char* e = getenv("MRAGAN_DGRAD_SPLIT");
   return e ? (atoi(e) ? 1 : 0) : -1;
@@ -334,6 +339,7 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
       return rc ? rc : conv_igemm_x3_shell(a, st);
     }
     if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+    if (int rc = need_fp32_pack(a)) return rc;
     // 32-output-channel stride-2 transposed convs (G up2, G down1's data gradient): brickT (round 4)
     if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
     MRAGAN_CHECK_ARG(a.x3 && a.cx % 32 == 0, "conv: a 16-bit operand plane input needs the bf16 / fp16 implicit GEMM "
@@ -346,6 +352,7 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
     return rc ? rc : conv_igemm_x3_shell(a, st);
   }
   if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+  if (int rc = need_fp32_pack(a)) return rc;
   if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_chunked(a, max_mc, total_m, st);
   if (a.cx % 32 == 0) return dispatch_tile<32>(a, max_mc, total_m, st);

@@ -38,18 +38,26 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // X16: the input is the producer's 16-bit operand plane (bf16 / fp16 words, rounded as the
 // staging would round them; the one-plane modes): an A row's BK channels are BK / 8 16-B loads
 // stored to LDS as they are — half the bytes of the fp32 input and no conversion.
-template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH, int X16>
+// W16: the weights are the pre-split fragment copy (IgemmArgs::wx3, pack tr 2-5: per (tap, 32-channel
+// chunk, 16-channel half) the hi words of every output row n, 8 channels in 16 B) instead of the fp32
+// pack — the B row's BK channels are BK / 8 16-B loads of hi words stored to LDS as they are, bit for
+// bit the RNE words the fp32 staging would produce.  The shell pass of the interior + shell data
+// gradient runs this way, so it reads the same weights as the interior brick and the fp32 pack of a
+// ResnetBlock conv is never needed in the one-plane modes (r05final2: a stale fp32 pack read here).
+template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH, int X16, int W16 = 0>
 __global__ void __launch_bounds__(256)
 conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
+  static_assert(!W16 || (!prec::has_lo<PM>() && BK == 32), "pre-split weights: one-plane modes, 32-channel chunks");
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int LDK = BK + 8;               // bf16 per padded row
   constexpr int LPR = BK / 4;               // float4 per row (global side)
   constexpr int LPRA = X16 ? BK / 8 : LPR;  // A loads per row (16 B each)
+  constexpr int LPRB = W16 ? BK / 8 : LPR;  // B loads per row (16 B each)
   constexpr int A_LOADS = (BM * LPRA + 255) / 256;
-  constexpr int B_LOADS = (BN * LPR + 255) / 256;
-  constexpr int ROWS_PER_PASS = 256 / LPR;
+  constexpr int B_LOADS = (BN * LPRB + 255) / 256;
+  constexpr int ROWS_PER_PASS = 256 / LPRB;
   constexpr int ROWS_PER_PASS_A = 256 / LPRA;
   constexpr int PLANE_A = BM * LDK, PLANE_B = BN * LDK;   // bf16 elements per plane
   // hi (+ lo in bf16x3) planes of A and B.  The one-plane modes drop the lo planes of the 2-tile
@@ -115,7 +123,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     out_off[r] = off;
   }
 
-  const int q = tid % LPR;
+  const int q = tid % LPRB;                 // B: this thread's 16-B slice of a row
   const int qa = tid % LPRA;                // A: this thread's 16-B slice of a row
   int a_nb[A_LOADS], a_bd[A_LOADS], a_bh[A_LOADS], a_bw[A_LOADS];
 #pragma unroll
@@ -143,8 +151,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   // DEPTH 2 (A/B only, measured slower): two register stages, the tiles of step ks + 2 loaded
   // while step ks runs and stored to LDS at the end of step ks + 1; DEPTH 1 (default): one stage
   using RegA = std::conditional_t<X16 != 0, uint4, float4>;   // X16: eight 16-bit words, else four fp32
+  using RegB = std::conditional_t<W16 != 0, uint4, float4>;   // W16: eight hi words, else four fp32
   RegA ra[2][A_LOADS];
-  float4 rb[2][B_LOADS];
+  RegB rb[2][B_LOADS];
 
   // Operands through buffer descriptors (byte offsets are 32-bit: the host checks the sizes).
   // A: per thread and row a fixed base offset of its (nb, bd, bh, bw) voxel + channel quad; a
@@ -156,7 +165,8 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   const __amdgpu_buffer_rsrc_t xrs = make_rsrc(a.x, __builtin_amdgcn_readfirstlane(a.N * a.Di * a.Hi * a.Wi * a.cx * ESA / (a.tmode == 2 ? 2 : 1)));
   // a.tmode (timing-only A/B, MRAGAN_IG_TIMING): 1 — the weight descriptor covers the first half
   // of the packed taps (the rest read as zeros: no memory traffic), 2 — the input's first half
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4 / (a.tmode == 1 ? 2 : 1)));
+  // (the pre-split copy has the fp32 pack's size: hi + lo words per weight)
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W16 ? a.wx3 : a.w, __builtin_amdgcn_readfirstlane(a.k * a.k * a.k * a.ny * a.cx * 4 / (a.tmode == 1 ? 2 : 1)));
   int a_base[A_LOADS];
 #pragma unroll
   for (int i = 0; i < A_LOADS; ++i)
@@ -164,8 +174,10 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   int b_voff[B_LOADS];
 #pragma unroll
   for (int i = 0; i < B_LOADS; ++i) {
-    const int r = tid / LPR + i * ROWS_PER_PASS, n = n0 + r;
-    b_voff[i] = (r < BN && n < a.ny) ? (n * a.cx * 4 + 16 * q) : (int)kOobOffset;
+    const int r = tid / LPRB + i * ROWS_PER_PASS, n = n0 + r;
+    // W16: slice q = 16-channel half (q >> 1) and 8-channel group (q & 1) of the chunk's fragments
+    const int lane_off = W16 ? ((q >> 1) * 32 * a.ny + n * 16 + (q & 1) * 8) * 2 : n * a.cx * 4 + 16 * q;
+    b_voff[i] = (r < BN && n < a.ny) ? lane_off : (int)kOobOffset;
   }
   int kc = ks0 % kchunks, tap0 = ks0 / kchunks;
   int kjw = tap0 % gw.ntap, kjh = (tap0 / gw.ntap) % gh.ntap, kjd = tap0 / gw.ntap / gh.ntap;
@@ -173,7 +185,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   // incrementally — one add per carry level instead of ~25 scalar multiplies per K-step (PMC r04:
   // 21.8 SALU per MFMA in G down1); the deltas are block constants
   const int rs_ = a.cx * ESA, rwo = a.ny * a.cx * 4;                       // one input voxel / weight tap
-  const int dC_t = BK * ESA, dC_w = BK * 4;
+  const int dC_t = BK * ESA, dC_w = W16 ? BK * 4 * a.ny : BK * 4;       // W16: a chunk's fragments span every row
   const int rC_t = (kchunks - 1) * dC_t, rC_w = (kchunks - 1) * dC_w;      // chunk wrap
   const int dW_t = gw.sign * rs_, dW_w = gw.tstep * rwo;
   const int dH_t = gh.sign * a.Wi * rs_, dH_w = gh.tstep * a.k * rwo;
@@ -183,7 +195,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   int dd = gd.sign * kjd, dh = gh.sign * kjh, dw = gw.sign * kjw;
   int toff = (((dd * a.Hi + dh) * a.Wi + dw) * a.cx + kc * BK) * ESA;
   int wso = ((((gd.t0 + gd.tstep * kjd) * a.k + gh.t0 + gh.tstep * kjh) * a.k + gw.t0 + gw.tstep * kjw) * a.ny * a.cx +
-             kc * BK) * 4;
+             kc * BK * (W16 ? a.ny : 1)) * 4;
   auto advance = [&]() __attribute__((always_inline)) {
     toff += dC_t; wso += dC_w;
     if (++kc == kchunks) {
@@ -201,7 +213,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
     }
   };
 
-  auto load_tiles = [&](RegA (&ra_)[A_LOADS], float4 (&rb_)[B_LOADS]) __attribute__((always_inline)) {
+  auto load_tiles = [&](RegA (&ra_)[A_LOADS], RegB (&rb_)[B_LOADS]) __attribute__((always_inline)) {
     const int toffu = __builtin_amdgcn_readfirstlane(toff);
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
@@ -216,11 +228,12 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
       const buf_f32x4 v = buf_load_16b(wrs, b_voff[i], wsou);
-      rb_[i] = make_float4(v.x, v.y, v.z, v.w);
+      if constexpr (W16) rb_[i] = __builtin_bit_cast(uint4, v);
+      else rb_[i] = make_float4(v.x, v.y, v.z, v.w);
     }
     advance();
   };
-  auto store_tiles = [&](int buf, const RegA (&ra_)[A_LOADS], const float4 (&rb_)[B_LOADS]) {
+  auto store_tiles = [&](int buf, const RegA (&ra_)[A_LOADS], const RegB (&rb_)[B_LOADS]) {
     __bf16* st = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < A_LOADS; ++i) {
@@ -231,15 +244,17 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
         } else {
           uint2 hi, lo;
           prec::split4<PM>(ra_[i], hi, lo);
-          *reinterpret_cast<uint2*>(st + r * LDK + 4 * q) = hi;
-          if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * q) = lo;
+          *reinterpret_cast<uint2*>(st + r * LDK + 4 * qa) = hi;      // (LPRA = LPR: qa is the float4 slot)
+          if constexpr (prec::has_lo<PM>()) *reinterpret_cast<uint2*>(st + PLANE_A + r * LDK + 4 * qa) = lo;
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < B_LOADS; ++i) {
-      int r = tid / LPR + i * ROWS_PER_PASS;
-      if (r < BN) {
+      int r = tid / LPRB + i * ROWS_PER_PASS;
+      if constexpr (W16) {
+        if (r < BN) *reinterpret_cast<uint4*>(st + NPL * PLANE_A + r * LDK + 8 * q) = rb_[i];
+      } else if (r < BN) {
         uint2 hi, lo;
         prec::split4<PM>(rb_[i], hi, lo);
         *reinterpret_cast<uint2*>(st + NPL * PLANE_A + r * LDK + 4 * q) = hi;
@@ -457,12 +472,23 @@ size_t conv_igemm_x3_ws_bytes(const IgemmArgs& a, int64_t max_mc, int64_t total_
 }
 
 template <int WM, int WN, int TM, int TN, int BK, int PM, int DEPTH>
-static void launch_x3_pm(const IgemmArgs& a, dim3 grid, int gm, int gn, int ntiles, int splits, hipStream_t st) {
+static void launch_x3_pm(const IgemmArgs& a, dim3 grid, int gm, int gn, int ntiles, int splits, hipStream_t st,
+                         bool w16 = false) {
   if constexpr (prec::has_lo<PM>()) {
     // BK 64 runs the one-plane modes only (the host's use64): two planes would not fit the LDS
     if constexpr (BK != 64)
       hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0>), grid, dim3(256), 0, st, a, gm, gn,
                          ntiles, splits);
+  } else if (w16) {
+    // the pre-split weights (the shell pass, conv_igemm_x3_shell: BK 32, one stage)
+    if constexpr (BK == 32 && DEPTH == 1) {
+      if (a.x16)
+        hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 1, 1>), grid, dim3(256), 0, st, a, gm,
+                           gn, ntiles, splits);
+      else
+        hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 0, 1>), grid, dim3(256), 0, st, a, gm,
+                           gn, ntiles, splits);
+    }
   } else {
     if (a.x16)
       hipLaunchKernelGGL((conv_igemm_x3_kernel<WM, WN, TM, TN, BK, PM, DEPTH, 1>), grid, dim3(256), 0, st, a, gm, gn,
@@ -474,7 +500,7 @@ static void launch_x3_pm(const IgemmArgs& a, dim3 grid, int gm, int gn, int ntil
 }
 
 template <int WM, int WN, int TM, int TN, int BK>
-static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t st) {
+static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t st, bool w16 = false) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   int gm = ceil_div(max_mc, BM), gn = ceil_div(a.ny, BN);
   int ntiles = gm * gn * a.nclass;
@@ -483,24 +509,26 @@ static int launch_x3(const IgemmArgs& a, int64_t max_mc, int splits, hipStream_t
   // 87.6 vs 72.8, D layer 2 28.8 vs 25.2 at N = 4) — the extra 24–32 VGPRs cost occupancy
   static const bool depth1 = getenv("MRAGAN_IG_DEPTH2") == nullptr;
   MRAGAN_PREC_DISPATCH(a.x3, {
-    if (depth1) launch_x3_pm<WM, WN, TM, TN, BK, PM, 1>(a, dim3(ntiles * splits), gm, gn, ntiles, splits, st);
+    if (depth1 || w16) launch_x3_pm<WM, WN, TM, TN, BK, PM, 1>(a, dim3(ntiles * splits), gm, gn, ntiles, splits, st, w16);
     else launch_x3_pm<WM, WN, TM, TN, BK, PM, 2>(a, dim3(ntiles * splits), gm, gn, ntiles, splits, st);
     return check_launch(a.x16 ? "conv_igemm_x3(op16)" : "conv_igemm_x3");
   })
 }
 
 template <int BK>
-static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int cfg, int splits, hipStream_t st) {
+static int dispatch_x3(const IgemmArgs& a, int64_t max_mc, int cfg, int splits, hipStream_t st, bool w16 = false) {
   switch (cfg) {
-    case 0: return launch_x3<2, 2, 2, 2, BK>(a, max_mc, splits, st);
-    case 1: return launch_x3<2, 2, 2, 1, BK>(a, max_mc, splits, st);
-    case 2: return launch_x3<2, 2, 1, 1, BK>(a, max_mc, splits, st);
-    case 3: return launch_x3<4, 1, 2, 1, BK>(a, max_mc, splits, st);
-    default: return launch_x3<4, 1, 1, 1, BK>(a, max_mc, splits, st);
+    case 0: return launch_x3<2, 2, 2, 2, BK>(a, max_mc, splits, st, w16);
+    case 1: return launch_x3<2, 2, 2, 1, BK>(a, max_mc, splits, st, w16);
+    case 2: return launch_x3<2, 2, 1, 1, BK>(a, max_mc, splits, st, w16);
+    case 3: return launch_x3<4, 1, 2, 1, BK>(a, max_mc, splits, st, w16);
+    default: return launch_x3<4, 1, 1, 1, BK>(a, max_mc, splits, st, w16);
   }
 }
 
-// the shell pass of a full k3 s1 transposed conv (see shell_geo): 6 classes, rows = shell outputs
+// the shell pass of a full k3 s1 transposed conv (see shell_geo): 6 classes, rows = shell outputs.
+// In the one-plane modes it reads the pre-split weights the interior brick reads (W16): the fp32
+// pack is then not needed at all, and a caller whose fp32 pack is stale passes none (w = null)
 int conv_igemm_x3_shell(IgemmArgs a, hipStream_t st) {
   a.shell = 1;
   a.nclass = 6;
@@ -508,11 +536,14 @@ int conv_igemm_x3_shell(IgemmArgs a, hipStream_t st) {
   const int64_t max_mc = (int64_t)a.N * O * O;                       // classes 0/1: one plane
   const int64_t total_m = (int64_t)a.N * ((int64_t)O * O * O - (int64_t)(O - 2) * (O - 2) * (O - 2));
   X3Plan pl = x3_plan(a, total_m);
+  const bool w16 = a.wx3 != nullptr && (a.x3 == kPrecBf16 || a.x3 == kPrecF16) && a.cx % 32 == 0;
+  MRAGAN_CHECK_ARG(w16 || a.w, "conv: the shell pass needs the fp32 weight pack (no pre-split copy usable)");
   // no split-K: its reduce would rewrite every output of the grid, not only the shell
-  return a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, 1, st) : dispatch_x3<16>(a, max_mc, pl.cfg, 1, st);
+  return a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, 1, st, w16) : dispatch_x3<16>(a, max_mc, pl.cfg, 1, st);
 }
 
 int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) {
+  MRAGAN_CHECK_ARG(a.w, "conv: this convolution needs the fp32 weight pack (only a pre-split copy was given)");
   MRAGAN_CHECK_ARG(!a.x16 || ((a.x3 == kPrecBf16 || a.x3 == kPrecF16) && a.cx % 32 == 0),
                    "conv (16-bit operand plane): the one-plane modes and multiples of 32 input channels only");
   // operand byte offsets are 32-bit (buffer descriptors)

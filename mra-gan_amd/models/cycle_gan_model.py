@@ -677,6 +677,10 @@ class CycleGANModel(BaseModel):
         ops.set_loss_scale(self.loss_scale)
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
             networks3D.ensure_flat(n)
+        if self._dist:
+            # one gradient buffer per optimizer (G_A + G_B, D_A + D_B): one all-reduce per phase
+            self._grad_groups = (networks3D.group_grads([self.netG_A, self.netG_B]),
+                                 networks3D.group_grads([self.netD_A, self.netD_B]))
         self._prepare_step()
         hG, hD = self._step_hyper[0:6], self._step_hyper[6:12]
         graphed = False
@@ -697,10 +701,10 @@ class CycleGANModel(BaseModel):
             run_D()
         else:
             sync_G = GradSync(self._dist.dist, self._dist.group)
-            sync_G.start([self.netG_A._flat_grad, self.netG_B._flat_grad])
+            sync_G.start([self._grad_groups[0]])         # G_A + G_B: one collective
             run_D()
             sync_D = GradSync(self._dist.dist, self._dist.group)
-            sync_D.start([self.netD_A._flat_grad, self.netD_B._flat_grad])
+            sync_D.start([self._grad_groups[1]])         # D_A + D_B
             sync_G.finish()
             self.optimizer_G.step_dev(hG)
             sync_D.finish()

@@ -236,7 +236,39 @@ def flatten_parameters(net: nn.Module):
     net._flat_param = flat
     net._flat_grad = gflat
     net._flat_ptrs = [p.data_ptr() for p in params]
+    net._grad_group = None
     return flat, gflat
+
+
+def group_grads(nets):
+    """One contiguous gradient buffer for several flattened networks — each net's `_flat_grad` (and
+    its parameters' .grad views) a slice of it, in order — so the data-parallel exchange of an
+    optimizer's networks is ONE all-reduce (G_A + G_B, D_A + D_B; mragan_hip/dist.py).  Returns the
+    buffer; idempotent while the grouping holds, regroups (copying the current gradients) after a
+    network was re-flattened."""
+    buf = getattr(nets[0], "_grad_group", None)
+    if buf is not None:
+        off, ok = 0, True
+        for n in nets:
+            k = n._flat_grad.numel()
+            ok = ok and getattr(n, "_grad_group", None) is buf and n._flat_grad.data_ptr() == buf[off:off + k].data_ptr()
+            off += k
+        if ok and off == buf.numel():
+            return buf
+    total = sum(n._flat_grad.numel() for n in nets)
+    buf = torch.empty(total, device=nets[0]._flat_grad.device, dtype=torch.float32)
+    off = 0
+    for n in nets:
+        k = n._flat_grad.numel()
+        buf[off:off + k].copy_(n._flat_grad)
+        n._flat_grad = buf[off:off + k]
+        n._grad_group = buf
+        o = 0
+        for p in n.parameters():
+            p.grad = n._flat_grad[o:o + p.numel()].view_as(p)
+            o += p.numel()
+        off += k
+    return buf
 
 
 def ensure_flat(net: nn.Module):

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (torch must be loaded first: the .so resolves libamd
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MRAGAN_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmragan_hip.so"))
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -113,6 +113,8 @@ SIGNATURES = {
                                            vp, sz, vp, vp]),
     "mragan_instnorm_bwd_partials": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, vp, vp, i32, vp, sz,
                                            vp]),
+    # ABI 19: the interior + shell data-gradient rule as a query
+    "mragan_conv3d_dgrad_split": (i32, [i32] * 6),
     "mragan_conv3d_presplit_bwd_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, i32,
                                                i32, vp, sz, vp, vp, vp, i32, vp, sz, vp, vp]),
 }

@@ -35,26 +35,23 @@ _NO_SKIP_STATS = __import__("os").environ.get("MRAGAN_NO_SKIP_STATS") is not Non
 # A/B: skip statistics only up to this batch (the N = 4 data gradient runs the 8-wave brick, whose
 # statistics epilogue costs ≈ 5 µs, r05ba)
 _SKIP_STATS_MAXN = int(__import__("os").environ.get("MRAGAN_SKIP_STATS_MAXN", "0") or "0")
-_SPLIT_ENV = __import__("os").environ.get("MRAGAN_DGRAD_SPLIT")
 # conv2's data gradient where the split runs: plain (split) + IN1's statistics pass, not the
 # backward-statistics brick (128³ step 29.10 / 29.02 vs 29.52 / 29.30 ms, r05bi); A/B switch
 _IN1_STATS_BIG = __import__("os").environ.get("MRAGAN_IN1_STATS_BIG") is not None
 
 
-def _dgrad_split(N, D, H, W):
-    """Mirror of conv_igemm.hip full_dgrad_split_applicable's size rule (a superset of its
-    conditions): for N ≥ 2 at 24³ / 32³ (multiples of 8 from 24) the plain ResnetBlock data
-    gradient runs as interior brick + shell
-    pass (faster than any whole-grid brick there, and than the backward-statistics brick plus the
-    saved statistics pass: 128³ step 29.07 / 29.10 ms with it against 29.40 / 29.44 with the
-    statistics brick, r05bg).  The shell pass reads the conv's fp32 data-gradient pack, which the
-    per-step repack skips for the brick convs: ConvLayer.fresh_fp32_bwd refreshes it first.  The skip
+def _dgrad_split(N, D, H, W, C):
+    """Scheduling hint, not a correctness rule: where conv_igemm.hip full_dgrad_split_applicable
+    runs the plain ResnetBlock data gradient as interior brick + shell pass (N ≥ 2 at 24³ / 32³,
+    multiples of 8 from 24; faster than any whole-grid brick there, and than the backward-statistics
+    brick plus the saved statistics pass: 128³ step 29.07 / 29.10 ms with it against 29.40 / 29.44
+    with the statistics brick, r05bg), the engine asks for the plain data gradient and runs the
+    statistics pass.  Both passes read the pre-split weights (ABI 19), so a disagreement with the C
+    rule would cost time, never correctness — and there is none: the library's rule is queried
+    (mragan_conv3d_dgrad_split, which also honours MRAGAN_DGRAD_SPLIT).  The skip
     statistics (ABI 18) are used below 32³ only: at 1 × 32³ too the statistics brick (K-split, large
     grid) costs about what the statistics pass saves (r05bh: 29.12 / 29.22 vs 29.08 / 29.07 ms)."""
-    if _SPLIT_ENV is not None:
-        return _SPLIT_ENV not in ("", "0")
-    return (N >= 2 and D >= 24 and D % 8 == 0 and H % 8 == 0 and W % 8 == 0
-            and ops.get_conv_precision() in ("bf16", "fp16"))
+    return ops.dgrad_split(N, D, H, W, C, C)
 # A/B switch: MRAGAN_NO_OP16=1 keeps the ResnetBlock tensors fp32 in the bf16 / fp16 modes (no
 # 16-bit operand planes, ABI 11)
 _NO_OP16 = bool(int(__import__("os").environ.get("MRAGAN_NO_OP16", "0") or "0"))
@@ -70,8 +67,7 @@ _IN_FIN = ops.in_tickets_enabled()
 # A/B switch: MRAGAN_FP32_PACKS=1 refreshes the fp32 packs of the brick convs in every mode
 _FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") or "0"))
                # the library's A/B switches that send those convs to the fp32-pack kernels
-               or any(v in __import__("os").environ for v in ("MRAGAN_NO_BRICK", "MRAGAN_BRICK_STAGED",
-                                                              "MRAGAN_DGRAD_SPLIT")))
+               or any(v in __import__("os").environ for v in ("MRAGAN_NO_BRICK", "MRAGAN_BRICK_STAGED")))
 
 IN_MOMENTUM = 0.1
 
@@ -92,10 +88,23 @@ class ConvLayer:
         self.op = getattr(module, "output_padding", 0)
         self.cin = module.in_channels
         self.cout = module.out_channels
-        self.wp_fwd: Optional[torch.Tensor] = None
-        self.wp_bwd: Optional[torch.Tensor] = None
+        self._wp_fwd: Optional[torch.Tensor] = None     # fp32 packs [t][Cout][Cin] / [t][Cin][Cout]
+        self._wp_bwd: Optional[torch.Tensor] = None
         self.ws_fwd: Optional[torch.Tensor] = None      # bf16x3 pre-split copies (brick convs only)
         self.ws_bwd: Optional[torch.Tensor] = None
+        self.fp32_stale = False                         # the fp32 packs were not refreshed (packs())
+
+    # The fp32 packs as the kernels may see them: None while stale (ABI 19 — the library then refuses
+    # every kernel that would read them, instead of computing with old weights; r05final2's garbage
+    # 128³ gradients were a stale pack read by the interior + shell data gradient's shell pass, which
+    # now stages the pre-split copy like the interior brick)
+    @property
+    def wp_fwd(self) -> Optional[torch.Tensor]:
+        return None if self.fp32_stale else self._wp_fwd
+
+    @property
+    def wp_bwd(self) -> Optional[torch.Tensor]:
+        return None if self.fp32_stale else self._wp_bwd
 
     @staticmethod
     def _splittable(k, s, ny, C):
@@ -106,15 +115,15 @@ class ConvLayer:
         """The two packs of this layer as (src, A, B, T, transpose_ab, dst) (buffers allocated)."""
         w = self.m.weight.data
         T = self.k ** 3
-        if self.wp_fwd is None or self.wp_fwd.device != w.device:
-            self.wp_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
-            self.wp_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+        if self._wp_fwd is None or self._wp_fwd.device != w.device:
+            self._wp_fwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
+            self._wp_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
         if not self.transposed:     # torch [Cout][Cin][t]
-            out = [(w, self.cout, self.cin, T, False, self.wp_fwd),      # [t][Cout][Cin]
-                   (w, self.cout, self.cin, T, True, self.wp_bwd)]       # [t][Cin][Cout]
+            out = [(w, self.cout, self.cin, T, False, self._wp_fwd),     # [t][Cout][Cin]
+                   (w, self.cout, self.cin, T, True, self._wp_bwd)]      # [t][Cin][Cout]
         else:
-            out = [(w, self.cin, self.cout, T, True, self.wp_fwd),       # torch [Cin][Cout][t] → [t][Cout][Cin]
-                   (w, self.cin, self.cout, T, False, self.wp_bwd)]      # [t][Cin][Cout]
+            out = [(w, self.cin, self.cout, T, True, self._wp_fwd),      # torch [Cin][Cout][t] → [t][Cout][Cin]
+                   (w, self.cin, self.cout, T, False, self._wp_bwd)]     # [t][Cin][Cout]
         # pre-split 16-bit fragment copies for the brick kernel, refreshed by the same pack launch
         # (tr 2|3: bf16 hi/lo — the bf16x3 and bf16 modes; tr 4|5: fp16 — the fp16 mode)
         (_, A, B, _, tf, _), (_, _, _, _, tb, _) = out
@@ -130,24 +139,15 @@ class ConvLayer:
             if self.ws_bwd is None or self.ws_bwd.device != w.device:
                 self.ws_bwd = torch.empty(w.numel(), device=w.device, dtype=torch.float32)
             out.append((w, A, B, T, base + int(tb), self.ws_bwd))
-        self.fp32_bwd_stale = False
+        self.fp32_stale = False
         if prec != "f32" and split_f and split_b and not self.transposed and not _FP32_PACKS:
-            # the MFMA-mode brick kernels read only the pre-split copies of a k3 s1 ResnetBlock
-            # conv (forward and data gradient): its two fp32 packs are not refreshed (the repack
-            # moves half the bytes; a mode switch repacks, ensure_packed) — except the data-gradient
-            # pack where the interior + shell split runs (fresh_fp32_bwd)
-            self.fp32_bwd_stale = True
+            # the MFMA-mode kernels of a k3 s1 ResnetBlock conv (the bricks both ways, the interior +
+            # shell data gradient) read only its pre-split copies: the two fp32 packs are not
+            # refreshed (the repack moves half the bytes; a mode switch repacks, ensure_packed) and
+            # are not handed to the library while stale (wp_fwd / wp_bwd are None)
+            self.fp32_stale = True
             out = out[2:]
         return out
-
-    def fresh_fp32_bwd(self):
-        """Refresh the fp32 data-gradient pack before a data gradient that may run the interior +
-        shell split (its shell pass reads it): once per repack, on the stream of the first such use
-        (captured into the step graph with it)."""
-        if getattr(self, "fp32_bwd_stale", False):
-            w = self.m.weight.data
-            ops.pack_weight(w, self.cout, self.cin, self.k ** 3, True, self.wp_bwd)
-            self.fp32_bwd_stale = False
 
     def repack(self):
         for src, A, B, T, tr, dst in self.packs():
@@ -226,13 +226,14 @@ class ConvLayer:
                                                     part)
         return dz, part, chunks, None
 
-    def dgrad_op16_in_stats_add(self, dy16, norm_x, mean, rstd, act, add):
+    def dgrad_op16_in_stats_add(self, dy16, norm_x, mean, rstd, act, add, fin=True):
         """dgrad_op16_in_stats for an InstanceNorm whose backward input is fold(dz) + add (ABI 18):
         conv1 of ResnetBlock i+1, whose input gradient meets block i+1's output gradient G (the
-        skip path) at block i's second IN.  Returns (dz, part, chunks, coef) as dgrad_op16_in_stats."""
+        skip path) at block i's second IN.  Returns (dz, part, chunks, coef) as dgrad_op16_in_stats;
+        fin=False when the consumer cannot take finalized coefficients (coef is then None)."""
         N, D, H, W, _ = dy16.shape
         part = ops.in_partials_buffer(N, (D + 2, H + 2, W + 2), self.cin, dy16.device)
-        if _IN_FIN:
+        if _IN_FIN and fin:
             dz, chunks, coef = ops.conv3d_op16_dgrad_in_stats(dy16, self.wp_bwd, self.cin, self.ws_bwd, norm_x, mean,
                                                               rstd, act, part, fin=True, x_add=add)
             return dz, part, chunks, coef
@@ -512,6 +513,30 @@ class NetPlan:
         ctx.out = cur
         return ctx
 
+    def _in_bwd_plane_paths(self, st, sc):
+        """(plane_bwd, plane_bwd_fwd, stem16): which 16-bit-plane backward a non-block stage with an
+        InstanceNorm takes (all False otherwise) — its IN backward then writes dY only as the plane
+        (and can take coefficients finalized in the producing launch).
+        plane_bwd — G up1 / up2 (ABI 16): the data gradient (forward-form implicit GEMM) and the
+        weight gradient (its gathered operand) read the plane;
+        plane_bwd_fwd — G down1 / down2 (inputs only planes already): the weight gradient reads both
+        planes, the data gradient (transposed implicit GEMM, or brickT for down1's 32 output
+        channels) dY's;
+        stem16 — the G stem (k7, nc → 32; ABI 17): its weight and data gradient (thinn_x3) read it."""
+        if st.kind == "block" or st.norm is None:
+            return False, False, False
+        conv = st.conv
+        op16 = self._op16_active()
+        x_any = sc.inp if sc.inp is not None else sc.inp16
+        plane_bwd = (x_any is not None and conv.transposed_plane_bwd_ok(x_any.shape[3])
+                     and op16 and not _NO_S2_PLANES and not st.use_bias)
+        plane_bwd_fwd = (sc.inp is None and sc.inp16 is not None and not st.use_bias
+                         and not conv.transposed and conv.s2_plane_ok(sc.inp16.shape[3])
+                         and (conv.cin != 32 or _BRICKT_PLANES) and op16 and not _NO_S2_PLANES)
+        stem16 = (not plane_bwd and not plane_bwd_fwd and sc.inp is not None and op16 and conv.cout == 32
+                  and conv.k7_wide16_ok())
+        return plane_bwd, plane_bwd_fwd, stem16
+
     def _op16_active(self):
         """16-bit operand planes for the ResnetBlock section: bf16 / fp16 mode, not switched off."""
         return not _NO_OP16 and ops.op16_dtype() is not None
@@ -528,21 +553,23 @@ class NetPlan:
         accumulated into the parameters' flat grad buffers.  Returns dL/dx (NDHWC) when
         need_input_grad (written to dx_out, plus dx_add if given)."""
         g, gpad, gadd = None, 0, None
-        bstats = None            # (part, chunks): backward statistics of the next IN, from the dgrad epilogue
+        # (part, chunks, coef): backward statistics of the next IN from a data-gradient epilogue; coef =
+        # its coefficients when that launch finalized them (ABI 15), else None
+        bstats = None
         last = len(self.stages) - 1
         for i in range(last, -1, -1):
             st, sc = self.stages[i], ctx.stages[i]
             want_dgrad = i > 0 or need_input_grad
             if st.kind == "block" and sc.inp16 is not None:
                 # 16-bit operand planes: the IN backwards write dY only as planes (the convs' sole use)
-                skip = bstats if (bstats is not None and len(bstats) == 3 and gpad == 1 and gadd is not None) else None
+                skip = bstats if (bstats is not None and gpad == 1 and gadd is not None) else None
                 own = bstats if (bstats is not None and gpad == 0 and gadd is None) else None
                 bstats = None
                 if gpad == 0 and gadd is None:
                     G = g
                     if own is not None:      # statistics from G up1's data-gradient epilogue
                         dh2 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, G, 0, None, None, *own[:2],
-                                                             coef=own[2] if len(own) > 2 else None)
+                                                             coef=own[2])
                     else:
                         dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, G, 0, None, act=None)
                 elif skip is not None:
@@ -556,8 +583,7 @@ class NetPlan:
                 if need_wgrad:
                     st.conv2.wgrad_op16(sc.z1, dh2)
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
-                if not _IN1_STATS_BIG and _dgrad_split(*dh2.shape[:4]):
-                    st.conv2.fresh_fp32_bwd()
+                if not _IN1_STATS_BIG and _dgrad_split(*dh2.shape):
                     dz1, part, chunks, coef = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4]), None, 0, None
                 else:
                     dz1, part, chunks, coef = st.conv2.dgrad_op16_in_stats(dh2, sc.h1, sc.mean1, sc.rstd1, "relu")
@@ -575,17 +601,22 @@ class NetPlan:
                     (nxt.kind == "block" and nsc.inp16 is not None)
                     or (nxt.kind != "block" and nxt.norm is not None and nsc.h is not None
                         and tuple(nsc.h.shape) == tuple(G.shape)))
-                if (skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS and dh1.shape[1] < 32
-                        and not _dgrad_split(*dh1.shape[:4])
+                # (measured below 32³ only, DESIGN §4: gated on the voxel count, so a 16 × 64 × 64 block
+                # takes the statistics pass like a 32³ one — ADVICE r05)
+                if (skip_in and not _NO_IN_STATS and not _NO_SKIP_STATS
+                        and dh1.shape[1] * dh1.shape[2] * dh1.shape[3] < 32 ** 3
+                        and not _dgrad_split(*dh1.shape)
                         and (_SKIP_STATS_MAXN <= 0 or dh1.shape[0] <= _SKIP_STATS_MAXN)):
                     # conv1's data gradient also accumulates that IN's backward statistics, with this
                     # block's output gradient G joining at the skip (ABI 18)
                     act_in = None if nxt.kind == "block" else nxt.act
-                    g, part, chunks, coef = st.conv1.dgrad_op16_in_stats_add(dh1, nsc.h, nsc.mean, nsc.rstd, act_in, G)
+                    # finalized coefficients only for a consumer with an apply-only entry (the plane
+                    # IN backwards): the fp32 one reduces the partials itself
+                    fin = nxt.kind == "block" or any(self._in_bwd_plane_paths(nxt, nsc))
+                    g, part, chunks, coef = st.conv1.dgrad_op16_in_stats_add(dh1, nsc.h, nsc.mean, nsc.rstd, act_in, G,
+                                                                             fin=fin)
                     bstats = (part, chunks, coef) if chunks else None
                 else:
-                    if _dgrad_split(*dh1.shape[:4]):
-                        st.conv1.fresh_fp32_bwd()
                     g = st.conv1.dgrad_op16(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue
@@ -600,36 +631,21 @@ class NetPlan:
                     dh2 = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
                     st.conv2.wgrad(sc.z1, dh2)
-                if _dgrad_split(*dh2.shape[:4]):     # the split's shell pass reads the fp32 pack
-                    st.conv2.fresh_fp32_bwd()
                 dz1 = st.conv2.dgrad(dh2, sc.z1.shape[1:4])
                 dh1 = ops.instnorm_bwd(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
                     st.conv1.wgrad(sc.inp, dh1)
-                if _dgrad_split(*dh1.shape[:4]):
-                    st.conv1.fresh_fp32_bwd()
                 g = st.conv1.dgrad(dh1, sc.inp.shape[1:4])
                 gpad, gadd = 1, G
                 continue
             conv = st.conv
-            # G up1 / up2 in the one-plane modes (ABI 16): the IN backward writes dY only as its plane;
-            # the data gradient (forward-form implicit GEMM) and the weight gradient (its gathered
-            # operand) read the plane — neither needs the fp32 tensor
             x_any = sc.inp if sc.inp is not None else sc.inp16
-            plane_bwd = (st.norm is not None and x_any is not None and conv.transposed_plane_bwd_ok(x_any.shape[3])
-                         and self._op16_active() and not _NO_S2_PLANES and not st.use_bias)
-            # G down1 / down2 (their inputs only planes already): dY as a plane too — the weight
-            # gradient reads both planes, the data gradient (transposed implicit GEMM, or brickT for
-            # down1's 32 output channels) dY's
-            plane_bwd_fwd = (st.norm is not None and sc.inp is None and sc.inp16 is not None and not st.use_bias
-                             and not conv.transposed and conv.s2_plane_ok(sc.inp16.shape[3])
-                             and (conv.cin != 32 or _BRICKT_PLANES)
-                             and self._op16_active() and not _NO_S2_PLANES)
+            plane_bwd, plane_bwd_fwd, stem16 = self._in_bwd_plane_paths(st, sc)
             dh16 = None
             if plane_bwd or plane_bwd_fwd:
                 if bstats is not None:
                     dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2],
-                                                          coef=bstats[2] if len(bstats) > 2 else None)
+                                                          coef=bstats[2])
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
                 in_spatial = x_any.shape[1:4]
@@ -654,19 +670,18 @@ class NetPlan:
                                                                in_spatial, nsc.h, nsc.mean, nsc.rstd,
                                                                None if blk_in else nxt.act, part,
                                                                transposed=not conv.transposed)
-                        bstats = (part, bchunks) if bchunks else None
+                        bstats = (part, bchunks, None) if bchunks else None
                     else:
                         g = ops.conv3d_op16(dh16, conv.wp_bwd, conv.cin, conv.k, conv.s, conv.p, in_spatial, None,
                                             transposed=not conv.transposed)[0]
                     gpad, gadd = st.prepad, None
                 continue
-            if (st.norm is not None and sc.inp is not None and self._op16_active() and conv.cout == 32
-                    and conv.k7_wide16_ok()):
+            if stem16:
                 # the G stem (k7, nc → 32; ABI 17): its IN backward writes dx only as the plane — the
                 # stem's weight gradient and data gradient (thinn_x3) are its only readers
                 if bstats is not None:
                     dh16 = ops.instnorm_bwd_partials_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2],
-                                                          coef=bstats[2] if len(bstats) > 2 else None)
+                                                          coef=bstats[2])
                 else:
                     dh16 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
                 bstats = None
@@ -679,6 +694,7 @@ class NetPlan:
                 continue
             if st.norm is not None:
                 if bstats is not None:
+                    # (no coefficients were asked for: this entry reduces the partials itself)
                     dh = ops.instnorm_bwd_partials(sc.h, sc.mean, sc.rstd, g, gpad, gadd, st.act, *bstats[:2])
                 else:
                     dh = ops.instnorm_bwd(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=st.act)
@@ -709,14 +725,14 @@ class NetPlan:
                     nsc = ctx.stages[i - 1]
                     g, bpart, bchunks = conv.dgrad_in_stats(dh, in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act,
                                                             st.prepad)
-                    bstats = (bpart, bchunks) if bchunks else None
+                    bstats = (bpart, bchunks, None) if bchunks else None
                 elif (nxt is not None and nxt.kind != "block" and nxt.norm is not None and not st.prepad
                         and conv.dgrad_bwd_stats_ok()):
                     # stride-2 layers: the data gradient's epilogue accumulates the next IN's
                     # backward statistics (no fold: that IN's output is this conv's input)
                     nsc = ctx.stages[i - 1]
                     g, bpart, bchunks = conv.dgrad_bwd_stats(dh, in_spatial, nsc.h, nsc.mean, nsc.rstd, nxt.act)
-                    bstats = (bpart, bchunks) if bchunks else None
+                    bstats = (bpart, bchunks, None) if bchunks else None
                 else:
                     g = conv.dgrad(dh, in_spatial)
                 gpad, gadd = st.prepad, None

@@ -21,6 +21,19 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def _check_weights(wp: Optional[torch.Tensor], wsplit: Optional[torch.Tensor], n: int, what: str):
+    """The packed weight (n fp32 elements) and / or its pre-split copy (n·4 bytes).  wp may be None
+    when wsplit is given (ABI 19): the caller's fp32 pack is stale (only the pre-split copy is
+    refreshed for a ResnetBlock conv in the one-plane modes), and the library then refuses any
+    kernel that would read the fp32 pack instead of reading stale weights."""
+    if wp is None and wsplit is None:
+        raise ValueError(f"{what}: neither the packed weight nor its pre-split copy given")
+    if wp is not None and wp.numel() != n:
+        raise ValueError(f"{what}: packed weight has {wp.numel()} elements, expected {n}")
+    if wsplit is not None and wsplit.numel() * wsplit.element_size() != n * 4:
+        raise ValueError(f"{what}: wsplit size does not match the packed weight")
+
+
 def _check(t: torch.Tensor, name: str, ndim: int = 5):
     if not t.is_cuda:
         raise ValueError(f"{name}: expected a device tensor (HIP); got {t.device}")
@@ -182,8 +195,7 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     _check(x, "conv3d.x")
     N, Di, Hi, Wi, cin = x.shape
     Do, Ho, Wo = out_spatial
-    if wp.numel() != k ** 3 * cin * cout:
-        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
+    _check_weights(wp, wsplit, k ** 3 * cin * cout, "conv3d")
     if out is None:
         out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
     elif tuple(out.shape) != (N, Do, Ho, Wo, cout):
@@ -192,8 +204,6 @@ def conv3d(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int,
     nbytes = query("mragan_conv3d_workspace", N, Di, Hi, Wi, cin, cout, k, s, p, Do, Ho, Wo, int(transposed))
     ws = WS.get(nbytes) if nbytes else None
     if wsplit is not None:
-        if wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-            raise ValueError("conv3d: wsplit size does not match the packed weight")
         fn = lambda: call("mragan_conv3d_presplit", _ptr(x), N, Di, Hi, Wi, cin, _ptr(wp), _ptr(wsplit), _ptr(bias),
                           cout, k, s, p, ACT[act], _ptr(out), Do, Ho, Wo, int(transposed), _ptr(ws), nbytes, _stream())
     else:
@@ -271,10 +281,7 @@ def conv3d_in_stats(x: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int
     _check(x, "conv3d.x")
     N, Di, Hi, Wi, cin = x.shape
     Do, Ho, Wo = out_spatial
-    if wp.numel() != k ** 3 * cin * cout:
-        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
-    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-        raise ValueError("conv3d: wsplit size does not match the packed weight")
+    _check_weights(wp, wsplit, k ** 3 * cin * cout, "conv3d_in_stats")
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("conv3d_in_stats: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x.device, dtype=torch.float32)
@@ -510,6 +517,20 @@ def _instnorm_apply_op16(x, act, ypad, resid, rpad, want_f32, stats):
     return out, out16, mean, rstd
 
 
+_SPLIT_CACHE = {}
+
+
+def dgrad_split(N: int, D: int, H: int, W: int, cin: int, cout: int) -> bool:
+    """Does the whole-grid k3 s1 data gradient from the plane of dY [N, D, H, W, cin] (→ cout
+    channels on the padded grid) run as interior brick + shell pass in the current mode?  The
+    library's own rule (mragan_conv3d_dgrad_split, ABI 19), cached per shape and mode."""
+    key = (N, D, H, W, cin, cout, get_conv_precision())
+    v = _SPLIT_CACHE.get(key)
+    if v is None:
+        v = _SPLIT_CACHE[key] = bool(query("mragan_conv3d_dgrad_split", N, D, H, W, cin, cout))
+    return v
+
+
 def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, p: int, out_spatial: Sequence[int],
                 wsplit: torch.Tensor, part: Optional[torch.Tensor] = None, transposed: bool = False, fin: bool = False):
     """conv3d (pre-split weights if any, no bias / act) on the operand plane x16 of its input (the
@@ -521,10 +542,7 @@ def conv3d_op16(x16: torch.Tensor, wp: torch.Tensor, cout: int, k: int, s: int, 
     _check16(x16, "conv3d_op16.x16")
     N, Di, Hi, Wi, cin = x16.shape
     Do, Ho, Wo = out_spatial
-    if wp.numel() != k ** 3 * cin * cout:
-        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
-    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-        raise ValueError("conv3d_op16: wsplit size does not match the packed weight")
+    _check_weights(wp, wsplit, k ** 3 * cin * cout, "conv3d_op16")
     if part is not None and (part.dtype != torch.float64 or not part.is_cuda):
         raise ValueError("conv3d_op16: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
@@ -542,10 +560,7 @@ def _conv3d_op16_fin(x16, wp, cout, k, s, p, out_spatial, wsplit, part, transpos
     _check16(x16, "conv3d_op16.x16")
     N, Di, Hi, Wi, cin = x16.shape
     Do, Ho, Wo = out_spatial
-    if wp.numel() != k ** 3 * cin * cout:
-        raise ValueError(f"conv3d: packed weight has {wp.numel()} elements, expected {k**3}x{cout}x{cin}")
-    if wsplit is not None and wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-        raise ValueError("conv3d_op16: wsplit size does not match the packed weight")
+    _check_weights(wp, wsplit, k ** 3 * cin * cout, "conv3d_op16")
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("conv3d_op16: part must be a float64 device tensor")
     out = torch.empty((N, Do, Ho, Wo, cout), device=x16.device, dtype=torch.float32)
@@ -582,8 +597,9 @@ def conv3d_op16_dgrad_in_stats(dy16: torch.Tensor, wp: torch.Tensor, cout: int, 
         _check(x_add, "dgrad_in_stats.x_add")
         if tuple(x_add.shape) != tuple(x_in.shape):
             raise ValueError(f"dgrad_in_stats: x_add shape {tuple(x_add.shape)} != {tuple(x_in.shape)}")
-    if wp.numel() != 27 * cin * cout or wsplit.numel() * wsplit.element_size() != wp.numel() * 4:
-        raise ValueError("dgrad_in_stats: packed / pre-split weight size mismatch")
+    if wsplit is None:
+        raise ValueError("dgrad_in_stats: the pre-split weight is required")
+    _check_weights(wp, wsplit, 27 * cin * cout, "dgrad_in_stats")
     if part.dtype != torch.float64 or not part.is_cuda:
         raise ValueError("dgrad_in_stats: part must be a float64 device tensor")
     osp = (Di + 2, Hi + 2, Wi + 2)

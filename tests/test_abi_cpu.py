@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
     assert set(header_functions()) == set(mragan_hip.exported_symbols())
-    assert lib.mragan_abi_version() == 18
+    assert lib.mragan_abi_version() == 19
 
 
 def test_library_built_for_gfx950():
@@ -50,6 +50,26 @@ def test_bad_args_reported_without_gpu():
     from mragan_hip._lib import MraganError, call
     with pytest.raises(MraganError, match="null pointer"):
         call("mragan_conv3d_fwd", None, 1, 4, 4, 4, 8, None, None, 8, 3, 1, 1, 0, None, 4, 4, 4, None, 0, None)
+
+
+def test_dgrad_split_rule_query():
+    """ABI 19: the interior + shell data-gradient rule is the library's (host-side, no GPU), and the
+    engine schedules by the same query — there is no mirrored copy to drift.  Split for N ≥ 2 at
+    24³ / 32³ in the one-plane modes; never at 16³, at N = 1, or in the fp32-grade modes."""
+    import mragan_hip
+    from mragan_hip import engine, ops
+    lib = mragan_hip.lib()
+    try:
+        for prec in ("bf16", "fp16"):
+            ops.set_conv_precision(prec)
+            for N, S, want in [(2, 32, 1), (2, 24, 1), (4, 24, 1), (4, 16, 0), (2, 16, 0), (1, 32, 0), (2, 28, 0)]:
+                assert lib.mragan_conv3d_dgrad_split(N, S, S, S, 128, 128) == want, (prec, N, S)
+                assert engine._dgrad_split(N, S, S, S, 128) == bool(want)
+        for prec in ("f32", "bf16x3"):
+            ops.set_conv_precision(prec)
+            assert lib.mragan_conv3d_dgrad_split(2, 32, 32, 32, 128, 128) == 0
+    finally:
+        ops.set_conv_precision("f32")
 
 
 def _build(name):

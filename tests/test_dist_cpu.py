@@ -87,3 +87,34 @@ def test_no_sync_without_process_group():
     if dist.is_initialized():
         pytest.skip("a process group is already initialised")
     assert default_sync() is None
+
+
+def test_group_grads_one_buffer_per_optimizer():
+    """DP exchanges one buffer per optimizer (G_A + G_B, D_A + D_B):
+    networks3D.group_grads makes each net's flat gradient (and its .grad views) a slice of one
+    contiguous buffer, keeps the current gradients, is idempotent, and regroups after a net is
+    re-flattened."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "mra-gan_amd")]
+    from models import networks3D as N3
+    torch.manual_seed(0)
+    nets = [N3.ResnetGenerator(1, 1, 4, norm_layer=N3.get_norm_layer("instance"), n_blocks=2) for _ in range(2)]
+    for n in nets:
+        N3.flatten_parameters(n)
+        n._flat_grad.normal_()
+    before = [n._flat_grad.clone() for n in nets]
+    buf = N3.group_grads(nets)
+    assert buf.numel() == sum(b.numel() for b in before)
+    assert torch.equal(buf, torch.cat(before))
+    p0 = next(nets[1].parameters())
+    p0.grad.fill_(7.0)                      # a .grad view writes into the shared buffer
+    off = nets[0]._flat_grad.numel()
+    assert float(buf[off]) == 7.0
+    assert N3.group_grads(nets) is buf      # idempotent
+    for n in nets:
+        assert not N3.ensure_flat(n)        # the grouping keeps the parameter storage
+    assert N3.group_grads(nets) is buf
+    N3.flatten_parameters(nets[0])          # re-flattened: a new, regrouped buffer
+    buf2 = N3.group_grads(nets)
+    assert buf2 is not buf and nets[0]._flat_grad.data_ptr() == buf2.data_ptr()

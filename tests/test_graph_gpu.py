@@ -12,7 +12,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(tmp_path, graph, steps, precision, batches=None, extra=(), size=24):
+def _run(tmp_path, graph, steps, precision, batches=None, extra=(), size=24, nc=1):
     from models import create_model
     from options.train_options import TrainOptions
     argv = sys.argv
@@ -34,8 +34,8 @@ def _run(tmp_path, graph, steps, precision, batches=None, extra=(), size=24):
     losses = []
     for step in range(steps):
         b = batches[step] if batches else 2
-        A = torch.randn(b, 1, size, size, size, generator=g)
-        B = torch.randn(b, 1, size, size, size, generator=g)
+        A = torch.randn(b, nc, size, size, size, generator=g)
+        B = torch.randn(b, nc, size, size, size, generator=g)
         model.set_input([A, B])
         model.optimize_parameters()
         losses.append(torch.stack([getattr(model, "loss_" + n).detach().clone() for n in model.loss_names]))
@@ -123,3 +123,68 @@ def test_stride2_planes_bit_identical(tmp_path, precision, monkeypatch):
         assert torch.equal(sr[k], sp[k]), k
     for k in vr:
         assert torch.equal(vr[k], vp[k]), k
+
+
+# the dispatch the bench times (BASELINE configs[1]: resnet_9blocks, ngf 32, 64³ b2, two lanes) and
+# configs[4]'s per-GPU unit (96³ nc2 b1 fp16: its first passes run N = 2 at the 24³ level — the
+# interior + shell data gradient)
+HEADLINE = ["--netG", "resnet_9blocks", "--ngf", "32", "--ndf", "32"]
+HEADLINE_CASES = [("bf16", 64, 2, 1), ("fp16", 64, 2, 1), ("fp16", 96, 1, 2)]
+
+
+@pytest.mark.parametrize("precision,size,batch,nc", HEADLINE_CASES,
+                         ids=[f"{p}-{s}-b{b}-nc{c}" for p, s, b, c in HEADLINE_CASES])
+def test_graph_step_bit_identical_headline(tmp_path, precision, size, batch, nc, monkeypatch):
+    """the replayed two-lane step at the BASELINE sizes is the eager step, bit
+    for bit, over 3 steps (the eager step 0 is what tests/test_step_gpu.py gates against the oracle;
+    steps 1-2 replay the capture) — and the dispatch under test is the headline's: counted at the
+    library boundary, the K-split brick's in-launch finalize (ABI 15), the skip-gradient statistics
+    epilogue (ABI 18) and, where the size rule holds, the interior + shell data gradient ran."""
+    from mragan_hip import ops
+    seen = {"fin": 0, "skip_stats": 0, "split": 0}
+    op16, fin16, st16 = ops.conv3d_op16, ops._conv3d_op16_fin, ops.conv3d_op16_dgrad_in_stats
+
+    def fin_w(*a, **kw):
+        r = fin16(*a, **kw)
+        seen["fin"] += r[2] is not None
+        return r
+
+    def op16_w(x16, wp, cout, k, s, p, osp, wsplit, part=None, transposed=False, fin=False):
+        if transposed and k == 3 and s == 1 and ops.dgrad_split(*x16.shape, cout):
+            seen["split"] += 1
+        return op16(x16, wp, cout, k, s, p, osp, wsplit, part=part, transposed=transposed, fin=fin)
+
+    def st_w(*a, x_add=None, **kw):
+        r = st16(*a, x_add=x_add, **kw)
+        seen["skip_stats"] += x_add is not None and r[1] > 0
+        return r
+
+    monkeypatch.setattr(ops, "_conv3d_op16_fin", fin_w)
+    monkeypatch.setattr(ops, "conv3d_op16", op16_w)
+    monkeypatch.setattr(ops, "conv3d_op16_dgrad_in_stats", st_w)
+    extra = HEADLINE + ["--batch_size", str(batch), "--input_nc", str(nc), "--output_nc", str(nc)]
+    try:
+        le, se, ve, me = _run(tmp_path / "e", False, 3, precision, [batch] * 3, extra, size=size, nc=nc)
+        assert me.parallel_lanes and me._aux_stream is not None
+        del me
+        torch.cuda.empty_cache()
+        eager_seen = dict(seen)
+        lg, sg, vg, mg = _run(tmp_path / "g", True, 3, precision, [batch] * 3, extra, size=size, nc=nc)
+        assert mg._graphs is not None and mg._n_captures == 1
+        del mg
+    finally:
+        ops.set_conv_precision("f32")
+        ops.set_loss_scale(1.0)
+        torch.cuda.empty_cache()
+    print(f"{precision} {size}³ b{batch} nc{nc}: library paths per eager run {eager_seen}")
+    assert eager_seen["skip_stats"] > 0, eager_seen
+    if size == 64:      # the 16³ level: K-split bricks with the in-launch finalize, no split
+        assert eager_seen["fin"] > 0 and eager_seen["split"] == 0, eager_seen
+    else:               # the 24³ level at N = 2: the interior + shell data gradient
+        assert eager_seen["split"] > 0, eager_seen
+    assert torch.isfinite(le).all()
+    assert torch.equal(le, lg), (le - lg).abs().max()
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+    for k in ve:
+        assert torch.equal(ve[k], vg[k]), k

@@ -660,27 +660,46 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
-@pytest.mark.parametrize("N,S", [(2, 32), (1, 32)])
-def test_op16_res_dgrad_interior_shell(op16, N, S):
-    """The ResnetBlock whole-grid data gradient from 2 × 32³ on runs as the interior brick (the 32³
-    "same" conv written one voxel in) plus the shell pass (conv_igemm.hip full_dgrad_split_applicable;
-    1 × 32³ keeps the whole-grid brick): fp64 on the rounded operands, and bit-identical between the
-    plane and the fp32 input.  (The shell pass reads the fp32 pack: the engine refreshes it,
-    ConvLayer.fresh_fp32_bwd — this test packs it itself.)"""
+@pytest.mark.parametrize("N,S,C", [(2, 32, 128), (1, 32, 128), (4, 24, 128), (2, 24, 64), (2, 16, 128)])
+def test_op16_res_dgrad_interior_shell(op16, N, S, C):
+    """The ResnetBlock whole-grid data gradient for N ≥ 2 at 24³ / 32³ runs as the interior brick (the
+    "same" conv written one voxel in) plus the shell pass (mragan_conv3d_dgrad_split; 1 × 32³ and
+    16³ keep the whole-grid brick): fp64 on the rounded operands, and bit-identical between the plane
+    and the fp32 input.  ABI 19: both passes read only the pre-split weights — the fp32 pack filled
+    with NaN changes nothing, and with no fp32 pack at all (NULL) the result is the same bits."""
     ops = op16
     dt = ops.op16_dtype()
-    C = 128
-    g = torch.Generator().manual_seed(N * 3 + S)
+    g = torch.Generator().manual_seed(N * 3 + S + C)
     w = torch.randn(C, C, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
     wp_b, ws_b = pack(ops, w, False, True), _presplit(ops, w, C, C, True)
+    wp_nan = torch.full_like(wp_b, float("nan"))
     dy = ndhwc(torch.randn(N, C, S, S, S, generator=g).float()).cuda()
     osp = (S + 2,) * 3
-    dx, _ = ops.conv3d_op16(dy.to(dt), wp_b, C, 3, 1, 0, osp, ws_b, transposed=True)
-    dx32 = ops.conv3d(dy, wp_b, C, 3, 1, 0, osp, transposed=True, wsplit=ws_b)
+    assert ops.dgrad_split(N, S, S, S, C, C) == (N >= 2 and S >= 24)
+    dx, _ = ops.conv3d_op16(dy.to(dt), wp_nan, C, 3, 1, 0, osp, ws_b, transposed=True)
+    dx_null, _ = ops.conv3d_op16(dy.to(dt), None, C, 3, 1, 0, osp, ws_b, transposed=True)
+    dx_fresh, _ = ops.conv3d_op16(dy.to(dt), wp_b, C, 3, 1, 0, osp, ws_b, transposed=True)
+    dx32 = ops.conv3d(dy, wp_nan, C, 3, 1, 0, osp, transposed=True, wsplit=ws_b)
     assert torch.isfinite(dx).all()
+    assert torch.equal(dx, dx_null) and torch.equal(dx, dx_fresh)
     assert torch.equal(dx, dx32)
     ref = F.conv_transpose3d(ncdhw(dy.to(dt).double().cpu()), w.float().to(dt).double())
     assert rel(ncdhw(dx.double().cpu()), ref) < 2e-5
+
+
+def test_null_fp32_pack_refused(op16):
+    """ABI 19: a kernel that needs the fp32 pack refuses a NULL one (the caller's pack is stale)
+    instead of computing with whatever the buffer holds: a k3 s1 conv with 32 output channels (no
+    brick shape: the implicit GEMM, which reads the fp32 pack)."""
+    from mragan_hip._lib import MraganError
+    ops = op16
+    C = 32
+    w = torch.randn(C, C, 3, 3, 3, dtype=torch.float64) * 0.05
+    ws = _presplit(ops, w, C, C, False)
+    x = ndhwc(torch.randn(1, C, 8, 8, 8).float()).cuda()
+    with pytest.raises(MraganError, match="fp32 weight pack"):
+        ops.conv3d(x, None, C, 3, 1, 1, (8, 8, 8), wsplit=ws)
+        torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("N,S,act,fin", [(4, 16, None, True), (2, 16, None, True), (2, 16, None, False),
@@ -1461,29 +1480,35 @@ def test_adam_rebias_skipped_steps(ops):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_fresh_fp32_bwd_pack(ops, prec):
-    """The per-step repack skips a ResnetBlock conv's fp32 packs in the one-plane modes (the bricks
-    read the pre-split copies); the split data gradient's shell pass reads the fp32 data-gradient
-    pack, so the engine refreshes it first (ConvLayer.fresh_fp32_bwd): after a repack the flag is
-    set, and the refresh writes exactly the pack the full repack would."""
+def test_stale_fp32_packs_not_exposed(ops, prec):
+    """The per-step repack skips a ResnetBlock conv's fp32 packs in the one-plane modes (its kernels
+    read the pre-split copies): the layer then exposes no fp32 pack (wp_fwd / wp_bwd are None, so no
+    kernel can read the stale buffers — ABI 19), and its forward and data gradient still run, on
+    the pre-split copies, against fp64 of the rounded operands."""
     from mragan_hip import engine
     ops.set_conv_precision(prec)
     try:
         import types
         torch.manual_seed(0)
-        w = torch.nn.Parameter(torch.randn(64, 64, 3, 3, 3, device="cuda") * 0.05)
-        m = types.SimpleNamespace(weight=w, kernel_size=3, stride=1, padding=0, in_channels=64, out_channels=64)
+        C = 64
+        w = torch.nn.Parameter(torch.randn(C, C, 3, 3, 3, device="cuda") * 0.05)
+        m = types.SimpleNamespace(weight=w, kernel_size=3, stride=1, padding=0, in_channels=C, out_channels=C)
         layer = engine.ConvLayer(m, False)
         for src, A, B, T, tr, dst in layer.packs():
             ops.pack_weight(src, A, B, T, tr, dst)
         if engine._FP32_PACKS:
             pytest.skip("fp32 packs refreshed by every repack in this environment")
-        assert layer.fp32_bwd_stale
-        layer.wp_bwd.fill_(float("nan"))
-        layer.fresh_fp32_bwd()
-        ref = torch.empty_like(layer.wp_bwd)
-        ops.pack_weight(m.weight.data, 64, 64, 27, True, ref)
-        assert not layer.fp32_bwd_stale
-        assert torch.equal(layer.wp_bwd, ref)
+        assert layer.fp32_stale and layer.wp_fwd is None and layer.wp_bwd is None
+        dt = ops.op16_dtype()
+        N, S = 2, 24
+        x = ndhwc(torch.randn(N, C, S + 2, S + 2, S + 2).float()).cuda()
+        y, _, _ = layer.forward_in_stats_op16(x.to(dt))
+        dz = layer.dgrad_op16(y.to(dt), (S + 2,) * 3)
+        torch.cuda.synchronize()
+        wr = w.detach().double().cpu().to(dt).double()
+        y64 = F.conv3d(ncdhw(x.to(dt).double().cpu()), wr)
+        assert rel(ncdhw(y.double().cpu()), y64) < 2e-5
+        dz64 = F.conv_transpose3d(ncdhw(y.to(dt).double().cpu()), wr)
+        assert rel(ncdhw(dz.double().cpu()), dz64) < 2e-5
     finally:
         ops.set_conv_precision("f32")
