@@ -331,6 +331,43 @@ def time_steps(model, inputs, warmup, steps, barrier, dist):
     return elapsed, median_ms
 
 
+def h2d_inclusive(model, inputs, warmup, steps, barrier):
+    """The same K steps with the inputs in pinned HOST memory: set_input's host→device copy (the
+    reference's .to(device) of the patch pair, cycle_gan_model.py:131-135) inside the timed region.
+    Returns ms per step (this rank)."""
+    host = [(a.cpu().pin_memory(), b.cpu().pin_memory()) for a, b in inputs[:warmup + steps]]
+    for i in range(warmup):
+        model.set_input(host[i])
+        model.optimize_parameters()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        model.set_input(host[warmup + i])
+        model.optimize_parameters()
+    barrier()
+    return 1e3 * (time.perf_counter() - t0) / steps
+
+
+def phase_times(model, reps=10):
+    """The replayed step's two HIP graphs timed apart (events on the current stream around `reps`
+    back-to-back replays each): the G phase (generator forwards, losses, every backward) and the D
+    phase (both discriminators' passes) — the D phase is the window the data-parallel G all-reduce
+    overlaps.  None when the step is not graphed."""
+    if getattr(model, "_graphs", None) is None:
+        return None
+    out = {}
+    for name, g in zip(("G", "D"), model._graphs):
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = round(e0.elapsed_time(e1) / reps, 3)
+    return out
+
+
 def kernel_classes(model, inputs, reps=10):
     """Launch classes of one step: two eager single-stream steps record every instrumented C-ABI
     call; each class's call is then re-issued `reps` times back to back between HIP events
@@ -350,9 +387,10 @@ def kernel_classes(model, inputs, reps=10):
     return ops.TIMER.classes(reps)
 
 
-def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=None, netG=None):
+def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=None, netG=None, extras=False):
     """One workload: the timed step in `precision`, its launch classes and roofline, and the same
-    protocol in each precision of `alts` (a fresh model each)."""
+    protocol in each precision of `alts` (a fresh model each).  extras (the headline): also the
+    host-input (H2D-inclusive) step time and the two graph phases timed apart."""
     from mragan_hip import ops
     nc, netG = nc or args.nc, netG or args.netG
     shape = (batch, nc, size, size, size)
@@ -360,6 +398,10 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=N
     model = build_model(args, precision, batch, nc, netG)
     elapsed, median_ms = time_steps(model, inputs, args.warmup, args.steps, barrier, dist)
     graphed = getattr(model, "_graphs", None) is not None
+    h2d_ms = phases = None
+    if extras:
+        h2d_ms = h2d_inclusive(model, inputs, args.warmup, args.steps, barrier)
+        phases = phase_times(model) if world == 1 else None
     classes = kernel_classes(model, inputs) if not args.no_kernel_timing else None
     loss_scale = model.loss_scale
     del model
@@ -403,6 +445,13 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=N
         "step_tflop": round(step_tf, 4),
         "step_tflops_achieved": round(step_tf / t_step, 2),
     }
+    if h2d_ms is not None:
+        leg["h2d_inclusive"] = {"ms_per_step": round(h2d_ms, 3), "value": round(world * batch * 1e3 / h2d_ms, 3),
+                                "note": "same steps with the input pair in pinned host memory: set_input's "
+                                        "host-to-device copy inside the timed region (never `value`)"}
+    if phases:
+        leg["phase_ms"] = dict(phases, note="G / D graph replayed alone (10x each, events): the D phase is the "
+                                            "window the DP G all-reduce overlaps")
     if alt:
         leg["alt_precisions"] = alt
     if classes:
@@ -511,7 +560,7 @@ def main():
         torch.cuda.synchronize()
 
     alts = [p for p in args.alt_precisions.split(",") if p and p != args.precision]
-    head = run_leg(args, args.size, args.batch, args.precision, alts, barrier, dist, world, rank)
+    head = run_leg(args, args.size, args.batch, args.precision, alts, barrier, dist, world, rank, extras=True)
     legs = {}
     for spec in [s for s in args.legs.split(",") if s]:
         f = spec.split(":")
@@ -554,10 +603,12 @@ def main():
                    "global_batch": world * args.batch, "patch": args.size, "ngf": args.ngf, "ndf": args.ngf,
                    "parallelism": f"dp{world}",
                    "step_launch": head["step_launch"],
-                   "streams": 1 if args.single_stream else 2},
+                   "streams": 1 if args.single_stream else 2,
+                   "inputs": "device-resident before the timed region (the per-step host-to-device copy of "
+                             "the patch pair is timed apart: h2d_inclusive)"},
     }
     for k in ("roofline", "step_roofline", "step_tflop", "step_tflops_achieved", "alt_precisions", "top_kernels",
-              "kernel_ms_per_step_serial"):
+              "kernel_ms_per_step_serial", "h2d_inclusive", "phase_ms"):
         if k in head:
             res[k] = head[k]
     if legs:

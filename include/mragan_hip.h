@@ -177,6 +177,17 @@ int mragan_instnorm_bwd_g(const float* x, const float* mean, const float* rstd, 
  * plus the shell pass in the current mode, else 0 — the rule the engine schedules by (that form
  * leaves no backward statistics), queried instead of mirrored.                              */
 int mragan_conv3d_dgrad_split(int N, int Di, int Hi, int Wi, int cin, int cout);
+/* ABI 19: mragan_conv3d_wgrad_op16 over two instance sets of one shape — Na instances of
+ * (dense16_a, gathered16_a) and Nb of (dense16_b, gathered16_b) — summed into dw.  The reference
+ * accumulates a generator's weight gradient from its first pass and its cycle pass in one
+ * loss_G.backward() (cycle_gan_model.py:163-225); here each ResnetBlock conv's weight gradient is
+ * one launch (+ its reduce) over both passes' saved planes where the k3 s1 valid kernel's aligned
+ * operand-plane path applies, two accumulating passes otherwise.  Workspace:
+ * mragan_conv3d_wgrad_workspace(Na + Nb, ...). */
+int mragan_conv3d_wgrad_op16_pair(const void* dense16_a, int Na, const void* gathered16_a, const void* dense16_b, int Nb,
+                                  const void* gathered16_b, int Dd, int Hd, int Wd, int Cd, int Dg, int Hg, int Wg, int Cg,
+                                  int k, int stride, int pad, float* dw, int accumulate, void* ws, size_t ws_bytes,
+                                  void* stream);
 int mragan_instnorm_fwd_op16(const float* x, int N, int D, int H, int W, int C, float* y, void* y16, int ypad, int act,
                              const float* resid, int rpad, float* mean, float* rstd, void* ws, size_t ws_bytes,
                              void* stream);

@@ -414,6 +414,22 @@ int mragan_conv3d_wgrad_op16(const void* dense16, int N, int Dd, int Hd, int Wd,
   return conv_wgrad(a, dw, accumulate, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
+int mragan_conv3d_wgrad_op16_pair(const void* dense16_a, int Na, const void* gathered16_a, const void* dense16_b, int Nb,
+                                  const void* gathered16_b, int Dd, int Hd, int Wd, int Cd, int Dg, int Hg, int Wg, int Cg,
+                                  int k, int stride, int pad, float* dw, int accumulate, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  if (int rc = op16_mode_ok()) return rc;
+  MRAGAN_CHECK_ARG(dense16_a && gathered16_a && dw && ws, "wgrad_op16_pair: null pointer");
+  MRAGAN_CHECK_ARG(Na >= 0 && Nb >= 0 && (Nb == 0 || (dense16_b && gathered16_b)), "wgrad_op16_pair: bad second set");
+  MRAGAN_CHECK_ARG(!thin_wgrad_side(Cd, Cg) && k >= 1 && stride >= 1 && pad >= 0, "wgrad_op16_pair: bad args");
+  WgradArgs a{static_cast<const float*>(dense16_a), Na, Dd, Hd, Wd, Cd, static_cast<const float*>(gathered16_a), Dg, Hg,
+              Wg, Cg, k, stride, pad, static_cast<float*>(ws), 0, 0, g_conv_precision, 1};
+  if (Nb > 0) {
+    a.D2 = static_cast<const float*>(dense16_b); a.G2 = static_cast<const float*>(gathered16_b); a.N2 = Nb;
+  }
+  return conv_wgrad(a, dw, accumulate, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
 int mragan_conv3d_wgrad_g16(const float* dense, int N, int Dd, int Hd, int Wd, int Cd, const void* gathered16, int Dg,
                             int Hg, int Wg, int Cg, int k, int stride, int pad, float* dw, int accumulate, void* ws,
                             size_t ws_bytes, void* stream) {

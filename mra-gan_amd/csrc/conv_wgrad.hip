@@ -383,6 +383,36 @@ size_t conv_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, int k)
 
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st) {
   MRAGAN_CHECK_ARG(a.Cd % 4 == 0 && a.Cg % 4 == 0, "conv_wgrad: channels must be multiples of 4 (%d,%d)", a.Cd, a.Cg);
+  if (a.N2 > 0) {
+    // two instance sets into one gradient (ABI 19): one wgrad3_x3 launch + one reduce where the
+    // aligned operand-plane path takes both, else set 1 then set 2 accumulating
+    WgradArgs b = a;
+    b.D2 = b.G2 = nullptr; b.N2 = 0;
+    WgradArgs c = b;
+    c.D = a.D2; c.G = a.G2; c.N = a.N2;
+    MRAGAN_CHECK_ARG(a.D2 && a.G2, "conv_wgrad: null second instance set");
+    static const bool no_pair = getenv("MRAGAN_NO_WGRAD_PAIR") != nullptr;   // A/B switch
+    if (!no_pair && a.in16 && getenv("MRAGAN_NO_WGRAD3") == nullptr && wgrad3_x3_applicable(b) &&
+        wgrad3_x3_applicable(c)) {
+      const int T = a.k * a.k * a.k;
+      bool big;
+      wgrad_plan(a.Cd, a.Cg, T, (int64_t)(a.N + a.N2) * a.Dd * a.Hd * a.Wd, &a.splits, &a.chunk, &big);
+      const size_t need = (size_t)a.splits * T * a.Cd * a.Cg * sizeof(float);
+      if (need > ws_bytes) {
+        set_error("conv_wgrad: workspace %zu < %zu", ws_bytes, need);
+        return kWorkspace;
+      }
+      const int used = conv_wgrad3_x3(a, wgrad3_x3_splits(a, a.splits), st);
+      if (used != -kUnsupported) {
+        if (used < 0) return -used;
+        int rc = check_launch("wgrad3_x3(op16)");
+        if (rc) return rc;
+        return launch_wgrad_reduce(a.ws, out, a.Cd, a.Cg, T, used, accumulate, st);
+      }
+    }
+    const int rc = conv_wgrad(b, out, accumulate, ws_bytes, st);
+    return rc ? rc : conv_wgrad(c, out, 1, ws_bytes, st);
+  }
   if (a.x3 && a.N > 1) {
     // the 16-bit MFMA kernels address their operands with 32-bit byte offsets: a batch whose
     // tensors exceed 2 GiB runs as consecutive instance ranges accumulating into `out` (each

@@ -94,6 +94,9 @@ struct Wgrad3Args {
   const float* x; int Cg;                 // X  [N][D+2][H+2][W+2][Cg]
   float* ws;                              // slabs [splits][27][Cd][Cg]
   int nseg, seg_per_split;                // row segments in total / per split (multiple of kR)
+  // second instance set (kW16 path): segments from nseg1 on are instances of dy2 / x2 (N2 of them);
+  // without one dy2 = dy, x2 = x, N2 = 0, nseg1 = nseg
+  const float* dy2; const float* x2; int N2, nseg1;
 };
 
 // TC × TI = 64 × 64: 4 waves (2 × 2 sub-tiles of 32 × 32), two blocks per CU.  128 × 64 (the
@@ -233,15 +236,23 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
       rgo[q] = __builtin_amdgcn_readfirstlane((r / nsw) * grow1 + (r % nsw) * gw16);
     }
   }
+  // the second instance set: a stage lies in one (n, d) plane, so in one set — the stage picks its
+  // descriptors (wave-uniform) and rebases its offsets by set 1's bytes (segment / X offsets stay
+  // linear across the set boundary)
+  const int xoff1 = a.N * Dg * Hg * Wg * a.Cg * ES;
   auto load16 = [&](int st) __attribute__((always_inline)) {
-    const int dso0 = __builtin_amdgcn_readfirstlane((seg_lo + st * kR) * dseg);
-    const int gso0 = __builtin_amdgcn_readfirstlane(sxo + gkdh);
+    const int s0 = seg_lo + st * kR;
+    const bool s2 = s0 >= a.nseg1;
+    const __amdgpu_buffer_rsrc_t dr = s2 ? make_rsrc(a.dy2, a.N2 * a.D * a.H * a.W * a.Cd * ES) : dyr;
+    const __amdgpu_buffer_rsrc_t gr = s2 ? make_rsrc(a.x2, a.N2 * Dg * Hg * Wg * a.Cg * ES) : xgr;
+    const int dso0 = __builtin_amdgcn_readfirstlane((s0 - (s2 ? a.nseg1 : 0)) * dseg);
+    const int gso0 = __builtin_amdgcn_readfirstlane(sxo - (s2 ? xoff1 : 0) + gkdh);
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
 #pragma unroll
-      for (int j = 0; j < DL; ++j) d16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(dyr, dlo[j], dso0 + rdo[q]));
+      for (int j = 0; j < DL; ++j) d16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(dr, dlo[j], dso0 + rdo[q]));
 #pragma unroll
-      for (int j = 0; j < GL; ++j) g16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(xgr, glo[j], gso0 + rgo[q]));
+      for (int j = 0; j < GL; ++j) g16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(gr, glo[j], gso0 + rgo[q]));
     }
   };
   auto load = [&](int st) __attribute__((always_inline)) {
@@ -487,7 +498,7 @@ bool wgrad3_x3_applicable(const WgradArgs& a) {
 // splits: at most 2 blocks per CU in total (one round: a 513th block doubles the time),
 // ≥ 4 stages per block; never more than the generic plan's (its workspace query sizes the slabs)
 int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
-  const int nseg = a.N * a.Dd * a.Hd * (a.Wd / w3_segw(a));
+  const int nseg = (a.N + a.N2) * a.Dd * a.Hd * (a.Wd / w3_segw(a));
   const bool wide = w3_wide(a);
   const int tiles = (a.Cd / (wide ? 128 : kTile)) * (a.Cg / kTile) * 9;
   static const int budget = [] {                              // A/B switch: MRAGAN_W3_BLOCKS
@@ -535,7 +546,9 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     set_error("wgrad3_x3: width %d is not a multiple of 16 (or of 24 on the operand-plane path)", g.Wd);
     return -kBadArg;
   }
-  a.nseg = g.N * g.Dd * g.Hd * (g.Wd / segw);
+  a.nseg = (g.N + g.N2) * g.Dd * g.Hd * (g.Wd / segw);
+  a.nseg1 = g.N * g.Dd * g.Hd * (g.Wd / segw);
+  a.dy2 = g.N2 ? g.D2 : g.D; a.x2 = g.N2 ? g.G2 : g.G; a.N2 = g.N2;
   int per = (a.nseg + splits - 1) / splits;
   per = (per + kR - 1) / kR * kR;
   a.seg_per_split = per;
@@ -554,6 +567,8 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     set_error("wgrad3_x3: 24-voxel segments need aligned stages on operand planes");
     return -kBadArg;
   }
+  // two instance sets: the aligned operand-plane path only (the caller runs two passes otherwise)
+  if (g.N2 && !(al && g.in16)) return -kUnsupported;
   MRAGAN_PREC_DISPATCH(g.x3, {
     // 64-row waves on the wide aligned operand-plane tiles: opt-in A/B (MRAGAN_W3_WM=2), measured
     // slower than the 8-wave tiles (res wgrad [4×16³] 34.2 vs 32.2 µs, [2×32³] 90.3 vs 81.9 µs,

@@ -142,6 +142,10 @@ struct WgradArgs {
   int in16;        // D and G are 16-bit operand planes (wgrad3_x3 in the bf16 / fp16 modes only)
   int in16g = 0;   // only G is a 16-bit operand plane (wgrad3s2_x3, the one-plane modes: the fine-grid
                    // operand of the 64³-level stride-2 layers)
+  // ABI 19: a second instance set (N2 instances of D2 / G2, same per-instance shape) summed into the
+  // same gradient — a generator's first-pass and cycle-pass operands of one ResnetBlock conv in one
+  // launch (wgrad3_x3 on operand planes, aligned stages; otherwise two passes)
+  const float* D2 = nullptr; const float* G2 = nullptr; int N2 = 0;
 };
 int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStream_t st);
 // bf16x3 weight gradient of valid k3 s1 convs on padded inputs, 3 kw taps per block (conv_wgrad3_x3.hip)

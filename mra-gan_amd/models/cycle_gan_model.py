@@ -486,21 +486,31 @@ class CycleGANModel(BaseModel):
         # weight gradients + d fake_B); lane 1 the mirror image.  The first-pass backwards of
         # G_A / G_B accumulate into the weight gradients the other lane's cycle pass wrote, so
         # each waits for that pass.
+        # The cycle passes leave their ResnetBlock weight-gradient operands (planes) to the first
+        # passes of the same generator, which run each conv's weight gradient once over both
+        # passes' instances (NetPlan.backward wgrad_defer / wgrad_pair).  The deferred tensors are
+        # made on one lane and read on the other after its wait: they stay referenced (defer_A/B)
+        # until the lanes are joined.
+        defer_A, defer_B = {}, {}
         with ln.on(0):
             self._cDA1 = head(pDA, self._fake_B, 1, self._cGB2.out, A, lA, d_recA, self._cGA1, dGA1, B, lB * li, 3, 2)
-            pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b])
+            pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b],
+                         wgrad_defer=defer_B)
             rec_done_0 = ln.mark(0)
         with ln.on(1):
             self._cDB1 = head(pDB, self._fake_A, 5, self._cGA2.out, B, lB, d_recB, self._cGB1, dGB1, A, lA * li, 7, 6)
-            pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b])
+            pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b],
+                         wgrad_defer=defer_A)
             rec_done_1 = ln.mark(1)
+        keep = (list(defer_A.values()), list(defer_B.values()))
         with ln.on(0):
             ln.wait(0, rec_done_1)
-            pGA.backward(self._cGA1, [dGA1])
+            pGA.backward(self._cGA1, [dGA1], wgrad_pair=defer_A)
         with ln.on(1):
             ln.wait(1, rec_done_0)
-            pGB.backward(self._cGB1, [dGB1])
+            pGB.backward(self._cGB1, [dGB1], wgrad_pair=defer_B)
         ln.join()
+        del keep
 
     def _lanes(self):
         if self.parallel_lanes and self._aux_stream is None:

@@ -115,6 +115,7 @@ SIGNATURES = {
                                            vp]),
     # ABI 19: the interior + shell data-gradient rule as a query
     "mragan_conv3d_dgrad_split": (i32, [i32] * 6),
+    "mragan_conv3d_wgrad_op16_pair": (i32, [vp, i32, vp, vp, i32, vp] + [i32] * 11 + [vp, i32, vp, sz, vp]),
     "mragan_conv3d_presplit_bwd_stats": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, i32,
                                                i32, vp, sz, vp, vp, vp, i32, vp, sz, vp, vp]),
 }

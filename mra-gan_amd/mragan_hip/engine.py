@@ -70,6 +70,9 @@ _FP32_PACKS = (bool(int(__import__("os").environ.get("MRAGAN_FP32_PACKS", "0") o
                or any(v in __import__("os").environ for v in ("MRAGAN_NO_BRICK", "MRAGAN_BRICK_STAGED")))
 
 IN_MOMENTUM = 0.1
+# A/B switch: MRAGAN_NO_WGRAD_DEFER=1 runs each pass's ResnetBlock weight gradients in that pass (no
+# first-pass + cycle-pass pairing, NetPlan.backward wgrad_defer / wgrad_pair)
+_NO_WGRAD_DEFER = __import__("os").environ.get("MRAGAN_NO_WGRAD_DEFER") is not None
 
 
 # --------------------------------------------------------------------------------------
@@ -548,10 +551,32 @@ class NetPlan:
     # ---- backward ----------------------------------------------------------------------
     def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,
                  need_input_grad: bool = False, dx_out: Optional[torch.Tensor] = None,
-                 dx_add: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                 dx_add: Optional[torch.Tensor] = None, wgrad_defer: Optional[dict] = None,
+                 wgrad_pair: Optional[dict] = None) -> Optional[torch.Tensor]:
         """dout: up to 3 gradient sources w.r.t. ctx.out (summed).  Weight gradients are
         accumulated into the parameters' flat grad buffers.  Returns dL/dx (NDHWC) when
-        need_input_grad (written to dx_out, plus dx_add if given)."""
+        need_input_grad (written to dx_out, plus dx_add if given).
+
+        wgrad_defer / wgrad_pair (ABI 19): the reference accumulates a generator's weight gradient
+        over its first pass and its cycle pass in one loss_G.backward() (cycle_gan_model.py:163-225).
+        A pass given `wgrad_defer` (a dict) leaves the operand planes of its ResnetBlock weight
+        gradients there instead of launching them; the other pass of the same network, given that
+        dict as `wgrad_pair`, runs each of those convs' weight gradient once over both passes'
+        instances (mragan_conv3d_wgrad_op16_pair: one launch + one reduce instead of two each).
+        The caller keeps the dict's tensors alive until both passes' work is joined."""
+        if _NO_WGRAD_DEFER:
+            wgrad_defer = None
+
+        def block_wgrad(conv, x16, dy16, key):
+            if wgrad_defer is not None:
+                wgrad_defer[key] = (conv, x16, dy16)
+                return
+            other = wgrad_pair.pop(key, None) if wgrad_pair is not None else None
+            if other is not None:
+                ops.conv3d_wgrad_op16_pair(dy16, x16, other[2], other[1], conv.k, conv.s, conv.p, conv.m.weight.grad,
+                                           True)
+            else:
+                conv.wgrad_op16(x16, dy16)
         g, gpad, gadd = None, 0, None
         # (part, chunks, coef): backward statistics of the next IN from a data-gradient epilogue; coef =
         # its coefficients when that launch finalized them (ABI 15), else None
@@ -581,7 +606,7 @@ class NetPlan:
                     G = torch.empty(sc.h.shape, device=sc.h.device, dtype=torch.float32)
                     dh2 = ops.instnorm_bwd_op16(sc.h, sc.mean, sc.rstd, g, gpad, gadd, act=None, g_out=G)
                 if need_wgrad:
-                    st.conv2.wgrad_op16(sc.z1, dh2)
+                    block_wgrad(st.conv2, sc.z1, dh2, (i, 2))
                 # conv2's data gradient also accumulates IN1's backward statistics (ABI 11)
                 if not _IN1_STATS_BIG and _dgrad_split(*dh2.shape):
                     dz1, part, chunks, coef = st.conv2.dgrad_op16(dh2, sc.z1.shape[1:4]), None, 0, None
@@ -593,7 +618,7 @@ class NetPlan:
                 else:
                     dh1 = ops.instnorm_bwd_op16(sc.h1, sc.mean1, sc.rstd1, dz1, 1, None, act="relu")
                 if need_wgrad:
-                    st.conv1.wgrad_op16(sc.inp16, dh1)
+                    block_wgrad(st.conv1, sc.inp16, dh1, (i, 1))
                 nxt = self.stages[i - 1] if i > 0 else None
                 nsc = ctx.stages[i - 1] if i > 0 else None
                 # the IN in front: the previous block's IN2 (no activation), or G down2's IN + ReLU
@@ -736,6 +761,11 @@ class NetPlan:
                 else:
                     g = conv.dgrad(dh, in_spatial)
                 gpad, gadd = st.prepad, None
+        if wgrad_pair:
+            # deferred weight gradients this pass had no partner for (its blocks took another path)
+            for conv, x16, dy16 in wgrad_pair.values():
+                conv.wgrad_op16(x16, dy16)
+            wgrad_pair.clear()
         if not need_input_grad:
             return None
         first = self.stages[0]
@@ -1019,8 +1049,10 @@ class UnetPlan:
 
     def backward(self, ctx: NetCtx, dout: List[Optional[torch.Tensor]], need_wgrad: bool = True,
                  need_input_grad: bool = False, dx_out: Optional[torch.Tensor] = None,
-                 dx_add: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-        """Same contract as NetPlan.backward."""
+                 dx_add: Optional[torch.Tensor] = None, wgrad_defer: Optional[dict] = None,
+                 wgrad_pair: Optional[dict] = None) -> Optional[torch.Tensor]:
+        """Same contract as NetPlan.backward (no ResnetBlocks: wgrad_defer / wgrad_pair stay empty,
+        every weight gradient runs in its pass)."""
         n = len(self.levels)
         skip = [None] * (n + 1)        # gradient w.r.t. level i's input through the skip half of the cat
         du = [None] * (n + 1)          # gradient w.r.t. ReLU(u_i) (raw, the IN backward applies ReLU')

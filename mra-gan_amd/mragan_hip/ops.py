@@ -803,6 +803,32 @@ def conv3d_wgrad_op16(dense16: torch.Tensor, gathered16: torch.Tensor, k: int, s
     return dw
 
 
+def conv3d_wgrad_op16_pair(dense16: torch.Tensor, gathered16: torch.Tensor, dense16_b: torch.Tensor,
+                           gathered16_b: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
+                           accumulate: bool) -> torch.Tensor:
+    """conv3d_wgrad_op16 summed over two instance sets of one per-instance shape (ABI 19): a
+    generator's first-pass and cycle-pass operands of one ResnetBlock conv in one launch."""
+    for t, n in ((dense16, "dense"), (gathered16, "gathered"), (dense16_b, "dense_b"), (gathered16_b, "gathered_b")):
+        _check16(t, f"wgrad_op16_pair.{n}")
+    N, Dd, Hd, Wd, Cd = dense16.shape
+    Nb = dense16_b.shape[0]
+    _, Dg, Hg, Wg, Cg = gathered16.shape
+    if gathered16.shape[0] != N or gathered16_b.shape[0] != Nb:
+        raise ValueError("wgrad_pair: batch mismatch")
+    if tuple(dense16_b.shape[1:]) != (Dd, Hd, Wd, Cd) or tuple(gathered16_b.shape[1:]) != (Dg, Hg, Wg, Cg):
+        raise ValueError("wgrad_pair: the two instance sets differ in shape")
+    if dw.numel() != Cd * Cg * k ** 3 or not dw.is_contiguous():
+        raise ValueError(f"wgrad: dw has {dw.numel()} elements, expected {Cd}x{Cg}x{k}^3 (contiguous)")
+    nbytes = query("mragan_conv3d_wgrad_workspace", N + Nb, Dd, Hd, Wd, Cd, Cg, k, s)
+    ws = WS.get(nbytes)
+    fn = lambda: call("mragan_conv3d_wgrad_op16_pair", _ptr(dense16), N, _ptr(gathered16), _ptr(dense16_b), Nb,
+                      _ptr(gathered16_b), Dd, Hd, Wd, Cd, Dg, Hg, Wg, Cg, k, s, p, _ptr(dw), int(accumulate), _ptr(ws),
+                      ws.numel(), _stream())
+    _timed(lambda: dict(op="wgrad", cls=f"wgrad {Cd}x{Cg} k{k} s{s} [{N}+{Nb}x{Dd}x{Hd}x{Wd}]",
+                        flops=2.0 * (N + Nb) * Dd * Hd * Wd * Cd * Cg * k ** 3), fn)
+    return dw
+
+
 def conv3d_wgrad_g16(dense: torch.Tensor, gathered16: torch.Tensor, k: int, s: int, p: int, dw: torch.Tensor,
                      accumulate: bool) -> torch.Tensor:
     """conv3d_wgrad (k3 s2 p1) with the gathered operand as its 16-bit plane, dense fp32 (ABI 14)."""

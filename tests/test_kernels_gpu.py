@@ -660,6 +660,37 @@ def test_op16_brick_conv_and_wgrad(op16, N, C, S, W):
     assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
 
 
+@pytest.mark.parametrize("N1,N2,C,S,W", [(4, 2, 128, 16, 16), (2, 1, 128, 24, 24), (1, 1, 64, 8, 32),
+                                          (2, 2, 128, 5, 16)])
+def test_op16_wgrad_pair(op16, N1, N2, C, S, W):
+    """ABI 19: one ResnetBlock weight gradient over two instance sets (a generator's first and cycle
+    pass) is bit-identical to the same kernel over the two sets concatenated in one tensor (same
+    segments, splits and reduce order) where the aligned plane path takes both (16³, 24³, 32-wide);
+    otherwise (5-row planes: unaligned stages) it is the two accumulating passes, bit for bit; and
+    it equals fp64 on the rounded operands."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N1 * 7 + N2 + C + S)
+    x = ndhwc(torch.randn(N1 + N2, C, S + 2, S + 2, W + 2, generator=g).float()).cuda().to(dt)
+    dy = ndhwc(torch.randn(N1 + N2, C, S, S, W, generator=g).float()).cuda().to(dt)
+    xa, xb = x[:N1].clone(), x[N1:].clone()              # separate allocations, as the two passes'
+    da, db = dy[:N1].clone(), dy[N1:].clone()
+    gw = torch.full((C * C * 27,), float("nan"), device="cuda")
+    ops.conv3d_wgrad_op16_pair(da, xa, db, xb, 3, 1, 0, gw, False)
+    nsw = W // (16 if W % 16 == 0 else 24)                # row segments per w-row (wgrad3 w3_segw)
+    aligned = S % (8 // nsw) == 0                         # whole rows per 8-segment stage
+    ref = torch.empty_like(gw)
+    if aligned:
+        ops.conv3d_wgrad_op16(dy, x, 3, 1, 0, ref, False)
+    else:
+        ops.conv3d_wgrad_op16(da, xa, 3, 1, 0, ref, False)
+        ops.conv3d_wgrad_op16(db, xb, 3, 1, 0, ref, True)
+    torch.cuda.synchronize()
+    assert torch.equal(gw, ref)
+    gw64 = F.conv3d(ncdhw(x.double().cpu()).transpose(0, 1), ncdhw(dy.double().cpu()).transpose(0, 1))
+    assert rel(gw.view(C, C, 3, 3, 3), gw64.transpose(0, 1)) < 2e-5
+
+
 @pytest.mark.parametrize("N,S,C", [(2, 32, 128), (1, 32, 128), (4, 24, 128), (2, 24, 64), (2, 16, 128)])
 def test_op16_res_dgrad_interior_shell(op16, N, S, C):
     """The ResnetBlock whole-grid data gradient for N ≥ 2 at 24³ / 32³ runs as the interior brick (the
