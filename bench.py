@@ -356,7 +356,8 @@ def phase_times(model, reps=10):
     if getattr(model, "_graphs", None) is None:
         return None
     out = {}
-    for name, g in zip(("G", "D"), model._graphs):
+    names = ("G", "D") if model._graphs[1] is not None else ("G+D overlapped",)
+    for name, g in zip(names, model._graphs):
         g.replay()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -450,8 +451,9 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=N
                                 "note": "same steps with the input pair in pinned host memory: set_input's "
                                         "host-to-device copy inside the timed region (never `value`)"}
     if phases:
-        leg["phase_ms"] = dict(phases, note="G / D graph replayed alone (10x each, events): the D phase is the "
-                                            "window the DP G all-reduce overlaps")
+        leg["phase_ms"] = dict(phases, note="the step's graphs replayed alone (10x each, events); single GPU runs "
+                                            "the D phase beside the G backward (one graph), data parallel the "
+                                            "two-phase schedule whose D phase the G all-reduce overlaps")
     if alt:
         leg["alt_precisions"] = alt
     if classes:

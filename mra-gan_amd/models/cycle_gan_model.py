@@ -29,6 +29,9 @@ from .base_model import BaseModel
 device = networks3D.device
 # A/B switch: MRAGAN_NO_GRAPH_CACHE=1 keeps only the latest capture (round-2 behaviour)
 _NO_GRAPH_CACHE = bool(int(__import__("os").environ.get("MRAGAN_NO_GRAPH_CACHE", "0") or "0"))
+# A/B switch: MRAGAN_TWO_PHASE=1 runs the D phase after the whole G phase (rounds 1-5) instead of
+# beside the G backward on two more streams (single GPU, two lanes)
+_TWO_PHASE = __import__("os").environ.get("MRAGAN_TWO_PHASE") is not None
 
 
 class ImagePool():
@@ -187,6 +190,42 @@ class _Lanes:
     def join(self):
         if self.parallel:
             self.s[0].wait_stream(self.s[1])
+
+
+class _SideLanes:
+    """Two more in-order streams forked from the current (origin) stream and joined back to it,
+    with workspace lanes 2 and 3: the D phase beside the G backward (which holds lanes 0 and 1).
+    Only origin ↔ side edges (fork: each side stream waits for the origin; join: the origin waits
+    for each) — the capture topology this ROCm accepts."""
+
+    def __init__(self, streams):
+        from mragan_hip import ops
+        self._ops = ops
+        cur = torch.cuda.current_stream()
+        self.cur = cur
+        self.s = list(streams)
+        for st in self.s:
+            st.wait_stream(cur)
+
+    def on(self, i):
+        lanes = self
+
+        class _On:
+            def __enter__(self_):
+                self_.st = torch.cuda.stream(lanes.s[i])
+                self_.ln = lanes._ops.lane(2 + i)
+                self_.st.__enter__()
+                self_.ln.__enter__()
+
+            def __exit__(self_, *exc):
+                self_.ln.__exit__(*exc)
+                self_.st.__exit__(*exc)
+                return False
+        return _On()
+
+    def join(self):
+        for st in self.s:
+            self.cur.wait_stream(st)
 
 
 def _to_ndhwc(x: torch.Tensor) -> torch.Tensor:
@@ -360,6 +399,7 @@ class CycleGANModel(BaseModel):
         self._use_graph = self.isTrain and not getattr(opt, 'no_cuda_graph', False) and self.device.type == 'cuda'
         self.parallel_lanes = not getattr(opt, 'single_stream', False)
         self._aux_stream = None
+        self._d_streams = None          # the D phase's two streams beside the G backward (_phase_GD)
         self._graphs = None          # (G-phase graph, D-phase graph) of the step being replayed
         self._rs_tables = None       # running-stat update tables of that capture
         self._graph_key = None
@@ -598,6 +638,34 @@ class CycleGANModel(BaseModel):
         self.optimizer_G.zero_grad()
         self.backward_G()
 
+    def _overlap_D(self):
+        """Single GPU with two lanes: the D phase runs beside the G backward (round 6)."""
+        return self.parallel_lanes and not self._dist and not _TWO_PHASE
+
+    def _phase_GD(self):
+        """G phase and D phase in one: the D phase needs only the fakes (made by the G forwards) and
+        the pre-update D weights — the reference's order (cycle_gan_model.py:227-240: G step, then D
+        step on the same fakes) is kept exactly, since no D weight changes before the D Adam and the
+        D gradients are written only by the D phase — so once the forwards are joined it runs on two
+        more streams (D_A, D_B) forked from the origin, beside the G backward on lanes 0 / 1, and is
+        joined at the end.  Its small, latency-bound launches fill CU slots the G backward leaves
+        idle.  Same kernels on the same operands as _phase_G then _phase_D: bit-identical results."""
+        self.forward_train()
+        self.set_requires_grad([self.netD_A, self.netD_B], False)
+        self.optimizer_G.zero_grad()
+        self.optimizer_D.zero_grad()
+        if self._d_streams is None:
+            self._d_streams = (torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device))
+        side = _SideLanes(self._d_streams)
+        with side.on(0):
+            self.backward_D_A()
+        with side.on(1):
+            self.backward_D_B()
+        self.backward_G()
+        side.join()
+        if not torch.cuda.is_current_stream_capturing():
+            self._running_stats()
+
     def _phase_D(self):
         self.set_requires_grad([self.netD_A, self.netD_B], True)
         self.optimizer_D.zero_grad()
@@ -662,10 +730,15 @@ class CycleGANModel(BaseModel):
         side.wait_stream(torch.cuda.current_stream())
         # thread_local: other threads (the process group's watchdog) may query the runtime
         # while this thread captures
-        with torch.cuda.graph(gG, stream=side, capture_error_mode="thread_local"):
-            self._phase_G()
-        with torch.cuda.graph(gD, pool=gG.pool(), stream=side, capture_error_mode="thread_local"):
-            self._phase_D()
+        if self._overlap_D():
+            with torch.cuda.graph(gG, stream=side, capture_error_mode="thread_local"):
+                self._phase_GD()
+            gD = None
+        else:
+            with torch.cuda.graph(gG, stream=side, capture_error_mode="thread_local"):
+                self._phase_G()
+            with torch.cuda.graph(gD, pool=gG.pool(), stream=side, capture_error_mode="thread_local"):
+                self._phase_D()
         torch.cuda.current_stream().wait_stream(side)
         self._rs_tables = None
         self._graphs = (gG, gD)
@@ -701,6 +774,22 @@ class CycleGANModel(BaseModel):
             if self._graphs is None or self._graph_key != self._capture_key():
                 self._use_capture()
             graphed = True
+        if self._overlap_D():
+            # one graph (or eager pass) for both phases, the D phase beside the G backward
+            if graphed:
+                self._graphs[0].replay()
+                self._running_stats_graphed()
+            else:
+                self._phase_GD()
+            self.optimizer_G.step_dev(hG)
+            self.optimizer_D.step_dev(hD)
+            if graphed:
+                for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
+                    n.mark_params_dirty()
+            else:
+                self._eager_steps += 1
+                self._eager_shapes.add(shape_key)
+            return
         run_G = self._graphs[0].replay if graphed else self._phase_G
         run_D = self._graphs[1].replay if graphed else self._phase_D
         run_G()

@@ -188,3 +188,31 @@ def test_graph_step_bit_identical_headline(tmp_path, precision, size, batch, nc,
         assert torch.equal(se[k], sg[k]), k
     for k in ve:
         assert torch.equal(ve[k], vg[k]), k
+
+
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_overlapped_d_phase_bit_identical(tmp_path, precision, monkeypatch):
+    """Round 6: on one GPU the D phase runs beside the G backward on two more streams, in the same
+    graph (CycleGANModel._phase_GD).  It computes the same kernels on the same operands as the
+    two-phase schedule (MRAGAN_TWO_PHASE, rounds 1-5: G phase, G Adam, D phase, D Adam), so over
+    several replayed steps every loss, parameter, running statistic and volume is bit-identical."""
+    from models import cycle_gan_model as cgm
+    extra = ["--netG", "resnet_9blocks", "--ngf", "16", "--ndf", "16"]
+    try:
+        monkeypatch.setattr(cgm, "_TWO_PHASE", True)
+        lt, st, vt, mt = _run(tmp_path / "t", True, 4, precision, extra=extra, size=32)
+        assert mt._graphs[1] is not None
+        del mt
+        monkeypatch.setattr(cgm, "_TWO_PHASE", False)
+        lo, so, vo, mo = _run(tmp_path / "o", True, 4, precision, extra=extra, size=32)
+        assert mo._graphs[1] is None and mo._d_streams is not None
+        del mo
+    finally:
+        from mragan_hip import ops
+        ops.set_conv_precision("f32")
+        ops.set_loss_scale(1.0)
+    assert torch.equal(lt, lo), (lt - lo).abs().max()
+    for k in st:
+        assert torch.equal(st[k], so[k]), k
+    for k in vt:
+        assert torch.equal(vt[k], vo[k]), k
