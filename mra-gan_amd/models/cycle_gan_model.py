@@ -32,6 +32,9 @@ _NO_GRAPH_CACHE = bool(int(__import__("os").environ.get("MRAGAN_NO_GRAPH_CACHE",
 # A/B switch: MRAGAN_TWO_PHASE=1 runs the D phase after the whole G phase (rounds 1-5) instead of
 # beside the G backward on two more streams (single GPU, two lanes)
 _TWO_PHASE = __import__("os").environ.get("MRAGAN_TWO_PHASE") is not None
+# A/B switch: MRAGAN_FROZEN_D_ON_LANES=1 keeps the frozen discriminator passes of backward_G on the
+# lanes, ahead of the cycle-pass backwards (the overlapped schedule then moves only the D phase)
+_FROZEN_D_ON_LANES = __import__("os").environ.get("MRAGAN_FROZEN_D_ON_LANES") is not None
 
 
 class ImagePool():
@@ -222,6 +225,11 @@ class _SideLanes:
                 self_.st.__exit__(*exc)
                 return False
         return _On()
+
+    def mark(self, i):
+        ev = torch.cuda.Event()
+        ev.record(self.s[i])
+        return ev
 
     def join(self):
         for st in self.s:
@@ -492,9 +500,27 @@ class CycleGANModel(BaseModel):
         if self._idt:
             self._publish(idt_A=self._cGA1.out[b:], idt_B=self._cGB1.out[b:])
 
-    def backward_G(self):
+    def backward_G(self, side=None):
         """cycle_gan_model.py:163-225: identity, GAN and cycle losses; backward through the 6
-        generator passes and (data gradient only) the 2 frozen discriminator passes."""
+        generator passes and (data gradient only) the 2 frozen discriminator passes.
+
+        The GAN losses' data gradients (D_A(fake_B) → d fake_B, D_B(fake_A) → d fake_A) feed only
+        the first-pass backwards, not the cycle-pass ones: each frozen discriminator writes its
+        data gradient into its own buffer (dD_A / dD_B), and the first passes take the two sources
+        [lane's gradient, D's] — summed in the head's tanh backward (fake half: cycle + GAN;
+        identity half: identity + 0).  With `side` (_SideLanes, the single-GPU overlapped
+        schedule, _phase_GD) the frozen passes, and after them the D phase, run on the two side
+        streams beside the cycle-pass backwards, and the origin (lane 0) waits for both frozen
+        passes before its first-pass backward (lane 1 waits for the origin there as before);
+        without it they run on the lanes ahead of the cycle passes.  Every schedule forms the same
+        sums in the same order: the results are bit-identical (tests/test_graph_gpu.py).
+
+        Lane 0 runs loss_cycle_A / loss_idt_A and then G_B's rec_A pass (G_B weight gradients +
+        d fake_B), lane 1 the mirror image.  The cycle passes leave their ResnetBlock
+        weight-gradient operands (planes) to the first passes of the same generator on the other
+        lane, which run each conv's weight gradient once over both passes' instances
+        (NetPlan.backward wgrad_defer / wgrad_pair); those tensors stay referenced until the lanes
+        are joined."""
         from mragan_hip import ops
         b, A, B = self._b, self._A, self._B
         lA, lB, li = self.opt.lambda_A, self.opt.lambda_B, self.opt.lambda_identity
@@ -502,53 +528,64 @@ class CycleGANModel(BaseModel):
         pDA, pDB = self.netD_A.plan, self.netD_B.plan
         pGA, pGB = self.netG_A.plan, self.netG_B.plan
         # allocated before the fork: both lanes' tensors outlive it
-        dGA1 = torch.empty_like(self._cGA1.out)     # d/d[fake_B; idt_A]
+        dGA1 = torch.empty_like(self._cGA1.out)     # d/d[fake_B; idt_A]: cycle + identity losses
         dGB1 = torch.empty_like(self._cGB1.out)     # d/d[fake_A; idt_B]
+        dDA = torch.empty_like(dGA1)                # d/d[fake_B; idt_A]: D_A's GAN loss (0 on idt_A)
+        dDB = torch.empty_like(dGB1)
         d_recA = torch.empty_like(self._cGB2.out)
         d_recB = torch.empty_like(self._cGA2.out)
         if not self._idt:                                                              # reference: 0
             ops.fill(L[3:4], 0.0)
             ops.fill(L[7:8], 0.0)
-        ln = self._lanes()
 
-        def head(pD, fake, slot, rec, real_rec, lam, d_rec, cG1, dG1, real_idt, lam_idt, idt_slot, cyc_slot):
+        def frozen(pD, fake, slot, dD):
             cD = pD.forward(fake)
             dlog = torch.empty_like(cD.out)
             ops.gan_loss(cD.out, 1.0, self.use_lsgan, 1.0, L[slot:slot + 1], dlog)
+            pD.backward(cD, [dlog], need_wgrad=False, need_input_grad=True, dx_out=dD[:b])
+            if self._idt:
+                ops.fill(dD[b:], 0.0)
+            return cD
+
+        def l1s(rec, real_rec, lam, d_rec, cG1, dG1, real_idt, lam_idt, idt_slot, cyc_slot):
             ops.l1_loss(rec, real_rec, lam, L[cyc_slot:cyc_slot + 1], d_rec)
             if self._idt:
                 ops.l1_loss(cG1.out[b:], real_idt, lam_idt, L[idt_slot:idt_slot + 1], dG1[b:])
-            # frozen D: data gradient only, written into the fake half
-            pD.backward(cD, [dlog], need_wgrad=False, need_input_grad=True, dx_out=dG1[:b])
-            return cD
 
-        # lane 0: D_A(fake_B), loss_G_A, loss_cycle_A, loss_idt_A, then G_B's rec_A pass (G_B
-        # weight gradients + d fake_B); lane 1 the mirror image.  The first-pass backwards of
-        # G_A / G_B accumulate into the weight gradients the other lane's cycle pass wrote, so
-        # each waits for that pass.
-        # The cycle passes leave their ResnetBlock weight-gradient operands (planes) to the first
-        # passes of the same generator, which run each conv's weight gradient once over both
-        # passes' instances (NetPlan.backward wgrad_defer / wgrad_pair).  The deferred tensors are
-        # made on one lane and read on the other after its wait: they stay referenced (defer_A/B)
-        # until the lanes are joined.
+        if side is not None:
+            with side.on(0):
+                self._cDA1 = frozen(pDA, self._fake_B, 1, dDA)
+                d_done_A = side.mark(0)
+                self.backward_D_A()
+            with side.on(1):
+                self._cDB1 = frozen(pDB, self._fake_A, 5, dDB)
+                d_done_B = side.mark(1)
+                self.backward_D_B()
+        ln = self._lanes()
         defer_A, defer_B = {}, {}
         with ln.on(0):
-            self._cDA1 = head(pDA, self._fake_B, 1, self._cGB2.out, A, lA, d_recA, self._cGA1, dGA1, B, lB * li, 3, 2)
-            pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], dx_add=dGA1[:b],
-                         wgrad_defer=defer_B)
-            rec_done_0 = ln.mark(0)
+            if side is None:
+                self._cDA1 = frozen(pDA, self._fake_B, 1, dDA)
+            l1s(self._cGB2.out, A, lA, d_recA, self._cGA1, dGA1, B, lB * li, 3, 2)
+            pGB.backward(self._cGB2, [d_recA], need_input_grad=True, dx_out=dGA1[:b], wgrad_defer=defer_B)
+            if side is not None:
+                cur = torch.cuda.current_stream()
+                cur.wait_event(d_done_A)            # origin ← side joins (the frozen passes)
+                cur.wait_event(d_done_B)
+            rec_done_0 = ln.mark(0)                 # lane 1 waits this: d fake_A complete too
         with ln.on(1):
-            self._cDB1 = head(pDB, self._fake_A, 5, self._cGA2.out, B, lB, d_recB, self._cGB1, dGB1, A, lA * li, 7, 6)
-            pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], dx_add=dGB1[:b],
-                         wgrad_defer=defer_A)
+            if side is None:
+                self._cDB1 = frozen(pDB, self._fake_A, 5, dDB)
+            l1s(self._cGA2.out, B, lB, d_recB, self._cGB1, dGB1, A, lA * li, 7, 6)
+            pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], wgrad_defer=defer_A)
             rec_done_1 = ln.mark(1)
         keep = (list(defer_A.values()), list(defer_B.values()))
         with ln.on(0):
             ln.wait(0, rec_done_1)
-            pGA.backward(self._cGA1, [dGA1], wgrad_pair=defer_A)
+            pGA.backward(self._cGA1, [dGA1, dDA], wgrad_pair=defer_A)
         with ln.on(1):
             ln.wait(1, rec_done_0)
-            pGB.backward(self._cGB1, [dGB1], wgrad_pair=defer_B)
+            pGB.backward(self._cGB1, [dGB1, dDB], wgrad_pair=defer_B)
         ln.join()
         del keep
 
@@ -657,11 +694,14 @@ class CycleGANModel(BaseModel):
         if self._d_streams is None:
             self._d_streams = (torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device))
         side = _SideLanes(self._d_streams)
-        with side.on(0):
-            self.backward_D_A()
-        with side.on(1):
-            self.backward_D_B()
-        self.backward_G()
+        if _FROZEN_D_ON_LANES:
+            with side.on(0):
+                self.backward_D_A()
+            with side.on(1):
+                self.backward_D_B()
+            self.backward_G()
+        else:
+            self.backward_G(side)                   # the frozen D passes and the D phase on `side`
         side.join()
         if not torch.cuda.is_current_stream_capturing():
             self._running_stats()

@@ -192,10 +192,12 @@ def test_graph_step_bit_identical_headline(tmp_path, precision, size, batch, nc,
 
 @pytest.mark.parametrize("precision", ["bf16", "f32"])
 def test_overlapped_d_phase_bit_identical(tmp_path, precision, monkeypatch):
-    """Round 6: on one GPU the D phase runs beside the G backward on two more streams, in the same
-    graph (CycleGANModel._phase_GD).  It computes the same kernels on the same operands as the
-    two-phase schedule (MRAGAN_TWO_PHASE, rounds 1-5: G phase, G Adam, D phase, D Adam), so over
-    several replayed steps every loss, parameter, running statistic and volume is bit-identical."""
+    """Round 6: on one GPU the D phase — and the frozen discriminator passes of backward_G — run
+    beside the G backward on two more streams, in the same graph (CycleGANModel._phase_GD).  They
+    compute the same kernels on the same operands and form the same sums as the two-phase schedule
+    (MRAGAN_TWO_PHASE: G phase, G Adam, D phase, D Adam) and as the overlapped schedule with the
+    frozen passes on the lanes (MRAGAN_FROZEN_D_ON_LANES), so over several replayed steps every
+    loss, parameter, running statistic and volume is bit-identical."""
     from models import cycle_gan_model as cgm
     extra = ["--netG", "resnet_9blocks", "--ngf", "16", "--ndf", "16"]
     try:
@@ -204,6 +206,10 @@ def test_overlapped_d_phase_bit_identical(tmp_path, precision, monkeypatch):
         assert mt._graphs[1] is not None
         del mt
         monkeypatch.setattr(cgm, "_TWO_PHASE", False)
+        monkeypatch.setattr(cgm, "_FROZEN_D_ON_LANES", True)
+        lf, sf, vf, mf = _run(tmp_path / "f", True, 4, precision, extra=extra, size=32)
+        del mf
+        monkeypatch.setattr(cgm, "_FROZEN_D_ON_LANES", False)
         lo, so, vo, mo = _run(tmp_path / "o", True, 4, precision, extra=extra, size=32)
         assert mo._graphs[1] is None and mo._d_streams is not None
         del mo
@@ -211,8 +217,9 @@ def test_overlapped_d_phase_bit_identical(tmp_path, precision, monkeypatch):
         from mragan_hip import ops
         ops.set_conv_precision("f32")
         ops.set_loss_scale(1.0)
-    assert torch.equal(lt, lo), (lt - lo).abs().max()
-    for k in st:
-        assert torch.equal(st[k], so[k]), k
-    for k in vt:
-        assert torch.equal(vt[k], vo[k]), k
+    for l2, s2, v2 in ((lf, sf, vf), (lo, so, vo)):   # frozen D passes on the lanes / on the side streams
+        assert torch.equal(lt, l2), (lt - l2).abs().max()
+        for k in st:
+            assert torch.equal(st[k], s2[k]), k
+        for k in vt:
+            assert torch.equal(vt[k], v2[k]), k
