@@ -35,6 +35,8 @@ _TWO_PHASE = __import__("os").environ.get("MRAGAN_TWO_PHASE") is not None
 # A/B switch: MRAGAN_FROZEN_D_ON_LANES=1 keeps the frozen discriminator passes of backward_G on the
 # lanes, ahead of the cycle-pass backwards (the overlapped schedule then moves only the D phase)
 _FROZEN_D_ON_LANES = __import__("os").environ.get("MRAGAN_FROZEN_D_ON_LANES") is not None
+# A/B switch: MRAGAN_ADAM_AFTER=1 runs the four Adam updates after the step's graph (rounds 1-5)
+_ADAM_AFTER = __import__("os").environ.get("MRAGAN_ADAM_AFTER") is not None
 
 
 class ImagePool():
@@ -322,6 +324,18 @@ class FusedAdam(torch.optim.Optimizer):
         # what torch's step wrapper records for an LR scheduler (it warns otherwise)
         self._opt_called = True
 
+    @torch.no_grad()
+    def step_net(self, n, hyper):
+        """step_dev for one of the optimizer's networks (no found-inf check: its flag spans every
+        network).  The overlapped single-GPU step issues each network's update at the end of the
+        stream that finished its gradients (CycleGANModel._phase_GD)."""
+        assert not self.check_finite, "step_net: the found-inf check needs every network's gradients"
+        networks3D.ensure_flat(n)
+        m, v = self._state(n)
+        ops_mod().adam_dev(n._flat_param, n._flat_grad, m, v, hyper)
+        n.mark_params_dirty()
+        self._opt_called = True
+
     def skipped(self) -> int:
         """Steps whose update was skipped for a non-finite gradient (synchronizes)."""
         return 0 if self._skipped is None else int(self._skipped.item())
@@ -553,14 +567,19 @@ class CycleGANModel(BaseModel):
                 ops.l1_loss(cG1.out[b:], real_idt, lam_idt, L[idt_slot:idt_slot + 1], dG1[b:])
 
         if side is not None:
+            adam_in = self._adam_in_lanes()
             with side.on(0):
                 self._cDA1 = frozen(pDA, self._fake_B, 1, dDA)
                 d_done_A = side.mark(0)
                 self.backward_D_A()
+                if adam_in:     # D_A's parameters are read on this stream only
+                    self.optimizer_D.step_net(self.netD_A, self._step_hyper[6:12])
             with side.on(1):
                 self._cDB1 = frozen(pDB, self._fake_A, 5, dDB)
                 d_done_B = side.mark(1)
                 self.backward_D_B()
+                if adam_in:
+                    self.optimizer_D.step_net(self.netD_B, self._step_hyper[6:12])
         ln = self._lanes()
         defer_A, defer_B = {}, {}
         with ln.on(0):
@@ -580,12 +599,17 @@ class CycleGANModel(BaseModel):
             pGA.backward(self._cGA2, [d_recB], need_input_grad=True, dx_out=dGB1[:b], wgrad_defer=defer_A)
             rec_done_1 = ln.mark(1)
         keep = (list(defer_A.values()), list(defer_B.values()))
+        adam_in = side is not None and self._adam_in_lanes()
         with ln.on(0):
             ln.wait(0, rec_done_1)
             pGA.backward(self._cGA1, [dGA1, dDA], wgrad_pair=defer_A)
+            if adam_in:         # every G_A gradient is done here (lane 1's G_A cycle pass is waited for)
+                self.optimizer_G.step_net(self.netG_A, self._step_hyper[0:6])
         with ln.on(1):
             ln.wait(1, rec_done_0)
             pGB.backward(self._cGB1, [dGB1, dDB], wgrad_pair=defer_B)
+            if adam_in:
+                self.optimizer_G.step_net(self.netG_B, self._step_hyper[0:6])
         ln.join()
         del keep
 
@@ -678,6 +702,14 @@ class CycleGANModel(BaseModel):
     def _overlap_D(self):
         """Single GPU with two lanes: the D phase runs beside the G backward (round 6)."""
         return self.parallel_lanes and not self._dist and not _TWO_PHASE
+
+    def _adam_in_lanes(self):
+        """In the overlapped schedule without a loss scale (no found-inf check spanning both
+        networks of an optimizer): each network's Adam update runs at the end of the stream that
+        completed its gradients, inside the step — D_A / D_B beside the G backward, G_A / G_B as
+        each lane finishes — instead of four launches after it.  Same kernel, same operands."""
+        return (self._overlap_D() and not _ADAM_AFTER and not self.optimizer_G.check_finite
+                and not self.optimizer_D.check_finite and not _FROZEN_D_ON_LANES)
 
     def _phase_GD(self):
         """G phase and D phase in one: the D phase needs only the fakes (made by the G forwards) and
@@ -821,8 +853,9 @@ class CycleGANModel(BaseModel):
                 self._running_stats_graphed()
             else:
                 self._phase_GD()
-            self.optimizer_G.step_dev(hG)
-            self.optimizer_D.step_dev(hD)
+            if not self._adam_in_lanes():
+                self.optimizer_G.step_dev(hG)
+                self.optimizer_D.step_dev(hD)
             if graphed:
                 for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
                     n.mark_params_dirty()
