@@ -376,6 +376,8 @@ void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short* rowvo
 }
 
 static const bool g_staged_x3 = getenv("MRAGAN_BRICK_STAGED") != nullptr;   // A/B switch
+// A/B switch: MRAGAN_NO_X3_FIN=1 leaves the 8-wave brick's statistics to the finalize launch
+static const bool g_no_x3_fin = getenv("MRAGAN_NO_X3_FIN") != nullptr;
 // the staged variant exists for bf16x3 only (MFMA split modes 2/3 always run conv_brick_x3.hip)
 bool conv_brick_x3_active(const IgemmArgs& a) {
   return a.x3 && !(g_staged_x3 && a.x3 == 1) && conv_brick_applicable(a);
@@ -446,6 +448,13 @@ int conv_brick(const IgemmArgs& g, hipStream_t st, bool interior) {
     if (g.in_part) {
       a.part = g.in_part;
       if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
+      // in-launch finalize (ABI 15) where the tile's columns fit the reducer (BN ≤ 128)
+      if (g.in_tick && c.bn <= 128 && !g_no_x3_fin) {
+        a.tick = g.in_tick; a.fin0 = g.in_fin0; a.fin1 = g.in_fin1;
+        a.fin_mode = g.bs_x ? 1 : 0;
+        a.fin_S = g.bs_x ? (double)g.Di * g.Hi * g.Wi : (double)a.Do * a.Ho * a.Wo;
+        if (g.in_finalized) *g.in_finalized = 1;
+      }
     }
     return conv_brick_x3_launch(a, c.bm, c.bn, g.ws, g.ws_bytes, g.wx3, g.x3, st);
   }

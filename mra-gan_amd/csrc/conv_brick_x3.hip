@@ -23,6 +23,7 @@
 // Precision modes (prec.h): bf16x3 as above; bf16 / fp16 run one MFMA per block product and
 // neither store nor load the lo planes (halo rows keep their layout, the lo half stays unused).
 #include "conv_geo.h"
+#include "in_ticket.h"
 #include "kernels.h"
 #include "prec.h"
 
@@ -389,8 +390,19 @@ conv_brick_x3_kernel(BrickArgs a) {
         q2 += red[(w * BN + c) * 2 + 1];
       }
       double* dst = a.part + (((int64_t)nb * chunks + brick) * a.ny + n0 + c) * 2;
-      dst[0] = s2;
-      dst[1] = q2;
+      if (a.tick) {                     // write-through: the tile's reducer reads them (in_ticket.h)
+        st_sc1(dst, s2);
+        st_sc1(dst + 1, q2);
+      } else {
+        dst[0] = s2;
+        dst[1] = q2;
+      }
+    }
+    // ABI 15 (round 6 for this kernel): the last block of this (instance, column tile) finalizes
+    // its statistics — μ / rstd, or the IN backward's coefficients — in the launch, as the K-split
+    // brick does: the 18³ data gradient at N = 4 (this kernel) no longer leaves a finalize launch
+    if (a.tick && in_ticket_draw(a.tick + nb * a.gn + nbk, chunks, reinterpret_cast<int*>(halo_buf))) {
+      if (tid < 256) in_ticket_reduce<BN>(a.part, chunks, a.ny, nb, n0, a.fin_mode, a.fin_S, a.fin0, a.fin1);
     }
   }
 }

@@ -490,13 +490,18 @@ class CycleGANModel(BaseModel):
         # waits for the other lane's generator pack only before its cycle pass: the four repacks
         # no longer run serially ahead of the fork
         ln = self._lanes()
+        # the discriminators are first used on the side streams in the overlapped schedule: their
+        # repacks run there (backward_G), off the lanes' critical start
+        d_here = not (self._overlap_D() and not _FROZEN_D_ON_LANES)
         with ln.on(0):
             pGA.ensure_packed()
-            self.netD_A.plan.ensure_packed()
+            if d_here:
+                self.netD_A.plan.ensure_packed()
             packed_0 = ln.mark(0)
         with ln.on(1):
             pGB.ensure_packed()
-            self.netD_B.plan.ensure_packed()
+            if d_here:
+                self.netD_B.plan.ensure_packed()
             packed_1 = ln.mark(1)
         with ln.on(0):          # lane 0: G_A(real_A) → G_B(fake_B)
             self._cGA1 = pGA.forward(torch.cat([A, B], 0) if self._idt else A)   # [fake_B; idt_A]
@@ -569,12 +574,14 @@ class CycleGANModel(BaseModel):
         if side is not None:
             adam_in = self._adam_in_lanes()
             with side.on(0):
+                pDA.ensure_packed()
                 self._cDA1 = frozen(pDA, self._fake_B, 1, dDA)
                 d_done_A = side.mark(0)
                 self.backward_D_A()
                 if adam_in:     # D_A's parameters are read on this stream only
                     self.optimizer_D.step_net(self.netD_A, self._step_hyper[6:12])
             with side.on(1):
+                pDB.ensure_packed()
                 self._cDB1 = frozen(pDB, self._fake_A, 5, dDB)
                 d_done_B = side.mark(1)
                 self.backward_D_B()

@@ -772,8 +772,9 @@ def test_op16_dgrad_skip_statistics(op16, N, S, act, fin):
 
 @pytest.mark.parametrize("N,S", [(2, 16), (4, 16), (1, 12)])
 def test_in_launch_finalize(op16, N, S):
-    """ABI 15: the K-split brick's last block per (instance, column tile) finalizes the InstanceNorm
-    statistics (ticket counters, write-through partials): the conv output and partials are
+    """ABI 15: the bricks' last block per (instance, column tile) finalizes the InstanceNorm
+    statistics (ticket counters, write-through partials; the K-split brick, and since round 6 the
+    8-wave brick of the 18³ data gradient at N = 4): the conv output and partials are
     bit-identical to the non-finalizing launch, μ / rstd and the backward coefficients agree with the
     finalize kernel to fp64 summation-order noise, and repeated launches (tickets reset by the last
     block) give bit-identical results."""
@@ -813,8 +814,8 @@ def test_in_launch_finalize(op16, N, S):
     dz, cb, coef = ops.conv3d_op16_dgrad_in_stats(dh2, wp_b, C, ws_b, y, m, r, "relu", pb, fin=True)
     assert torch.equal(dz, dz_ref) and cb == cb_ref > 0
     ref = ops.instnorm_bwd_partials_op16(y, m, r, dz_ref, 1, None, "relu", pb_ref, cb_ref)
-    if coef is None:
-        pytest.skip("this data-gradient shape runs the 8-wave brick (no in-launch finalize)")
+    # the 8-wave brick (the 18³ data gradient at N = 4) finalizes in-launch too since round 6
+    assert coef is not None, "the data gradient did not finalize in-launch"
     got = ops.instnorm_bwd_partials_op16(y, m, r, dz, 1, None, "relu", pb, cb, coef=coef)
     assert (got != ref).float().mean().item() < 1e-3
 
