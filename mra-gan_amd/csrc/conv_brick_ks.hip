@@ -624,6 +624,13 @@ int conv_brick_ks(BrickArgs a, int ny, void* ws, size_t ws_bytes, const void* ws
   const bool big_bs = ks_big && a.sx && best[0] >= 6.0;
   if (!force && best[0] > 2.0 && !big_bs) return kUnsupported;
   const int* b = shapes[best_s];
+  // experiment (A/B switch MRAGAN_KS_SMALL_DB1=1): a grid of at most one block per CU in the
+  // two-per-CU variant (N = 2 at 16³: 256 blocks) may be packed two to a CU by the dispatcher,
+  // leaving half the CUs idle; the one-per-CU variant cannot be
+  static const bool small_db1 = getenv("MRAGAN_KS_SMALL_DB1") != nullptr;
+  if (small_db1 && !force && best_v == 0 &&
+      (int64_t)a.N * ceil_div(a.Do, b[0]) * ceil_div(a.Ho, b[1]) * ceil_div(a.Wo, b[2]) * (ny / 32) <= 256)
+    best_v = 1;
   const Var& V = vars[best_v];
   a.BD = b[0]; a.BH = b[1]; a.BW = b[2];
   a.HD = b[0] + 2; a.HH = b[1] + 2; a.HW = b[2] + 2;

@@ -302,8 +302,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
     const int er0 = tid / kBW, er1 = (tid + 256) / kBW, ep = tid % kBW;
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 0] = __builtin_amdgcn_s_memtime();
 
-    // the item's instance's μ / rstd of the backward statistics' x̂ (EPI 2), read from LDS in the
-    // epilogue (32 registers fewer: the two-waves-per-SIMD form fits 256)
+    // the item's instance's μ / rstd of the backward statistics' x̂ (EPI 2), staged through LDS;
+    // each lane keeps its 4 store-layout channels' values in registers (below)
     float* sstat = reinterpret_cast<float*>(smem + (CMP ? kFLdsC : kFLds) + 4 * kC * 2 * 8);
     if constexpr (EPI == 2) {
       if (tid < 2 * kC) sstat[tid] = tid < kC ? a.smean[nb * kC + tid] : a.srstd[nb * kC + tid - kC];
@@ -332,6 +332,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
     }
     __syncthreads();
     if (a.stamp && tid == 0 && item < kMaxItemsStamped) g_thin1_stamps[item * 3 + 1] = __builtin_amdgcn_s_memtime();
+    // EPI 2: μ / rstd of this lane's 4 store-layout channels 16·lh + 4·kq4 + c (8 registers per item)
+    float smu[4], srs[4];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        smu[c] = sstat[16 * lh + 4 * kq4 + c];
+        srs[c] = sstat[kC + 16 * lh + 4 * kq4 + c];
+      }
+    }
 
     // InstanceNorm partials of this item (a.part): lane (li, lh) holds channels 16·lh + q of its
     // voxels; fp64 throughout, y² formed in fp64 as the other producers do (fp32 sums of y and y²
@@ -340,7 +349,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
     // The backward statistics (EPI 2: Σg, Σg·x̂ — no variance formula, nothing cancels against a
     // square) accumulate in fp32 over the item's ≤ 32 values per lane and channel and join the fp64
     // sums at the item's end: 4 VALU fewer per value than fp64 throughout (r05i PMC: 10 VALU per MFMA)
-    constexpr int NS = EPI ? 16 : 1;
+    // (EPI 2, round 6: in the store layout — 4 channels per lane, see the epilogue)
+    constexpr int NS = EPI == 1 ? 16 : EPI == 2 ? 4 : 1;
     using AccT = typename std::conditional<EPI == 2, float, double>::type;
     AccT ps[NS], pq[NS];
 #pragma unroll
@@ -361,8 +371,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
       // under them (loaded in the epilogue they stalled every depth step: +0.17 ms per step)
       // Loaded in the store layout (below): lane (4m + k, lh) reads the 16-B piece k of the four
       // voxels 4m … 4m + 3 of its tile row — each load instruction then covers 8 voxels' whole
-      // 128-B rows instead of 16-B pieces of 32 rows — and a quad transpose after the MFMAs
-      // turns them into this lane's own voxel's pieces
+      // 128-B rows instead of 16-B pieces of 32 rows — and the statistics are formed in that layout
+      // against the quad-transposed accumulators the stores use
       float4 sxv[2][EPI == 2 ? 4 : 1];
       if constexpr (EPI == 2) {
         const int Sd = a.Do - 2 * a.sfold, Sh = a.Ho - 2 * a.sfold, Sw = a.Wo - 2 * a.sfold;
@@ -384,9 +394,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
       // issued a whole K-step earlier
       constexpr bool kTwo = prec::has_lo<PM>() || C2;
       auto frag = [&](int ks, bf16x8& ah, bf16x8& al, bf16x8 (&xh)[2], bf16x8 (&xl)[2]) __attribute__((always_inline)) {
-        const int g = 2 * ks + lh;
+        // (EPI 2 at TW 2: lh made opaque per K-step, so the compiler forms this K-step's (kd, kh)
+        // and addresses here — two multiply-adds — instead of hoisting all 25 steps' per-lane values
+        // out of the item loop, where they spilled: 40 registers over the 256 budget)
+        int lhv = lh;
+        if constexpr (EPI == 2 && TW == 2) asm volatile("" : "+v"(lhv));
+        const int g = 2 * ks + lhv;
         const int g0 = 2 * ks, g1 = 2 * ks + 1 < kK * kK ? 2 * ks + 1 : kK * kK - 1;
-        const int kd = lh ? g1 / kK : g0 / kK, kh = lh ? g1 % kK : g0 % kK;
+        const int kd = g0 / kK + lhv * (g1 / kK - g0 / kK), kh = g0 % kK + lhv * (g1 % kK - g0 % kK);
         if constexpr (!WREG) {
           ah = wsm[wsel(g, 0, co)];
           al = kTwo ? wsm[wsel(g, 1, co)] : ah;
@@ -450,43 +465,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
             ps[e] += u;
             pq[e] += (double)u * u;
           }
-      } else {
-        // sx pieces from the store layout to this lane's own voxel (component-wise quad transposes:
-        // lane k held piece k of voxels 0 … 3 of its quad, now pieces 0 … 3 of voxel k)
-        float4 own[2][4];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          f32x4v t[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            f32x4v v;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = c == 0 ? sxv[i][j].x : c == 1 ? sxv[i][j].y : c == 2 ? sxv[i][j].z : sxv[i][j].w;
-            t[c] = quad_transpose(v, kq4);
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) own[i][q] = make_float4(t[0][q], t[1][q], t[2][q], t[3][q]);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 xv = own[i][q];
-            const float4 mu4 = *reinterpret_cast<const float4*>(sstat + 16 * lh + 4 * q);
-            const float4 rs4 = *reinterpret_cast<const float4*>(sstat + kC + 16 * lh + 4 * q);
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, smu[4] = {mu4.x, mu4.y, mu4.z, mu4.w},
-                        srs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float vs = acc[i][4 * q + e];
-              const float xh = (xs[e] - smu[e]) * srs[e];
-              const float g0 = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
-                               : (a.sact == kActLrelu && !(xh > 0.f)) ? vs * kLreluSlope : vs;
-              const float gv = in[i] ? g0 : 0.f;
-              ps[4 * q + e] += gv;
-              pq[4 * q + e] = fmaf(gv, xh, pq[4 * q + e]);
-            }
-          }
       }
       if constexpr (EPI == 2) {
         // the compiler sinks the statistics below the stores; this empty asm reads the sx values
@@ -510,6 +488,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
           t[c] = quad_transpose(v, kq4);
         }
         const int oh = oh0 + bh0 + 2 * i;
+        if constexpr (EPI == 2) {
+          // backward statistics in the store layout (round 6): t[c][j] and sxv[i][j] are channel
+          // 16·lh + 4·kq4 + c of voxel (oh, ow0 + bwq + j) — no transposes of x̂ to the lane's own
+          // voxel, 8 accumulators instead of 32 (the two-blocks-per-CU form fits 256 registers)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool vin = oh < a.Ho && ow0 + bwq + j < a.Wo;
+            const float xs[4] = {sxv[i][j].x, sxv[i][j].y, sxv[i][j].z, sxv[i][j].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float vs = t[c][j];
+              const float xh = (xs[c] - smu[c]) * srs[c];
+              const float g0 = (a.sact == kActRelu && !(xh > 0.f)) ? 0.f
+                               : (a.sact == kActLrelu && !(xh > 0.f)) ? vs * kLreluSlope : vs;
+              const float gv = vin ? g0 : 0.f;
+              ps[c] += gv;
+              pq[c] = fmaf(gv, xh, pq[c]);
+            }
+          }
+        }
         float* yrow = a.y + (((int64_t)nb * a.Do + od) * a.Ho + oh) * (int64_t)a.Wo * kC + 16 * lh + 4 * kq4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -528,16 +526,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TW, TW
       // item = nb · (items per instance) + (chunk · nbh + chh) · nbw + cw: the partials' chunk order
       double* red = reinterpret_cast<double*>(smem + (CMP ? kFLdsC : kFLds));
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < NS; ++q) {
         double s2 = (double)ps[q], q2 = (double)pq[q];
+        // EPI 1: lane (li, lh) holds channels 16·lh + q; EPI 2: channels 16·lh + 4·(li & 3) + q
 #pragma unroll
-        for (int m = 1; m < 32; m <<= 1) {
+        for (int m = EPI == 2 ? 4 : 1; m < 32; m <<= 1) {
           s2 += __shfl_xor(s2, m);
           q2 += __shfl_xor(q2, m);
         }
-        if (li == 0) {
-          red[(wave * kC + 16 * lh + q) * 2] = s2;
-          red[(wave * kC + 16 * lh + q) * 2 + 1] = q2;
+        const int ch = EPI == 2 ? 16 * lh + 4 * li + q : 16 * lh + q;
+        if (EPI == 2 ? li < 4 : li == 0) {
+          red[(wave * kC + ch) * 2] = s2;
+          red[(wave * kC + ch) * 2 + 1] = q2;
         }
       }
       __syncthreads();
@@ -588,7 +588,7 @@ template <int PM, int C2, int TW>
 static void launch_thin1_fwd(const Thin1RArgs& a, int grid, hipStream_t st) {
   if (!a.part) launch_thin1_fwd_e<PM, C2, 0, TW>(a, grid, st);
   else if (!a.sx) launch_thin1_fwd_e<PM, C2, 1, TW>(a, grid, st);
-  else launch_thin1_fwd_e<PM, C2, 2, 1>(a, grid, st);   // (the caller picks TW 1: its registers spill at 256)
+  else launch_thin1_fwd_e<PM, C2, 2, TW>(a, grid, st);
 }
 
 // two blocks per CU in the one-plane one-channel case (A/B switch: MRAGAN_THIN1_TW=1)
@@ -635,7 +635,10 @@ static int conv_thin1_pm(const ThinArgs& t, void* ws, size_t ws_bytes, hipStream
                              : !t.trans);
   // two blocks per CU for the plain and forward-statistics forms (the backward-statistics one
   // needs more than 256 registers)
-  const int tw = (!prec::has_lo<PM>() && !c2 && !(stats && t.bs_x)) ? thin1_tw() : 1;
+  // (the backward-statistics form too since round 6: its statistics in the store layout take 215
+  // registers; A/B switch MRAGAN_THIN1_BS_TW1 keeps it at one block per CU)
+  static const bool bs_tw1 = getenv("MRAGAN_THIN1_BS_TW1") != nullptr;
+  const int tw = (!prec::has_lo<PM>() && !c2 && !(stats && t.bs_x && bs_tw1)) ? thin1_tw() : 1;
   pick_chunk(columns, t.Do, tw * cu_count(), a.L, a.nch, grid);
   a.items = (int)(columns * a.nch);
   if (stats) {

@@ -115,6 +115,10 @@ def main():
         "res_fwd16": lambda: ops.conv3d_op16(x_res16, w_res, c4, 3, 1, 0, (s4, s4, s4), ws_res_f, part_res),
         "res_dgrad16": lambda: ops.conv3d_op16(dy_res16, w_res, c4, 3, 1, 0, (s4 + 2,) * 3, ws_res_b, transposed=True),
         "res_wgrad16": lambda: ops.conv3d_wgrad_op16(dy_res16, x_res16, 3, 1, 0, gw_res, False),
+        # the step's form since round 6 (ABI 19): a generator's first-pass (N) and cycle-pass (N/2)
+        # instances of one ResnetBlock conv in one launch
+        "res_wgrad16p": lambda: ops.conv3d_wgrad_op16_pair(dy_res16, x_res16, dy_res16[:N // 2], x_res16[:N // 2],
+                                                           3, 1, 0, gw_res, False),
         # the step's form of the res dgrad: with the backward statistics of the IN in front (ABI 11)
         "res_dgrad16s": lambda: ops.conv3d_op16_dgrad_in_stats(dy_res16, w_res, c4, ws_res_b, h1_res, m_res, r_res,
                                                                "relu", part_bs),
