@@ -24,11 +24,28 @@
 // planes), bf16 and fp16 (one MFMA per block product, hi planes only).
 #include <type_traits>
 
+#include <atomic>
+
 #include "conv_geo.h"
+#include "in_ticket.h"
 #include "kernels.h"
 #include "prec.h"
 
 namespace mragan {
+
+// Split-K reduction in the launch (round 6, opt-in: MRAGAN_SK_FUSE=1): the slices of an output tile
+// store their partial tiles write-through, draw a ticket from the tile's counter (in_ticket.h's
+// hand-off), and the block that draws the last one sums the tile's slabs in slice order and writes
+// y = act(bias + Σ_z slab_z) — conv_splitk_reduce's arithmetic element for element (bit-identical),
+// without its launch and the dependency gap in front of it — and, for forward statistics, the
+// InstanceNorm partials of the tile.  Measured SLOWER on the UNet leg (same box, alternating:
+// 3.62-3.63 against 3.55-3.57 ms with the reduce launch, profiles/r06/r06o_sk_fuse_ab.txt): one block
+// per tile sums every slice of it (a 64×64 tile of a 16-way split: 256 loads per thread) while the
+// reduce launch spreads the same sums over the whole chip, and a graph-replayed launch gap is short.
+// Counters: a zeroed device pool, slots handed out round-robin per launch by the host; the reducer
+// resets its counter.
+constexpr int kSkSlots = 1 << 20;
+__device__ unsigned g_sk_tickets[kSkSlots];
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -75,6 +92,7 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
 
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
   __shared__ int out_off[BM];
+  __shared__ int sk_flag;
 
   // XCD-aware tile order: hardware puts block L on XCD L % 8; give each XCD a contiguous range
   const int kz = blockIdx.x / ntiles;                 // split-K slice
@@ -330,7 +348,9 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
   // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Split-K slices write raw partial tiles to their slab; conv_splitk_reduce applies bias/act.
   if (ksplit > 1) {
-    float* slab = a.ws + (int64_t)kz * ((int64_t)a.N * a.Do * a.Ho * a.Wo * a.ny);
+    const int64_t E = (int64_t)a.N * a.Do * a.Ho * a.Wo * a.ny;     // one slab
+    float* slab = a.ws + (int64_t)kz * E;
+    const bool fused = a.sk_slot >= 0;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       int col = n0 + wn0 + j * 32 + li;
@@ -340,8 +360,76 @@ conv_igemm_x3_kernel(IgemmArgs a, int gm, int gn, int ntiles, int ksplit) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           int off = out_off[wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh];
-          if (off >= 0) slab[(int64_t)off * a.ny + col] = acc[i][j][r];
+          if (off >= 0) {
+            float* p = slab + (int64_t)off * a.ny + col;
+            if (fused) __hip_atomic_store(p, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else *p = acc[i][j][r];
+          }
         }
+    }
+    if (!fused || !in_ticket_draw(&g_sk_tickets[a.sk_slot + L], ksplit, &sk_flag)) return;
+    // the last slice of this tile: conv_splitk_reduce's sum for the tile's outputs (columns fastest;
+    // per thread EB outputs × ZB slices of loads in flight at once, summed in slice order)
+    constexpr int EB = 8, ZB = 4;
+    static_assert(256 % BN == 0, "a reducer thread keeps one column");
+    double rps = 0.0, rpq = 0.0;             // its column's Σy, Σy² (InstanceNorm partials, a.in_part)
+    for (int e0 = tid; e0 < BM * BN; e0 += 256 * EB) {
+      int64_t idx[EB];
+      float v[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int e = e0 + u * 256;
+        const int r = e / BN, col = n0 + e % BN;
+        const int off = e < BM * BN ? out_off[r] : -1;
+        idx[u] = (off < 0 || col >= a.ny) ? -1 : (int64_t)off * a.ny + col;
+        v[u] = (idx[u] >= 0 && a.bias) ? a.bias[col] : 0.f;
+      }
+      for (int z0 = 0; z0 < ksplit; z0 += ZB) {
+        float t[ZB][EB];
+#pragma unroll
+        for (int zz = 0; zz < ZB; ++zz)
+#pragma unroll
+          for (int u = 0; u < EB; ++u)
+            t[zz][u] = (z0 + zz < ksplit && idx[u] >= 0)
+                           ? __hip_atomic_load(a.ws + (int64_t)(z0 + zz) * E + idx[u], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.f;
+#pragma unroll
+        for (int zz = 0; zz < ZB; ++zz)
+#pragma unroll
+          for (int u = 0; u < EB; ++u)
+            if (z0 + zz < ksplit) v[u] += t[zz][u];
+      }
+#pragma unroll
+      for (int u = 0; u < EB; ++u)
+        if (idx[u] >= 0) {
+          const float yv = act_fwd(v[u], a.act);
+          a.y[idx[u]] = yv;
+          rps += yv;
+          rpq += (double)yv * yv;
+        }
+    }
+    if (a.in_part) {
+      // the tile's partial as the unsplit epilogue leaves it (same chunk index; the host allows it
+      // for forward statistics without bias / activation): the 256 / BN threads of a column in order
+      double* red = reinterpret_cast<double*>(smem);
+      red[2 * tid] = rps;
+      red[2 * tid + 1] = rpq;
+      __syncthreads();
+      if (tid < BN && n0 + tid < a.ny) {
+        double s2 = 0.0, q2 = 0.0;
+        for (int k = tid; k < 256; k += BN) {
+          s2 += red[2 * k];
+          q2 += red[2 * k + 1];
+        }
+        const int64_t qv = Mc / a.N;
+        const int nb = (int)(m0 / qv);
+        const int cpc = (int)(qv / BM);
+        const int chunk = cls * cpc + (int)((m0 - (int64_t)nb * qv) / BM);
+        double* dst = a.in_part + (((int64_t)nb * (a.nclass * cpc) + chunk) * a.ny + n0 + tid) * 2;
+        dst[0] = s2;
+        dst[1] = q2;
+      }
     }
     return;
   }
@@ -562,14 +650,31 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
       return kWorkspace;
     }
   }
-  // InstanceNorm partials from the epilogue: no K split, every tile inside one instance and one
-  // class, every class the same row count (forward convs, and transposed ones whose output is a
-  // whole multiple of the stride)
+  // split-K reduced in the launch (opt-in MRAGAN_SK_FUSE=1, see g_sk_tickets); the tile counters of
+  // one launch are consecutive pool slots, handed out round-robin
+  static const bool sk_fuse = getenv("MRAGAN_SK_FUSE") != nullptr;
+  a.sk_slot = -1;
+  if (sk_fuse && pl.splits > 1) {
+    const int bm = kX3Cfg[pl.cfg].bm, bn = kX3Cfg[pl.cfg].bn;
+    const int64_t nt = (int64_t)ceil_div(max_mc, bm) * ceil_div(a.ny, bn) * a.nclass;
+    if (nt <= kSkSlots / 4) {
+      static std::atomic<int64_t> next{0};
+      int64_t s0 = next.fetch_add(nt) % kSkSlots;
+      if (s0 + nt > kSkSlots) s0 = 0;     // (a wrap skips the pool's tail: slots stay disjoint)
+      a.sk_slot = (int)s0;
+    }
+  }
+  // InstanceNorm partials from the epilogue: no K split (or one the launch reduces itself), every
+  // tile inside one instance and one class, every class the same row count (forward convs, and
+  // transposed ones whose output is a whole multiple of the stride)
   if (a.in_part) {
     const int bm = kX3Cfg[pl.cfg].bm;
     const int64_t per_cls = total_m / ((int64_t)a.N * a.nclass);
     const bool even = per_cls * a.N * a.nclass == total_m && per_cls == max_mc / a.N && max_mc % a.N == 0;
-    if (pl.splits == 1 && !a.shell && even && per_cls % bm == 0 && a.bias == nullptr && a.act == kActNone) {
+    // (split-K: where the launch reduces its slices itself, forward statistics only — the reducer
+    // forms them from the summed outputs)
+    const bool split_ok = pl.splits == 1 || (a.sk_slot >= 0 && a.bs_x == nullptr);
+    if (split_ok && !a.shell && even && per_cls % bm == 0 && a.bias == nullptr && a.act == kActNone) {
       if (a.in_chunks) *a.in_chunks = (int)(a.nclass * (per_cls / bm));
     } else {
       a.in_part = nullptr;
@@ -586,7 +691,7 @@ int conv_igemm_x3(IgemmArgs a, int64_t max_mc, int64_t total_m, hipStream_t st) 
   int rc = use64 ? dispatch_x3<64>(a, max_mc, pl.cfg, pl.splits, st)
            : a.cx % 32 == 0 ? dispatch_x3<32>(a, max_mc, pl.cfg, pl.splits, st)
                             : dispatch_x3<16>(a, max_mc, pl.cfg, pl.splits, st);
-  if (rc || pl.splits == 1) return rc;
+  if (rc || pl.splits == 1 || a.sk_slot >= 0) return rc;
   const int64_t E = total_m * a.ny;
   int blocks = (int)((E + 255) / 256);
   if (blocks > 4096) blocks = 4096;

@@ -30,6 +30,7 @@ struct IgemmArgs {
   // (BrickArgs::tick …); *in_finalized = 1 when it did, else left 0 (the caller finalizes)
   unsigned* in_tick = nullptr; float* in_fin0 = nullptr; float* in_fin1 = nullptr; int* in_finalized = nullptr;
   int tmode = 0;    // conv_igemm_x3 timing-only A/B (MRAGAN_IG_TIMING; wrong results by design)
+  int sk_slot = -1; // conv_igemm_x3 split-K: first ticket slot of the in-launch reduction (< 0: reduce launch)
 };
 int conv_igemm(IgemmArgs a, hipStream_t st);
 size_t conv_igemm_ws_bytes(IgemmArgs a);

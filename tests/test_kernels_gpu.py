@@ -321,6 +321,57 @@ def test_conv3d_bf16x3_fwd_dgrad(x3, N, cin, cout, S, k, s, p):
     check_rounded(ncdhw(dx), dx_rnd, dx_ref)
 
 
+def test_splitk_in_launch_reduce_bit_identical(ops, tmp_path):
+    """Round 6, opt-in (MRAGAN_SK_FUSE=1, run in a child process): the implicit GEMM's split-K
+    slices reduce in the launch (the last slice of a tile, by ticket, sums the slabs in slice order)
+    — bit-identical to the separate conv_splitk_reduce launch of the default path, in every mode,
+    on the PatchGAN and UNet split-K shapes (forward with bias + LeakyReLU, and the transposed k4 s2
+    form); its InstanceNorm partials match the statistics pass."""
+    import os
+    import subprocess
+    import sys
+    g = torch.Generator().manual_seed(606)
+    cases = []
+    for prec in ("bf16x3", "bf16", "fp16"):
+        for N, cin, cout, S, k, s, p, tr, act in [(4, 64, 128, 16, 4, 2, 1, False, "lrelu"),   # PatchGAN layer 3
+                                                  (4, 128, 256, 8, 4, 1, 1, False, "lrelu"),   # PatchGAN layer 4
+                                                  (1, 256, 256, 8, 4, 2, 1, False, "none"),    # UNet inner down
+                                                  (2, 128, 64, 8, 4, 2, 1, True, "none")]:     # UNet up (convT)
+            x = torch.randn(N, S, S, S, cin, generator=g)
+            if tr:
+                w = pack(ops, torch.randn(cin, cout, k, k, k, generator=g, dtype=torch.float64) * 0.05, True, False)
+                o = ops.convT_out_size(S, k, s, p, 0)
+            else:
+                w = pack(ops, torch.randn(cout, cin, k, k, k, generator=g, dtype=torch.float64) * 0.05, False, False)
+                o = ops.conv_out_size(S, k, s, p)
+            b = torch.randn(cout, generator=g) if act != "none" else None
+            cases.append(dict(prec=prec, x=x, w=w.cpu(), b=b, cout=cout, k=k, s=s, p=p, osp=[o, o, o], act=act, tr=tr,
+                              stats=(act == "none" and not tr)))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _splitk_child
+    mine = _splitk_child.run(ops, cases)
+    fin, fout = tmp_path / "in.pt", tmp_path / "out.pt"
+    torch.save(cases, fin)
+    env = dict(os.environ, MRAGAN_SK_FUSE="1")
+    subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "_splitk_child.py"),
+                    str(fin), str(fout)], env=env, check=True, timeout=300)
+    fused = torch.load(fout, weights_only=True)
+    assert len(fused) == len(mine)
+    i = 0
+    for c in cases:
+        a, b = mine[i], fused[i]
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b), (c["prec"], c["x"].shape, c["cout"], c["tr"])
+        i += 1
+        if c["stats"]:
+            assert float(fused[i]) > 0 and float(mine[i]) == 0       # partials only from the fused launch
+            ops.set_conv_precision(c["prec"])
+            _, m_ref, r_ref = ops.instnorm_fwd(a.cuda(), act="lrelu", ypad=1)   # statistics pass
+            ops.set_conv_precision("f32")
+            assert rel(fused[i + 1], m_ref) < 1e-6 and rel(fused[i + 2], r_ref) < 1e-6
+            i += 3
+
+
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p", X3_CASES + [(2, 32, 32, 9, 3, 1, 1), (1, 64, 256, 6, 4, 1, 1),
                                                    (2, 64, 32, 10, 3, 2, 1), (3, 32, 64, 11, 3, 2, 1),
                                                    # one split (the UNet's inner layers)
@@ -1102,6 +1153,7 @@ def test_op16_rejected_outside_16bit_modes(ops):
     (2, 2, 32, 22, 7, 1, 0, False, "1p", 0),       # nc = 2 stem: thin1 with two channels (one-plane modes)
     (1, 2, 32, 27, 7, 1, 0, False, "1p", 0),       # … with partial output columns
     (2, 32, 64, 16, 4, 2, 1, False, False, 0),     # PatchGAN layer 2 (k4 s2 p1): split in K → stats pass
+    (1, 256, 256, 8, 4, 2, 1, False, False, 0),    # UNet inner down conv: 16 slices → stats pass
     (1, 128, 256, 8, 4, 1, 1, False, False, 0),    # PatchGAN layer 4: 7³ rows, no whole tiles → stats pass
 ])
 def test_igemm_in_stats_partials(x3, N, cin, cout, S, k, s, p, tr, expect, dc):
