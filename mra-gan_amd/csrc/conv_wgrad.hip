@@ -357,6 +357,87 @@ static int launch_wgrad_reduce(const float* ws, float* out, int Cd, int Cg, int 
   return check_launch("wgrad_reduce");
 }
 
+// Short-contraction weight gradient (round 6): the UNet's innermost layers
+// (networks3D.py:300-330 — Conv3d / ConvTranspose3d(8ngf, 8ngf, k4 s2) on 4³ / 2³ grids, the k4 s2
+// layers on 4³) contract over M = N·Dd·Hd·Wd ≤ 128 voxels but write Cd·Cg·64 outputs (16.8 MB at
+// 256 × 256).  On the split-K path that is one MFMA K-step per block, a 4-B-strided slab write of
+// the whole gradient and a reduce that reads it back: 26-30 µs per launch, launch-latency and
+// store bound at 0.001-0.002 of peak.  Here one thread owns one (gn, tap) column of the torch layout
+// [dn][gn][t] for kSmR consecutive dn: per contraction voxel one gathered G load feeds kSmR FMAs
+// whose D values come from an LDS broadcast, and the block stores kSmR runs of 256 contiguous
+// floats straight into `out` — no slab, no reduce.  One-plane modes (bf16 / fp16) only: the
+// operands are rounded RNE exactly as the MFMA staging rounds them and a product of two rounded
+// operands is exact in fp32, so this is the MFMA kernel's arithmetic in another (fixed) summation
+// order; the fp32-grade modes keep their kernels (their fixtures' emulation follows those).
+constexpr int kSmR = 16;       // dn rows per thread
+constexpr int kSmMaxM = 128;   // longest contraction this kernel takes
+__global__ void __launch_bounds__(256) wgrad_small_kernel(WgradArgs a, float* __restrict__ out, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float dcol[kSmMaxM][kSmR];     // D[m][dn0 + r], rounded
+  const int T = a.k * a.k * a.k;
+  const int J = a.Cg * T;                                                 // outputs per dn row
+  const int dn0 = blockIdx.y * kSmR;
+  const int M = a.N * a.Dd * a.Hd * a.Wd;
+  for (int e = threadIdx.x; e < M * kSmR; e += 256) {
+    const int m = e / kSmR, r = e % kSmR;
+    dcol[m][r] = op_round(a.D[(int64_t)m * a.Cd + dn0 + r], a.x3);
+  }
+  __syncthreads();
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= J) return;
+  const int gn = j / T, t = j - gn * T;
+  const int tw = t % a.k, th = (t / a.k) % a.k, td = t / (a.k * a.k);
+  float acc[kSmR];
+#pragma unroll
+  for (int r = 0; r < kSmR; ++r) acc[r] = 0.f;
+  int m = 0;
+  for (int nb = 0; nb < a.N; ++nb)
+    for (int md = 0; md < a.Dd; ++md) {
+      const int gd = md * a.s - a.p + td;
+      for (int mh = 0; mh < a.Hd; ++mh) {
+        const int gh = mh * a.s - a.p + th;
+        const bool okdh = (unsigned)gd < (unsigned)a.Dg && (unsigned)gh < (unsigned)a.Hg;
+        for (int mw = 0; mw < a.Wd; ++mw, ++m) {
+          const int gw = mw * a.s - a.p + tw;
+          if (!okdh || (unsigned)gw >= (unsigned)a.Wg) continue;     // zero fill: the product adds 0
+          const float g = op_round(a.G[((((int64_t)nb * a.Dg + gd) * a.Hg + gh) * a.Wg + gw) * a.Cg + gn], a.x3);
+          const float4* dp = reinterpret_cast<const float4*>(dcol[m]);
+#pragma unroll
+          for (int q = 0; q < kSmR / 4; ++q) {
+            const float4 d = dp[q];
+            acc[4 * q] = fmaf(d.x, g, acc[4 * q]);
+            acc[4 * q + 1] = fmaf(d.y, g, acc[4 * q + 1]);
+            acc[4 * q + 2] = fmaf(d.z, g, acc[4 * q + 2]);
+            acc[4 * q + 3] = fmaf(d.w, g, acc[4 * q + 3]);
+          }
+        }
+      }
+    }
+#pragma unroll
+  for (int r = 0; r < kSmR; ++r) {
+    float* dst = out + (int64_t)(dn0 + r) * J + j;
+    *dst = accumulate ? *dst + acc[r] : acc[r];
+  }
+}
+
+// the short-contraction kernel takes this launch (A/B switch MRAGAN_WGRAD_SMALL_M: the longest
+// contraction it takes, 0 = off)
+static bool wgrad_small_applicable(const WgradArgs& a) {
+  static const int max_m = [] {
+    const char* e = getenv("MRAGAN_WGRAD_SMALL_M");
+    const int v = e ? atoi(e) : 64;
+    return v < kSmMaxM ? v : kSmMaxM;
+  }();
+  const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
+  return (a.x3 == kPrecBf16 || a.x3 == kPrecF16) && !a.in16 && !a.in16g && a.N2 == 0 && M <= max_m &&
+         a.Cd % kSmR == 0 && (int64_t)a.Cd * a.Cg * a.k * a.k * a.k < ((int64_t)1 << 31);
+}
+
+static int launch_wgrad_small(const WgradArgs& a, float* out, int accumulate, hipStream_t st) {
+  const int J = a.Cg * a.k * a.k * a.k;
+  hipLaunchKernelGGL(wgrad_small_kernel, dim3(ceil_div(J, 256), a.Cd / kSmR), dim3(256), 0, st, a, out, accumulate);
+  return check_launch("wgrad_small");
+}
+
 static int wgrad_plan(int Cd, int Cg, int T, int64_t M, int* splits, int64_t* chunk, bool* big) {
   *big = (Cd >= 128 && Cg >= 128);
   int bm = *big ? 128 : 64, bn = *big ? 128 : 64;
@@ -433,6 +514,7 @@ int conv_wgrad(WgradArgs a, float* out, int accumulate, size_t ws_bytes, hipStre
       return kOk;
     }
   }
+  if (wgrad_small_applicable(a)) return launch_wgrad_small(a, out, accumulate, st);
   const int T = a.k * a.k * a.k;
   const int64_t M = (int64_t)a.N * a.Dd * a.Hd * a.Wd;
   bool big;

@@ -471,6 +471,43 @@ def test_wgrad_s2_four_tap(x3, N, cin, cout, dims):
     check_rounded(dwt, dwt_rnd, dwt_ref)
 
 
+@pytest.mark.parametrize("N,cin,cout,dims,transposed", [
+    (1, 256, 256, (4, 4, 4), False), (2, 256, 256, (4, 4, 4), False),     # UNet innermost down: M = N·2³
+    (1, 256, 256, (4, 4, 4), True), (2, 256, 256, (4, 4, 4), True),       # innermost up (2³ → 4³)
+    (1, 128, 512, (8, 8, 8), True), (1, 128, 256, (8, 8, 8), False),     # M = 64, the threshold
+    (2, 128, 512, (8, 8, 8), True),                                        # M = 128: the split-K path
+    (1, 20, 48, (4, 6, 2), False), (3, 48, 20, (2, 4, 6), True)])         # ragged dims, 20-wide tiles
+def test_wgrad_short_contraction(x3, N, cin, cout, dims, transposed):
+    """Weight gradients whose contraction is a few voxels (conv_wgrad.hip wgrad_small_kernel in the
+    one-plane modes: the UNet's innermost k4 s2 layers, networks3D.py:300-330) — torch-layout
+    output, no slab, accumulate on and off — vs the fp64 result on the mode's rounded operands."""
+    ops = x3
+    g = torch.Generator().manual_seed(41 + N + cin + 3 * cout + int(transposed))
+    if not transposed:
+        x = torch.randn(N, cin, *dims, generator=g, dtype=torch.float64)
+        w = torch.randn(cout, cin, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1
+        dy = torch.randn(F.conv3d(x, w, stride=2, padding=1).shape, generator=g, dtype=torch.float64)
+        ref = torch.nn.grad.conv3d_weight(x, w.shape, dy, stride=2, padding=1)
+        rnd = torch.nn.grad.conv3d_weight(R(x), w.shape, R(dy), stride=2, padding=1)
+        dense, gathered = ndhwc(dy.float()).cuda(), ndhwc(x.float()).cuda()
+    else:
+        # ConvTranspose3d(cin → cout) on the coarse grid `dims` / 2: D = its input, G = dY
+        xt = torch.randn(N, cin, *[d // 2 for d in dims], generator=g, dtype=torch.float64)
+        wt = (torch.randn(cin, cout, 4, 4, 4, generator=g, dtype=torch.float64) * 0.1).requires_grad_()
+        yt = F.conv_transpose3d(xt, wt, stride=2, padding=1)
+        assert tuple(yt.shape[2:]) == tuple(dims)
+        dyt = torch.randn(yt.shape, generator=g, dtype=torch.float64)
+        (ref,) = torch.autograd.grad(yt, wt, dyt)
+        wr = R(wt).requires_grad_()
+        (rnd,) = torch.autograd.grad(F.conv_transpose3d(R(xt), wr, stride=2, padding=1), wr, R(dyt))
+        dense, gathered = ndhwc(xt.float()).cuda(), ndhwc(dyt.float()).cuda()
+    dw = torch.full(tuple(ref.shape), 3.0, device="cuda")
+    ops.conv3d_wgrad(dense, gathered, 4, 2, 1, dw, accumulate=False)
+    check_rounded(dw, rnd, ref)
+    ops.conv3d_wgrad(dense, gathered, 4, 2, 1, dw, accumulate=True)
+    check_rounded(dw, 2 * rnd, 2 * ref)
+
+
 @pytest.mark.parametrize("N,cin,cout,S,k,s,p,op", CONVT_CASES)
 def test_conv_transpose3d_bf16x3(x3, N, cin, cout, S, k, s, p, op):
     ops = x3
