@@ -35,6 +35,9 @@
 #ifndef MRAGAN_BRICK_KAD1
 #define MRAGAN_BRICK_KAD1 2
 #endif
+#ifndef MRAGAN_BRICK_S2_KPF
+#define MRAGAN_BRICK_S2_KPF 18
+#endif
 
 namespace mragan {
 
@@ -95,7 +98,17 @@ __device__ __forceinline__ void halo_store(char* row, int q, const float4& v) {
 
 }  // namespace
 
-template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16>
+// S = 2 (round 6): the stride-2 forward convs k3 s2 p1 (G down1 / down2,
+// networks3D.py:191-197) on the same kernel.  The output brick's input halo is (2BD+1)(2BH+1)(2BW+1)
+// positions; each halo row of HW = 2BW + 1 positions is stored as its even-w positions then its
+// odd-w ones, so the 32 output voxels of an A fragment (consecutive bw) read consecutive LDS rows in
+// every tap (tap kw = 0 / 2: the even half at sw = bw / bw + 1, kw = 1: the odd half at sw = bw) —
+// the stride-1 kernel's 80-B row stride and brick_row_perm_s's conflict-free GEMM-row assignment
+// hold, and the implicit GEMM's per-K-step tap addressing, bounds checks, LDS stores and barrier
+// (≈ 15 VALU + 17 SALU per MFMA, PMC r05) are gone: one barrier per 32-channel chunk.
+// STREAM = 0: one halo buffer (the 128-row bricks' 1377-position halo fills 110 KB); a further
+// chunk is loaded after the previous one's MFMAs behind a barrier instead of streamed.
+template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16, int S = 1, int STREAM = 1>
 __global__ void __launch_bounds__(WM * WN * 64)
 conv_brick_x3_kernel(BrickArgs a) {
   static_assert(!X16 || !prec::has_lo<PM>(), "16-bit operand planes exist in the one-plane modes only");
@@ -112,11 +125,14 @@ conv_brick_x3_kernel(BrickArgs a) {
   // 3 float4); vmcnt drains in issue order, so a load's real deadline is the next weight wait
   // kPF steps on — kHD < kPF keeps the store inside that window
   constexpr int kHD = 8;
-  static_assert(3 * (NSL - 1) + kHD < kSteps, "halo slices do not fit the chunk's steps");
+  static_assert(!STREAM || 3 * (NSL - 1) + kHD < kSteps, "halo slices do not fit the chunk's steps");
+  static_assert(S == 1 || (S == 2 && !prec::has_lo<PM>()), "stride 2: the one-plane modes only");
   static_assert(BN % 32 == 0 && BM % 32 == 0, "tile");
   // weight prefetch distance in steps; divides kSteps so a ring slot maps to the same step
   // residue in every chunk
-  constexpr int kPF = (!prec::has_lo<PM>() && TN == 1) ? MRAGAN_BRICK_KPF1 : 9;
+  // (S = 2: 18 — one block per CU leaves one wave per SIMD, and 9 steps of 2 MFMAs do not cover the
+  // weight loads' latency under the whole chip's halo traffic)
+  constexpr int kPF = S == 2 ? MRAGAN_BRICK_S2_KPF : (!prec::has_lo<PM>() && TN == 1) ? MRAGAN_BRICK_KPF1 : 9;
   constexpr int kP = 18;                             // unrolled period: ring slots compile-time
   constexpr int kAD = prec::has_lo<PM>() ? 1 : MRAGAN_BRICK_KAD1;    // A-fragment read distance (steps)
   static_assert(kP % (kAD + 1) == 0, "A ring period");
@@ -124,8 +140,9 @@ conv_brick_x3_kernel(BrickArgs a) {
 
   constexpr int kRow = row_bytes<PM>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* halo_buf = smem;                                                // [2][HMAX][kRow]
-  int* out_off = reinterpret_cast<int*>(smem + 2 * HMAX * kRow);       // [BM]
+  constexpr int NBUF = STREAM ? 2 : 1;
+  char* halo_buf = smem;                                                // [NBUF][HMAX][kRow]
+  int* out_off = reinterpret_cast<int*>(smem + NBUF * HMAX * kRow);    // [BM]
   int* hoff = out_off + BM;                                            // [HMAX]
   int* xoff = hoff + HMAX;                                             // [BM] (backward statistics)
 
@@ -168,7 +185,9 @@ conv_brick_x3_kernel(BrickArgs a) {
   }
   for (int pos = tid; pos < HP; pos += NT) {
     const int hw = pos % a.HW, hh = (pos / a.HW) % a.HH, hd = pos / (a.HW * a.HH);
-    const int id = od0 - a.p + hd, ih = oh0 - a.p + hh, iw = ow0 - a.p + hw;
+    // S = 2: halo row position hw < BW + 1 is even w 2·hw, the rest odd w 2·(hw − BW − 1) + 1
+    const int iwl = S == 1 ? hw : (hw <= a.BW ? 2 * hw : 2 * (hw - a.BW - 1) + 1);
+    const int id = S * od0 - a.p + hd, ih = S * oh0 - a.p + hh, iw = S * ow0 - a.p + iwl;
     const bool ok = (unsigned)id < (unsigned)a.Di && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
     hoff[pos] = ok ? ((id * a.Hi + ih) * a.Wi + iw) * a.C : -1;
   }
@@ -179,8 +198,10 @@ conv_brick_x3_kernel(BrickArgs a) {
     int v = a.rowvox[wm0 + i * 32 + li];
     if (v < 0) v = -v - 1;
     const int bd = v / (a.BH * a.BW), bh = (v / a.BW) % a.BH, bw = v % a.BW;
-    abase[i] = ((bd * a.HH + bh) * a.HW + bw) * kRow + lh * 16;
+    abase[i] = ((S * bd * a.HH + S * bh) * a.HW + bw) * kRow + lh * 16;
   }
+  // S = 2: LDS position of tap kw = 1 (the odd half of a halo row)
+  const int wodd = __builtin_amdgcn_readfirstlane(a.BW + 1);
   // B: this lane's 16-B fragment inside each (tap, chunk, half, hi|lo) block of the packed weights,
   // read through a buffer descriptor: the lane part of the offset is fixed (VGPR), the step part
   // is wave-uniform (SGPR soffset) — no per-step 64-bit address arithmetic in VALU (the flat-
@@ -203,21 +224,27 @@ conv_brick_x3_kernel(BrickArgs a) {
   const int nchunks = nch_;
   __syncthreads();
 
-  // whole halo of chunk 0
-  {
-    float4 pv[NSL];                      // all loads in flight before the first store
+  // whole halo of chunk c into buffer 0: all loads in flight before the first store, in batches of
+  // ≤ kWB slices (the stride-2 halos run to 44 slices per thread)
+  constexpr int kWB = NSL < 24 ? NSL : 24;
+  auto halo_whole = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
-    for (int sl = 0; sl < NSL; ++sl) {
-      const int e = sl * NT + tid, pos = e / SPP;
-      const int o = pos < HP ? hoff[pos] : -1;
-      pv[sl] = buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + CPS * (e % SPP)) * (uint32_t)ES);
-    }
+    for (int s0 = 0; s0 < NSL; s0 += kWB) {
+      float4 pv[kWB];
 #pragma unroll
-    for (int sl = 0; sl < NSL; ++sl) {
-      const int e = sl * NT + tid, pos = e / SPP;
-      if (pos < HP) halo_store<PM, X16>(halo_buf + pos * kRow, e % SPP, pv[sl]);
+      for (int q = 0; q < kWB; ++q) {
+        const int sl = s0 + q, e = sl * NT + tid, pos = e / SPP;
+        const int o = (sl < NSL && pos < HP) ? hoff[pos] : -1;
+        pv[q] = buf_load_f32x4(xr, o < 0 ? kOobOffset : (uint32_t)(o + c * kBK + CPS * (e % SPP)) * (uint32_t)ES);
+      }
+#pragma unroll
+      for (int q = 0; q < kWB; ++q) {
+        const int sl = s0 + q, e = sl * NT + tid, pos = e / SPP;
+        if (sl < NSL && pos < HP) halo_store<PM, X16>(halo_buf + pos * kRow, e % SPP, pv[q]);
+      }
     }
-  }
+  };
+  halo_whole(0);
 
   // weight prefetch ring: slot s holds the two float4 of every n-tile for some step ≡ s (mod kPF)
   bf16x8 rb[kPF][TN][2];
@@ -242,16 +269,18 @@ conv_brick_x3_kernel(BrickArgs a) {
   __syncthreads();
 
   for (int c = 0; c < nchunks; ++c) {
-    const char* H = halo_buf + (c & 1) * HMAX * kRow;
+    const char* H = halo_buf + (STREAM ? (c & 1) * HMAX * kRow : 0);
     char* Hn = halo_buf + ((c + 1) & 1) * HMAX * kRow;
-    const bool stream = c + 1 < nchunks;
+    const bool stream = STREAM && c + 1 < nchunks;
     float4 rh[3];
     // A fragments kAD steps ahead (ring of kAD + 1): one LDS round trip (~120 cycles under load)
     // outlasts a one-plane mode's step (1–2 MFMAs), so those read two steps ahead
     bf16x8 af[kAD + 1][2][TM];   // [step mod kAD+1][hi|lo][fragment]
     auto a_read = [&](int u, bf16x8 (&dst)[2][TM]) __attribute__((always_inline)) {
       const int t = u >> 1, kk = u & 1;
-      const int tap_off = (((t / 9) * a.HH + (t / 3) % 3) * a.HW + t % 3) * kRow + kk * 32;
+      const int tw = t % 3;
+      const int tap_off = (((t / 9) * a.HH + (t / 3) % 3) * a.HW + (S == 1 ? tw : tw == 1 ? wodd : tw >> 1)) * kRow +
+                          kk * 32;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         dst[0][i] = *reinterpret_cast<const bf16x8*>(H + abase[i] + tap_off);
@@ -268,7 +297,7 @@ conv_brick_x3_kernel(BrickArgs a) {
       // step's A reads next to their MFMAs and every step waits out a full LDS round trip
       __builtin_amdgcn_sched_barrier(0);
       // next chunk's halo: slice s = u/3 loaded into ring slot s mod 3 (u0/3 ≡ 0 mod 3) …
-      if (du % 3 == 0 && u / 3 < NSL) {
+      if (STREAM && du % 3 == 0 && u / 3 < NSL) {
         const int e = (u / 3) * NT + tid, hpos = e / SPP;
         const int o = (stream && hpos < HP) ? hoff[hpos] : -1;
         rh[(du / 3) % 3] = buf_load_f32x4(
@@ -276,7 +305,7 @@ conv_brick_x3_kernel(BrickArgs a) {
                       : (uint32_t)(o + (c + 1 < nchunks ? c + 1 : c) * kBK + CPS * (e % SPP)) * (uint32_t)ES);
       }
       // … and split + stored kHD steps later
-      if ((du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
+      if (STREAM && (du + kP - kHD) % 3 == 0 && u >= kHD && (u - kHD) / 3 < NSL) {
         const int e = ((u - kHD) / 3) * NT + tid, hpos = e / SPP;
         if (stream && hpos < HP) halo_store<PM, X16>(Hn + hpos * kRow, e % SPP, rh[((du + kP - kHD) / 3) % 3]);
       }
@@ -307,6 +336,11 @@ conv_brick_x3_kernel(BrickArgs a) {
     }
     }
     __syncthreads();
+    if (!STREAM && c + 1 < nchunks) {
+      // one buffer: the next chunk's whole halo after every wave's last reads of this one
+      halo_whole(c + 1);
+      __syncthreads();
+    }
   }
 
   double ps[TN], pq[TN];                 // InstanceNorm statistics of the written values
@@ -407,11 +441,12 @@ conv_brick_x3_kernel(BrickArgs a) {
   }
 }
 
-template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16>
+template <int WM, int WN, int TM, int TN, int HMAX, int PM, int X16, int S = 1, int STREAM = 1>
 static int launch_brick_x3_as(const BrickArgs& a, hipStream_t st) {
   constexpr int BM = WM * TM * 32;
-  const size_t lds = (size_t)2 * HMAX * row_bytes<PM>() + (size_t)(2 * BM + HMAX) * sizeof(int);
-  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM, X16>;
+  const size_t lds = (size_t)(STREAM ? 2 : 1) * HMAX * row_bytes<PM>() + (size_t)(2 * BM + HMAX) * sizeof(int);
+  static_assert((STREAM ? 2 : 1) * HMAX * row_bytes<PM>() + (2 * BM + HMAX) * 4 <= 160 * 1024, "LDS");
+  auto kern = conv_brick_x3_kernel<WM, WN, TM, TN, HMAX, PM, X16, S, STREAM>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -487,6 +522,85 @@ static int brick_x3_launch_pm(BrickArgs a, int bm, int bn, void* ws, size_t ws_b
 int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes, const void* wsplit, int mode,
                          hipStream_t st) {
   MRAGAN_PREC_DISPATCH(mode, return brick_x3_launch_pm<PM>(a, bm, bn, ws, ws_bytes, wsplit, st))
+}
+
+// ---- k3 s2 p1 forward on the brick (S = 2) -------------------------------------------------------
+// Variants (A/B switch MRAGAN_BRICK_S2_VAR):
+//   1: 128-row bricks 4×8×4 (halo 9×17×9 = 1377 positions, 110 KB: one buffer), 128×64 tiles on 4
+//      waves of 64×32;
+//   2: 64-row bricks 2×8×4 (halo 5×17×9 = 765, two buffers streamed), 64×64 tiles on 4 waves of 32×32;
+//   3: 64-row bricks, 64×128 tiles on 4 waves of 64×32;
+//   4: as 2 with one halo buffer (61 KB: two blocks per CU, the next chunk loaded behind a barrier);
+//   5: as 1 on 8 waves of 32×32 (two per SIMD).
+// Both shapes' tap-0 halo rows have at most BM / 16 voxels per residue mod 16 (brick_row_perm: every
+// A read conflict-free).
+// The fp32-input form (the kernel rounds the staged values to the very words of the operand plane)
+// runs the same kernel with one halo buffer: a plane input and an fp32 input give the same bits
+// (tests/test_graph_gpu.py::test_stride2_planes_bit_identical).
+bool conv_brick_s2_applicable(const IgemmArgs& g) {
+  static const bool off = getenv("MRAGAN_NO_BRICK_S2") != nullptr;
+  return !off && (g.x3 == kPrecBf16 || g.x3 == kPrecF16) && g.wx3 && g.k == 3 && g.s == 2 && g.p == 1 &&
+         !g.trans && !g.bs_x && g.act == kActNone && g.cx % kBK == 0 && g.ny % 64 == 0 && g.Di > 0 &&
+         (int64_t)g.Di * g.Hi * g.Wi * g.cx * 4 < ((int64_t)1 << 31);
+}
+
+int conv_brick_s2(const IgemmArgs& g, hipStream_t st) {
+  MRAGAN_CHECK_ARG(conv_brick_s2_applicable(g), "conv_brick_s2: not a k3 s2 p1 operand-plane forward conv");
+  static const int var_env = [] {
+    const char* e = getenv("MRAGAN_BRICK_S2_VAR");
+    return e ? atoi(e) : 0;
+  }();
+  // default 4 (rocprof kernel traces, bf16, r06u: G down2 [4×32³] 21.6 vs the implicit GEMM's 26.4 µs,
+  // [2×32³] 15.7 vs 21.7; G down1 [4×64³] 54.2 vs 56.4, [2×64³] 29.4 vs 29.9 — down1's 64³ input is
+  // streamed once either way, its HBM bytes bound both; variants 1 / 2 / 5 lost on down1, 65.6 /
+  // 82.9 / 59.0 µs: one block per CU leaves one wave per SIMD to wait out its own loads)
+  int var = var_env ? var_env : 4;
+  if (var == 3 && g.ny % 128) var = 2;                 // 64×128 tiles: whole column tiles only
+  BrickArgs a{};
+  a.x = g.x; a.N = g.N; a.Di = g.Di; a.Hi = g.Hi; a.Wi = g.Wi; a.C = g.cx;
+  a.w = g.w; a.wx3 = g.wx3; a.bias = g.bias; a.y = g.y; a.Do = g.Do; a.Ho = g.Ho; a.Wo = g.Wo; a.ny = g.ny;
+  a.act = g.act; a.p = g.p; a.flip = 0;
+  a.ye = 0; a.Yd = g.Do; a.Yh = g.Ho; a.Yw = g.Wo;
+  a.x16 = g.x16;
+  const int bm = (var == 1 || var == 5) ? 128 : 64, bn = var == 3 ? 128 : 64;
+  MRAGAN_CHECK_ARG(g.ny % bn == 0, "conv_brick_s2: %d output channels are not a multiple of the %d-column tile", g.ny, bn);
+  a.BD = (var == 1 || var == 5) ? 4 : 2; a.BH = 8; a.BW = 4;
+  a.HD = 2 * a.BD + 1; a.HH = 2 * a.BH + 1; a.HW = 2 * a.BW + 1;
+  a.nbd = ceil_div(a.Do, a.BD); a.nbh = ceil_div(a.Ho, a.BH); a.nbw = ceil_div(a.Wo, a.BW);
+  a.gn = ceil_div(g.ny, bn);
+  const int64_t ntiles = (int64_t)a.N * a.nbd * a.nbh * a.nbw * a.gn;
+  MRAGAN_CHECK_ARG(ntiles < ((int64_t)1 << 31), "conv_brick_s2: grid too large");
+  a.ntiles = (int)ntiles;
+  if (a.ntiles == 0) return kOk;
+  if (g.in_part) {
+    a.part = g.in_part;
+    if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
+    if (g.in_tick && bn <= 128 && !getenv("MRAGAN_NO_X3_FIN")) {
+      a.tick = g.in_tick; a.fin0 = g.in_fin0; a.fin1 = g.in_fin1;
+      a.fin_mode = 0;
+      a.fin_S = (double)a.Do * a.Ho * a.Wo;
+      if (g.in_finalized) *g.in_finalized = 1;
+    }
+  }
+  brick_row_perm(a.BD, a.BH, a.BW, a.HH, a.HW, bm, a.rowvox, 2);
+  MRAGAN_PREC_DISPATCH(g.x3, {
+    if constexpr (prec::has_lo<PM>()) {
+      set_error("conv_brick_s2: the one-plane modes only");
+      return kBadArg;
+    } else {
+      if (g.x16) {
+        if (var == 1) return launch_brick_x3_as<2, 2, 2, 1, 1380, PM, 1, 2, 0>(a, st);
+        if (var == 3) return launch_brick_x3_as<1, 4, 2, 1, 768, PM, 1, 2, 1>(a, st);
+        if (var == 4) return launch_brick_x3_as<2, 2, 1, 1, 768, PM, 1, 2, 0>(a, st);
+        if (var == 5) return launch_brick_x3_as<4, 2, 1, 1, 1380, PM, 1, 2, 0>(a, st);
+        return launch_brick_x3_as<2, 2, 1, 1, 768, PM, 1, 2, 1>(a, st);
+      }
+      if (var == 1) return launch_brick_x3_as<2, 2, 2, 1, 1380, PM, 0, 2, 0>(a, st);
+      if (var == 3) return launch_brick_x3_as<1, 4, 2, 1, 768, PM, 0, 2, 0>(a, st);
+      if (var == 5) return launch_brick_x3_as<4, 2, 1, 1, 1380, PM, 0, 2, 0>(a, st);
+      return launch_brick_x3_as<2, 2, 1, 1, 768, PM, 0, 2, 0>(a, st);
+    }
+  })
 }
 
 }  // namespace mragan

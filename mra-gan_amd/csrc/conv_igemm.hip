@@ -339,6 +339,8 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
       return rc ? rc : conv_igemm_x3_shell(a, st);
     }
     if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+    // G down1 / down2 (k3 s2 p1 forward) with their pre-split weights: the stride-2 brick (round 6)
+    if (!g_brick_off && conv_brick_s2_applicable(a)) return conv_brick_s2(a, st);
     if (int rc = need_fp32_pack(a)) return rc;
     // 32-output-channel stride-2 transposed convs (G up2, G down1's data gradient): brickT (round 4)
     if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
@@ -352,6 +354,7 @@ int conv_igemm(IgemmArgs a, hipStream_t st) {
     return rc ? rc : conv_igemm_x3_shell(a, st);
   }
   if (!g_brick_off && conv_brick_applicable(a)) return conv_brick(a, st);
+  if (!g_brick_off && conv_brick_s2_applicable(a)) return conv_brick_s2(a, st);
   if (int rc = need_fp32_pack(a)) return rc;
   if (!g_brick_off && brickT_x3_applicable(a)) return conv_brickT_x3(a, st);
   if (a.x3 && a.cx % 16 == 0) return conv_igemm_x3_chunked(a, max_mc, total_m, st);

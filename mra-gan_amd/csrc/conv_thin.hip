@@ -823,10 +823,18 @@ static int thin_wgrad_setup(ThinWgradArgs& a, ThinWgradPlan* pl) {
   const int K = a.k;
   a.nroles = a.vec_dn ? (a.Cd / 4) * K * K : a.Cd * K * K;
   MRAGAN_CHECK_ARG(a.nroles <= 512, "thin_wgrad: %d roles > 512", a.nroles);
+  // ≤ 256 roles: 512 threads (round 6 — the UNet's outermost k4 s2 weight gradients, 32 / 64 × 1
+  // channels: one tile per block, so the tile rows split over RS ≥ 2 threads halve each thread's
+  // serial FMA chain; A/B switch MRAGAN_THIN_WGRAD_T=256 restores 256 threads)
+  static const int nthr = [] {
+    const char* e = getenv("MRAGAN_THIN_WGRAD_T");
+    return e && atoi(e) == 256 ? 256 : 512;
+  }();
   if (a.nroles <= 256) {
-    pl->threads = 256;
-    a.RS = 256 / a.nroles;
+    a.RS = nthr / a.nroles;
     if (a.RS > TW_D * TW_H) a.RS = TW_D * TW_H;
+    pl->threads = (a.nroles * a.RS + 63) / 64 * 64;
+    if (pl->threads < 256) pl->threads = 256;
   } else {
     pl->threads = (a.nroles + 63) / 64 * 64;
     a.RS = 1;

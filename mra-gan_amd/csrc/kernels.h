@@ -80,7 +80,11 @@ int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes,
 size_t conv_brick_x3_ws_bytes(int C, int ny);
 int brick_x3_pack(const float* w, int ny, int C, void* out, int mode, hipStream_t st);
 // GEMM-row → brick-voxel permutation that makes the brick kernels' A reads bank-conflict free
-void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short* rowvox);
+// (S = 2: the stride-2 brick's halo, voxel (bd, bh, bw) reads row (2bd·HH + 2bh)·HW + bw in tap 0)
+void brick_row_perm(int BD, int BH, int BW, int HH, int HW, int BM, short* rowvox, int S = 1);
+// the k3 s2 p1 forward conv on the brick kernel's stride-2 form (conv_brick_x3.hip, round 6)
+bool conv_brick_s2_applicable(const IgemmArgs& a);
+int conv_brick_s2(const IgemmArgs& a, hipStream_t st);
 // bf16 / fp16 k3 s1 brick with the contraction split over the block's 4 waves (conv_brick_ks.hip)
 bool conv_brick_ks_applicable(const IgemmArgs& a);
 int ks_debug_stamps(unsigned long long* host, int n);

@@ -132,7 +132,10 @@ class ConvLayer:
         (_, A, B, _, tf, _), (_, _, _, _, tb, _) = out
         prec = ops.get_conv_precision()
         base = 4 if prec == "fp16" else 2
-        split_f = self._splittable(self.k, self.s, self.cout, self.cin)
+        # (+ the k3 s2 p1 down convs' forward: the stride-2 brick reads the same fragment copy, round 6)
+        split_f = (self._splittable(self.k, self.s, self.cout, self.cin)
+                   or (self.k == 3 and self.s == 2 and self.p == 1 and not self.transposed and self.cin % 32 == 0
+                       and self.cout % 64 == 0))
         split_b = self._splittable(self.k, self.s, self.cin, self.cout)
         if split_f:
             if self.ws_fwd is None or self.ws_fwd.device != w.device:

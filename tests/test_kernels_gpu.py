@@ -948,6 +948,46 @@ def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
     assert rel(gw.view(cout, cin, 3, 3, 3), gw64) < 2e-5
 
 
+@pytest.mark.parametrize("N,cin,cout,dims", [(4, 32, 64, (64, 64, 64)), (2, 64, 128, (32, 32, 32)),
+                                              (1, 32, 64, (20, 18, 26)), (2, 64, 128, (24, 24, 24)),
+                                              (1, 64, 64, (14, 30, 10)), (2, 32, 128, (16, 16, 16))])
+def test_stride2_brick(op16, N, cin, cout, dims):
+    """Round 6: G down1 / down2 (Conv3d k3 s2 p1, networks3D.py:191-197) on the
+    brick kernel's stride-2 form (conv_brick_x3.hip S = 2: LDS halo with even / odd w halves, the
+    pre-split weights).  The operand-plane input and the fp32 input give the same bits (output and
+    InstanceNorm partials); against the fp64 convolution of the rounded operands to 2e-5, the
+    partials against the output's own sums; ragged volumes (partial bricks) included."""
+    ops = op16
+    dt = ops.op16_dtype()
+    g = torch.Generator().manual_seed(N * 13 + cin + cout + dims[2])
+    D, H, W = dims
+    x16 = ndhwc(torch.randn(N, cin, D, H, W, generator=g).float()).cuda().to(dt)
+    x = x16.float()
+    w = torch.randn(cout, cin, 3, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wp_f = pack(ops, w, False, False)
+    ws = _presplit(ops, w, cin, cout, False)
+    osp = tuple((d + 1) // 2 for d in dims)
+    part16 = ops.in_partials_buffer(N, osp, cout, "cuda")
+    # no fp32 pack: only the brick can run (the implicit GEMM refuses without one, ABI 19)
+    y16, ch16 = ops.conv3d_op16(x16, None, cout, 3, 2, 1, osp, ws, part16)
+    part32 = ops.in_partials_buffer(N, osp, cout, "cuda")
+    y32, ch32 = ops.conv3d_in_stats(x, None, cout, 3, 2, 1, osp, ws, part32)
+    assert ch16 == ch32 and ch16 > 0
+    assert torch.equal(y16, y32)
+    n = N * ch16 * cout * 2
+    assert torch.equal(part16[:n], part32[:n])
+    sums = part16[:n].view(N, ch16, cout, 2).sum(1)
+    yd = y16.double()
+    assert rel(sums[..., 0], yd.sum((1, 2, 3))) < 1e-9
+    assert rel(sums[..., 1], (yd * yd).sum((1, 2, 3))) < 1e-9
+    # the implicit GEMM on the same rounded operands (no pre-split copy: the pre-round-6 dispatch)
+    y_ig, _ = ops.conv3d_op16(x16, wp_f, cout, 3, 2, 1, osp, None, None)
+    assert rel(y16, y_ig) < 1e-6
+    if D * H * W <= 40 ** 3:
+        ref = F.conv3d(ncdhw(x.double().cpu()), R(w.float()), stride=2, padding=1)
+        assert rel(ncdhw(y16.double().cpu()), ref) < 2e-5
+
+
 @pytest.mark.parametrize("N,nc,S,W", [(2, 1, 20, 20), (1, 2, 17, 23), (1, 1, 64, 64)])
 def test_k7_planes_bit_identical(op16, N, nc, S, W):
     """ABI 17: the k7 layers on the 16-bit operand plane of their 32-channel operand — the G head

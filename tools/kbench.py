@@ -107,9 +107,17 @@ def main():
         part_bs = ops.in_partials_buffer(N, (s4 + 2,) * 3, c4, dev)
         # G down1 / down2 on the planes of their inputs (ABI 14)
         x_dn1_16, x_dn2_16 = x_dn1.to(dt16), x_dn2.to(dt16)
+        # ... with their pre-split forward weights and IN partials: the stride-2 brick (round 6)
+        ws_dn1, ws_dn2 = torch.empty(w_dn1.numel(), device=dev), torch.empty(w_dn2.numel(), device=dev)
+        ops.pack_weight(w_dn1, 2 * ngf, ngf, 27, base, ws_dn1)
+        ops.pack_weight(w_dn2, c4, 2 * ngf, 27, base, ws_dn2)
+        part_dn1 = ops.in_partials_buffer(N, (s2, s2, s2), 2 * ngf, dev)
+        part_dn2 = ops.in_partials_buffer(N, (s4, s4, s4), c4, dev)
     table = {
         "down1_fwd16": lambda: ops.conv3d_op16(x_dn1_16, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2), None),
         "down2_fwd16": lambda: ops.conv3d_op16(x_dn2_16, w_dn2, c4, 3, 2, 1, (s4, s4, s4), None),
+        "down1_fwd16s": lambda: ops.conv3d_op16(x_dn1_16, w_dn1, 2 * ngf, 3, 2, 1, (s2, s2, s2), ws_dn1, part_dn1),
+        "down2_fwd16s": lambda: ops.conv3d_op16(x_dn2_16, w_dn2, c4, 3, 2, 1, (s4, s4, s4), ws_dn2, part_dn2),
         "down1_wgrad16": lambda: ops.conv3d_wgrad_g16(dy_dn1, x_dn1_16, 3, 2, 1, gw_dn1, False),
         "down2_wgrad16": lambda: ops.conv3d_wgrad_g16(dy_dn2, x_dn2_16, 3, 2, 1, gw_dn2, False),
         "res_fwd16": lambda: ops.conv3d_op16(x_res16, w_res, c4, 3, 1, 0, (s4, s4, s4), ws_res_f, part_res),
@@ -159,7 +167,7 @@ def main():
                                              act="relu"),
         "in_bwd": lambda: ops.instnorm_bwd(x_in, *ops.instnorm_fwd(x_in, act="relu")[1:], dy_in, 3, None, act="relu"),
     }
-    names = [n for n in table if not n.endswith("16")] if args.ops == "all" else args.ops.split(",")
+    names = [n for n in table if not n.endswith(("16", "16s"))] if args.ops == "all" else args.ops.split(",")
     for name in names:
         fn = table[name]
         fn()
