@@ -537,9 +537,14 @@ int conv_brick_x3_launch(BrickArgs a, int bm, int bn, void* ws, size_t ws_bytes,
 // The fp32-input form (the kernel rounds the staged values to the very words of the operand plane)
 // runs the same kernel with one halo buffer: a plane input and an fp32 input give the same bits
 // (tests/test_graph_gpu.py::test_stride2_planes_bit_identical).
+// G down1 (32 input channels) stays on the implicit GEMM: its 64³ / 128³ input is HBM-bound either way
+// (r06u: [4×64³] 54.2 vs 56.4 µs, [2×64³] 29.4 vs 29.9) and the 128³ step ran 0.08 ms slower with the
+// brick on it (r06v: 28.24-28.28 vs 28.16-28.17 ms); MRAGAN_BRICK_S2_VAR set forces the brick on it too
 bool conv_brick_s2_applicable(const IgemmArgs& g) {
   static const bool off = getenv("MRAGAN_NO_BRICK_S2") != nullptr;
-  return !off && (g.x3 == kPrecBf16 || g.x3 == kPrecF16) && g.wx3 && g.k == 3 && g.s == 2 && g.p == 1 &&
+  static const bool forced = getenv("MRAGAN_BRICK_S2_VAR") != nullptr;
+  return !off && (forced || g.cx >= 2 * kBK) && (g.x3 == kPrecBf16 || g.x3 == kPrecF16) && g.wx3 && g.k == 3 &&
+         g.s == 2 && g.p == 1 &&
          !g.trans && !g.bs_x && g.act == kActNone && g.cx % kBK == 0 && g.ny % 64 == 0 && g.Di > 0 &&
          (int64_t)g.Di * g.Hi * g.Wi * g.cx * 4 < ((int64_t)1 << 31);
 }

@@ -1,6 +1,9 @@
 """Per-kernel parity: every HIP entry point (through the C ABI) against a float64 PyTorch-CPU
 evaluation of the same op.  Tolerances are relative L2 errors; fp32 kernels reach ~1e-6, the
 gate is 1e-5 (SURVEY §8c per-op gate)."""
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -948,16 +951,39 @@ def test_op16_stride2_conv_and_wgrad(op16, N, cin, cout, dims):
     assert rel(gw.view(cout, cin, 3, 3, 3), gw64) < 2e-5
 
 
-@pytest.mark.parametrize("N,cin,cout,dims", [(4, 32, 64, (64, 64, 64)), (2, 64, 128, (32, 32, 32)),
-                                              (1, 32, 64, (20, 18, 26)), (2, 64, 128, (24, 24, 24)),
-                                              (1, 64, 64, (14, 30, 10)), (2, 32, 128, (16, 16, 16))])
+S2_DEFAULT = [(2, 64, 128, (32, 32, 32)), (4, 64, 128, (32, 32, 32)), (2, 64, 128, (24, 24, 24)),
+              (1, 64, 64, (14, 30, 10)), (1, 96, 128, (20, 18, 26))]
+S2_FORCED = [(4, 32, 64, (64, 64, 64)), (1, 32, 64, (20, 18, 26)), (2, 32, 128, (16, 16, 16))]
+
+
+@pytest.mark.parametrize("N,cin,cout,dims", S2_DEFAULT)
 def test_stride2_brick(op16, N, cin, cout, dims):
-    """Round 6: G down1 / down2 (Conv3d k3 s2 p1, networks3D.py:191-197) on the
-    brick kernel's stride-2 form (conv_brick_x3.hip S = 2: LDS halo with even / odd w halves, the
-    pre-split weights).  The operand-plane input and the fp32 input give the same bits (output and
-    InstanceNorm partials); against the fp64 convolution of the rounded operands to 2e-5, the
-    partials against the output's own sums; ragged volumes (partial bricks) included."""
-    ops = op16
+    """Round 6: G down2 (Conv3d k3 s2 p1, networks3D.py:191-197) on the brick
+    kernel's stride-2 form (conv_brick_x3.hip S = 2: LDS halo with even / odd w halves, the pre-split
+    weights) — see stride2_brick_case."""
+    stride2_brick_case(op16, N, cin, cout, dims)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_stride2_brick_forced_down1(prec):
+    """The 32-input-channel form (G down1, on the implicit GEMM by default) forced onto the stride-2
+    brick (MRAGAN_BRICK_S2_VAR, read once per process: a child process), every variant."""
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "from mragan_hip import ops\nimport test_kernels_gpu as t\nops.set_conv_precision(%r)\n"
+            "for c in t.S2_FORCED: t.stride2_brick_case(ops, *c)\nprint('ok')\n"
+            % (here, os.path.join(os.path.dirname(here), "mra-gan_amd"), prec))
+    for var in ("1", "2", "4", "5"):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MRAGAN_BRICK_S2_VAR=var),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (var, r.stdout[-2000:], r.stderr[-3000:])
+
+
+def stride2_brick_case(ops, N, cin, cout, dims):
+    """The operand-plane input and the fp32 input give the same bits (output and InstanceNorm
+    partials); against the fp64 convolution of the rounded operands to 2e-5, the partials against the
+    output's own sums; ragged volumes (partial bricks) included."""
     dt = ops.op16_dtype()
     g = torch.Generator().manual_seed(N * 13 + cin + cout + dims[2])
     D, H, W = dims
