@@ -25,7 +25,7 @@ cd /tmp && export TMPDIR=/tmp
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o bench \
     -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-kernel-timing --alt-precisions '' --legs '' --no-cpu-baseline \
     > "$O/trace.log" 2>&1
-KB="$R/tools/kbench.py --ops res_dgrad16,res_wgrad16,res_fwd16,down1_fwd16,down1_wgrad16 --reps 10 --precision bf16 --N 4"
+KB="$R/tools/kbench.py --ops res_wgrad16p,res_dgrad16s,res_fwd16,down1_fwd16,down2_fwd16s,down1_wgrad16 --reps 10 --precision bf16 --N 4"
 step ktrace 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace" -o run -- python3 $KB > "$O/ktrace.log" 2>&1
 step fetch 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python3 $KB > "$O/fetch.log" 2>&1
 step write 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o run -- python3 $KB > "$O/write.log" 2>&1
