@@ -63,7 +63,9 @@ def build(verbose=False, jobs=None):
                 raise RuntimeError(f"hipcc failed for {cmd[-3]}")
             _check_no_scratch(cmd[-3], r.stderr)
     so = os.path.join(LIB, "libmragan_hip.so")
-    if cmds or not os.path.exists(so):
+    # relink also when an object is newer than the library (an object compiled by hand for a
+    # register-usage check would otherwise never reach the .so)
+    if cmds or not os.path.exists(so) or any(os.path.getmtime(o) > os.path.getmtime(so) for o in objs):
         r = subprocess.run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,--no-undefined", *objs, "-o", so],
                            capture_output=True, text=True)
         if r.returncode:
