@@ -106,7 +106,11 @@ struct Wgrad3Args {
 // WM = 2 (128 × 64 on operand planes, aligned stages; opt-in, measured slower — see the launch):
 // 4 waves of 64 × 32 instead of 8 of 32 × 32.  Per K-step a wave then reads 2 A + 3 B fragments
 // for 6 MFMAs instead of 1 + 3 for 3 (0.85 instead of 1.37 KB of transposing LDS reads per MFMA).
-template <int TC, int TI, int PM, int X16, int AL, int SW, int WM>
+// PF2 (round 6, operand-plane aligned path, opt-in MRAGAN_W3_PF2=1): two register sets for the staged
+// operands — the loads of stage st + 3 leave at the end of stage st and are stored at the end of stage
+// st + 2, two stages of MFMAs in between (one set leaves one stage, ≈ 1.5 k cycles, to cover an HBM /
+// L2 round trip; PMC r06x: waves parked 32 % of their cycles).  Measured neutral (r06y): kept opt-in.
+template <int TC, int TI, int PM, int X16, int AL, int SW, int WM, int PF2 = 0>
 __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_x3_kernel(Wgrad3Args a) {
   constexpr int NT = TC * TI / (16 * WM); // 32·WM × 32 sub-tile per wave
   constexpr int WC = TC / (32 * WM);      // waves along co
@@ -216,7 +220,9 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
   constexpr int DO8 = TC / 8, GO8 = TI / 8;                    // 16-B octets per voxel
   constexpr int DL = kSegW * DO8 / 64, GU = (kSegW + 2) * GO8, GL = (GU + 63) / 64;
   static_assert(kR % NW == 0 && (kSegW * DO8) % 64 == 0, "wave-per-segment staging");
+  static_assert(!PF2 || kW16, "two register sets: the aligned operand-plane path only");
   uint4 d16[kW16 ? SPW : 1][kW16 ? DL : 1], g16[kW16 ? SPW : 1][kW16 ? GL : 1];
+  uint4 d16b[PF2 ? SPW : 1][PF2 ? DL : 1], g16b[PF2 ? SPW : 1][PF2 ? GL : 1];
   int dlo[kW16 ? DL : 1], glo[kW16 ? GL : 1], rdo[kW16 ? SPW : 1], rgo[kW16 ? SPW : 1];
   if constexpr (kW16) {
 #pragma unroll
@@ -240,7 +246,7 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
   // descriptors (wave-uniform) and rebases its offsets by set 1's bytes (segment / X offsets stay
   // linear across the set boundary)
   const int xoff1 = a.N * Dg * Hg * Wg * a.Cg * ES;
-  auto load16 = [&](int st) __attribute__((always_inline)) {
+  auto load16x = [&](int st, auto& D16, auto& G16) __attribute__((always_inline)) {
     const int s0 = seg_lo + st * kR;
     const bool s2 = s0 >= a.nseg1;
     const __amdgpu_buffer_rsrc_t dr = s2 ? make_rsrc(a.dy2, a.N2 * a.D * a.H * a.W * a.Cd * ES) : dyr;
@@ -250,11 +256,12 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
 #pragma unroll
-      for (int j = 0; j < DL; ++j) d16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(dr, dlo[j], dso0 + rdo[q]));
+      for (int j = 0; j < DL; ++j) D16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(dr, dlo[j], dso0 + rdo[q]));
 #pragma unroll
-      for (int j = 0; j < GL; ++j) g16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(gr, glo[j], gso0 + rgo[q]));
+      for (int j = 0; j < GL; ++j) G16[q][j] = __builtin_bit_cast(uint4, buf_load_16b(gr, glo[j], gso0 + rgo[q]));
     }
   };
+  auto load16 = [&](int st) __attribute__((always_inline)) { load16x(st, d16, g16); };
   auto load = [&](int st) __attribute__((always_inline)) {
     if constexpr (kW16) {
       load16(st);
@@ -326,22 +333,23 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
       *reinterpret_cast<uint2*>(base + row * RB + 16 * ((q >> 1) ^ tr_swz<RB>(row)) + 8 * (q & 1)) = h;
     }
   };
-  auto store16 = [&]() __attribute__((always_inline)) {
+  auto store16x = [&](const auto& D16, const auto& G16) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < SPW; ++q) {
       const int r = wave + NW * q;
 #pragma unroll
       for (int j = 0; j < DL; ++j) {
         const int u = lane + 64 * j, row = (u / DO8) * kR + r;
-        *reinterpret_cast<uint4*>(Ds + row * RBD + 16 * ((u % DO8) ^ tr_swz<RBD>(row))) = d16[q][j];
+        *reinterpret_cast<uint4*>(Ds + row * RBD + 16 * ((u % DO8) ^ tr_swz<RBD>(row))) = D16[q][j];
       }
 #pragma unroll
       for (int j = 0; j < GL; ++j) {
         const int u = lane + 64 * j, row = (u / GO8) * kR + r;
-        if (u < GU) *reinterpret_cast<uint4*>(Gs + row * RBG + 16 * ((u % GO8) ^ tr_swz<RBG>(row))) = g16[q][j];
+        if (u < GU) *reinterpret_cast<uint4*>(Gs + row * RBG + 16 * ((u % GO8) ^ tr_swz<RBG>(row))) = G16[q][j];
       }
     }
   };
+  auto store16 = [&]() __attribute__((always_inline)) { store16x(d16, g16); };
   auto store = [&]() __attribute__((always_inline)) {
     if constexpr (kW16) {
       store16();
@@ -380,31 +388,8 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
     Ds = smem + b * kStage;
     Gs = Ds + kTrRowsD * RBD;
   };
-  if constexpr (kTr) {
-    // prologue: stage 0 staged, stage 1 in registers
-    if (nstage > 0) {
-      load(0);
-      store();
-    }
-    if (nstage > 1) {
-      adv_stage();
-      load(1);
-    }
-  } else if (nstage > 0) {
-    load(0);
-  }
-  for (int st = 0; st < nstage; ++st) {
-    if constexpr (kTr) {
-      use_buf(st & 1);
-      __syncthreads();              // stage st staged by every wave; buffer (st+1)&1 read by nobody now
-    } else {
-      store();
-      __syncthreads();
-      if (st + 1 < nstage) {                        // lands during this stage's MFMAs
-        adv_stage();
-        load(st + 1);
-      }
-    }
+  // the MFMAs of one staged stage (Ds / Gs: its buffers)
+  auto compute = [&]() __attribute__((always_inline)) {
     const char* arow = kTr ? Ds + trA[0] : Ds + (wm0 + li) * kDRow + lh * 16;
     const char* brow = kTr ? Gs + trB : Gs + (wn0 + li) * kGRow + lh * 16;
     // fragments of K-step ks: A hi/lo (dY) and B hi/lo for the three kw taps (X shifted by kw
@@ -446,6 +431,69 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
           acc[kw][i] = prec::mma<PM>(fa[c][i][0], fa[c][i][1], fb[c][kw][0], fb[c][kw][1], acc[kw][i]);
       __builtin_amdgcn_sched_barrier(0);
     }
+  };
+
+  if constexpr (PF2) {
+    // prologue: stage 0 staged; stages 1 and 2 in the register sets B and A
+    use_buf(0);
+    if (nstage > 0) {
+      load16x(0, d16, g16);
+      store16x(d16, g16);
+    }
+    if (nstage > 1) {
+      adv_stage();
+      load16x(1, d16b, g16b);
+    }
+    if (nstage > 2) {
+      adv_stage();
+      load16x(2, d16, g16);
+    }
+    // stage st: its MFMAs, then stage st + 1 from the set that holds it into the other buffer, and
+    // stage st + 3 into that set (unrolled by two: the set is compile-time)
+    auto step = [&](int st, auto& D16, auto& G16) __attribute__((always_inline)) {
+      use_buf(st & 1);
+      __syncthreads();              // stage st staged by every wave; buffer (st+1)&1 read by nobody now
+      compute();
+      if (st + 1 < nstage) {
+        use_buf((st + 1) & 1);
+        store16x(D16, G16);
+        if (st + 3 < nstage) {
+          adv_stage();
+          load16x(st + 3, D16, G16);
+        }
+      }
+    };
+    for (int st = 0; st < nstage; st += 2) {
+      step(st, d16b, g16b);
+      if (st + 1 < nstage) step(st + 1, d16, g16);
+    }
+  } else {
+  if constexpr (kTr) {
+    // prologue: stage 0 staged, stage 1 in registers
+    if (nstage > 0) {
+      load(0);
+      store();
+    }
+    if (nstage > 1) {
+      adv_stage();
+      load(1);
+    }
+  } else if (nstage > 0) {
+    load(0);
+  }
+  for (int st = 0; st < nstage; ++st) {
+    if constexpr (kTr) {
+      use_buf(st & 1);
+      __syncthreads();              // stage st staged by every wave; buffer (st+1)&1 read by nobody now
+    } else {
+      store();
+      __syncthreads();
+      if (st + 1 < nstage) {                        // lands during this stage's MFMAs
+        adv_stage();
+        load(st + 1);
+      }
+    }
+    compute();
     if constexpr (kTr) {
       if (st + 1 < nstage) {
         use_buf((st + 1) & 1);
@@ -458,6 +506,7 @@ __global__ void __launch_bounds__(TC * TI / (16 * WM), TC == 64 ? 2 : 1) wgrad3_
     } else {
       __syncthreads();
     }
+  }
   }
 
   // slab[z][t][co][ci]: lane li = ci column, register r = co row (r & 3) + 8 (r >> 2) + 4 lh
@@ -517,9 +566,9 @@ int wgrad3_x3_splits(const WgradArgs& a, int max_splits) {
   return s;
 }
 
-template <int TC, int TI, int PM, int X16, int AL, int SW = kSegW, int WM = 1>
+template <int TC, int TI, int PM, int X16, int AL, int SW = kSegW, int WM = 1, int PF2 = 0>
 static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
-  if constexpr ((X16 && prec::has_lo<PM>()) || ((SW != kSegW || WM != 1) && !(X16 && AL))) {
+  if constexpr ((X16 && prec::has_lo<PM>()) || ((SW != kSegW || WM != 1 || PF2) && !(X16 && AL))) {
     return;                                     // rejected by the caller
   } else {
     constexpr bool tr = !prec::has_lo<PM>();
@@ -528,11 +577,12 @@ static void launch_wgrad3(const Wgrad3Args& a, int blocks, hipStream_t st) {
     static_assert(SW == kSegW || lds_tr<SW, TC>() <= 160 * 1024, "LDS");
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM, PF2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM>), dim3(blocks), dim3(TC * TI / (16 * WM)), lds, st, a);
+    hipLaunchKernelGGL((wgrad3_x3_kernel<TC, TI, PM, X16, AL, SW, WM, PF2>), dim3(blocks), dim3(TC * TI / (16 * WM)), lds,
+                       st, a);
   }
 }
 
@@ -574,9 +624,15 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     // slower than the 8-wave tiles (res wgrad [4×16³] 34.2 vs 32.2 µs, [2×32³] 90.3 vs 81.9 µs,
     // r04r): the LDS reads were not the limiter, the two waves per SIMD are worth more
     static const bool wm2 = [] { const char* e = getenv("MRAGAN_W3_WM"); return e && atoi(e) == 2; }();
+    // two register sets of staged operands on the wide operand-plane tiles: opt-in A/B
+    // (MRAGAN_W3_PF2=1), measured neutral — res wgrad [4+2×16³] 37.5 vs 37.4 µs (rocprof), headline
+    // 9.75-9.77 vs 9.71-9.78 ms, 128³ 28.50-28.52 vs 28.53-28.57 ms (r06y): the staged loads' latency
+    // is not what parks these waves
+    static const bool pf1 = getenv("MRAGAN_W3_PF2") == nullptr;
     if (segw != kSegW) {
       if (wide) {
         if (wm2) launch_wgrad3<128, 64, PM, 1, 1, 24, 2>(a, blocks, st);
+        else if (!pf1) launch_wgrad3<128, 64, PM, 1, 1, 24, 1, 1>(a, blocks, st);
         else launch_wgrad3<128, 64, PM, 1, 1, 24>(a, blocks, st);
       } else {
         launch_wgrad3<64, 64, PM, 1, 1, 24>(a, blocks, st);
@@ -585,7 +641,11 @@ int conv_wgrad3_x3(const WgradArgs& g, int splits, hipStream_t st) {
     }
     if (wide) {
       if (g.in16 && al && wm2) launch_wgrad3<128, 64, PM, 1, 1, kSegW, 2>(a, blocks, st);
-      else if (g.in16) { if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st); }
+      else if (g.in16) {
+        if (al && !pf1) launch_wgrad3<128, 64, PM, 1, 1, kSegW, 1, 1>(a, blocks, st);
+        else if (al) launch_wgrad3<128, 64, PM, 1, 1>(a, blocks, st);
+        else launch_wgrad3<128, 64, PM, 1, 0>(a, blocks, st);
+      }
       else { if (al) launch_wgrad3<128, 64, PM, 0, 1>(a, blocks, st); else launch_wgrad3<128, 64, PM, 0, 0>(a, blocks, st); }
     } else {
       if (g.in16) { if (al) launch_wgrad3<64, 64, PM, 1, 1>(a, blocks, st); else launch_wgrad3<64, 64, PM, 1, 0>(a, blocks, st); }
