@@ -31,5 +31,8 @@ step fetch 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o ru
 step write 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o run -- python3 $KB > "$O/write.log" 2>&1
 step mix 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     SQ_ACTIVE_INST_ANY --output-format csv -d "$O/mix" -o run -- python3 $KB > "$O/mix.log" 2>&1
+# LDS pass (the res weight gradient's staging stores + transposing reads): array cycles and conflicts
+step lds 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVE_CYCLES \
+    --output-format csv -d "$O/lds" -o run -- python3 $KB > "$O/lds.log" 2>&1
 python3 "$R/tools/pmc_summary.py" "$O" brick wgrad igemm > "$O/pmc.txt" || true
 echo "[final] done"
