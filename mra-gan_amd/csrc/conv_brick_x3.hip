@@ -580,7 +580,8 @@ int conv_brick_s2(const IgemmArgs& g, hipStream_t st) {
   if (g.in_part) {
     a.part = g.in_part;
     if (g.in_chunks) *g.in_chunks = a.nbd * a.nbh * a.nbw;
-    if (g.in_tick && bn <= 128 && !getenv("MRAGAN_NO_X3_FIN")) {
+    static const bool no_fin = getenv("MRAGAN_NO_X3_FIN") != nullptr;   // A/B switch, as conv_brick's
+    if (g.in_tick && bn <= 128 && !no_fin) {
       a.tick = g.in_tick; a.fin0 = g.in_fin0; a.fin1 = g.in_fin1;
       a.fin_mode = 0;
       a.fin_S = (double)a.Do * a.Ho * a.Wo;
