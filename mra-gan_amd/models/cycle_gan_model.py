@@ -37,6 +37,9 @@ _TWO_PHASE = __import__("os").environ.get("MRAGAN_TWO_PHASE") is not None
 _FROZEN_D_ON_LANES = __import__("os").environ.get("MRAGAN_FROZEN_D_ON_LANES") is not None
 # A/B switch: MRAGAN_ADAM_AFTER=1 runs the four Adam updates after the step's graph (rounds 1-5)
 _ADAM_AFTER = __import__("os").environ.get("MRAGAN_ADAM_AFTER") is not None
+# A/B switch: MRAGAN_PACK_AT_START=1 repacks the generators' weights at the start of each lane (rounds
+# 1-6 first session) instead of right after their Adam update at the end of the previous step
+_PACK_AT_START = __import__("os").environ.get("MRAGAN_PACK_AT_START") is not None
 
 
 class ImagePool():
@@ -607,18 +610,31 @@ class CycleGANModel(BaseModel):
             rec_done_1 = ln.mark(1)
         keep = (list(defer_A.values()), list(defer_B.values()))
         adam_in = side is not None and self._adam_in_lanes()
+        tail = adam_in and self._pack_tail()
         with ln.on(0):
             ln.wait(0, rec_done_1)
             pGA.backward(self._cGA1, [dGA1, dDA], wgrad_pair=defer_A)
             if adam_in:         # every G_A gradient is done here (lane 1's G_A cycle pass is waited for)
                 self.optimizer_G.step_net(self.netG_A, self._step_hyper[0:6])
+                if tail:        # the next step's packs, at this lane's tail instead of its next start
+                    pGA.ensure_packed()
         with ln.on(1):
             ln.wait(1, rec_done_0)
             pGB.backward(self._cGB1, [dGB1, dDB], wgrad_pair=defer_B)
             if adam_in:
                 self.optimizer_G.step_net(self.netG_B, self._step_hyper[0:6])
+                if tail:
+                    pGB.ensure_packed()
         ln.join()
         del keep
+
+    def _pack_tail(self):
+        """The generators' weights are repacked right after their Adam update, at the end of their
+        lanes (the overlapped single-GPU schedule with the updates inside it): the next step's lanes
+        start with their forwards, and a graph replay leaves the generator packs fresh (the host's
+        dirty flag stays clear; a parameter change from outside the step sets it, and the next step
+        then repacks before its replay)."""
+        return self._overlap_D() and self._adam_in_lanes() and not _PACK_AT_START
 
     def _lanes(self):
         if self.parallel_lanes and self._aux_stream is None:
@@ -801,8 +817,15 @@ class CycleGANModel(BaseModel):
         """Record the G phase and the D phase as two HIP graphs (one memory pool).  Capturing
         launches nothing; the caller replays them for this step."""
         self._n_captures = getattr(self, '_n_captures', 0) + 1
+        # the graphs must contain the weight repacks: the discriminators' (and, without the tail
+        # repack, the generators') at the start of the step; with it the generators' are captured at
+        # their lanes' tails and the step starts from the packs the previous step left
+        tail = self._pack_tail()
         for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
-            n.mark_params_dirty()            # the graphs must contain the weight repacks
+            if tail and n in (self.netG_A, self.netG_B):
+                n.plan.ensure_packed()
+            else:
+                n.mark_params_dirty()
         torch.cuda.synchronize()
         gG, gD = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         side = torch.cuda.Stream()
@@ -855,7 +878,13 @@ class CycleGANModel(BaseModel):
             graphed = True
         if self._overlap_D():
             # one graph (or eager pass) for both phases, the D phase beside the G backward
+            tail = self._pack_tail()
             if graphed:
+                if tail:
+                    # parameters changed since the last step (a load, a manual edit) mark the plan
+                    # dirty: repack before the graph, which starts from the packs as they are
+                    for n in (self.netG_A, self.netG_B):
+                        n.plan.ensure_packed()
                 self._graphs[0].replay()
                 self._running_stats_graphed()
             else:
@@ -865,7 +894,8 @@ class CycleGANModel(BaseModel):
                 self.optimizer_D.step_dev(hD)
             if graphed:
                 for n in (self.netG_A, self.netG_B, self.netD_A, self.netD_B):
-                    n.mark_params_dirty()
+                    if not (tail and n in (self.netG_A, self.netG_B)):   # (the graph repacked those)
+                        n.mark_params_dirty()
             else:
                 self._eager_steps += 1
                 self._eager_shapes.add(shape_key)
