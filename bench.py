@@ -19,8 +19,9 @@ touching the GPU and exits with its status.
 Prints ONE JSON line on rank 0 (contract in the task description), with:
   roofline      — the dominant kernel BY TIME: one eager single-stream step (right after the timed
                   region) records every instrumented C-ABI call by launch class (op + shape); each
-                  class's call is re-issued 10× back to back between HIP events on its stream, so
-                  the class mean is the kernels' own duration; the class with the largest
+                  class's call is re-issued 10× back to back (captured once as a HIP graph and
+                  replayed) between HIP events on its stream, so the class mean is the kernels' own
+                  duration; the class with the largest
                   per-step total is reported with its algorithmic FLOP (or bytes) per launch ÷ that
                   mean;
   step_roofline — SURVEY §8(d)'s whole-step figure, (F/P_mfma + B_ew/BW_hbm) / T_step;
@@ -474,7 +475,8 @@ def run_leg(args, size, batch, precision, alts, barrier, dist, world, rank, nc=N
             "ms_per_step": round(dom["total_ms"], 4),
             "flop_per_launch": dom["flops"], "bytes_per_launch": dom["bytes"],
             "timing": f"dominant launch class by time; its C-ABI call re-issued {dom['reps']}x back to back "
-                      "between HIP events on the step's stream (after one warm launch), mean per launch"}
+                      + ("as one captured HIP graph replayed " if dom.get("graphed") else "")
+                      + "between HIP events on the step's stream (after one warm launch), mean per launch"}
         leg["top_kernels"] = [
             dict(cls=c, kernels=v["kernels"], launches_per_step=v["n"], ms_per_step=round(v["total_ms"], 4),
                  mean_us=round(1e3 * v["mean_ms"], 2),

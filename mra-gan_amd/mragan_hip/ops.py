@@ -4,6 +4,7 @@ torch stream; no call allocates inside the library (workspaces come from `Worksp
 from __future__ import annotations
 
 import ctypes as _ct
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -89,6 +90,10 @@ class Workspace:
 WS = Workspace()
 
 
+# A/B switch: MRAGAN_EAGER_CLASS_TIMING=1 times the launch classes by eager re-issue (rounds 1-6)
+_EAGER_CLASS_TIMING = os.environ.get("MRAGAN_EAGER_CLASS_TIMING") is not None
+
+
 class KernelTimer:
     """Per-launch-class timing of the instrumented C-ABI calls (bench.py's dominant-kernel
     roofline).  While `match` is set, each instrumented wrapper hands its call to `run(info, fn)`:
@@ -96,8 +101,11 @@ class KernelTimer:
     (MFMA-bound) or `bytes` (HBM-bound), the kernels it launched (library launch log) and the
     call itself.  `classes(reps)` then re-issues ONE recorded call of each class `reps` times back
     to back on the current stream between two HIP events (one warm launch first), so a class's
-    mean is the kernels' own duration: no host submission gap inside the interval and no spin
-    kernel in a profile of the run."""
+    mean is the kernels' own duration and no spin kernel appears in a profile of the run.  Since
+    round 6 the `reps` re-issues are captured once as a HIP graph and the graph is replayed between
+    the events: eagerly, a host slower than ~25 µs per ctypes call (a busy box) left submission gaps
+    inside the interval and inflated the short classes by up to 25 % (r06ac); a class whose call
+    cannot be captured falls back to the eager re-issue (`timing` then says so)."""
 
     def __init__(self):
         self.match = None       # callable(info: dict) -> bool
@@ -127,14 +135,34 @@ class KernelTimer:
             fn = c.pop("fn")
             fn()                                    # warm: first-touch of the operands, code load
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            graph = None
+            if not _EAGER_CLASS_TIMING:
+                try:
+                    torch.cuda.synchronize()
+                    graph = torch.cuda.CUDAGraph()
+                    side = torch.cuda.Stream()
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+                        for _ in range(reps):
+                            fn()
+                    torch.cuda.current_stream().wait_stream(side)
+                    graph.replay()                  # warm replay
+                except Exception:                   # not capturable: the eager re-issue below
+                    graph = None
+                    torch.cuda.synchronize()
             s.record()
-            for _ in range(reps):
-                fn()
+            if graph is not None:
+                graph.replay()
+            else:
+                for _ in range(reps):
+                    fn()
             e.record()
             e.synchronize()
             c["mean_ms"] = s.elapsed_time(e) / reps
             c["total_ms"] = c["mean_ms"] * c["n"]
             c["reps"] = reps
+            c["graphed"] = graph is not None
+            del graph
         self.calls = []
         return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_ms"]))
 
