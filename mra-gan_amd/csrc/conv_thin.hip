@@ -662,8 +662,8 @@ int conv_thin(ThinArgs a, hipStream_t st) {
 // ---------------------------------------------------------------------------------------
 constexpr int TW_D = 4, TW_H = 4, TW_W = 16, TW_M = TW_D * TW_H * TW_W;
 
-template <int K, int S, bool VDN>
-__global__ void __launch_bounds__(512) thin_wgrad_kernel(ThinWgradArgs a) {
+template <int K, int S, bool VDN, bool BIG = false>
+__global__ void __launch_bounds__(BIG ? 1024 : 512) thin_wgrad_kernel(ThinWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int RD = (TW_D - 1) * S + K, RH = (TW_H - 1) * S + K, RW = (TW_W - 1) * S + K;
   constexpr int WLEN = (TW_W - 1) * S + K;      // G row window of one tile row
@@ -825,13 +825,15 @@ static int thin_wgrad_setup(ThinWgradArgs& a, ThinWgradPlan* pl) {
   MRAGAN_CHECK_ARG(a.nroles <= 512, "thin_wgrad: %d roles > 512", a.nroles);
   // ≤ 256 roles: 512 threads (round 6 — the UNet's outermost k4 s2 weight gradients, 32 / 64 × 1
   // channels: one tile per block, so the tile rows split over RS ≥ 2 threads halve each thread's
-  // serial FMA chain; A/B switch MRAGAN_THIN_WGRAD_T=256 restores 256 threads)
+  // serial FMA chain; A/B switch MRAGAN_THIN_WGRAD_T=256 restores 256 threads, =1024 tries 1024 on
+  // the k4 layers)
   static const int nthr = [] {
     const char* e = getenv("MRAGAN_THIN_WGRAD_T");
-    return e && atoi(e) == 256 ? 256 : 512;
+    const int v = e ? atoi(e) : 512;
+    return v == 256 || v == 1024 ? v : 512;
   }();
   if (a.nroles <= 256) {
-    a.RS = nthr / a.nroles;
+    a.RS = (nthr > 512 && K != 4 ? 512 : nthr) / a.nroles;      // (1024 threads: the k4 instances only)
     if (a.RS > TW_D * TW_H) a.RS = TW_D * TW_H;
     pl->threads = (a.nroles * a.RS + 63) / 64 * 64;
     if (pl->threads < 256) pl->threads = 256;
@@ -866,6 +868,13 @@ size_t conv_thin_wgrad_ws_bytes(int N, int Dd, int Hd, int Wd, int Cd, int Cg, i
 template <int K, int S>
 static void launch_thin_wgrad(const ThinWgradArgs& a, const ThinWgradPlan& pl, hipStream_t st) {
   dim3 grid(pl.gx, pl.gy);
+  if constexpr (K == 4) {
+    if (pl.threads > 512) {            // the 1024-thread A/B form (MRAGAN_THIN_WGRAD_T=1024)
+      if (a.vec_dn) hipLaunchKernelGGL((thin_wgrad_kernel<K, S, true, true>), grid, dim3(pl.threads), pl.lds, st, a);
+      else hipLaunchKernelGGL((thin_wgrad_kernel<K, S, false, true>), grid, dim3(pl.threads), pl.lds, st, a);
+      return;
+    }
+  }
   if (a.vec_dn) hipLaunchKernelGGL((thin_wgrad_kernel<K, S, true>), grid, dim3(pl.threads), pl.lds, st, a);
   else hipLaunchKernelGGL((thin_wgrad_kernel<K, S, false>), grid, dim3(pl.threads), pl.lds, st, a);
 }
